@@ -1,0 +1,96 @@
+/*
+ * fqz_oracle.h -- CPU restatement of the SeqArc-1.6 no-reference block encoder.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (fastqueeze_amd/, the
+ * C-ABI library, the CLI) may link, load or call this code.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, and only as
+ * the checker / the timed CPU baseline.
+ *
+ * The reference (/root/reference) ships a single prebuilt executable
+ * (SeqArc-1.6) and no sources; this file restates its algorithm from static
+ * disassembly (objdump -d of the binary, read as text -- never executed).
+ * Every function cites SeqArc-1.6@0xADDR of the routine it restates.
+ *
+ * Parity pinning: the reference ships no output fixtures and its binary may not
+ * be run here, so byte-level parity is anchored on (1) the reference's own
+ * input files (test/ERR2755197_test_{1,2}.fq) together with the per-stream
+ * encoded sizes recorded in SURVEY.md section 6 from a reference run, and
+ * (2) exact restatement of the disassembly.  See DESIGN.md "Oracle".
+ */
+#ifndef FQZ_ORACLE_H
+#define FQZ_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Encoder parameters (SeqArcParam fields used by the no-ref path). */
+typedef struct {
+    int slevel;        /* param+0x1b54, default 3; seq order k = slevel + 7   */
+    int qlevel;        /* param+0x1b58, default 2                             */
+    int md5;           /* param+0x1880, default 1                             */
+    int bin_mode;      /* param+0x18a4 (ID template byte 0): encodeIDS path   */
+} orc_cfg;
+
+/* One parsed block (SeqArcMemBuf SoA; PE reads interleaved r1,r2). */
+typedef struct {
+    const uint8_t  *names;      /* concatenated IDs without '@'              */
+    const uint16_t *name_lens;
+    const uint8_t  *seq;        /* concatenated bases                        */
+    const int32_t  *seq_lens;
+    const uint8_t  *qual;       /* concatenated quals (same lengths as seq)  */
+    uint32_t        nreads;
+} orc_block;
+
+/* Encode one block exactly as EncapFqzComp::doFqzEncode@0x42d2d0 (after
+ * SeqArcMemBuf::calcBlockMd5@0x414d90 and DegeInfoProcess@0x433a10).
+ * Returns bytes written, or -1 on error / insufficient capacity. */
+int64_t orc_encode_block(const orc_block *b, const orc_cfg *cfg,
+                         uint8_t *out, size_t cap);
+
+/* Individual streams, each returning the complete encap (ID + size + payload)
+ * exactly as the corresponding compressX routine writes it. */
+int64_t orc_encap_seq(const orc_block *b, const orc_cfg *cfg, uint8_t *out, size_t cap);
+int64_t orc_encap_qual(const orc_block *b, const orc_cfg *cfg, uint8_t *out, size_t cap);
+int64_t orc_encap_len(const orc_block *b, uint8_t *out, size_t cap);
+int64_t orc_encap_id(const orc_block *b, const orc_cfg *cfg, uint8_t *out, size_t cap);
+
+/* Range-coded payload only (no encap header, no MD5) -- handy for tests. */
+int64_t orc_seq_payload(const orc_block *b, int k, uint8_t *out, size_t cap);
+int64_t orc_qual_payload(const orc_block *b, int qlevel, uint8_t *out, size_t cap);
+
+/* ID template analysis on the first block, IDProcess::analysisIDBinType@0x4310a0.
+ * tmpl is the 512-byte param+0x18a4 area (in/out, caller zero-initialises);
+ * se = 1 for single-end input. Returns 0, or -1 if the reference would throw. */
+int orc_analyze_idbin(const orc_block *first, int se, uint8_t tmpl[512]);
+
+/* RFC1321 MD5 (the vendored RSA implementation, MDString@0x4058f0). */
+void orc_md5(const uint8_t *data, size_t len, uint8_t digest[16]);
+
+/* FASTQ block cutting: SeqArcRead::doReadJob@0x432a80 / cultbuf@0x432530 /
+ * getEndPos@0x4320c0 (SE) and doReadPEJob@0x432d10 / cultPEbuf@0x432180 (PE).
+ * Fills block_ends[] with the end offset (exclusive) of each block in the
+ * input text; returns the number of blocks (or -1 if max_blocks too small).
+ * For PE, block_ends2[] receives the matching offsets in file 2. */
+int64_t orc_cut_se(const uint8_t *text, size_t len, size_t block_size,
+                   size_t *block_ends, size_t max_blocks);
+int64_t orc_cut_pe(const uint8_t *t1, size_t len1, const uint8_t *t2, size_t len2,
+                   size_t block_size, size_t *ends1, size_t *ends2, size_t max_blocks);
+
+/* Parse one block of FASTQ text into SoA: getBlockRead@0x411b60 (SE) and
+ * getBlockReadPE@0x412920 (PE, interleaving r1,r2).  The arrays must be large
+ * enough: names/seq/qual >= text length, lens >= text length / 4 + 1.
+ * Returns nreads or -1. */
+int64_t orc_parse_se(const uint8_t *text, size_t len,
+                     uint8_t *names, uint16_t *name_lens,
+                     uint8_t *seq, int32_t *seq_lens, uint8_t *qual);
+int64_t orc_parse_pe(const uint8_t *t1, size_t len1, const uint8_t *t2, size_t len2,
+                     uint8_t *names, uint16_t *name_lens,
+                     uint8_t *seq, int32_t *seq_lens, uint8_t *qual);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
