@@ -1,0 +1,260 @@
+"""fastqueeze_amd -- MI355X (gfx950) SeqArc no-reference block encoder.
+
+Thin ctypes binding of libseqarc_amd.so (include/seqarc_amd.h) used by the
+tests and bench.py.  The product path is the HIP library; there is no CPU
+fallback: if the library or a gfx950 device is missing, the calls raise.
+
+Reference interface mirrored (SeqArc-1.6, cited by address in the binary):
+  Encoder.encode()   EncapFqzComp::doFqzEncode@0x42d2d0 for a batch of blocks
+  cut_se / cut_pe    SeqArcRead::doReadJob@0x432a80 / doReadPEJob@0x432d10
+  parse_se / parse_pe AlignEncodeSEJob::getBlockRead@0x411b60 / getBlockReadPE@0x412920
+  analyze_ids        IDProcess::analysisIDBinType@0x4310a0
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import build as _build
+
+__all__ = ["SeqArcError", "blocks_from_fastq", "Block", "Config", "Encoder", "cut_se", "cut_pe", "parse_se", "parse_pe", "analyze_ids",
+           "load_library", "BLOCK_SIZE"]
+
+BLOCK_SIZE = 50 << 20   # SeqArcParam BlockSize(M) = 50 (ctor @0x40776f)
+
+_lib = None
+
+
+class SeqArcError(RuntimeError):
+    pass
+
+
+class _SaBlock(C.Structure):
+    _fields_ = [("names", C.c_void_p), ("name_lens", C.c_void_p), ("seq", C.c_void_p),
+                ("seq_lens", C.c_void_p), ("qual", C.c_void_p), ("nreads", C.c_uint32)]
+
+
+class _SaCfg(C.Structure):
+    _fields_ = [("slevel", C.c_int32), ("qlevel", C.c_int32), ("md5", C.c_int32), ("bin_mode", C.c_int32)]
+
+
+class _SaOut(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("cap", C.c_uint64), ("size", C.c_uint64)]
+
+
+def load_library(path: str | None = None):
+    """Load libseqarc_amd.so (building it first if the sources are newer)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if path is None:
+        path = _build.LIB
+        if _build.needs_build():
+            _build.build()
+    if not os.path.exists(path):
+        raise SeqArcError(f"libseqarc_amd.so not found at {path}")
+    lib = C.CDLL(path)
+    P, U64, I64, I32 = C.c_void_p, C.c_uint64, C.c_int64, C.c_int
+    sigs = {
+        "sa_create": ([I32], P), "sa_destroy": ([P], None), "sa_last_error": ([P], C.c_char_p),
+        "sa_version": ([], C.c_char_p), "sa_output_bound": ([P], U64),
+        "sa_encode_blocks": ([P, P, I32, P, P], I32), "sa_stage": ([P, P, I32], I32),
+        "sa_run": ([P, P], I32), "sa_fetch": ([P, P, I32], I32),
+        "sa_phase_times": ([P, P, P, I32], I32), "sa_set_timing": ([P, I32], None),
+        "sa_cut_se": ([P, U64, U64, P, U64], I64), "sa_cut_pe": ([P, U64, P, U64, U64, P, P, U64], I64),
+        "sa_parse_se": ([P, U64, P, P, P, P, P], I64), "sa_parse_pe": ([P, U64, P, U64, P, P, P, P, P], I64),
+        "sa_analyze_ids": ([P, I32, P], I32),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+@dataclass
+class Block:
+    """One parsed block: the SeqArcMemBuf SoA (PE reads interleaved r1, r2)."""
+    names: np.ndarray       # uint8, IDs without '@'
+    name_lens: np.ndarray   # uint16
+    seq: np.ndarray         # uint8
+    seq_lens: np.ndarray    # int32
+    qual: np.ndarray        # uint8
+    text_bytes: int = 0     # FASTQ bytes this block was parsed from
+
+    @property
+    def nreads(self) -> int:
+        return int(self.name_lens.shape[0])
+
+    def _c(self) -> _SaBlock:
+        return _SaBlock(_ptr(self.names), _ptr(self.name_lens), _ptr(self.seq), _ptr(self.seq_lens),
+                        _ptr(self.qual), self.nreads)
+
+
+@dataclass
+class Config:
+    """SeqArcParam fields of the no-ref path (defaults of SeqArcParam::SeqArcParam@0x407490)."""
+    slevel: int = 3
+    qlevel: int = 2
+    md5: bool = True
+    bin_mode: int = 0
+
+    def _c(self) -> _SaCfg:
+        return _SaCfg(self.slevel, self.qlevel, 1 if self.md5 else 0, 1 if self.bin_mode else 0)
+
+
+def _as_u8(text) -> np.ndarray:
+    if isinstance(text, np.ndarray):
+        return text.view(np.uint8).reshape(-1)
+    return np.frombuffer(text, dtype=np.uint8)
+
+
+def cut_se(text, block_size: int = BLOCK_SIZE) -> list[tuple[int, int]]:
+    lib = load_library()
+    t = _as_u8(text)
+    maxb = t.size // 1024 + 16
+    ends = np.zeros(maxb, dtype=np.uint64)
+    n = lib.sa_cut_se(_ptr(t), t.size, block_size, _ptr(ends), maxb)
+    if n < 0:
+        raise SeqArcError("block cut failed")
+    e = [0] + ends[:n].astype(np.int64).tolist()
+    return [(e[i], e[i + 1]) for i in range(n)]
+
+
+def cut_pe(t1, t2, block_size: int = BLOCK_SIZE):
+    lib = load_library()
+    a, b = _as_u8(t1), _as_u8(t2)
+    maxb = (a.size + b.size) // 1024 + 16
+    e1 = np.zeros(maxb, dtype=np.uint64)
+    e2 = np.zeros(maxb, dtype=np.uint64)
+    n = lib.sa_cut_pe(_ptr(a), a.size, _ptr(b), b.size, block_size, _ptr(e1), _ptr(e2), maxb)
+    if n < 0:
+        raise SeqArcError("PE block cut failed")
+    x = [0] + e1[:n].astype(np.int64).tolist()
+    y = [0] + e2[:n].astype(np.int64).tolist()
+    return [((x[i], x[i + 1]), (y[i], y[i + 1])) for i in range(n)]
+
+
+def _alloc(nbytes: int):
+    return (np.empty(nbytes + 16, np.uint8), np.empty(nbytes // 4 + 8, np.uint16), np.empty(nbytes + 16, np.uint8),
+            np.empty(nbytes // 4 + 8, np.int32), np.empty(nbytes + 16, np.uint8))
+
+
+def _trim(names, nl, seq, sl, qual, n, text_bytes) -> Block:
+    nl = nl[:n].copy()
+    sl = sl[:n].copy()
+    tn = int(nl.sum(dtype=np.int64))
+    ts = int(sl.sum(dtype=np.int64))
+    return Block(names[:tn].copy(), nl, seq[:ts].copy(), sl, qual[:ts].copy(), text_bytes)
+
+
+def parse_se(text) -> Block:
+    lib = load_library()
+    t = _as_u8(text)
+    names, nl, seq, sl, qual = _alloc(t.size)
+    n = lib.sa_parse_se(_ptr(t), t.size, _ptr(names), _ptr(nl), _ptr(seq), _ptr(sl), _ptr(qual))
+    if n < 0:
+        raise SeqArcError("FASTQ parse failed")
+    return _trim(names, nl, seq, sl, qual, n, t.size)
+
+
+def parse_pe(t1, t2) -> Block:
+    lib = load_library()
+    a, b = _as_u8(t1), _as_u8(t2)
+    names, nl, seq, sl, qual = _alloc(a.size + b.size)
+    n = lib.sa_parse_pe(_ptr(a), a.size, _ptr(b), b.size, _ptr(names), _ptr(nl), _ptr(seq), _ptr(sl), _ptr(qual))
+    if n < 0:
+        raise SeqArcError("PE FASTQ parse failed")
+    return _trim(names, nl, seq, sl, qual, n, a.size + b.size)
+
+
+def analyze_ids(first: Block, single_end: bool) -> np.ndarray:
+    lib = load_library()
+    tmpl = np.zeros(512, dtype=np.uint8)
+    cb = first._c()
+    if lib.sa_analyze_ids(C.byref(cb), 1 if single_end else 0, _ptr(tmpl)) != 0:
+        raise SeqArcError("ID template analysis failed (the reference would throw)")
+    return tmpl
+
+
+def blocks_from_fastq(t1, t2=None, block_size: int = BLOCK_SIZE) -> list[Block]:
+    """Cut and parse FASTQ text exactly as the reference's reader does."""
+    if t2 is None:
+        a = _as_u8(t1)
+        return [parse_se(a[s:e]) for s, e in cut_se(a, block_size)]
+    a, b = _as_u8(t1), _as_u8(t2)
+    return [parse_pe(a[s1:e1], b[s2:e2]) for (s1, e1), (s2, e2) in cut_pe(a, b, block_size)]
+
+
+class Encoder:
+    """A gfx950 device context of libseqarc_amd (one per device / host thread)."""
+
+    PHASES = 10
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        self._ctx = self._lib.sa_create(device)
+        if not self._ctx:
+            raise SeqArcError(f"no usable gfx950 device {device} (the HIP path is the only path)")
+        self._staged: list[Block] = []
+
+    def close(self):
+        if self._ctx:
+            self._lib.sa_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, what: str):
+        msg = self._lib.sa_last_error(self._ctx)
+        raise SeqArcError(f"{what}: {msg.decode() if msg else 'unknown error'}")
+
+    def set_timing(self, on: bool = True):
+        self._lib.sa_set_timing(self._ctx, 1 if on else 0)
+
+    def stage(self, blocks: list[Block]):
+        self._staged = list(blocks)
+        arr = (_SaBlock * max(1, len(blocks)))(*[b._c() for b in blocks])
+        if self._lib.sa_stage(self._ctx, arr, len(blocks)) != 0:
+            self._err("sa_stage")
+
+    def run(self, cfg: Config):
+        c = cfg._c()
+        if self._lib.sa_run(self._ctx, C.byref(c)) != 0:
+            self._err("sa_run")
+
+    def fetch(self) -> list[bytes]:
+        outs, keep = [], []
+        for b in self._staged:
+            cb = b._c()
+            cap = int(self._lib.sa_output_bound(C.byref(cb)))
+            buf = np.empty(cap, dtype=np.uint8)
+            keep.append(buf)
+            outs.append(_SaOut(_ptr(buf), cap, 0))
+        arr = (_SaOut * max(1, len(outs)))(*outs)
+        if self._lib.sa_fetch(self._ctx, arr, len(outs)) != 0:
+            self._err("sa_fetch")
+        return [keep[i][: arr[i].size].tobytes() for i in range(len(outs))]
+
+    def encode(self, blocks: list[Block], cfg: Config) -> list[bytes]:
+        self.stage(blocks)
+        self.run(cfg)
+        return self.fetch()
+
+    def phase_times(self) -> dict[str, float]:
+        names = (C.c_char_p * self.PHASES)()
+        ms = (C.c_float * self.PHASES)()
+        n = self._lib.sa_phase_times(self._ctx, names, ms, self.PHASES)
+        return {names[i].decode(): float(ms[i]) for i in range(n)}

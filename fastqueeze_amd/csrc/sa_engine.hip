@@ -1,0 +1,594 @@
+// sa_engine.hip -- host orchestration of the gfx950 block encoder and the C-ABI
+// (include/seqarc_amd.h).  Replaces EncapFqzComp::doFqzEncode@0x42d2d0 for a
+// batch of blocks: all blocks of a batch are encoded concurrently, every
+// stream of every block on its own range-coder lane.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/seqarc_amd.h"
+#include "sa_kernels.hip"
+#include "sa_plan.h"
+
+using namespace sa;
+
+namespace {
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes)
+    {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        size_t want = std::max(bytes, cap + cap / 4);
+        want = std::max<size_t>(want, 256);
+        hipError_t e = hipMalloc(&p, want);
+        cap = e == hipSuccess ? want : 0;
+        return e;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+const char* kPhaseNames[] = {"prep+scan", "emit", "sort_seq", "sort_aux", "replay_seq", "replay_aux",
+                             "coder", "md5", "assemble", "total"};
+enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX, PH_CODER, PH_MD5,
+       PH_ASM, PH_TOTAL, PH_N };
+
+}  // namespace
+
+struct sa_ctx {
+    int device = 0;
+    hipStream_t st = nullptr, st2 = nullptr;
+    std::string err;
+    bool timing = false;
+    hipEvent_t ev_beg[PH_N], ev_end[PH_N];
+    float ph_ms[PH_N];
+
+    // staged batch
+    std::vector<DevBlock> blocks;
+    uint32_t nblocks = 0, nreads = 0;
+    uint64_t names_bytes = 0, seq_bytes = 0;
+    DBuf d_names, d_seq, d_qual, d_read_block, d_name_off, d_name_len, d_seq_off, d_seq_len, d_blocks;
+    std::vector<uint32_t> h_read_block, h_name_off, h_seq_off, h_seq_len;
+    std::vector<uint16_t> h_name_len;
+
+    // work
+    DBuf d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
+    DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_aux_sym, d_rec_seq, d_rec_aux;
+    DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
+    DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
+    DBuf d_recip;
+    int seq_sorted_buf = 0, aux_sorted_buf = 0;
+
+    // last run
+    std::vector<uint64_t> final_base, final_len;
+    bool have_output = false;
+
+    ~sa_ctx()
+    {
+        DBuf* all[] = {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off,
+                       &d_seq_len, &d_blocks, &d_counts, &d_totals, &d_name_p, &d_name_s, &d_maxlen, &d_err,
+                       &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
+                       &d_aux_v[0], &d_aux_v[1], &d_aux_sym, &d_rec_seq, &d_rec_aux, &d_hist_seq,
+                       &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
+                       &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
+                       &d_final_len, &d_recip};
+        for (DBuf* b : all) b->release();
+        for (int i = 0; i < PH_N; i++) {
+            if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
+            if (ev_end[i]) (void)hipEventDestroy(ev_end[i]);
+        }
+        if (st) (void)hipStreamDestroy(st);
+        if (st2) (void)hipStreamDestroy(st2);
+    }
+};
+
+#define SA_CHECK(ctx, expr)                                                              \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+            return -1;                                                                   \
+        }                                                                                \
+    } while (0)
+
+namespace {
+
+int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
+             DBuf* keys, DBuf* vals, int bits, int& result_buf)
+{
+    result_buf = 0;
+    if (plan.total == 0 || bits <= 0) return 0;
+    SortView sv{};
+    sv.segs = segs.as<SortSeg>();
+    sv.tile_seg = tiles.as<uint32_t>();
+    sv.hist = hist.as<uint32_t>();
+    sv.total = plan.total;
+    sv.ntiles = (uint32_t)plan.tile_seg.size();
+    sv.nsegs = (uint32_t)plan.segs.size();
+    int cur = 0;
+    for (int shift = 0; shift < bits; shift += 8) {
+        hipLaunchKernelGGL(k_sort_hist, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,
+                           keys[cur].as<uint32_t>(), (uint32_t)shift);
+        hipLaunchKernelGGL(k_sort_scan, dim3(sv.nsegs), dim3(1024), 0, st, sv);
+        hipLaunchKernelGGL(k_sort_scatter, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,
+                           keys[cur].as<uint32_t>(), vals[cur].as<uint32_t>(), keys[cur ^ 1].as<uint32_t>(),
+                           vals[cur ^ 1].as<uint32_t>(), (uint32_t)shift);
+        cur ^= 1;
+    }
+    SA_CHECK(c, hipGetLastError());
+    result_buf = cur;
+    return 0;
+}
+
+void ev_begin(sa_ctx* c, int ph, hipStream_t st)
+{
+    if (c->timing) (void)hipEventRecord(c->ev_beg[ph], st);
+}
+void ev_finish(sa_ctx* c, int ph, hipStream_t st)
+{
+    if (c->timing) (void)hipEventRecord(c->ev_end[ph], st);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sa_version(void) { return "seqarc_amd 0.1 (gfx950)"; }
+
+sa_ctx* sa_create(int device)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return nullptr;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::fprintf(stderr, "seqarc_amd: device %d is %s, this library is built for gfx950 only\n", device,
+                     prop.gcnArchName);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    sa_ctx* c = new sa_ctx();
+    c->device = device;
+    for (int i = 0; i < PH_N; i++) c->ev_beg[i] = c->ev_end[i] = nullptr;
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    for (int i = 0; i < PH_N; i++) {
+        if (hipEventCreate(&c->ev_beg[i]) != hipSuccess || hipEventCreate(&c->ev_end[i]) != hipSuccess) {
+            delete c;
+            return nullptr;
+        }
+    }
+    // reciprocal table M = ceil(2^64 / t), t < 65536 (tot of any model <= 0xffe0)
+    std::vector<uint64_t> recip(65536, 0);
+    for (uint32_t t = 2; t < 65536; t++) recip[t] = ~0ull / t + 1;
+    if (c->d_recip.ensure(recip.size() * 8) != hipSuccess ||
+        hipMemcpy(c->d_recip.p, recip.data(), recip.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void sa_destroy(sa_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    delete ctx;
+}
+
+const char* sa_last_error(const sa_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+void sa_set_timing(sa_ctx* ctx, int on)
+{
+    if (ctx) ctx->timing = on != 0;
+}
+
+uint64_t sa_output_bound(const sa_block* b)
+{
+    uint64_t nb = 0, nn = 0;
+    for (uint32_t r = 0; r < b->nreads; r++) {
+        nb += (uint64_t)(b->seq_lens[r] > 0 ? b->seq_lens[r] : 0);
+        nn += b->name_lens[r];
+    }
+    // every stream's coder output is bounded by 2 bytes per symbol + flush
+    return 4096 + 2 * (nb + 3ull * b->nreads)          /* seq, len  */
+           + 2 * (nn + 3ull * b->nreads)                /* names     */
+           + 2 * (nb + b->nreads)                       /* qual      */
+           + 2 * (b->nreads + 2 * nb) + 68ull * 2 * nb  /* dege      */
+           + nn;
+}
+
+int sa_stage(sa_ctx* c, const sa_block* in, int n)
+{
+    if (!c) return -1;
+    SA_CHECK(c, hipSetDevice(c->device));
+    c->have_output = false;
+    c->nblocks = (uint32_t)n;
+    c->blocks.assign((size_t)n, DevBlock{});
+    uint64_t nb = 0, sb = 0;
+    uint32_t nr = 0;
+    for (int b = 0; b < n; b++) {
+        DevBlock& d = c->blocks[(size_t)b];
+        d.nreads = in[b].nreads;
+        d.read0 = nr;
+        uint64_t ln = 0, ls = 0;
+        for (uint32_t r = 0; r < in[b].nreads; r++) {
+            if (in[b].seq_lens[r] < 0) {
+                c->err = "negative read length";
+                return -1;
+            }
+            ln += in[b].name_lens[r];
+            ls += (uint64_t)in[b].seq_lens[r];
+        }
+        if (ls >= (1ull << 30) || ln >= (1ull << 32)) {
+            c->err = "block too large (a reference block is 50 MiB of FASTQ)";
+            return -1;
+        }
+        d.name_base = nb;
+        d.seq_base = sb;
+        d.name_bytes = ln;
+        d.seq_bytes = ls;
+        nb = align_up(nb + ln, 16);
+        sb = align_up(sb + ls, 16);
+        nr += in[b].nreads;
+    }
+    c->nreads = nr;
+    c->names_bytes = nb;
+    c->seq_bytes = sb;
+    c->h_read_block.resize(nr);
+    c->h_name_off.resize(nr);
+    c->h_name_len.resize(nr);
+    c->h_seq_off.resize(nr);
+    c->h_seq_len.resize(nr);
+    for (int b = 0; b < n; b++) {
+        const DevBlock& d = c->blocks[(size_t)b];
+        uint32_t no = 0, so = 0;
+        for (uint32_t r = 0; r < d.nreads; r++) {
+            const uint32_t g = d.read0 + r;
+            c->h_read_block[g] = (uint32_t)b;
+            c->h_name_off[g] = no;
+            c->h_name_len[g] = in[b].name_lens[r];
+            c->h_seq_off[g] = so;
+            c->h_seq_len[g] = (uint32_t)in[b].seq_lens[r];
+            no += in[b].name_lens[r];
+            so += (uint32_t)in[b].seq_lens[r];
+        }
+    }
+    SA_CHECK(c, c->d_names.ensure(nb + 16));
+    SA_CHECK(c, c->d_seq.ensure(sb + 16));
+    SA_CHECK(c, c->d_qual.ensure(sb + 16));
+    const size_t nr4 = (size_t)std::max<uint32_t>(nr, 1) * 4;
+    SA_CHECK(c, c->d_read_block.ensure(nr4));
+    SA_CHECK(c, c->d_name_off.ensure(nr4));
+    SA_CHECK(c, c->d_name_len.ensure(nr4));
+    SA_CHECK(c, c->d_seq_off.ensure(nr4));
+    SA_CHECK(c, c->d_seq_len.ensure(nr4));
+    for (int b = 0; b < n; b++) {
+        const DevBlock& d = c->blocks[(size_t)b];
+        if (d.name_bytes)
+            SA_CHECK(c, hipMemcpyAsync(c->d_names.as<uint8_t>() + d.name_base, in[b].names, d.name_bytes,
+                                       hipMemcpyHostToDevice, c->st));
+        if (d.seq_bytes) {
+            SA_CHECK(c, hipMemcpyAsync(c->d_seq.as<uint8_t>() + d.seq_base, in[b].seq, d.seq_bytes,
+                                       hipMemcpyHostToDevice, c->st));
+            SA_CHECK(c, hipMemcpyAsync(c->d_qual.as<uint8_t>() + d.seq_base, in[b].qual, d.seq_bytes,
+                                       hipMemcpyHostToDevice, c->st));
+        }
+    }
+    if (nr) {
+        SA_CHECK(c, hipMemcpyAsync(c->d_read_block.p, c->h_read_block.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_name_off.p, c->h_name_off.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_name_len.p, c->h_name_len.data(), nr * 2ull, hipMemcpyHostToDevice, c->st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_seq_off.p, c->h_seq_off.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_seq_len.p, c->h_seq_len.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
+    }
+    SA_CHECK(c, hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int sa_run(sa_ctx* c, const sa_cfg* cfg)
+{
+    if (!c) return -1;
+    SA_CHECK(c, hipSetDevice(c->device));
+    c->have_output = false;
+    const uint32_t nbk = c->nblocks;
+    if (nbk == 0) {
+        c->final_base.clear();
+        c->final_len.clear();
+        c->have_output = true;
+        return 0;
+    }
+    if (cfg->slevel < 0 || cfg->slevel > 9 || cfg->qlevel < 0 || cfg->qlevel > 3) {
+        c->err = "unsupported slevel/qlevel";
+        return -1;
+    }
+    const int k = cfg->slevel + 7;
+    const uint32_t ns = 1u << ((2 * k) & 31);
+    const int seq_bits = (2 * k) & 31;   // NS = 1 << seq_bits (x86 shl masks the count)
+    const int aux_bits = cfg->qlevel > 2 ? 21 : 17;
+    hipStream_t st = c->st;
+    const uint32_t nr = c->nreads;
+
+    SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
+    SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, c->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
+    SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
+    SA_CHECK(c, c->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_err.ensure(16));
+    SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 16, st));
+
+    BatchView bv{};
+    bv.blocks = c->d_blocks.as<DevBlock>();
+    bv.nblocks = nbk;
+    bv.nreads_total = nr;
+    bv.read_block = c->d_read_block.as<uint32_t>();
+    bv.names = c->d_names.as<uint8_t>();
+    bv.seq = c->d_seq.as<uint8_t>();
+    bv.qual = c->d_qual.as<uint8_t>();
+    bv.name_off = c->d_name_off.as<uint32_t>();
+    bv.name_len = c->d_name_len.as<uint16_t>();
+    bv.seq_off = c->d_seq_off.as<uint32_t>();
+    bv.seq_len = c->d_seq_len.as<uint32_t>();
+    bv.seq_mask = ns - 1;
+    bv.qlevel = cfg->qlevel;
+    bv.bin_mode = cfg->bin_mode ? 1 : 0;
+    bv.md5 = cfg->md5 ? 1 : 0;
+    uint32_t* d_err = c->d_err.as<uint32_t>();
+
+    ev_begin(c, PH_TOTAL, st);
+    ev_begin(c, PH_PREP, st);
+    const uint32_t rgrid = (nr + 255) / 256;
+    if (nr) {
+        hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                           c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
+    }
+    hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
+                       c->d_totals.as<uint32_t>(), c->d_maxlen.as<uint16_t>());
+    SA_CHECK(c, hipGetLastError());
+    ev_finish(c, PH_PREP, st);
+    std::vector<uint32_t> tot((size_t)nbk * NCOL);
+    uint32_t herr[4];
+    SA_CHECK(c, hipMemcpyAsync(tot.data(), c->d_totals.p, tot.size() * 4, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipMemcpyAsync(herr, c->d_err.p, 16, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipStreamSynchronize(st));
+    if (herr[0]) {
+        char buf[128];
+        std::snprintf(buf, sizeof buf, "input rejected (error bits 0x%x)", herr[0]);
+        c->err = buf;
+        return -1;
+    }
+
+    // ---- layout of the symbol spaces, coder tasks, md5 tasks, outputs ----
+    BatchPlan bp;
+    if (!plan_batch(c->blocks, tot, bp)) {
+        c->err = "block symbol space too large";
+        return -1;
+    }
+    const SortPlan& ps = bp.seq;
+    const SortPlan& pa = bp.aux;
+    const std::vector<CoderTask>& tasks = bp.tasks;
+    const std::vector<uint64_t>& task_out_base = bp.task_out_base;
+    const std::vector<AsmBlock>& asmb = bp.asmb;
+    const uint64_t payload = bp.payload_bytes, final_bytes = bp.final_bytes;
+    std::vector<Md5Task> md5t;
+    c->final_base.assign(nbk, 0);
+    for (uint32_t b = 0; b < nbk; b++) {
+        const DevBlock& d = c->blocks[b];
+        c->final_base[b] = asmb[b].out_base;
+        for (int f = 0; f < 3; f++) {
+            Md5Task m{};
+            if (f == 0) {
+                m.ptr = c->d_names.as<uint8_t>() + d.name_base;
+                m.len = d.name_bytes;
+            } else {
+                m.ptr = (f == 1 ? c->d_seq.as<uint8_t>() : c->d_qual.as<uint8_t>()) + d.seq_base;
+                m.len = d.seq_bytes;
+            }
+            md5t.push_back(m);
+        }
+    }
+
+    // ---- device buffers ----
+    const uint64_t stot = std::max<uint64_t>(ps.total, 1), atot = std::max<uint64_t>(pa.total, 1);
+    for (int i = 0; i < 2; i++) {
+        SA_CHECK(c, c->d_seq_k[i].ensure(stot * 4));
+        SA_CHECK(c, c->d_seq_v[i].ensure(stot * 4));
+        SA_CHECK(c, c->d_aux_k[i].ensure(atot * 4));
+        SA_CHECK(c, c->d_aux_v[i].ensure(atot * 4));
+    }
+    SA_CHECK(c, c->d_aux_sym.ensure(atot));
+    SA_CHECK(c, c->d_rec_seq.ensure(stot * sizeof(Rec)));
+    SA_CHECK(c, c->d_rec_aux.ensure(atot * sizeof(Rec)));
+    SA_CHECK(c, c->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
+    SA_CHECK(c, c->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
+    SA_CHECK(c, c->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
+    SA_CHECK(c, c->d_segs_aux.ensure(sizeof(SortSeg) * nbk));
+    SA_CHECK(c, c->d_tile_seq.ensure(std::max<size_t>(ps.tile_seg.size(), 1) * 4));
+    SA_CHECK(c, c->d_tile_aux.ensure(std::max<size_t>(pa.tile_seg.size(), 1) * 4));
+    SA_CHECK(c, c->d_tasks.ensure(sizeof(CoderTask) * tasks.size()));
+    SA_CHECK(c, c->d_out_len.ensure(4 * tasks.size()));
+    SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
+    SA_CHECK(c, c->d_md5tasks.ensure(sizeof(Md5Task) * md5t.size()));
+    SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
+    SA_CHECK(c, c->d_asm.ensure(sizeof(AsmBlock) * nbk));
+    SA_CHECK(c, c->d_task_out_base.ensure(8 * task_out_base.size()));
+    SA_CHECK(c, c->d_final.ensure(std::max<uint64_t>(final_bytes, 16)));
+    SA_CHECK(c, c->d_final_len.ensure(8 * nbk));
+
+    SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_segs_seq.p, ps.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_segs_aux.p, pa.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
+    if (!ps.tile_seg.empty())
+        SA_CHECK(c, hipMemcpyAsync(c->d_tile_seq.p, ps.tile_seg.data(), ps.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
+    if (!pa.tile_seg.empty())
+        SA_CHECK(c, hipMemcpyAsync(c->d_tile_aux.p, pa.tile_seg.data(), pa.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_asm.p, asmb.data(), sizeof(AsmBlock) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_task_out_base.p, task_out_base.data(), 8 * task_out_base.size(),
+                               hipMemcpyHostToDevice, st));
+
+    // ---- MD5 on the second stream (inputs only) ----
+    if (cfg->md5) {
+        hipEvent_t ready;
+        SA_CHECK(c, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        SA_CHECK(c, hipEventRecord(ready, st));
+        SA_CHECK(c, hipStreamWaitEvent(c->st2, ready, 0));
+        (void)hipEventDestroy(ready);
+        ev_begin(c, PH_MD5, c->st2);
+        hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(64), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
+                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>());
+        ev_finish(c, PH_MD5, c->st2);
+        SA_CHECK(c, hipGetLastError());
+    }
+
+    // ---- emit ----
+    ev_begin(c, PH_EMIT, st);
+    SA_CHECK(c, hipMemsetAsync(c->d_seq_k[0].p, 0xff, ps.total * 4, st));
+    SA_CHECK(c, hipMemsetAsync(c->d_aux_k[0].p, 0xff, pa.total * 4, st));
+    if (nr) {
+        hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                           c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), c->d_maxlen.as<uint16_t>(),
+                           c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(), c->d_aux_k[0].as<uint32_t>(),
+                           c->d_aux_v[0].as<uint32_t>(), c->d_aux_sym.as<uint8_t>(), d_err);
+    }
+    SA_CHECK(c, hipGetLastError());
+    ev_finish(c, PH_EMIT, st);
+
+    // ---- sorts ----
+    ev_begin(c, PH_SORT_SEQ, st);
+    if (run_sort(c, st, ps, c->d_segs_seq, c->d_tile_seq, c->d_hist_seq, c->d_seq_k, c->d_seq_v,
+                 ns > 1 ? seq_bits : 0, c->seq_sorted_buf))
+        return -1;
+    ev_finish(c, PH_SORT_SEQ, st);
+    ev_begin(c, PH_SORT_AUX, st);
+    if (run_sort(c, st, pa, c->d_segs_aux, c->d_tile_aux, c->d_hist_aux, c->d_aux_k, c->d_aux_v, aux_bits,
+                 c->aux_sorted_buf))
+        return -1;
+    ev_finish(c, PH_SORT_AUX, st);
+
+    // ---- replays ----
+    SortView svs{c->d_segs_seq.as<SortSeg>(), c->d_tile_seq.as<uint32_t>(), c->d_hist_seq.as<uint32_t>(),
+                 ps.total, (uint32_t)ps.tile_seg.size(), nbk};
+    SortView sva{c->d_segs_aux.as<SortSeg>(), c->d_tile_aux.as<uint32_t>(), c->d_hist_aux.as<uint32_t>(),
+                 pa.total, (uint32_t)pa.tile_seg.size(), nbk};
+    ev_begin(c, PH_REPLAY_SEQ, st);
+    if (ps.total)
+        hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)((ps.total + 255) / 256)), dim3(256), 0, st, svs,
+                           c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
+                           c->d_rec_seq.as<Rec>(), c->d_recip.as<uint64_t>());
+    ev_finish(c, PH_REPLAY_SEQ, st);
+    ev_begin(c, PH_REPLAY_AUX, st);
+    if (pa.total)
+        hipLaunchKernelGGL(k_replay_aux, dim3((uint32_t)((pa.total + RP_THREADS - 1) / RP_THREADS)),
+                           dim3(RP_THREADS), 0, st, sva, c->d_aux_k[c->aux_sorted_buf].as<uint32_t>(),
+                           c->d_aux_v[c->aux_sorted_buf].as<uint32_t>(), c->d_aux_sym.as<uint8_t>(),
+                           c->d_rec_aux.as<Rec>(), c->d_recip.as<uint64_t>(), d_err);
+    SA_CHECK(c, hipGetLastError());
+    ev_finish(c, PH_REPLAY_AUX, st);
+
+    // ---- range coders ----
+    ev_begin(c, PH_CODER, st);
+    hipLaunchKernelGGL(k_coder, dim3((uint32_t)tasks.size()), dim3(64), 0, st, c->d_tasks.as<CoderTask>(),
+                       (uint32_t)tasks.size(), c->d_rec_seq.as<Rec>(), c->d_rec_aux.as<Rec>(),
+                       c->d_payload.as<uint8_t>(), c->d_out_len.as<uint32_t>(), d_err);
+    SA_CHECK(c, hipGetLastError());
+    ev_finish(c, PH_CODER, st);
+
+    // ---- assembly ----
+    if (cfg->md5) {
+        hipEvent_t done;
+        SA_CHECK(c, hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        SA_CHECK(c, hipEventRecord(done, c->st2));
+        SA_CHECK(c, hipStreamWaitEvent(st, done, 0));
+        (void)hipEventDestroy(done);
+    }
+    ev_begin(c, PH_ASM, st);
+    AsmView av{c->d_asm.as<AsmBlock>(), c->d_task_out_base.as<uint64_t>()};
+    hipLaunchKernelGGL(k_assemble, dim3(nbk), dim3(256), 0, st, bv, av, c->d_payload.as<uint8_t>(),
+                       c->d_out_len.as<uint32_t>(), c->d_digests.as<uint32_t>(), c->d_final.as<uint8_t>(),
+                       c->d_final_len.as<uint64_t>());
+    SA_CHECK(c, hipGetLastError());
+    ev_finish(c, PH_ASM, st);
+    ev_finish(c, PH_TOTAL, st);
+
+    c->final_len.assign(nbk, 0);
+    SA_CHECK(c, hipMemcpyAsync(c->final_len.data(), c->d_final_len.p, 8ull * nbk, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipMemcpyAsync(herr, c->d_err.p, 16, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipStreamSynchronize(st));
+    if (herr[0]) {
+        char buf[128];
+        std::snprintf(buf, sizeof buf, "device error bits 0x%x", herr[0]);
+        c->err = buf;
+        return -1;
+    }
+    if (c->timing) {
+        for (int i = 0; i < PH_N; i++) {
+            c->ph_ms[i] = 0.f;
+            if (i == PH_MD5 && !cfg->md5) continue;
+            (void)hipEventElapsedTime(&c->ph_ms[i], c->ev_beg[i], c->ev_end[i]);
+        }
+    }
+    c->have_output = true;
+    return 0;
+}
+
+int sa_phase_times(const sa_ctx* c, const char** names, float* ms, int max)
+{
+    if (!c || !c->timing) return 0;
+    int n = std::min(max, (int)PH_N);
+    for (int i = 0; i < n; i++) {
+        if (names) names[i] = kPhaseNames[i];
+        if (ms) ms[i] = c->ph_ms[i];
+    }
+    return n;
+}
+
+int sa_fetch(sa_ctx* c, sa_out* out, int n)
+{
+    if (!c || !c->have_output) return -1;
+    if ((uint32_t)n != c->final_len.size()) {
+        c->err = "sa_fetch: block count mismatch";
+        return -1;
+    }
+    SA_CHECK(c, hipSetDevice(c->device));
+    for (int b = 0; b < n; b++) {
+        if (c->final_len[(size_t)b] > out[b].cap) {
+            c->err = "sa_fetch: output buffer too small";
+            return -1;
+        }
+        SA_CHECK(c, hipMemcpyAsync(out[b].data, c->d_final.as<uint8_t>() + c->final_base[(size_t)b],
+                                   c->final_len[(size_t)b], hipMemcpyDeviceToHost, c->st));
+        out[b].size = c->final_len[(size_t)b];
+    }
+    SA_CHECK(c, hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, sa_out* out)
+{
+    if (!ctx || !cfg || (n > 0 && (!in || !out))) return -1;
+    if (sa_stage(ctx, in, n)) return -1;
+    if (sa_run(ctx, cfg)) return -1;
+    return sa_fetch(ctx, out, n);
+}
+
+}  // extern "C"

@@ -1,0 +1,471 @@
+// sa_kernels.hip -- gfx950 kernels of the SeqArc no-reference block encoder.
+//
+// Pipeline per batch of blocks:
+//   k_prep        per read: symbol counts of every stream, name prefix/suffix
+//   k_scan_reads  per block: exclusive scan of the counts over its reads
+//   k_emit        per read: (model id, symbol, stream position) of every symbol
+//   k_sort_*      per block: stable LSD radix sort of the symbols by model id
+//   k_replay_*    per model: replay the adaptive model in stream order
+//   k_coder       per (block, stream): the serial carry-less range coder
+//   k_md5         per (block, field): RFC1321 digest (runs on a second stream)
+//   k_assemble    per block: encaps in doFqzEncode@0x42d2d0 order
+#include <hip/hip_runtime.h>
+
+#include "sa_common.h"
+#include "sa_device.h"
+#include "sa_logic.h"
+
+namespace sa {
+
+// ---------------------------------------------------------------------------
+// wave / workgroup helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ inline uint32_t lane_id() { return __lane_id(); }
+
+__device__ inline uint32_t wave_incl_scan(uint32_t v)
+{
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += t;
+    }
+    return v;
+}
+
+// exclusive scan across a 1024-thread workgroup; returns the workgroup total
+__device__ inline uint32_t wg1024_excl_scan(uint32_t v, uint32_t& excl, uint32_t* sh /*16*/)
+{
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t s = lane < 16 ? sh[lane] : 0;
+        s = wave_incl_scan(s);
+        if (lane < 16) sh[lane] = s;
+    }
+    __syncthreads();
+    uint32_t wpre = w ? sh[w - 1] : 0;
+    uint32_t total = sh[15];
+    excl = wpre + inc - v;
+    __syncthreads();
+    return total;
+}
+
+// ---------------------------------------------------------------------------
+// k_prep: one thread per read
+// ---------------------------------------------------------------------------
+__global__ void k_prep(const BatchView bv, uint32_t* __restrict__ counts,
+                       int16_t* __restrict__ name_p, int16_t* __restrict__ name_s,
+                       uint32_t* __restrict__ err)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bv.nreads_total) return;
+    const uint32_t e = prep_read(bv, r, counts, name_p, name_s);
+    if (e) atomicOr(err, e);
+}
+
+// ---------------------------------------------------------------------------
+// k_scan_reads: one 1024-thread workgroup per block; exclusive scan of the
+// count columns over the block's reads (in place) and per-block totals.  Also
+// the running maximum of name lengths before each read (name_maxlen).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan_reads(const BatchView bv, uint32_t* __restrict__ counts,
+                                                     uint32_t* __restrict__ totals,
+                                                     uint16_t* __restrict__ name_maxlen)
+{
+    __shared__ uint32_t sh[16];
+    __shared__ uint32_t shmax[16];
+    const uint32_t b = blockIdx.x;
+    const DevBlock& blk = bv.blocks[b];
+    const uint32_t r0 = blk.read0, n = blk.nreads;
+    uint32_t carry[NCOL];
+#pragma unroll
+    for (int k = 0; k < NCOL; k++) carry[k] = 0;
+    uint32_t mcarry = 0;
+    for (uint32_t base = 0; base < n; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const bool in = i < n;
+        uint32_t* c = counts + (size_t)(r0 + i) * NCOL;
+#pragma unroll
+        for (int k = 0; k < NCOL; k++) {
+            uint32_t v = in ? c[k] : 0;
+            uint32_t ex;
+            uint32_t tot = wg1024_excl_scan(v, ex, sh);
+            if (in) c[k] = carry[k] + ex;
+            carry[k] += tot;
+        }
+        // exclusive running max of name lengths
+        uint32_t v = in ? bv.name_len[r0 + i] : 0;
+        const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+        uint32_t m = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint32_t t = __shfl_up(m, d, 64);
+            if (lane >= (uint32_t)d) m = m > t ? m : t;
+        }
+        if (lane == 63) shmax[w] = m;
+        __syncthreads();
+        uint32_t wmax = mcarry;
+        for (uint32_t k = 0; k < w; k++) wmax = wmax > shmax[k] ? wmax : shmax[k];
+        uint32_t prev_incl = __shfl_up(m, 1, 64);
+        uint32_t excl = lane ? (prev_incl > wmax ? prev_incl : wmax) : wmax;
+        if (in) name_maxlen[r0 + i] = (uint16_t)excl;
+        uint32_t all = mcarry;
+        for (uint32_t k = 0; k < 16; k++) all = all > shmax[k] ? all : shmax[k];
+        __syncthreads();
+        mcarry = all;
+    }
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NCOL; k++) totals[(size_t)b * NCOL + k] = carry[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_emit: one thread per read; writes every symbol of the read.
+// ---------------------------------------------------------------------------
+__global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts,
+                       const int16_t* __restrict__ name_p, const int16_t* __restrict__ name_s,
+                       const uint16_t* __restrict__ name_maxlen,
+                       uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
+                       uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
+                       uint8_t* __restrict__ aux_sym, uint32_t* __restrict__ err)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bv.nreads_total) return;
+    const uint32_t e = emit_read(bv, r, counts, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key,
+                                 aux_val, aux_sym);
+    if (e) atomicOr(err, e);
+}
+
+// ---------------------------------------------------------------------------
+// Segmented stable LSD radix sort (8-bit digits).
+// A segment is one block's symbol space, padded with key 0xffffffff to a whole
+// number of tiles.  Tile = 256 threads x 16 keys; each wave owns 1024
+// consecutive keys processed in 16 rounds of 64, ranked with an 8-ballot
+// match (the wavefront "multi-split"), so the scatter is stable.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, const uint32_t* __restrict__ keys,
+                                                            uint32_t shift)
+{
+    __shared__ uint32_t h[256];
+    const uint32_t t = blockIdx.x;
+    const SortSeg& sg = sv.segs[sv.tile_seg[t]];
+    const uint32_t lt = t - sg.tile0;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t* K = keys + sg.base + (size_t)lt * SORT_TILE;
+#pragma unroll
+    for (int i = 0; i < SORT_ITEMS; i++) {
+        uint32_t k = K[threadIdx.x + i * SORT_THREADS];
+        atomicAdd(&h[(k >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    sv.hist[sg.hist_base + (size_t)threadIdx.x * sg.ntiles + lt] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
+{
+    __shared__ uint32_t sh[16];
+    const SortSeg& sg = sv.segs[blockIdx.x];
+    uint32_t* H = sv.hist + sg.hist_base;
+    const size_t n = (size_t)sg.ntiles * 256;
+    uint32_t carry = 0;
+    for (size_t base = 0; base < n; base += 4096) {
+        uint32_t v[4];
+        uint32_t loc = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            size_t i = base + (size_t)threadIdx.x * 4 + j;
+            v[j] = i < n ? H[i] : 0;
+            loc += v[j];
+        }
+        uint32_t ex;
+        uint32_t tot = wg1024_excl_scan(loc, ex, sh);
+        uint32_t run = carry + ex;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            size_t i = base + (size_t)threadIdx.x * 4 + j;
+            if (i < n) H[i] = run;
+            run += v[j];
+        }
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv,
+                                                               const uint32_t* __restrict__ kin,
+                                                               const uint32_t* __restrict__ vin,
+                                                               uint32_t* __restrict__ kout,
+                                                               uint32_t* __restrict__ vout, uint32_t shift)
+{
+    __shared__ uint32_t wc[SORT_THREADS / 64][256];
+    const uint32_t t = blockIdx.x;
+    const SortSeg& sg = sv.segs[sv.tile_seg[t]];
+    const uint32_t lt = t - sg.tile0;
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    for (uint32_t i = threadIdx.x; i < (SORT_THREADS / 64) * 256; i += SORT_THREADS) (&wc[0][0])[i] = 0;
+    __syncthreads();
+    const size_t wbase = sg.base + (size_t)lt * SORT_TILE + (size_t)w * (64 * SORT_ITEMS);
+    uint32_t k[SORT_ITEMS], v[SORT_ITEMS], rk[SORT_ITEMS];
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+        k[r] = kin[wbase + (size_t)r * 64 + lane];
+        v[r] = vin[wbase + (size_t)r * 64 + lane];
+    }
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+        const uint32_t d = (k[r] >> shift) & 255;
+        uint64_t peers = ~0ull;
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const uint64_t bal = __ballot((d >> bit) & 1);
+            peers &= ((d >> bit) & 1) ? bal : ~bal;
+        }
+        const uint32_t before = wc[w][d];
+        rk[r] = before + (uint32_t)__popcll(peers & lt_mask);
+        if ((peers & lt_mask) == 0) wc[w][d] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+        const uint32_t d = threadIdx.x;   // SORT_THREADS == 256 digits
+        uint32_t acc = sv.hist[sg.hist_base + (size_t)d * sg.ntiles + lt];
+#pragma unroll
+        for (int ww = 0; ww < SORT_THREADS / 64; ww++) {
+            uint32_t tcount = wc[ww][d];
+            wc[ww][d] = acc;
+            acc += tcount;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+        const uint32_t d = (k[r] >> shift) & 255;
+        const size_t dst = sg.base + wc[w][d] + rk[r];
+        kout[dst] = k[r];
+        vout[dst] = v[r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sequence model replay: BASE_MODEL<u8> of encode_seq@0x421f30.  Thread i
+// starts a segment when its key differs from the previous key of the block;
+// it walks the segment and writes the coder record of every base.
+// ---------------------------------------------------------------------------
+__global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ keys,
+                             const uint32_t* __restrict__ vals, Rec* __restrict__ rec,
+                             const uint64_t* __restrict__ recip)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= sv.total) return;
+    const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
+    const uint32_t key = keys[i];
+    if (key == SORT_PAD) return;
+    if (i != sg.base && keys[i - 1] == key) return;
+    replay_seq_run(keys, vals, i, sg.base + sg.count, key, rec + sg.base, recip);
+}
+
+// ---------------------------------------------------------------------------
+// AUX model replay: SIMPLE_MODEL<N> (kModelEncode@0x42ccb0 and every inlined
+// copy).  One thread per segment start; the model lives in LDS, one 261-dword
+// region per thread (odd stride -> conflict-free).  Entry = sym<<16 | freq.
+// ---------------------------------------------------------------------------
+constexpr int RP_THREADS = 64;
+constexpr int RP_STRIDE = 261;
+
+__global__ __launch_bounds__(RP_THREADS) void k_replay_aux(const SortView sv, const uint32_t* __restrict__ keys,
+                                                           const uint32_t* __restrict__ vals,
+                                                           const uint8_t* __restrict__ syms,
+                                                           Rec* __restrict__ rec,
+                                                           const uint64_t* __restrict__ recip,
+                                                           uint32_t* __restrict__ err)
+{
+    __shared__ uint32_t lds[RP_THREADS * RP_STRIDE];
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= sv.total) return;
+    const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
+    const uint32_t key = keys[i];
+    if (key == SORT_PAD) return;
+    if (i != sg.base && keys[i - 1] == key) return;
+    uint32_t* F = lds + threadIdx.x * RP_STRIDE;
+    const uint32_t e = replay_simple_run(keys, vals, syms + sg.base, i, sg.base + sg.count, key, rec + sg.base,
+                                         recip, F);
+    if (e) atomicOr(err, e);
+}
+
+// ---------------------------------------------------------------------------
+// Range coder: one lane per (block, stream) task.  Carry-less 64-bit coder of
+// encode_seq@0x422010-0x422085, finish = 8 x (low>>56) @0x424a1c.
+// q = range / tot via the per-symbol reciprocal M = ceil(2^64 / tot).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_coder(const CoderTask* __restrict__ tasks, uint32_t ntasks,
+                                              const Rec* __restrict__ rec_seq, const Rec* __restrict__ rec_aux,
+                                              uint8_t* __restrict__ out, uint32_t* __restrict__ out_len,
+                                              uint32_t* __restrict__ err)
+{
+    const uint32_t t = blockIdx.x;
+    if (t >= ntasks || threadIdx.x != 0) return;
+    const CoderTask tk = tasks[t];
+    const Rec* R = (tk.space ? rec_aux : rec_seq) + tk.rec_base;
+    uint32_t len = 0;
+    const uint32_t e = code_stream(R, tk.n, out + tk.out_base, tk.out_cap, len);
+    out_len[t] = len;
+    if (e) atomicOr(err, e);
+}
+
+// ---------------------------------------------------------------------------
+// MD5 (RFC 1321; MDString@0x4058f0): one lane per message.  Messages start at
+// 16-byte aligned offsets (the host aligns every block's name/seq/qual base).
+// ---------------------------------------------------------------------------
+__device__ inline uint32_t rotl(uint32_t x, int c) { return __builtin_amdgcn_alignbit(x, x, 32 - c); }
+
+#define MD5_STEP(F, a, b, c, d, x, k, s) \
+    a = b + rotl(a + F(b, c, d) + x + k, s)
+#define MD5_F(b, c, d) (((c ^ d) & b) ^ d)
+#define MD5_G(b, c, d) (((b ^ c) & d) ^ c)
+#define MD5_H(b, c, d) (b ^ c ^ d)
+#define MD5_I(b, c, d) (c ^ (b | ~d))
+
+__device__ inline void md5_block(uint32_t h[4], const uint32_t M[16])
+{
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+    MD5_STEP(MD5_F, a, b, c, d, M[0], 0xd76aa478, 7);
+    MD5_STEP(MD5_F, d, a, b, c, M[1], 0xe8c7b756, 12);
+    MD5_STEP(MD5_F, c, d, a, b, M[2], 0x242070db, 17);
+    MD5_STEP(MD5_F, b, c, d, a, M[3], 0xc1bdceee, 22);
+    MD5_STEP(MD5_F, a, b, c, d, M[4], 0xf57c0faf, 7);
+    MD5_STEP(MD5_F, d, a, b, c, M[5], 0x4787c62a, 12);
+    MD5_STEP(MD5_F, c, d, a, b, M[6], 0xa8304613, 17);
+    MD5_STEP(MD5_F, b, c, d, a, M[7], 0xfd469501, 22);
+    MD5_STEP(MD5_F, a, b, c, d, M[8], 0x698098d8, 7);
+    MD5_STEP(MD5_F, d, a, b, c, M[9], 0x8b44f7af, 12);
+    MD5_STEP(MD5_F, c, d, a, b, M[10], 0xffff5bb1, 17);
+    MD5_STEP(MD5_F, b, c, d, a, M[11], 0x895cd7be, 22);
+    MD5_STEP(MD5_F, a, b, c, d, M[12], 0x6b901122, 7);
+    MD5_STEP(MD5_F, d, a, b, c, M[13], 0xfd987193, 12);
+    MD5_STEP(MD5_F, c, d, a, b, M[14], 0xa679438e, 17);
+    MD5_STEP(MD5_F, b, c, d, a, M[15], 0x49b40821, 22);
+    MD5_STEP(MD5_G, a, b, c, d, M[1], 0xf61e2562, 5);
+    MD5_STEP(MD5_G, d, a, b, c, M[6], 0xc040b340, 9);
+    MD5_STEP(MD5_G, c, d, a, b, M[11], 0x265e5a51, 14);
+    MD5_STEP(MD5_G, b, c, d, a, M[0], 0xe9b6c7aa, 20);
+    MD5_STEP(MD5_G, a, b, c, d, M[5], 0xd62f105d, 5);
+    MD5_STEP(MD5_G, d, a, b, c, M[10], 0x02441453, 9);
+    MD5_STEP(MD5_G, c, d, a, b, M[15], 0xd8a1e681, 14);
+    MD5_STEP(MD5_G, b, c, d, a, M[4], 0xe7d3fbc8, 20);
+    MD5_STEP(MD5_G, a, b, c, d, M[9], 0x21e1cde6, 5);
+    MD5_STEP(MD5_G, d, a, b, c, M[14], 0xc33707d6, 9);
+    MD5_STEP(MD5_G, c, d, a, b, M[3], 0xf4d50d87, 14);
+    MD5_STEP(MD5_G, b, c, d, a, M[8], 0x455a14ed, 20);
+    MD5_STEP(MD5_G, a, b, c, d, M[13], 0xa9e3e905, 5);
+    MD5_STEP(MD5_G, d, a, b, c, M[2], 0xfcefa3f8, 9);
+    MD5_STEP(MD5_G, c, d, a, b, M[7], 0x676f02d9, 14);
+    MD5_STEP(MD5_G, b, c, d, a, M[12], 0x8d2a4c8a, 20);
+    MD5_STEP(MD5_H, a, b, c, d, M[5], 0xfffa3942, 4);
+    MD5_STEP(MD5_H, d, a, b, c, M[8], 0x8771f681, 11);
+    MD5_STEP(MD5_H, c, d, a, b, M[11], 0x6d9d6122, 16);
+    MD5_STEP(MD5_H, b, c, d, a, M[14], 0xfde5380c, 23);
+    MD5_STEP(MD5_H, a, b, c, d, M[1], 0xa4beea44, 4);
+    MD5_STEP(MD5_H, d, a, b, c, M[4], 0x4bdecfa9, 11);
+    MD5_STEP(MD5_H, c, d, a, b, M[7], 0xf6bb4b60, 16);
+    MD5_STEP(MD5_H, b, c, d, a, M[10], 0xbebfbc70, 23);
+    MD5_STEP(MD5_H, a, b, c, d, M[13], 0x289b7ec6, 4);
+    MD5_STEP(MD5_H, d, a, b, c, M[0], 0xeaa127fa, 11);
+    MD5_STEP(MD5_H, c, d, a, b, M[3], 0xd4ef3085, 16);
+    MD5_STEP(MD5_H, b, c, d, a, M[6], 0x04881d05, 23);
+    MD5_STEP(MD5_H, a, b, c, d, M[9], 0xd9d4d039, 4);
+    MD5_STEP(MD5_H, d, a, b, c, M[12], 0xe6db99e5, 11);
+    MD5_STEP(MD5_H, c, d, a, b, M[15], 0x1fa27cf8, 16);
+    MD5_STEP(MD5_H, b, c, d, a, M[2], 0xc4ac5665, 23);
+    MD5_STEP(MD5_I, a, b, c, d, M[0], 0xf4292244, 6);
+    MD5_STEP(MD5_I, d, a, b, c, M[7], 0x432aff97, 10);
+    MD5_STEP(MD5_I, c, d, a, b, M[14], 0xab9423a7, 15);
+    MD5_STEP(MD5_I, b, c, d, a, M[5], 0xfc93a039, 21);
+    MD5_STEP(MD5_I, a, b, c, d, M[12], 0x655b59c3, 6);
+    MD5_STEP(MD5_I, d, a, b, c, M[3], 0x8f0ccc92, 10);
+    MD5_STEP(MD5_I, c, d, a, b, M[10], 0xffeff47d, 15);
+    MD5_STEP(MD5_I, b, c, d, a, M[1], 0x85845dd1, 21);
+    MD5_STEP(MD5_I, a, b, c, d, M[8], 0x6fa87e4f, 6);
+    MD5_STEP(MD5_I, d, a, b, c, M[15], 0xfe2ce6e0, 10);
+    MD5_STEP(MD5_I, c, d, a, b, M[6], 0xa3014314, 15);
+    MD5_STEP(MD5_I, b, c, d, a, M[13], 0x4e0811a1, 21);
+    MD5_STEP(MD5_I, a, b, c, d, M[4], 0xf7537e82, 6);
+    MD5_STEP(MD5_I, d, a, b, c, M[11], 0xbd3af235, 10);
+    MD5_STEP(MD5_I, c, d, a, b, M[2], 0x2ad7d2bb, 15);
+    MD5_STEP(MD5_I, b, c, d, a, M[9], 0xeb86d391, 21);
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+}
+
+__global__ __launch_bounds__(64) void k_md5(const Md5Task* __restrict__ tasks, uint32_t ntasks,
+                                            uint32_t* __restrict__ digests)
+{
+    const uint32_t t = blockIdx.x;
+    if (t >= ntasks || threadIdx.x != 0) return;
+    const Md5Task tk = tasks[t];
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    const uint4* p = reinterpret_cast<const uint4*>(tk.ptr);
+    const uint64_t nfull = tk.len / 64;
+    uint32_t M[16];
+    for (uint64_t blkn = 0; blkn < nfull; blkn++) {
+        const uint4 a = p[4 * blkn + 0], b = p[4 * blkn + 1], c = p[4 * blkn + 2], d = p[4 * blkn + 3];
+        M[0] = a.x; M[1] = a.y; M[2] = a.z; M[3] = a.w;
+        M[4] = b.x; M[5] = b.y; M[6] = b.z; M[7] = b.w;
+        M[8] = c.x; M[9] = c.y; M[10] = c.z; M[11] = c.w;
+        M[12] = d.x; M[13] = d.y; M[14] = d.z; M[15] = d.w;
+        md5_block(h, M);
+    }
+    // tail + padding (bit length of the u32 length, as the RSA MDString)
+    const uint32_t rem = (uint32_t)(tk.len - nfull * 64);
+    const uint8_t* tail = tk.ptr + nfull * 64;
+    uint8_t buf[128];
+    for (uint32_t k = 0; k < 128; k++) buf[k] = 0;
+    for (uint32_t k = 0; k < rem; k++) buf[k] = tail[k];
+    buf[rem] = 0x80;
+    const uint32_t tl = rem < 56 ? 64 : 128;
+    const uint64_t bits = (uint64_t)(uint32_t)tk.len << 3;
+    for (int k = 0; k < 8; k++) buf[tl - 8 + k] = (uint8_t)(bits >> (8 * k));
+    for (uint32_t o = 0; o < tl; o += 64) {
+        for (int k = 0; k < 16; k++)
+            M[k] = (uint32_t)buf[o + 4 * k] | ((uint32_t)buf[o + 4 * k + 1] << 8) |
+                   ((uint32_t)buf[o + 4 * k + 2] << 16) | ((uint32_t)buf[o + 4 * k + 3] << 24);
+        md5_block(h, M);
+    }
+    for (int k = 0; k < 4; k++) digests[(size_t)t * 4 + k] = h[k];
+}
+
+// ---------------------------------------------------------------------------
+// Block assembly (doFqzEncode@0x42d2d0): one workgroup per block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_assemble(const BatchView bv, const AsmView av,
+                                                  const uint8_t* __restrict__ payload,
+                                                  const uint32_t* __restrict__ out_len,
+                                                  const uint32_t* __restrict__ digests,
+                                                  uint8_t* __restrict__ final_out,
+                                                  uint64_t* __restrict__ final_len)
+{
+    __shared__ uint32_t seg_dst[16], seg_src_task[16], seg_len[16];
+    __shared__ uint32_t nseg;
+    const uint32_t b = blockIdx.x;
+    const AsmBlock& ab = av.blocks[b];
+    uint8_t* o = final_out + ab.out_base;
+    if (threadIdx.x == 0) {
+        uint32_t ns = 0;
+        final_len[b] = assemble_plan(bv, b, ab, out_len, digests, o, seg_dst, seg_src_task, seg_len, ns);
+        nseg = ns;
+    }
+    __syncthreads();
+    for (uint32_t sgi = 0; sgi < nseg; sgi++) {
+        const uint8_t* src = payload + av.task_out_base[seg_src_task[sgi]];
+        uint8_t* dst = o + seg_dst[sgi];
+        const uint32_t L = seg_len[sgi];
+        for (uint32_t k = threadIdx.x; k < L; k += blockDim.x) dst[k] = src[k];
+    }
+}
+
+}  // namespace sa

@@ -1,0 +1,406 @@
+// sa_logic.h -- per-thread logic of the encoder kernels, written once as
+// host+device functions.  sa_kernels.hip wraps each in a kernel; the CPU
+// decomposition test (tests/cpu_emu) drives the same functions sequentially to
+// check the decomposition against the oracle before it runs on the GPU.
+#pragma once
+#include "sa_common.h"
+#include "sa_device.h"
+
+namespace sa {
+
+// ---- per-read counts (k_prep) ----------------------------------------------
+SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int16_t* name_p, int16_t* name_s)
+{
+    const uint32_t b = bv.read_block[r];
+    const DevBlock& blk = bv.blocks[b];
+    const uint32_t lr = r - blk.read0;
+    const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
+    const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
+    const uint32_t len = bv.seq_len[r];
+    uint32_t e = 0;
+
+    SeqStat st = seq_stat(s, q, len);
+    e |= st.err;
+    uint32_t* c = counts + (size_t)r * NCOL;
+    c[C_SEQ] = st.valid;
+    if (len > 0xffff) e |= E_LONGREAD;
+    c[C_LEN] = len == 0 ? 1 : 3;
+    uint32_t n = qual_nonhash(q, len);
+    c[C_QUAL] = n + (n != len ? 1 : 0);
+    for (uint32_t i = 0; i < n; i++)
+        if (q[i] < 33 || q[i] > 126) { e |= E_QUALRANGE; break; }
+    c[C_TIP] = 1;
+    c[C_CH] = st.nch;
+    const uint32_t has = st.nch ? 1 : 0;
+    c[C_MAXQ] = has;
+    if (has && (st.maxq < 33 || st.maxq > 127)) e |= E_QUALRANGE;
+    c[C_NCNT] = has ? 1 + (uint32_t)nbits_u32(st.exc) : 0;
+    c[C_NPOS] = has ? st.npos_syms : 0;
+    c[C_NPOSV] = has ? st.exc : 0;
+
+    if (bv.bin_mode) {
+        c[C_NAME] = 0;
+    } else {
+        const uint8_t* nm = bv.names + blk.name_base + bv.name_off[r];
+        const int nl = bv.name_len[r];
+        int p = 0, sfx = 0;
+        if (lr > 0) {
+            const uint8_t* pv = bv.names + blk.name_base + bv.name_off[r - 1];
+            name_prefix_suffix(nm, nl, pv, bv.name_len[r - 1], p, sfx);
+        } else {
+            name_prefix_suffix(nm, nl, nm, 0, p, sfx);
+        }
+        if (nl > 255) e |= E_NAME;
+        name_p[r] = (int16_t)p;
+        name_s[r] = (int16_t)sfx;
+        int mid = nl - sfx - p;
+        c[C_NAME] = 3 + (mid > 0 ? (uint32_t)mid : 0);
+    }
+    return e;
+}
+
+// ---- symbol emission (k_emit) ----------------------------------------------
+struct AuxEmit {
+    uint32_t* key;
+    uint32_t* val;
+    uint8_t* sym;
+    uint32_t pos;
+    SA_HD void operator()(uint32_t model, uint32_t s)
+    {
+        key[pos] = model;
+        val[pos] = pos;
+        sym[pos] = (uint8_t)s;
+        pos++;
+    }
+};
+
+SA_HD void emit_kmodel(AuxEmit& em, uint32_t v)
+{
+    int nb = nbits_u32(v);
+    em(M_KBITS, (uint32_t)nb);
+    for (int i = 0; i < nb; i++) em(M_KBIT0 + (uint32_t)i, (v >> i) & 1);
+}
+
+SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts, const int16_t* name_p,
+                         const int16_t* name_s, const uint16_t* name_maxlen, uint32_t* seq_key,
+                         uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val, uint8_t* aux_sym)
+{
+    uint32_t e = 0;
+    const uint32_t b = bv.read_block[r];
+    const DevBlock& blk = bv.blocks[b];
+    const uint32_t lr = r - blk.read0;
+    const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
+    const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
+    const uint32_t len = bv.seq_len[r];
+    const uint32_t* off = counts + (size_t)r * NCOL;
+
+    // sequence: BASE_MODEL contexts (encode_seq@0x421f30)
+    {
+        uint32_t* K = seq_key + blk.seq_sym_base;
+        uint32_t* V = seq_val + blk.seq_sym_base;
+        uint32_t d = off[C_SEQ];
+        const uint32_t mask = bv.seq_mask;
+        uint32_t ctx = 0x7616c7u & mask;
+        for (uint32_t i = 0; i < len; i++) {
+            uint32_t cd = base_code(s[i]);
+            if (cd > 3) continue;
+            K[d] = ctx;
+            V[d] = (d << 2) | cd;
+            d++;
+            ctx = ((ctx << 2) + cd) & mask;
+        }
+    }
+    AuxEmit em{aux_key + blk.aux_sym_base, aux_val + blk.aux_sym_base, aux_sym + blk.aux_sym_base, 0};
+    // lengths (encode_len_short@0x4239a0; last_len stays 0)
+    em.pos = blk.sbase[ST_LEN] + off[C_LEN];
+    if (len == 0) {
+        em(M_LEN_SAME, 1);
+    } else {
+        em(M_LEN_SAME, 0);
+        em(M_LEN_LO, len & 0xff);
+        em(M_LEN_HI, (len >> 8) & 0xff);
+    }
+    // names (encode_name@0x421070)
+    if (!bv.bin_mode) {
+        em.pos = blk.sbase[ST_NAME] + off[C_NAME];
+        const uint8_t* nm = bv.names + blk.name_base + bv.name_off[r];
+        const int nl = bv.name_len[r];
+        const int ll = lr ? bv.name_len[r - 1] : 0;
+        const int lp = lr ? name_p[r - 1] : 0;
+        const int ls = lr ? name_s[r - 1] : 0;
+        const int p = name_p[r], sf = name_s[r];
+        em(M_NAME_PRE + (uint32_t)lp, (uint32_t)p);
+        em(M_NAME_SUF + (uint32_t)ls, (uint32_t)sf);
+        em(M_NAME_LEN + (uint32_t)ll, (uint32_t)nl);
+        // the reference's last-name buffer: each byte j holds the latest earlier
+        // name of the block longer than j, or ' ' (reset per block @0x42452c)
+        const uint32_t maxlen = name_maxlen[r];
+        const uint32_t rb = blk.read0;
+        auto last = [&](int j) -> uint8_t {
+            if (j < 0) return 0;
+            if ((uint32_t)j >= maxlen) return ' ';
+            for (uint32_t m = r; m > rb; m--) {
+                if ((uint32_t)bv.name_len[m - 1] > (uint32_t)j)
+                    return bv.names[blk.name_base + bv.name_off[m - 1] + (uint32_t)j];
+            }
+            return ' ';
+        };
+        auto emid = [&](uint32_t ctx, uint32_t sym) { em(M_NAME_MID + ctx, sym); };
+        if (!name_mid(nm, nl, p, sf, last, emid)) e |= E_NAME;
+    }
+    // qualities (encode_qual@0x422180)
+    {
+        em.pos = blk.sbase[ST_QUAL] + off[C_QUAL];
+        const uint32_t n = qual_nonhash(q, len);
+        QualCtx qc{0, 0, 5};
+        uint32_t last = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            int sym = (uint8_t)(q[i] - 33);
+            em(M_QUAL + last, (uint32_t)sym);
+            last = qual_next_ctx(qc, sym, i, bv.qlevel);
+        }
+        if (n != len) em(M_QUAL + last, 94);
+    }
+    // degenerate-base side streams (DegeInfoProcess@0x433a10)
+    {
+        em.pos = blk.sbase[ST_TIP] + off[C_TIP];
+        SeqStat st = seq_stat(s, q, len);
+        em(M_TIP, st.nch ? 1u : 0u);
+        if (st.nch) {
+            em.pos = blk.sbase[ST_CH] + off[C_CH];
+            for (uint32_t i = 0; i < len; i++) {
+                uint32_t cd = base_code(s[i]);
+                if (cd > 3) em(M_CH, cd - 4);
+            }
+            em.pos = blk.sbase[ST_MAXQ] + off[C_MAXQ];
+            em(M_MAXQ, (uint8_t)(st.maxq - 33));
+            em.pos = blk.sbase[ST_NCNT] + off[C_NCNT];
+            emit_kmodel(em, st.exc);
+            em.pos = blk.sbase[ST_NPOS] + off[C_NPOS];
+            uint32_t gap = 0;
+            for (uint32_t i = 0; i < len; i++) {
+                if ((int)st.maxq < (int)(int8_t)q[i]) continue;
+                if (base_code(s[i]) > 3) {
+                    gap++;
+                } else {
+                    emit_kmodel(em, gap);
+                    gap = 0;
+                }
+            }
+        }
+    }
+    return e;
+}
+
+// ---- BASE_MODEL replay of one context run (k_replay_seq) -------------------
+// keys/vals: the block's sorted SEQ symbols; run starts at i; rec: the block's
+// SEQ records (indexed by stream position).
+SA_HD void replay_seq_run(const uint32_t* keys, const uint32_t* vals, size_t i, size_t end, uint32_t key,
+                          Rec* rec, const uint64_t* recip)
+{
+    uint32_t st = 0x03030303u;
+    for (size_t j = i; j < end && keys[j] == key; j++) {
+        const uint32_t v = vals[j];
+        const uint32_t b = v & 3, pos = v >> 2;
+        uint32_t tot = (st & 0xff) + ((st >> 8) & 0xff) + ((st >> 16) & 0xff) + (st >> 24);
+        if (tot > 253) {
+            st -= (st >> 1) & 0x7f7f7f7fu;
+            tot = (st & 0xff) + ((st >> 8) & 0xff) + ((st >> 16) & 0xff) + (st >> 24);
+        }
+        const uint32_t below = b ? (st & (0xffffffffu >> (32 - 8 * b))) : 0u;
+        const uint32_t cum = (below & 0xff) + ((below >> 8) & 0xff) + ((below >> 16) & 0xff);
+        const uint32_t f = (st >> (8 * b)) & 0xff;
+        const uint64_t m = recip[tot];
+        Rec rr;
+        rr.cumfreq = cum | (f << 16);
+        rr.m_lo = (uint32_t)m;
+        rr.m_hi = (uint32_t)(m >> 32);
+        rr.tag = tot;
+        rec[pos] = rr;
+        st += 1u << (8 * b);
+    }
+}
+
+// ---- SIMPLE_MODEL<N> replay of one model run (k_replay_aux) ----------------
+// F: scratch for N+1 entries (sym<<16 | freq).  S/rec: the block's AUX symbol
+// and record arrays (indexed by stream position).
+SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, const uint8_t* S, size_t i,
+                                 size_t end, uint32_t key, Rec* rec, const uint64_t* recip, uint32_t* F)
+{
+    const uint32_t N = model_nsym(key);
+    for (uint32_t k = 0; k < N; k++) F[k] = (k << 16) | 1u;
+    F[N] = 0;
+    uint32_t tot = N, bub = 0;
+    for (size_t j = i; j < end && keys[j] == key; j++) {
+        const uint32_t pos = vals[j];
+        const uint32_t sym = S[pos];
+        uint32_t idx = 0, cum = 0, e = F[0];
+        while ((e >> 16) != sym) {
+            cum += e & 0xffff;
+            if (++idx >= N) break;
+            e = F[idx];
+        }
+        if (idx >= N) {   // symbol outside the model: the reference runs off the array
+            return E_CODER;
+        }
+        const uint32_t f = e & 0xffff;
+        const uint64_t m = recip[tot];
+        Rec rr;
+        rr.cumfreq = cum | (f << 16);
+        rr.m_lo = (uint32_t)m;
+        rr.m_hi = (uint32_t)(m >> 32);
+        rr.tag = tot;
+        rec[pos] = rr;
+        e += 8;
+        F[idx] = e;
+        tot += 8;
+        if (tot > 0xffe0) {
+            tot = 0;
+            for (uint32_t k = 0; k < N; k++) {
+                uint32_t x = F[k], fr = x & 0xffff;
+                fr -= fr >> 1;
+                F[k] = (x & 0xffff0000u) | fr;
+                tot += fr;
+            }
+        }
+        if (((++bub) & 15) == 0 && idx > 0) {
+            const uint32_t cur = F[idx], prv = F[idx - 1];
+            if ((cur & 0xffff) > (prv & 0xffff)) {
+                F[idx] = prv;
+                F[idx - 1] = cur;
+            }
+        }
+    }
+    return 0;
+}
+
+// ---- serial range coder of one stream (k_coder) -----------------------------
+// Carry-less 64-bit coder of encode_seq@0x422010-0x422085; finish = 8 bytes.
+SA_HD uint32_t code_stream(const Rec* R, uint32_t n, uint8_t* o, uint32_t cap, uint32_t& out_len)
+{
+    uint32_t op = 0;
+    uint64_t low = 0;
+    uint32_t range = 0xffffffffu;
+    uint32_t bad = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const Rec r = R[i];
+        const uint32_t cum = r.cumfreq & 0xffff, f = r.cumfreq >> 16;
+        const uint32_t t1 = (uint32_t)(((uint64_t)r.m_lo * range) >> 32);
+        const uint32_t qq = (uint32_t)(((uint64_t)r.m_hi * range + t1) >> 32);
+        low += (uint32_t)(cum * qq);
+        range = qq * f;
+        while (range < (1u << 24)) {
+            if ((low ^ (low + range)) >> 56) range = ((uint32_t)low | 0xffffffu) - (uint32_t)low;
+            if (op < cap) o[op] = (uint8_t)(low >> 56);
+            op++;
+            range <<= 8;
+            low <<= 8;
+        }
+    }
+    for (int k = 0; k < 8; k++) {
+        if (op < cap) o[op] = (uint8_t)(low >> 56);
+        op++;
+        low <<= 8;
+    }
+    out_len = op;
+    return op > cap ? E_OVERFLOW : bad;
+}
+
+// ---- block assembly plan (k_assemble; doFqzEncode@0x42d2d0) ----------------
+SA_HD uint32_t put_id(uint8_t* o, uint32_t id) { o[0] = (uint8_t)(0x80 | id); return 1; }
+SA_HD void put_size4(uint8_t* o, uint32_t v)
+{
+    v |= 1u << 28;
+    o[0] = (uint8_t)(v >> 24); o[1] = (uint8_t)(v >> 16); o[2] = (uint8_t)(v >> 8); o[3] = (uint8_t)v;
+}
+SA_HD void put_u32le(uint8_t* o, uint32_t v)
+{
+    o[0] = (uint8_t)v; o[1] = (uint8_t)(v >> 8); o[2] = (uint8_t)(v >> 16); o[3] = (uint8_t)(v >> 24);
+}
+
+// Writes every header, MD5 and the ID-bin payload of block b into o, and lists
+// the coder payloads still to copy (destination offset, coder task, length).
+// Returns the block's total length.
+SA_HD uint32_t assemble_plan(const BatchView& bv, uint32_t b, const AsmBlock& ab, const uint32_t* out_len,
+                             const uint32_t* digests, uint8_t* o, uint32_t* seg_dst, uint32_t* seg_src_task,
+                             uint32_t* seg_len, uint32_t& nseg)
+{
+    const DevBlock& blk = bv.blocks[b];
+    uint32_t p = 5;   // 0x81 + size4
+    // count (compressCount@0x422a00)
+    o[p++] = 0x81; o[p++] = 0x84; put_u32le(o + p, blk.nreads); p += 4;
+    uint32_t ns = 0;
+    const int md5 = bv.md5;
+    // length
+    {
+        uint32_t L = out_len[ab.task[ST_LEN]];
+        p += put_id(o + p, 4); put_size4(o + p, L); p += 4;
+        seg_dst[ns] = p; seg_src_task[ns] = ab.task[ST_LEN]; seg_len[ns] = L; ns++; p += L;
+    }
+    // ID (compressID@0x4247c0)
+    {
+        p += put_id(o + p, 5);
+        uint32_t szp = p; p += 4;
+        uint32_t h = 0;
+        if (md5) {
+            for (int k = 0; k < 4; k++) put_u32le(o + p + 4 * k, digests[(size_t)ab.md5_task[0] * 4 + k]);
+            p += 16; h = 16;
+        }
+        uint32_t L;
+        if (bv.bin_mode) {   // IDProcess::encodeIDS@0x430040: u16 len + first ID
+            const uint32_t l0 = blk.nreads ? bv.name_len[blk.read0] : 0;
+            o[p] = (uint8_t)l0; o[p + 1] = (uint8_t)(l0 >> 8);
+            const uint8_t* nm = bv.names + blk.name_base;
+            for (uint32_t k = 0; k < l0; k++) o[p + 2 + k] = nm[k];
+            L = 2 + l0; p += L;
+        } else {
+            L = out_len[ab.task[ST_NAME]];
+            seg_dst[ns] = p; seg_src_task[ns] = ab.task[ST_NAME]; seg_len[ns] = L; ns++; p += L;
+        }
+        put_size4(o + szp, h + L);
+    }
+    // quality
+    {
+        p += put_id(o + p, 7);
+        uint32_t szp = p; p += 4;
+        uint32_t h = 0;
+        if (md5) {
+            for (int k = 0; k < 4; k++) put_u32le(o + p + 4 * k, digests[(size_t)ab.md5_task[2] * 4 + k]);
+            p += 16; h = 16;
+        }
+        uint32_t L = out_len[ab.task[ST_QUAL]];
+        seg_dst[ns] = p; seg_src_task[ns] = ab.task[ST_QUAL]; seg_len[ns] = L; ns++; p += L;
+        put_size4(o + szp, h + L);
+    }
+    // degenerate-base streams: encap omitted when its value count is 0
+    const uint32_t ids[5] = {23, 14, 24, 25, 26};
+    for (int k = 0; k < 5; k++) {
+        const int st = ST_TIP + k;
+        const uint32_t cnt = blk.vcount[st];
+        if (!cnt) continue;
+        uint32_t L = out_len[ab.task[st]];
+        p += put_id(o + p, ids[k]);
+        put_size4(o + p, L + 4); p += 4;
+        put_u32le(o + p, cnt); p += 4;
+        seg_dst[ns] = p; seg_src_task[ns] = ab.task[st]; seg_len[ns] = L; ns++; p += L;
+    }
+    // sequence
+    {
+        p += put_id(o + p, 6);
+        uint32_t szp = p; p += 4;
+        uint32_t h = 0;
+        if (md5) {
+            for (int k = 0; k < 4; k++) put_u32le(o + p + 4 * k, digests[(size_t)ab.md5_task[1] * 4 + k]);
+            p += 16; h = 16;
+        }
+        uint32_t L = out_len[ab.task[ST_SEQ]];
+        seg_dst[ns] = p; seg_src_task[ns] = ab.task[ST_SEQ]; seg_len[ns] = L; ns++; p += L;
+        put_size4(o + szp, h + L);
+    }
+    o[0] = 0x81;
+    put_size4(o + 1, p - 5);
+    nseg = ns;
+    return p;
+}
+
+}  // namespace sa

@@ -1,0 +1,97 @@
+/*
+ * seqarc_amd.h -- C-ABI of the MI355X SeqArc block encoder (libseqarc_amd.so).
+ *
+ * Plain pointers and sizes only.  The reference (SeqArc-1.6) is one monolithic
+ * executable with no plugin API; the seam this library replaces is the per-block
+ * encoder call inside the encode thread:
+ *
+ *   int EncapFqzComp::doFqzEncode(SeqArcMemBuf*, DebugInfo*)   SeqArc-1.6@0x42d2d0
+ *     called from ISeqArcEncodeThread::doTask                   SeqArc-1.6@0x433dd0
+ *     after SeqArcMemBuf::calcBlockMd5@0x414d90 and DegeInfoProcess@0x433a10
+ *
+ * sa_encode_blocks() takes a batch of parsed blocks (the SeqArcMemBuf SoA:
+ * IDs + u16 lengths, bases + i32 lengths, qualities; PE reads interleaved
+ * r1,r2) and returns, per block, exactly the bytes doFqzEncode writes
+ * ("81 <size4> ..." : count, len, ID, qual, dege streams, seq).
+ *
+ * Errors: a non-zero return and sa_last_error(); the reference abort()s on a
+ * coder invariant violation -- here the batch fails and no output is produced.
+ * Thread-safety: one sa_ctx per host thread / device; contexts are independent.
+ */
+#ifndef SEQARC_AMD_H
+#define SEQARC_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sa_ctx sa_ctx;
+
+/* One parsed block (SeqArcMemBuf fields +0x80/+0xc0, +0x88/+0xd0, +0x90, +0x4). */
+typedef struct {
+    const uint8_t *names;       /* concatenated IDs without '@'            */
+    const uint16_t *name_lens;  /* nreads entries                           */
+    const uint8_t *seq;         /* concatenated bases                       */
+    const int32_t *seq_lens;    /* nreads entries                           */
+    const uint8_t *qual;        /* concatenated quals (same lengths)        */
+    uint32_t nreads;
+} sa_block;
+
+/* Encoder parameters (SeqArcParam fields of the no-reference path). */
+typedef struct {
+    int32_t slevel;    /* param+0x1b54 (default 3): seq order k = slevel + 7      */
+    int32_t qlevel;    /* param+0x1b58 (default 2)                                */
+    int32_t md5;       /* param+0x1880 (default 1): per-block MD5 of ID/seq/qual  */
+    int32_t bin_mode;  /* param+0x18a4 (ID template byte 0, see sa_analyze_ids)   */
+} sa_cfg;
+
+typedef struct {
+    uint8_t *data;     /* caller-allocated, >= sa_output_bound() bytes  */
+    uint64_t cap;
+    uint64_t size;     /* written                                     */
+} sa_out;
+
+/* ---- lifecycle ------------------------------------------------------- */
+sa_ctx *sa_create(int device);               /* NULL if no usable gfx950 device */
+void sa_destroy(sa_ctx *ctx);
+const char *sa_last_error(const sa_ctx *ctx);
+const char *sa_version(void);
+
+/* ---- one-shot batch: replaces doFqzEncode@0x42d2d0 per block ---------- */
+uint64_t sa_output_bound(const sa_block *blk);
+int sa_encode_blocks(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, sa_out *out);
+
+/* ---- staged API (inputs resident in HBM; used by bench.py) ------------ */
+int sa_stage(sa_ctx *ctx, const sa_block *in, int n);     /* H2D copy of a batch   */
+int sa_run(sa_ctx *ctx, const sa_cfg *cfg);                /* encode the staged batch */
+int sa_fetch(sa_ctx *ctx, sa_out *out, int n);             /* D2H of the encaps     */
+/* per-phase device time (ms) of the last sa_run, measured with HIP events on
+ * the stream each phase runs on; returns the number of phases written */
+int sa_phase_times(const sa_ctx *ctx, const char **names, float *ms, int max);
+void sa_set_timing(sa_ctx *ctx, int on);
+
+/* ---- host-side mirrors of the reference's block plumbing -------------- */
+/* Block cut: SeqArcRead::doReadJob@0x432a80 / cultbuf@0x432530 / getEndPos@0x4320c0
+ * (SE) and doReadPEJob@0x432d10 / cultPEbuf@0x432180 (PE).  Returns #blocks. */
+int64_t sa_cut_se(const uint8_t *text, uint64_t len, uint64_t block_size,
+                  uint64_t *ends, uint64_t max_blocks);
+int64_t sa_cut_pe(const uint8_t *t1, uint64_t len1, const uint8_t *t2, uint64_t len2,
+                  uint64_t block_size, uint64_t *ends1, uint64_t *ends2, uint64_t max_blocks);
+/* Block parse: getBlockRead@0x411b60 (SE) / getBlockReadPE@0x412920 (PE).
+ * Output arrays sized >= text bytes (names/seq/qual) and text/4+1 (lens). */
+int64_t sa_parse_se(const uint8_t *text, uint64_t len, uint8_t *names, uint16_t *name_lens,
+                    uint8_t *seq, int32_t *seq_lens, uint8_t *qual);
+int64_t sa_parse_pe(const uint8_t *t1, uint64_t len1, const uint8_t *t2, uint64_t len2,
+                    uint8_t *names, uint16_t *name_lens, uint8_t *seq, int32_t *seq_lens,
+                    uint8_t *qual);
+/* ID template ("adaptive binning") detection on the first block:
+ * IDProcess::analysisIDBinType@0x4310a0.  tmpl = the 512-byte param+0x18a4
+ * area, caller zero-initialised; tmpl[0] is sa_cfg.bin_mode. */
+int sa_analyze_ids(const sa_block *first, int single_end, uint8_t tmpl[512]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

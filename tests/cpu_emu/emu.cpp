@@ -1,0 +1,256 @@
+// emu.cpp -- CPU check of the GPU decomposition (test infrastructure only).
+//
+// Runs the encoder's per-thread logic (fastqueeze_amd/csrc/sa_logic.h) and the
+// batch plan (sa_plan.h) sequentially on the host, with std::stable_sort in
+// place of the radix sort and the oracle's MD5, then compares every block with
+// the CPU restatement (oracle/fqz_oracle.c).  This validates the
+// extract -> sort -> replay -> code decomposition before it runs on MI355X;
+// the GPU parity tests (tests/test_gpu_parity.py) check the kernels themselves.
+//
+//   emu [-b block_bytes] [-s slevel] [-q qlevel] in1.fq [in2.fq]
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../fastqueeze_amd/csrc/sa_logic.h"
+#include "../../fastqueeze_amd/csrc/sa_plan.h"
+#include "../../include/seqarc_amd.h"
+#include "../../oracle/fqz_oracle.h"
+
+using namespace sa;
+
+static std::vector<uint8_t> slurp(const char* p)
+{
+    std::vector<uint8_t> v;
+    FILE* f = std::fopen(p, "rb");
+    if (!f) return v;
+    std::fseek(f, 0, SEEK_END);
+    long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    v.resize((size_t)n);
+    if (std::fread(v.data(), 1, (size_t)n, f) != (size_t)n) v.clear();
+    std::fclose(f);
+    return v;
+}
+
+struct HostBlock {
+    std::vector<uint8_t> names, seq, qual;
+    std::vector<uint16_t> nl;
+    std::vector<int32_t> sl;
+    uint32_t nreads = 0;
+};
+
+int main(int argc, char** argv)
+{
+    uint64_t bs = 50ull << 20;
+    int slevel = 3, qlevel = 2;
+    std::vector<const char*> in;
+    for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "-b") && i + 1 < argc) bs = std::strtoull(argv[++i], nullptr, 10);
+        else if (!std::strcmp(argv[i], "-s") && i + 1 < argc) slevel = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "-q") && i + 1 < argc) qlevel = std::atoi(argv[++i]);
+        else in.push_back(argv[i]);
+    }
+    if (in.empty()) return 2;
+    std::vector<uint8_t> t1 = slurp(in[0]), t2 = in.size() > 1 ? slurp(in[1]) : std::vector<uint8_t>();
+    const bool pe = in.size() > 1;
+    std::vector<uint64_t> e1(4096), e2(4096);
+    int64_t nb = pe ? sa_cut_pe(t1.data(), t1.size(), t2.data(), t2.size(), bs, e1.data(), e2.data(), 4096)
+                    : sa_cut_se(t1.data(), t1.size(), bs, e1.data(), 4096);
+    // the oracle's cut must agree
+    {
+        std::vector<size_t> o1(4096), o2(4096);
+        int64_t onb = pe ? orc_cut_pe(t1.data(), t1.size(), t2.data(), t2.size(), bs, o1.data(), o2.data(), 4096)
+                         : orc_cut_se(t1.data(), t1.size(), bs, o1.data(), 4096);
+        if (onb != nb) { std::printf("FAIL cut count %lld vs oracle %lld\n", (long long)nb, (long long)onb); return 1; }
+        for (int64_t b = 0; b < nb; b++)
+            if (o1[b] != e1[b] || (pe && o2[b] != e2[b])) { std::printf("FAIL cut boundary %lld\n", (long long)b); return 1; }
+    }
+    std::vector<HostBlock> hb((size_t)nb);
+    uint64_t p1 = 0, p2 = 0;
+    for (int64_t b = 0; b < nb; b++) {
+        HostBlock& h = hb[(size_t)b];
+        uint64_t l1 = e1[b] - p1, l2 = pe ? e2[b] - p2 : 0;
+        h.names.resize(l1 + l2 + 16); h.seq.resize(l1 + l2 + 16); h.qual.resize(l1 + l2 + 16);
+        h.nl.resize((l1 + l2) / 4 + 8); h.sl.resize((l1 + l2) / 4 + 8);
+        int64_t nr = pe ? sa_parse_pe(t1.data() + p1, l1, t2.data() + p2, l2, h.names.data(), h.nl.data(), h.seq.data(), h.sl.data(), h.qual.data())
+                        : sa_parse_se(t1.data() + p1, l1, h.names.data(), h.nl.data(), h.seq.data(), h.sl.data(), h.qual.data());
+        if (nr < 0) { std::printf("FAIL parse block %lld\n", (long long)b); return 1; }
+        h.nreads = (uint32_t)nr;
+        p1 = e1[b];
+        if (pe) p2 = e2[b];
+    }
+    uint8_t T[512] = {0}, To[512] = {0};
+    sa_block first{hb[0].names.data(), hb[0].nl.data(), hb[0].seq.data(), hb[0].sl.data(), hb[0].qual.data(), hb[0].nreads};
+    if (sa_analyze_ids(&first, !pe, T)) { std::printf("FAIL id analysis\n"); return 1; }
+    orc_block ofirst{hb[0].names.data(), hb[0].nl.data(), hb[0].seq.data(), hb[0].sl.data(), hb[0].qual.data(), hb[0].nreads};
+    orc_analyze_idbin(&ofirst, !pe, To);
+    if (std::memcmp(T, To, 512)) { std::printf("FAIL id template differs from oracle\n"); return 1; }
+
+    // ---- host BatchView (what sa_stage uploads) ----
+    std::vector<DevBlock> blocks((size_t)nb);
+    std::vector<uint8_t> names, seq, qual;
+    std::vector<uint32_t> read_block, name_off, seq_off, seq_len;
+    std::vector<uint16_t> name_len;
+    uint32_t nr = 0;
+    for (int64_t b = 0; b < nb; b++) {
+        HostBlock& h = hb[(size_t)b];
+        DevBlock& d = blocks[(size_t)b];
+        d.nreads = h.nreads;
+        d.read0 = nr;
+        uint64_t ln = 0, ls = 0;
+        for (uint32_t r = 0; r < h.nreads; r++) { ln += h.nl[r]; ls += (uint64_t)h.sl[r]; }
+        d.name_base = names.size();
+        d.seq_base = seq.size();
+        d.name_bytes = ln;
+        d.seq_bytes = ls;
+        names.insert(names.end(), h.names.begin(), h.names.begin() + (long)ln);
+        seq.insert(seq.end(), h.seq.begin(), h.seq.begin() + (long)ls);
+        qual.insert(qual.end(), h.qual.begin(), h.qual.begin() + (long)ls);
+        names.resize(align_up(names.size(), 16));
+        seq.resize(align_up(seq.size(), 16));
+        qual.resize(align_up(qual.size(), 16));
+        uint32_t no = 0, so = 0;
+        for (uint32_t r = 0; r < h.nreads; r++) {
+            read_block.push_back((uint32_t)b);
+            name_off.push_back(no);
+            name_len.push_back(h.nl[r]);
+            seq_off.push_back(so);
+            seq_len.push_back((uint32_t)h.sl[r]);
+            no += h.nl[r];
+            so += (uint32_t)h.sl[r];
+        }
+        nr += h.nreads;
+    }
+    const int k = slevel + 7;
+    const uint32_t ns = 1u << ((2 * k) & 31);
+    BatchView bv{};
+    bv.blocks = blocks.data();
+    bv.nblocks = (uint32_t)nb;
+    bv.nreads_total = nr;
+    bv.read_block = read_block.data();
+    bv.names = names.data();
+    bv.seq = seq.data();
+    bv.qual = qual.data();
+    bv.name_off = name_off.data();
+    bv.name_len = name_len.data();
+    bv.seq_off = seq_off.data();
+    bv.seq_len = seq_len.data();
+    bv.seq_mask = ns - 1;
+    bv.qlevel = qlevel;
+    bv.bin_mode = T[0];
+    bv.md5 = 1;
+
+    // ---- prep + scan ----
+    std::vector<uint32_t> counts((size_t)nr * NCOL);
+    std::vector<int16_t> name_p(nr), name_s(nr);
+    std::vector<uint16_t> maxlen(nr);
+    uint32_t err = 0;
+    for (uint32_t r = 0; r < nr; r++) err |= prep_read(bv, r, counts.data(), name_p.data(), name_s.data());
+    if (err) { std::printf("FAIL prep error bits %x\n", err); return 1; }
+    std::vector<uint32_t> totals((size_t)nb * NCOL);
+    for (int64_t b = 0; b < nb; b++) {
+        const DevBlock& d = blocks[(size_t)b];
+        uint32_t carry[NCOL] = {0};
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < d.nreads; i++) {
+            uint32_t* c = &counts[(size_t)(d.read0 + i) * NCOL];
+            for (int col = 0; col < NCOL; col++) { uint32_t v = c[col]; c[col] = carry[col]; carry[col] += v; }
+            maxlen[d.read0 + i] = (uint16_t)m;
+            m = std::max<uint32_t>(m, name_len[d.read0 + i]);
+        }
+        for (int col = 0; col < NCOL; col++) totals[(size_t)b * NCOL + col] = carry[col];
+    }
+    BatchPlan bp;
+    if (!plan_batch(blocks, totals, bp)) { std::printf("FAIL plan\n"); return 1; }
+
+    // ---- emit ----
+    std::vector<uint32_t> sk(bp.seq.total, SORT_PAD), sv(bp.seq.total), ak(bp.aux.total, SORT_PAD), av(bp.aux.total);
+    std::vector<uint8_t> asym(bp.aux.total);
+    for (uint32_t r = 0; r < nr; r++)
+        err |= emit_read(bv, r, counts.data(), name_p.data(), name_s.data(), maxlen.data(), sk.data(), sv.data(),
+                         ak.data(), av.data(), asym.data());
+    if (err) { std::printf("FAIL emit error bits %x\n", err); return 1; }
+
+    // ---- stable sort per segment (what k_sort_* computes) ----
+    auto sort_space = [](std::vector<uint32_t>& K, std::vector<uint32_t>& V, const SortPlan& p) {
+        for (const SortSeg& g : p.segs) {
+            const size_t n = (size_t)g.ntiles * SORT_TILE;
+            std::vector<uint32_t> idx(n);
+            std::iota(idx.begin(), idx.end(), 0u);
+            std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return K[g.base + a] < K[g.base + b]; });
+            std::vector<uint32_t> k2(n), v2(n);
+            for (size_t i = 0; i < n; i++) { k2[i] = K[g.base + idx[i]]; v2[i] = V[g.base + idx[i]]; }
+            std::copy(k2.begin(), k2.end(), K.begin() + (long)g.base);
+            std::copy(v2.begin(), v2.end(), V.begin() + (long)g.base);
+        }
+    };
+    sort_space(sk, sv, bp.seq);
+    sort_space(ak, av, bp.aux);
+
+    // ---- replays ----
+    std::vector<uint64_t> recip(65536, 0);
+    for (uint32_t t = 2; t < 65536; t++) recip[t] = ~0ull / t + 1;
+    std::vector<Rec> rs(bp.seq.total), ra(bp.aux.total);
+    std::vector<uint32_t> F(261);
+    for (const SortSeg& g : bp.seq.segs)
+        for (size_t i = g.base; i < g.base + g.count; i++)
+            if (i == g.base || sk[i - 1] != sk[i])
+                replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], rs.data() + g.base, recip.data());
+    for (const SortSeg& g : bp.aux.segs)
+        for (size_t i = g.base; i < g.base + g.count; i++)
+            if (i == g.base || ak[i - 1] != ak[i])
+                err |= replay_simple_run(ak.data(), av.data(), asym.data() + g.base, i, g.base + g.count, ak[i],
+                                         ra.data() + g.base, recip.data(), F.data());
+    if (err) { std::printf("FAIL replay error bits %x\n", err); return 1; }
+
+    // ---- coders, md5, assembly ----
+    std::vector<uint8_t> payload(bp.payload_bytes + 16);
+    std::vector<uint32_t> out_len(bp.tasks.size());
+    for (size_t t = 0; t < bp.tasks.size(); t++) {
+        const CoderTask& tk = bp.tasks[t];
+        const Rec* R = (tk.space ? ra.data() : rs.data()) + tk.rec_base;
+        err |= code_stream(R, tk.n, payload.data() + tk.out_base, tk.out_cap, out_len[t]);
+    }
+    if (err) { std::printf("FAIL coder error bits %x\n", err); return 1; }
+    std::vector<uint32_t> digests((size_t)nb * 12);
+    for (int64_t b = 0; b < nb; b++) {
+        const DevBlock& d = blocks[(size_t)b];
+        uint8_t dg[16];
+        const uint8_t* src[3] = {names.data() + d.name_base, seq.data() + d.seq_base, qual.data() + d.seq_base};
+        const uint64_t ln[3] = {d.name_bytes, d.seq_bytes, d.seq_bytes};
+        for (int f = 0; f < 3; f++) {
+            orc_md5(src[f], ln[f], dg);
+            std::memcpy(&digests[((size_t)b * 3 + f) * 4], dg, 16);
+        }
+    }
+    int fails = 0;
+    uint64_t total_out = 0;
+    for (int64_t b = 0; b < nb; b++) {
+        std::vector<uint8_t> o(bp.final_bytes + 64);
+        uint32_t dst[16], tsk[16], len[16], nseg = 0;
+        uint32_t L = assemble_plan(bv, (uint32_t)b, bp.asmb[(size_t)b], out_len.data(), digests.data(), o.data(), dst, tsk,
+                                   len, nseg);
+        for (uint32_t s = 0; s < nseg; s++) std::memcpy(o.data() + dst[s], payload.data() + bp.task_out_base[tsk[s]], len[s]);
+        HostBlock& h = hb[(size_t)b];
+        orc_block ob{h.names.data(), h.nl.data(), h.seq.data(), h.sl.data(), h.qual.data(), h.nreads};
+        orc_cfg oc{slevel, qlevel, 1, T[0]};
+        std::vector<uint8_t> ref(2 * (h.seq.size() + h.names.size()) + 4096);
+        int64_t rl = orc_encode_block(&ob, &oc, ref.data(), ref.size());
+        bool ok = rl == (int64_t)L && std::memcmp(ref.data(), o.data(), L) == 0;
+        if (!ok) {
+            size_t at = 0;
+            while (at < L && at < (size_t)rl && ref[at] == o[at]) at++;
+            std::printf("block %lld MISMATCH emu %u oracle %lld first diff at %zu\n", (long long)b, L, (long long)rl, at);
+            fails++;
+        }
+        total_out += L;
+    }
+    std::printf("%s blocks %lld reads %u out %llu bin_mode %d\n", fails ? "FAIL" : "OK", (long long)nb, nr,
+                (unsigned long long)total_out, T[0]);
+    return fails ? 1 : 0;
+}

@@ -1,0 +1,81 @@
+"""ctypes binding of the CPU restatement (oracle/liboracle.so) -- test
+infrastructure only: used by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker / CPU baseline, never by the product."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+CLI = os.path.join(ORACLE_DIR, "_build", "orc_cli")
+
+_lib = None
+
+
+class _Blk(C.Structure):
+    _fields_ = [("names", C.c_void_p), ("name_lens", C.c_void_p), ("seq", C.c_void_p),
+                ("seq_lens", C.c_void_p), ("qual", C.c_void_p), ("nreads", C.c_uint32)]
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("slevel", C.c_int), ("qlevel", C.c_int), ("md5", C.c_int), ("bin_mode", C.c_int)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fqz_oracle.c", "fqz_oracle.h", "orc_cli.c")]
+        if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
+            build()
+        l = C.CDLL(LIB)
+        P = C.c_void_p
+        l.orc_encode_block.argtypes = [P, P, P, C.c_size_t]
+        l.orc_encode_block.restype = C.c_int64
+        l.orc_analyze_idbin.argtypes = [P, C.c_int, P]
+        l.orc_analyze_idbin.restype = C.c_int
+        l.orc_md5.argtypes = [P, C.c_size_t, P]
+        l.orc_md5.restype = None
+        _lib = l
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data if a.size else 0
+
+
+def _blk(b) -> _Blk:
+    return _Blk(_p(b.names), _p(b.name_lens), _p(b.seq), _p(b.seq_lens), _p(b.qual), b.nreads)
+
+
+def encode_block(b, slevel=3, qlevel=2, md5=True, bin_mode=0) -> bytes:
+    cap = 2 * (b.seq.size + b.names.size) + 16 * b.nreads + 4096
+    out = np.empty(cap, dtype=np.uint8)
+    cb, cc = _blk(b), _Cfg(slevel, qlevel, 1 if md5 else 0, 1 if bin_mode else 0)
+    n = lib().orc_encode_block(C.byref(cb), C.byref(cc), _p(out), cap)
+    if n < 0:
+        raise RuntimeError("oracle encode failed")
+    return out[:n].tobytes()
+
+
+def analyze_ids(b, single_end: bool) -> np.ndarray:
+    t = np.zeros(512, dtype=np.uint8)
+    cb = _blk(b)
+    if lib().orc_analyze_idbin(C.byref(cb), 1 if single_end else 0, _p(t)) != 0:
+        raise RuntimeError("oracle id analysis failed")
+    return t
+
+
+def md5(data: bytes) -> bytes:
+    a = np.frombuffer(data, dtype=np.uint8)
+    d = np.zeros(16, dtype=np.uint8)
+    lib().orc_md5(_p(a), a.size, _p(d))
+    return d.tobytes()

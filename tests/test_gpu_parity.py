@@ -1,0 +1,100 @@
+"""GPU parity: libseqarc_amd on MI355X against the CPU restatement, byte for byte,
+through the C-ABI (sa_stage / sa_run / sa_fetch)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py
+import synth
+from conftest import GOLDEN
+
+import fastqueeze_amd as fq
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def enc():
+    e = fq.Encoder(0)
+    yield e
+    e.close()
+
+
+def _oracle_outs(blocks, cfg):
+    return [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode) for b in blocks]
+
+
+def _check(enc, blocks, cfg):
+    got = enc.encode(blocks, cfg)
+    want = _oracle_outs(blocks, cfg)
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        if g != w:
+            at = next((k for k in range(min(len(g), len(w))) if g[k] != w[k]), min(len(g), len(w)))
+            pytest.fail(f"block {i}: gpu {len(g)} B vs oracle {len(w)} B, first difference at byte {at}")
+    return got
+
+
+def test_reference_test_pair(enc, test_pair):
+    blocks = fq.blocks_from_fastq(*test_pair)
+    tmpl = fq.analyze_ids(blocks[0], False)
+    out = _check(enc, blocks, fq.Config(bin_mode=int(tmpl[0])))
+    assert len(out[0]) == 820818
+    se = fq.blocks_from_fastq(test_pair[0])
+    _check(enc, se, fq.Config(bin_mode=1))
+    # tokenizer path on the same reads
+    _check(enc, se, fq.Config(bin_mode=0))
+
+
+@pytest.mark.parametrize("name", ["test_pe_600k", "synth_pe_4k", "synth_pe_4k_s4", "synth_se_4k_q3", "edge_se",
+                                  "edge_se_s9"])
+def test_golden_cases(enc, name):
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+    g = json.load(open(os.path.join(GOLDEN, "golden.json")))[name]
+    case = g["case"]
+    t1, t2 = make_golden.inputs(case)
+    blocks = fq.blocks_from_fastq(t1, t2, case.get("bs", fq.BLOCK_SIZE))
+    tmpl = fq.analyze_ids(blocks[0], t2 is None)
+    cfg = fq.Config(slevel=case.get("slevel", 3), qlevel=case.get("qlevel", 2), bin_mode=int(tmpl[0]))
+    out = _check(enc, blocks, cfg)
+    assert [len(o) for o in out] == g["blocks"]
+
+
+def test_md5_off_and_empty_reads(enc):
+    blocks = fq.blocks_from_fastq(synth.edge_cases())
+    _check(enc, blocks, fq.Config(md5=False))
+    empty = fq.parse_se(b"@a\n\n+\n\n@b\n\n+\n\n")
+    _check(enc, [empty], fq.Config())
+
+
+def test_many_blocks_one_batch(enc):
+    a, b = synth.generate(30000, paired=True, seed=21)
+    blocks = fq.blocks_from_fastq(a, b, 400_000)
+    assert len(blocks) > 20
+    _check(enc, blocks, fq.Config())
+
+
+def test_full_size_block(enc):
+    """One full 50 MiB block (146,716 x 150 bp reads) -- the bench's unit of work."""
+    a, _ = synth.generate(150_000, seed=5)
+    blocks = fq.blocks_from_fastq(a)
+    assert blocks[0].text_bytes > 50_000_000
+    _check(enc, blocks[:1], fq.Config())
+
+
+def test_deterministic_rerun(enc):
+    a, b = synth.generate(2000, paired=True, seed=4)
+    blocks = fq.blocks_from_fastq(a, b)
+    first = enc.encode(blocks, fq.Config())
+    enc.run(fq.Config())
+    assert enc.fetch() == first
+
+
+def test_rejects_out_of_model_quality(enc):
+    bad = fq.parse_se(b"@r\nACGT\n+\nII\x7fI\n")
+    with pytest.raises(fq.SeqArcError):
+        enc.encode([bad], fq.Config())

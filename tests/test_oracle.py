@@ -1,0 +1,102 @@
+"""Oracle pinning (CPU): the restatement against the reference-run sizes recorded
+in SURVEY.md section 6, RFC 1321 vectors, and the committed golden digests."""
+import hashlib
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py
+from conftest import GOLDEN, ROOT, TEST1, TEST2
+
+import fastqueeze_amd as fq
+
+
+def _encaps(block: bytes):
+    """Split a block (81 size4 ...) into {encap id: total encap length}."""
+    assert block[0] == 0x81
+    size = int.from_bytes(block[1:5], "big") & 0x0FFFFFFF
+    assert size == len(block) - 5
+    p, out = 5, {}
+    while p < len(block):
+        eid = block[p] & 0x7F
+        if eid == 1:  # count: 81 84 u32
+            out[1] = 6
+            p += 6
+            continue
+        ln = int.from_bytes(block[p + 1:p + 5], "big") & 0x0FFFFFFF
+        out[eid] = 1 + 4 + ln
+        p += 5 + ln
+    assert p == len(block)
+    return out
+
+
+def test_rfc1321_vectors():
+    vec = {b"": "d41d8cd98f00b204e9800998ecf8427e", b"a": "0cc175b9c0f1b6a831c399e269772661",
+           b"abc": "900150983cd24fb0d6963f7d28e17f72",
+           b"message digest": "f96b697d7cb7938d525a2f31aaf161d0",
+           b"12345678901234567890123456789012345678901234567890123456789012345678901234567890":
+               "57edf4a22be3c955ac49da2e2107b67a"}
+    for m, h in vec.items():
+        assert oracle_py.md5(m).hex() == h
+    data = bytes(range(256)) * 300
+    assert oracle_py.md5(data) == hashlib.md5(data).digest()
+
+
+def test_reference_size_pins(test_pair):
+    """reference `SeqArc -c -t 1` on the test PE pair printed
+    name 48, seq 74,610 (seq + len + dege encaps), qual 746,149 compressed bytes."""
+    blocks = fq.blocks_from_fastq(*test_pair)
+    assert len(blocks) == 1 and blocks[0].nreads == 20000
+    tmpl = oracle_py.analyze_ids(blocks[0], False)
+    assert (tmpl[0], tmpl[1]) == (1, 1)          # "bOrderBin 1 petype 1"
+    enc = _encaps(oracle_py.encode_block(blocks[0], bin_mode=1))
+    assert enc[5] == 48
+    assert enc[7] == 746149
+    assert enc[6] + enc[4] + sum(enc.get(i, 0) for i in (23, 14, 24, 25, 26)) == 74610
+    # orgsize columns of the same table: name 655,576 = IDs + 2/read; seq 2,020,000
+    assert int(blocks[0].name_lens.sum()) + 2 * 20000 == 655576
+    assert int(blocks[0].seq_lens.sum()) + 20000 == 2020000
+
+
+
+@pytest.fixture(scope="module")
+def golden():
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return make_golden, json.load(f)
+
+
+@pytest.mark.parametrize("name", ["test_pe", "test_se", "test_pe_600k", "synth_pe_4k", "synth_pe_4k_s4",
+                                  "synth_se_4k_q3", "edge_se", "edge_se_s9"])
+def test_oracle_golden(golden, name):
+    mg, g = golden
+    case = g[name]["case"]
+    blocks, tmpl, outs = mg.run_case(case)
+    assert [len(o) for o in outs] == g[name]["blocks"]
+    assert hashlib.sha256(b"".join(outs)).hexdigest() == g[name]["sha256"]
+
+
+def test_cpu_decomposition(tmp_path):
+    """The GPU decomposition (sa_logic.h driven on the host) equals the oracle."""
+    exe = tmp_path / "emu"
+    src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
+                    os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c")], check=True)
+    import synth
+    pe1, pe2 = synth.generate(3000, paired=True, seed=3)
+    (tmp_path / "a.fq").write_bytes(pe1)
+    (tmp_path / "b.fq").write_bytes(pe2)
+    (tmp_path / "e.fq").write_bytes(synth.edge_cases())
+    runs = [[TEST1, TEST2], [TEST1], ["-b", "600000", TEST1, TEST2], [str(tmp_path / "a.fq"), str(tmp_path / "b.fq")],
+            ["-s", "4", "-b", "300000", str(tmp_path / "a.fq"), str(tmp_path / "b.fq")],
+            ["-q", "3", str(tmp_path / "a.fq")], [str(tmp_path / "e.fq")], ["-s", "9", str(tmp_path / "e.fq")]]
+    for args in runs:
+        r = subprocess.run([str(exe)] + args, capture_output=True, text=True)
+        assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
