@@ -283,20 +283,18 @@ SA_HD bool name_mid(const uint8_t* name, int len, int p, int s, Last last, Emit 
 //   q = hi32( M_hi * R + mulhi(M_lo, R) )   (Lemire, Kaser & Kurz 2019)
 SA_HD uint64_t recip64(uint32_t t)
 {
-    // ceil(2^64 / t) = floor((2^64 - 1) / t) + 1 for t not a power of two,
-    // and 2^64 / t exactly otherwise
-    uint64_t q = ~0ull / t;
-    if ((t & (t - 1)) != 0) q += 1;
-    else q += 1;   // (2^64-1)/t = 2^64/t - 1/t floors to 2^64/t - 1
-    return q;
+    return ~0ull / t + 1;   // ceil(2^64 / t) = floor((2^64 - 1) / t) + 1, t >= 2
 }
 
-// One symbol's coder record: cum | freq<<16, M (64 bits), tag.
-struct alignas(16) Rec {
+// One symbol's coder record (written by the model replay, read by the coder):
+// cum | freq << 16 and the model total; the coder divides via recip64(tot).
+struct alignas(8) Rec {
     uint32_t cumfreq;
-    uint32_t m_lo;
-    uint32_t m_hi;
-    uint32_t tag;
+    uint32_t tot;
 };
+
+// AUX sort keys carry the symbol in the low 8 bits (not sorted on):
+// key = model << 8 | symbol; the radix sort orders by bits [8, 8 + model bits).
+constexpr uint32_t AUX_SYM_BITS = 8;
 
 }  // namespace sa

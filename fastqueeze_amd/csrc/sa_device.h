@@ -67,6 +67,13 @@ struct SortView {
     uint32_t nsegs;
 };
 
+// A model run long enough for its own wave (k_replay_aux_long).
+struct LongRun {
+    uint64_t start, end;   // run start; end of its block's sorted AUX keys (the run ends earlier)
+    uint64_t rec_base;     // the block's first AUX record
+    uint32_t model, pad_;
+};
+
 struct CoderTask {
     uint64_t rec_base;   // first record (element offset into the space's record array)
     uint64_t out_base;   // byte offset into the payload arena

@@ -66,10 +66,10 @@ struct sa_ctx {
 
     // work
     DBuf d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
-    DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_aux_sym, d_rec_seq, d_rec_aux;
+    DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_rec_seq, d_rec_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
-    DBuf d_recip;
+    DBuf d_recip, d_longs, d_nlong;
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
 
     // last run
@@ -81,10 +81,10 @@ struct sa_ctx {
         DBuf* all[] = {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off,
                        &d_seq_len, &d_blocks, &d_counts, &d_totals, &d_name_p, &d_name_s, &d_maxlen, &d_err,
                        &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
-                       &d_aux_v[0], &d_aux_v[1], &d_aux_sym, &d_rec_seq, &d_rec_aux, &d_hist_seq,
+                       &d_aux_v[0], &d_aux_v[1], &d_rec_seq, &d_rec_aux, &d_hist_seq,
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
                        &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
-                       &d_final_len, &d_recip};
+                       &d_final_len, &d_recip, &d_longs, &d_nlong};
         for (DBuf* b : all) b->release();
         for (int i = 0; i < PH_N; i++) {
             if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
@@ -106,11 +106,12 @@ struct sa_ctx {
 
 namespace {
 
+// sorts keys by bits [lo, hi) in 8-bit digits (bits below lo ride along)
 int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
-             DBuf* keys, DBuf* vals, int bits, int& result_buf)
+             DBuf* keys, DBuf* vals, int lo, int hi, int& result_buf)
 {
     result_buf = 0;
-    if (plan.total == 0 || bits <= 0) return 0;
+    if (plan.total == 0 || hi <= lo) return 0;
     SortView sv{};
     sv.segs = segs.as<SortSeg>();
     sv.tile_seg = tiles.as<uint32_t>();
@@ -119,7 +120,7 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     sv.ntiles = (uint32_t)plan.tile_seg.size();
     sv.nsegs = (uint32_t)plan.segs.size();
     int cur = 0;
-    for (int shift = 0; shift < bits; shift += 8) {
+    for (int shift = lo; shift < hi; shift += 8) {
         hipLaunchKernelGGL(k_sort_hist, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,
                            keys[cur].as<uint32_t>(), (uint32_t)shift);
         hipLaunchKernelGGL(k_sort_scan, dim3(sv.nsegs), dim3(1024), 0, st, sv);
@@ -407,16 +408,19 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     }
 
     // ---- device buffers ----
-    const uint64_t stot = std::max<uint64_t>(ps.total, 1), atot = std::max<uint64_t>(pa.total, 1);
+    // slack: the replay and coder loops read up to 2 chunks past a run's end
+    const uint64_t stot = ps.total + 64, atot = pa.total + 64;
     for (int i = 0; i < 2; i++) {
         SA_CHECK(c, c->d_seq_k[i].ensure(stot * 4));
         SA_CHECK(c, c->d_seq_v[i].ensure(stot * 4));
         SA_CHECK(c, c->d_aux_k[i].ensure(atot * 4));
         SA_CHECK(c, c->d_aux_v[i].ensure(atot * 4));
     }
-    SA_CHECK(c, c->d_aux_sym.ensure(atot));
     SA_CHECK(c, c->d_rec_seq.ensure(stot * sizeof(Rec)));
     SA_CHECK(c, c->d_rec_aux.ensure(atot * sizeof(Rec)));
+    const uint64_t max_long = pa.total / LONG_RUN + 1;
+    SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
+    SA_CHECK(c, c->d_nlong.ensure(4));
     SA_CHECK(c, c->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
     SA_CHECK(c, c->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
     SA_CHECK(c, c->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
@@ -462,26 +466,28 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
 
     // ---- emit ----
     ev_begin(c, PH_EMIT, st);
-    SA_CHECK(c, hipMemsetAsync(c->d_seq_k[0].p, 0xff, ps.total * 4, st));
-    SA_CHECK(c, hipMemsetAsync(c->d_aux_k[0].p, 0xff, pa.total * 4, st));
+    SA_CHECK(c, hipMemsetAsync(c->d_seq_k[0].p, 0xff, stot * 4, st));
+    SA_CHECK(c, hipMemsetAsync(c->d_aux_k[0].p, 0xff, atot * 4, st));
+    SA_CHECK(c, hipMemsetAsync(c->d_seq_k[1].p, 0xff, stot * 4, st));
+    SA_CHECK(c, hipMemsetAsync(c->d_aux_k[1].p, 0xff, atot * 4, st));
     if (nr) {
         hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
                            c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), c->d_maxlen.as<uint16_t>(),
                            c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(), c->d_aux_k[0].as<uint32_t>(),
-                           c->d_aux_v[0].as<uint32_t>(), c->d_aux_sym.as<uint8_t>(), d_err);
+                           c->d_aux_v[0].as<uint32_t>(), d_err);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);
 
     // ---- sorts ----
     ev_begin(c, PH_SORT_SEQ, st);
-    if (run_sort(c, st, ps, c->d_segs_seq, c->d_tile_seq, c->d_hist_seq, c->d_seq_k, c->d_seq_v,
+    if (run_sort(c, st, ps, c->d_segs_seq, c->d_tile_seq, c->d_hist_seq, c->d_seq_k, c->d_seq_v, 0,
                  ns > 1 ? seq_bits : 0, c->seq_sorted_buf))
         return -1;
     ev_finish(c, PH_SORT_SEQ, st);
     ev_begin(c, PH_SORT_AUX, st);
-    if (run_sort(c, st, pa, c->d_segs_aux, c->d_tile_aux, c->d_hist_aux, c->d_aux_k, c->d_aux_v, aux_bits,
-                 c->aux_sorted_buf))
+    if (run_sort(c, st, pa, c->d_segs_aux, c->d_tile_aux, c->d_hist_aux, c->d_aux_k, c->d_aux_v, AUX_SYM_BITS,
+                 AUX_SYM_BITS + aux_bits, c->aux_sorted_buf))
         return -1;
     ev_finish(c, PH_SORT_AUX, st);
 
@@ -494,14 +500,19 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     if (ps.total)
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)((ps.total + 255) / 256)), dim3(256), 0, st, svs,
                            c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
-                           c->d_rec_seq.as<Rec>(), c->d_recip.as<uint64_t>());
+                           c->d_rec_seq.as<Rec>());
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_REPLAY_AUX, st);
-    if (pa.total)
-        hipLaunchKernelGGL(k_replay_aux, dim3((uint32_t)((pa.total + RP_THREADS - 1) / RP_THREADS)),
-                           dim3(RP_THREADS), 0, st, sva, c->d_aux_k[c->aux_sorted_buf].as<uint32_t>(),
-                           c->d_aux_v[c->aux_sorted_buf].as<uint32_t>(), c->d_aux_sym.as<uint8_t>(),
-                           c->d_rec_aux.as<Rec>(), c->d_recip.as<uint64_t>(), d_err);
+    if (pa.total) {
+        SA_CHECK(c, hipMemsetAsync(c->d_nlong.p, 0, 4, st));
+        const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();
+        const uint32_t* av = c->d_aux_v[c->aux_sorted_buf].as<uint32_t>();
+        hipLaunchKernelGGL(k_replay_aux_short, dim3((uint32_t)((pa.total + RP_THREADS - 1) / RP_THREADS)),
+                           dim3(RP_THREADS), 0, st, sva, ak, av, c->d_rec_aux.as<Rec>(), c->d_longs.as<LongRun>(),
+                           c->d_nlong.as<uint32_t>(), d_err);
+        hipLaunchKernelGGL(k_replay_aux_long, dim3((uint32_t)max_long), dim3(64), 0, st, c->d_longs.as<LongRun>(),
+                           c->d_nlong.as<uint32_t>(), ak, av, c->d_rec_aux.as<Rec>(), d_err);
+    }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_AUX, st);
 
@@ -509,7 +520,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     ev_begin(c, PH_CODER, st);
     hipLaunchKernelGGL(k_coder, dim3((uint32_t)tasks.size()), dim3(64), 0, st, c->d_tasks.as<CoderTask>(),
                        (uint32_t)tasks.size(), c->d_rec_seq.as<Rec>(), c->d_rec_aux.as<Rec>(),
-                       c->d_payload.as<uint8_t>(), c->d_out_len.as<uint32_t>(), d_err);
+                       c->d_recip.as<uint64_t>(), c->d_payload.as<uint8_t>(), c->d_out_len.as<uint32_t>(), d_err);
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_CODER, st);
 

@@ -131,12 +131,12 @@ __global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts,
                        const uint16_t* __restrict__ name_maxlen,
                        uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
                        uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
-                       uint8_t* __restrict__ aux_sym, uint32_t* __restrict__ err)
+                       uint32_t* __restrict__ err)
 {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= bv.nreads_total) return;
     const uint32_t e = emit_read(bv, r, counts, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key,
-                                 aux_val, aux_sym);
+                                 aux_val);
     if (e) atomicOr(err, e);
 }
 
@@ -256,8 +256,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 // it walks the segment and writes the coder record of every base.
 // ---------------------------------------------------------------------------
 __global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ keys,
-                             const uint32_t* __restrict__ vals, Rec* __restrict__ rec,
-                             const uint64_t* __restrict__ recip)
+                             const uint32_t* __restrict__ vals, Rec* __restrict__ rec)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= sv.total) return;
@@ -265,23 +264,28 @@ __global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ key
     const uint32_t key = keys[i];
     if (key == SORT_PAD) return;
     if (i != sg.base && keys[i - 1] == key) return;
-    replay_seq_run(keys, vals, i, sg.base + sg.count, key, rec + sg.base, recip);
+    replay_seq_run(keys, vals, i, sg.base + sg.count, key, rec + sg.base);
 }
 
 // ---------------------------------------------------------------------------
 // AUX model replay: SIMPLE_MODEL<N> (kModelEncode@0x42ccb0 and every inlined
-// copy).  One thread per segment start; the model lives in LDS, one 261-dword
-// region per thread (odd stride -> conflict-free).  Entry = sym<<16 | freq.
+// copy), one model run = the symbols of one (block, model) in stream order.
+//   k_replay_aux_short: one lane per run start; runs of >= LONG_RUN symbols are
+//     appended to a list instead.  Model in LDS, one RP_STRIDE region per lane.
+//   k_replay_aux_long: one wave per long run.  The wave loads 64 keys/positions
+//     per step coalesced; the serial model update runs on wave-uniform values
+//     (scalar unit), each lane collects the record of "its" symbol with
+//     writelane, and the 64 records are stored once per step.
 // ---------------------------------------------------------------------------
 constexpr int RP_THREADS = 64;
-constexpr int RP_STRIDE = 261;
+constexpr int RP_STRIDE = 253;   // >= 256 - RP_REG entries, odd -> conflict-free
+constexpr uint32_t LONG_RUN = 2048;
 
-__global__ __launch_bounds__(RP_THREADS) void k_replay_aux(const SortView sv, const uint32_t* __restrict__ keys,
-                                                           const uint32_t* __restrict__ vals,
-                                                           const uint8_t* __restrict__ syms,
-                                                           Rec* __restrict__ rec,
-                                                           const uint64_t* __restrict__ recip,
-                                                           uint32_t* __restrict__ err)
+__global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView sv, const uint32_t* __restrict__ keys,
+                                                                 const uint32_t* __restrict__ vals,
+                                                                 Rec* __restrict__ rec, LongRun* __restrict__ longs,
+                                                                 uint32_t* __restrict__ nlong,
+                                                                 uint32_t* __restrict__ err)
 {
     __shared__ uint32_t lds[RP_THREADS * RP_STRIDE];
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -289,31 +293,170 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux(const SortView sv, co
     const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
     const uint32_t key = keys[i];
     if (key == SORT_PAD) return;
-    if (i != sg.base && keys[i - 1] == key) return;
+    const uint32_t model = key >> AUX_SYM_BITS;
+    if (i != sg.base && (keys[i - 1] >> AUX_SYM_BITS) == model) return;
+    const size_t end = sg.base + sg.count;
+    if (i + LONG_RUN <= end && (keys[i + LONG_RUN - 1] >> AUX_SYM_BITS) == model) {
+        const uint32_t slot = atomicAdd(nlong, 1u);
+        longs[slot] = LongRun{i, end, sg.base, model, 0};
+        return;
+    }
     uint32_t* F = lds + threadIdx.x * RP_STRIDE;
-    const uint32_t e = replay_simple_run(keys, vals, syms + sg.base, i, sg.base + sg.count, key, rec + sg.base,
-                                         recip, F);
+    const uint32_t e = replay_simple_run(keys, vals, i, end, model, rec + sg.base, F);
     if (e) atomicOr(err, e);
 }
 
+__global__ __launch_bounds__(64) void k_replay_aux_long(const LongRun* __restrict__ longs,
+                                                        const uint32_t* __restrict__ nlong,
+                                                        const uint32_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ vals, Rec* __restrict__ rec_all,
+                                                        uint32_t* __restrict__ err)
+{
+    __shared__ uint32_t F[256];
+    if (blockIdx.x >= *nlong) return;
+    const LongRun lr = longs[blockIdx.x];
+    const uint32_t lane = threadIdx.x;
+    Rec* rec = rec_all + lr.rec_base;
+    SModel m;
+    sm_init(m, model_nsym(lr.model), F, lane, 64);
+    __syncthreads();
+    auto load = [&](size_t j, uint32_t& k, uint32_t& v) {
+        if (j + lane < lr.end) {
+            k = keys[j + lane];
+            v = vals[j + lane];
+        } else {
+            k = SORT_PAD;
+            v = 0;
+        }
+    };
+    uint32_t k0, v0;
+    load(lr.start, k0, v0);
+    for (size_t j = lr.start; j < lr.end; j += 64) {
+        uint32_t k1, v1;
+        load(j + 64, k1, v1);
+        // the run is contiguous in the sorted keys: its symbols in this step are a lane prefix
+        const uint32_t cnt = (uint32_t)__popcll(__ballot((k0 >> AUX_SYM_BITS) == lr.model));
+        const uint32_t sym_v = k0 & 0xff;
+        uint32_t cfb = 0, tb = 0;
+        bool ok = true;
+        if (cnt == 64) {
+#pragma unroll 16
+            for (int q = 0; q < 64; q++) {
+                uint32_t cf, t;
+                ok &= sm_code(m, F, __builtin_amdgcn_readlane(sym_v, q), cf, t);
+                if (lane == (uint32_t)q) { cfb = cf; tb = t; }
+            }
+        } else {
+            for (uint32_t q = 0; q < cnt; q++) {
+                uint32_t cf, t;
+                ok &= sm_code(m, F, __builtin_amdgcn_readlane(sym_v, q), cf, t);
+                if (lane == (uint32_t)q) { cfb = cf; tb = t; }
+            }
+        }
+        if (!ok) {
+            if (lane == 0) atomicOr(err, (uint32_t)E_CODER);
+            return;
+        }
+        if (lane < cnt) rec[v0] = Rec{cfb, tb};
+        if (cnt < 64) break;
+        k0 = k1;
+        v0 = v1;
+    }
+}
+
 // ---------------------------------------------------------------------------
-// Range coder: one lane per (block, stream) task.  Carry-less 64-bit coder of
+// Range coder: one wave per (block, stream) task.  Carry-less 64-bit coder of
 // encode_seq@0x422010-0x422085, finish = 8 x (low>>56) @0x424a1c.
 // q = range / tot via the per-symbol reciprocal M = ceil(2^64 / tot).
+// The wave loads the records (and gathers their reciprocals) 64 at a time,
+// one and two steps ahead; the serial coder runs on wave-uniform values and
+// writes its bytes into an LDS ring that the wave flushes 4 KiB at a time.
 // ---------------------------------------------------------------------------
+constexpr uint32_t CODER_RING = 8192;
+constexpr uint32_t CODER_HALF = CODER_RING / 2;
+
+struct RingPut {
+    uint8_t* ring;
+    uint32_t op;
+    __device__ void operator()(uint8_t b)
+    {
+        ring[op & (CODER_RING - 1)] = b;   // every lane writes the same byte
+        op++;
+    }
+};
+
+// Copy ring bytes [from, to) (to - from <= CODER_RING) to o, bytes >= cap dropped.
+__device__ inline void ring_flush(const uint8_t* ring, uint8_t* o, uint32_t from, uint32_t to, uint32_t cap,
+                                  uint32_t lane)
+{
+    __syncthreads();
+    if (to - from == CODER_HALF && (from & (CODER_HALF - 1)) == 0 && to <= cap) {
+        const uint4* src = reinterpret_cast<const uint4*>(ring + (from & (CODER_RING - 1)));
+        uint4* dst = reinterpret_cast<uint4*>(o + from);
+#pragma unroll
+        for (uint32_t w = 0; w < CODER_HALF / 16 / 64; w++) dst[w * 64 + lane] = src[w * 64 + lane];
+    } else {
+        for (uint32_t p = from + lane; p < to; p += 64)
+            if (p < cap) o[p] = ring[p & (CODER_RING - 1)];
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(64) void k_coder(const CoderTask* __restrict__ tasks, uint32_t ntasks,
                                               const Rec* __restrict__ rec_seq, const Rec* __restrict__ rec_aux,
-                                              uint8_t* __restrict__ out, uint32_t* __restrict__ out_len,
-                                              uint32_t* __restrict__ err)
+                                              const uint64_t* __restrict__ recip, uint8_t* __restrict__ out,
+                                              uint32_t* __restrict__ out_len, uint32_t* __restrict__ err)
 {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[CODER_RING];
     const uint32_t t = blockIdx.x;
-    if (t >= ntasks || threadIdx.x != 0) return;
+    if (t >= ntasks) return;
+    const uint32_t lane = threadIdx.x;
     const CoderTask tk = tasks[t];
     const Rec* R = (tk.space ? rec_aux : rec_seq) + tk.rec_base;
-    uint32_t len = 0;
-    const uint32_t e = code_stream(R, tk.n, out + tk.out_base, tk.out_cap, len);
-    out_len[t] = len;
-    if (e) atomicOr(err, e);
+    uint8_t* o = out + tk.out_base;
+    const uint32_t n = tk.n;
+    auto load = [&](uint32_t base) -> Rec { return base + lane < n ? R[base + lane] : Rec{0x10000u, 2u}; };
+    RCState s{0, 0xffffffffu};
+    RingPut put{ring, 0};
+    uint32_t flushed = 0;
+    Rec r0 = load(0), r1 = load(64);
+    uint64_t m0 = recip[r0.tot & 0xffff];
+    for (uint32_t base = 0; base < n; base += 64) {
+        const Rec r2 = load(base + 128);
+        const uint64_t m1 = recip[r1.tot & 0xffff];
+        const uint32_t cum_v = r0.cumfreq & 0xffff, f_v = r0.cumfreq >> 16;
+        const uint32_t mlo_v = (uint32_t)m0, mhi_v = (uint32_t)(m0 >> 32);
+        const uint32_t cnt = min(64u, n - base);
+        if (cnt == 64) {
+#pragma unroll 16
+            for (int q = 0; q < 64; q++)
+                rc_step(s, __builtin_amdgcn_readlane(cum_v, q), __builtin_amdgcn_readlane(f_v, q),
+                        __builtin_amdgcn_readlane(mlo_v, q), __builtin_amdgcn_readlane(mhi_v, q), put);
+        } else {
+            for (uint32_t q = 0; q < cnt; q++)
+                rc_step(s, __builtin_amdgcn_readlane(cum_v, q), __builtin_amdgcn_readlane(f_v, q),
+                        __builtin_amdgcn_readlane(mlo_v, q), __builtin_amdgcn_readlane(mhi_v, q), put);
+        }
+        // <= 3 bytes per symbol -> <= 192 per step: the ring never overruns
+        if (put.op - flushed >= CODER_HALF) {
+            ring_flush(ring, o, flushed, flushed + CODER_HALF, tk.out_cap, lane);
+            flushed += CODER_HALF;
+        }
+        r0 = r1;
+        r1 = r2;
+        m0 = m1;
+    }
+    rc_finish(s, put);
+    while (put.op - flushed > CODER_HALF) {
+        ring_flush(ring, o, flushed, flushed + CODER_HALF, tk.out_cap, lane);
+        flushed += CODER_HALF;
+    }
+    ring_flush(ring, o, flushed, put.op, tk.out_cap, lane);
+    if (lane == 0) {
+        out_len[t] = put.op;
+        if (put.op > tk.out_cap) atomicOr(err, (uint32_t)E_OVERFLOW);
+        if (!s.range) atomicOr(err, (uint32_t)E_CODER);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -63,13 +63,11 @@ SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int1
 struct AuxEmit {
     uint32_t* key;
     uint32_t* val;
-    uint8_t* sym;
     uint32_t pos;
     SA_HD void operator()(uint32_t model, uint32_t s)
     {
-        key[pos] = model;
+        key[pos] = (model << AUX_SYM_BITS) | s;
         val[pos] = pos;
-        sym[pos] = (uint8_t)s;
         pos++;
     }
 };
@@ -83,7 +81,7 @@ SA_HD void emit_kmodel(AuxEmit& em, uint32_t v)
 
 SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts, const int16_t* name_p,
                          const int16_t* name_s, const uint16_t* name_maxlen, uint32_t* seq_key,
-                         uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val, uint8_t* aux_sym)
+                         uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val)
 {
     uint32_t e = 0;
     const uint32_t b = bv.read_block[r];
@@ -110,7 +108,7 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
             ctx = ((ctx << 2) + cd) & mask;
         }
     }
-    AuxEmit em{aux_key + blk.aux_sym_base, aux_val + blk.aux_sym_base, aux_sym + blk.aux_sym_base, 0};
+    AuxEmit em{aux_key + blk.aux_sym_base, aux_val + blk.aux_sym_base, 0};
     // lengths (encode_len_short@0x4239a0; last_len stays 0)
     em.pos = blk.sbase[ST_LEN] + off[C_LEN];
     if (len == 0) {
@@ -193,117 +191,204 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
 }
 
 // ---- BASE_MODEL replay of one context run (k_replay_seq) -------------------
-// keys/vals: the block's sorted SEQ symbols; run starts at i; rec: the block's
-// SEQ records (indexed by stream position).
+// keys/vals: the block's sorted SEQ symbols (val = stream position << 2 | base);
+// the run of `key` starts at i.  rec: the block's SEQ records.  Keys and
+// values are read 8 ahead so the loads overlap the serial model update.
+constexpr int RP_CHUNK = 8;
+
 SA_HD void replay_seq_run(const uint32_t* keys, const uint32_t* vals, size_t i, size_t end, uint32_t key,
-                          Rec* rec, const uint64_t* recip)
+                          Rec* rec)
 {
     uint32_t st = 0x03030303u;
-    for (size_t j = i; j < end && keys[j] == key; j++) {
-        const uint32_t v = vals[j];
-        const uint32_t b = v & 3, pos = v >> 2;
-        uint32_t tot = (st & 0xff) + ((st >> 8) & 0xff) + ((st >> 16) & 0xff) + (st >> 24);
-        if (tot > 253) {
-            st -= (st >> 1) & 0x7f7f7f7fu;
-            tot = (st & 0xff) + ((st >> 8) & 0xff) + ((st >> 16) & 0xff) + (st >> 24);
+    uint32_t kk[RP_CHUNK], vv[RP_CHUNK];
+    for (int c = 0; c < RP_CHUNK; c++) { kk[c] = keys[i + c]; vv[c] = vals[i + c]; }
+    for (size_t j = i;; j += RP_CHUNK) {
+        uint32_t kn[RP_CHUNK], vn[RP_CHUNK];
+        for (int c = 0; c < RP_CHUNK; c++) { kn[c] = keys[j + RP_CHUNK + c]; vn[c] = vals[j + RP_CHUNK + c]; }
+        for (int c = 0; c < RP_CHUNK; c++) {
+            if (j + c >= end || kk[c] != key) return;
+            const uint32_t b = vv[c] & 3, pos = vv[c] >> 2;
+            uint32_t tot = (st & 0xff) + ((st >> 8) & 0xff) + ((st >> 16) & 0xff) + (st >> 24);
+            if (tot > 253) {
+                st -= (st >> 1) & 0x7f7f7f7fu;
+                tot = (st & 0xff) + ((st >> 8) & 0xff) + ((st >> 16) & 0xff) + (st >> 24);
+            }
+            const uint32_t below = b ? (st & (0xffffffffu >> (32 - 8 * b))) : 0u;
+            const uint32_t cum = (below & 0xff) + ((below >> 8) & 0xff) + ((below >> 16) & 0xff);
+            const uint32_t f = (st >> (8 * b)) & 0xff;
+            rec[pos] = Rec{cum | (f << 16), tot};
+            st += 1u << (8 * b);
         }
-        const uint32_t below = b ? (st & (0xffffffffu >> (32 - 8 * b))) : 0u;
-        const uint32_t cum = (below & 0xff) + ((below >> 8) & 0xff) + ((below >> 16) & 0xff);
-        const uint32_t f = (st >> (8 * b)) & 0xff;
-        const uint64_t m = recip[tot];
-        Rec rr;
-        rr.cumfreq = cum | (f << 16);
-        rr.m_lo = (uint32_t)m;
-        rr.m_hi = (uint32_t)(m >> 32);
-        rr.tag = tot;
-        rec[pos] = rr;
-        st += 1u << (8 * b);
+        for (int c = 0; c < RP_CHUNK; c++) { kk[c] = kn[c]; vv[c] = vn[c]; }
     }
 }
 
-// ---- SIMPLE_MODEL<N> replay of one model run (k_replay_aux) ----------------
-// F: scratch for N+1 entries (sym<<16 | freq).  S/rec: the block's AUX symbol
-// and record arrays (indexed by stream position).
-SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, const uint8_t* S, size_t i,
-                                 size_t end, uint32_t key, Rec* rec, const uint64_t* recip, uint32_t* F)
+// ---- SIMPLE_MODEL<N> (kModelEncode@0x42ccb0 and every inlined copy) --------
+// Model = {TotFreq, BubCnt, sentinel, F[0..N-1] of {symbol, freq}}.  The first
+// RP_REG entries live in registers (the hot symbols bubble there); the rest in
+// F (LDS), indexed from RP_REG.  Entry = sym << 16 | freq; an unused register
+// slot (N < RP_REG) has sym 0xffff and freq 0.
+constexpr int RP_REG = 4;
+
+struct SModel {
+    uint32_t R[RP_REG];
+    uint32_t N, tot, bub;
+};
+
+SA_HD void sm_init(SModel& m, uint32_t N, uint32_t* F, uint32_t first, uint32_t step)
 {
-    const uint32_t N = model_nsym(key);
-    for (uint32_t k = 0; k < N; k++) F[k] = (k << 16) | 1u;
-    F[N] = 0;
-    uint32_t tot = N, bub = 0;
-    for (size_t j = i; j < end && keys[j] == key; j++) {
-        const uint32_t pos = vals[j];
-        const uint32_t sym = S[pos];
-        uint32_t idx = 0, cum = 0, e = F[0];
-        while ((e >> 16) != sym) {
+    for (int k = 0; k < RP_REG; k++) m.R[k] = (uint32_t)k < N ? (((uint32_t)k << 16) | 1u) : 0xffff0000u;
+    for (uint32_t k = RP_REG + first; k < N; k += step) F[k - RP_REG] = (k << 16) | 1u;
+    m.N = N;
+    m.tot = N;
+    m.bub = 0;
+}
+
+// Codes one symbol: cf = cum | freq << 16 and t = TotFreq before the update,
+// then applies the update (freq += 8, TotFreq += 8, halve when > 0xffe0, and
+// every 16th update bubble the symbol one place forward).  false if `sym` is
+// not in the model (the reference would run off the array).
+SA_HD bool sm_code(SModel& m, uint32_t* F, uint32_t sym, uint32_t& cf, uint32_t& t)
+{
+    // register slots first, as an early-exit chain (the hot symbol is R[0])
+    uint32_t cum = 0, f = 0, idx = RP_REG;
+#pragma unroll
+    for (int k = 0; k < RP_REG; k++) {
+        if ((m.R[k] >> 16) == sym) {
+            idx = (uint32_t)k;
+            f = m.R[k] & 0xffff;
+            m.R[k] += 8;
+            break;
+        }
+        cum += m.R[k] & 0xffff;
+    }
+    if (idx == RP_REG) {
+        uint32_t k = RP_REG;
+        for (;; k++) {
+            if (k >= m.N) return false;
+            const uint32_t e = F[k - RP_REG];
+            if ((e >> 16) == sym) { f = e & 0xffff; break; }
             cum += e & 0xffff;
-            if (++idx >= N) break;
-            e = F[idx];
         }
-        if (idx >= N) {   // symbol outside the model: the reference runs off the array
-            return E_CODER;
+        idx = k;
+        F[idx - RP_REG] += 8;
+    }
+    cf = cum | (f << 16);
+    t = m.tot;
+    m.tot += 8;
+    if (m.tot > 0xffe0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < RP_REG; k++) {
+            const uint32_t fr = m.R[k] & 0xffff, h = fr - (fr >> 1);
+            m.R[k] = (m.R[k] & 0xffff0000u) | h;
+            tot += h;
         }
-        const uint32_t f = e & 0xffff;
-        const uint64_t m = recip[tot];
-        Rec rr;
-        rr.cumfreq = cum | (f << 16);
-        rr.m_lo = (uint32_t)m;
-        rr.m_hi = (uint32_t)(m >> 32);
-        rr.tag = tot;
-        rec[pos] = rr;
-        e += 8;
-        F[idx] = e;
-        tot += 8;
-        if (tot > 0xffe0) {
-            tot = 0;
-            for (uint32_t k = 0; k < N; k++) {
-                uint32_t x = F[k], fr = x & 0xffff;
-                fr -= fr >> 1;
-                F[k] = (x & 0xffff0000u) | fr;
-                tot += fr;
+        for (uint32_t k = RP_REG; k < m.N; k++) {
+            const uint32_t x = F[k - RP_REG], fr = x & 0xffff, h = fr - (fr >> 1);
+            F[k - RP_REG] = (x & 0xffff0000u) | h;
+            tot += h;
+        }
+        m.tot = tot;
+    }
+    if (((++m.bub) & 15) == 0 && idx > 0) {
+        if (idx < RP_REG) {
+#pragma unroll
+            for (int k = 1; k < RP_REG; k++) {
+                if (idx == (uint32_t)k && (m.R[k] & 0xffff) > (m.R[k - 1] & 0xffff)) {
+                    const uint32_t x = m.R[k];
+                    m.R[k] = m.R[k - 1];
+                    m.R[k - 1] = x;
+                }
             }
-        }
-        if (((++bub) & 15) == 0 && idx > 0) {
-            const uint32_t cur = F[idx], prv = F[idx - 1];
+        } else if (idx == RP_REG) {
+            const uint32_t cur = F[0];
+            if ((cur & 0xffff) > (m.R[RP_REG - 1] & 0xffff)) {
+                F[0] = m.R[RP_REG - 1];
+                m.R[RP_REG - 1] = cur;
+            }
+        } else {
+            const uint32_t cur = F[idx - RP_REG], prv = F[idx - RP_REG - 1];
             if ((cur & 0xffff) > (prv & 0xffff)) {
-                F[idx] = prv;
-                F[idx - 1] = cur;
+                F[idx - RP_REG] = prv;
+                F[idx - RP_REG - 1] = cur;
             }
         }
+    }
+    return true;
+}
+
+// Per-lane replay of one model run (short runs; k_replay_aux_short).
+SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, size_t i, size_t end, uint32_t model,
+                                 Rec* rec, uint32_t* F)
+{
+    SModel m;
+    sm_init(m, model_nsym(model), F, 0, 1);
+    for (size_t j = i; j < end; j++) {
+        const uint32_t key = keys[j];
+        if ((key >> AUX_SYM_BITS) != model) break;
+        uint32_t cf, t;
+        if (!sm_code(m, F, key & 0xff, cf, t)) return E_CODER;
+        rec[vals[j]] = Rec{cf, t};
     }
     return 0;
 }
 
-// ---- serial range coder of one stream (k_coder) -----------------------------
-// Carry-less 64-bit coder of encode_seq@0x422010-0x422085; finish = 8 bytes.
-SA_HD uint32_t code_stream(const Rec* R, uint32_t n, uint8_t* o, uint32_t cap, uint32_t& out_len)
+// ---- carry-less range coder step (encode_seq@0x422010-0x422085) ------------
+// q = range / tot = hi32(M_hi * range + mulhi(M_lo, range)), M = recip64(tot).
+struct RCState {
+    uint64_t low;
+    uint32_t range;
+};
+
+template <class Put>
+SA_HD void rc_step(RCState& s, uint32_t cum, uint32_t f, uint32_t m_lo, uint32_t m_hi, Put& put)
 {
-    uint32_t op = 0;
-    uint64_t low = 0;
-    uint32_t range = 0xffffffffu;
-    uint32_t bad = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const Rec r = R[i];
-        const uint32_t cum = r.cumfreq & 0xffff, f = r.cumfreq >> 16;
-        const uint32_t t1 = (uint32_t)(((uint64_t)r.m_lo * range) >> 32);
-        const uint32_t qq = (uint32_t)(((uint64_t)r.m_hi * range + t1) >> 32);
-        low += (uint32_t)(cum * qq);
-        range = qq * f;
-        while (range < (1u << 24)) {
-            if ((low ^ (low + range)) >> 56) range = ((uint32_t)low | 0xffffffu) - (uint32_t)low;
-            if (op < cap) o[op] = (uint8_t)(low >> 56);
-            op++;
-            range <<= 8;
-            low <<= 8;
-        }
+    const uint32_t t1 = (uint32_t)(((uint64_t)m_lo * s.range) >> 32);
+    const uint32_t q = (uint32_t)(((uint64_t)m_hi * s.range + t1) >> 32);
+    s.low += (uint32_t)(cum * q);
+    s.range = q * f;
+    while (s.range < (1u << 24)) {
+        if ((s.low ^ (s.low + s.range)) >> 56) s.range = ((uint32_t)s.low | 0xffffffu) - (uint32_t)s.low;
+        put((uint8_t)(s.low >> 56));
+        s.range <<= 8;
+        s.low <<= 8;
+        if (!s.range) break;   // only from a corrupt record (f == 0): never loop forever
     }
+}
+
+template <class Put>
+SA_HD void rc_finish(RCState& s, Put& put)
+{
     for (int k = 0; k < 8; k++) {
-        if (op < cap) o[op] = (uint8_t)(low >> 56);
-        op++;
-        low <<= 8;
+        put((uint8_t)(s.low >> 56));
+        s.low <<= 8;
     }
-    out_len = op;
-    return op > cap ? E_OVERFLOW : bad;
+}
+
+// Host-side (and reference-order) serial coder of one stream.
+struct BytePut {
+    uint8_t* o;
+    uint32_t cap, op;
+    SA_HD void operator()(uint8_t b)
+    {
+        if (op < cap) o[op] = b;
+        op++;
+    }
+};
+
+SA_HD uint32_t code_stream(const Rec* R, uint32_t n, const uint64_t* recip, uint8_t* o, uint32_t cap,
+                           uint32_t& out_len)
+{
+    RCState s{0, 0xffffffffu};
+    BytePut put{o, cap, 0};
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t m = recip[R[i].tot & 0xffff];
+        rc_step(s, R[i].cumfreq & 0xffff, R[i].cumfreq >> 16, (uint32_t)m, (uint32_t)(m >> 32), put);
+    }
+    rc_finish(s, put);
+    out_len = put.op;
+    return (put.op > cap ? E_OVERFLOW : 0) | (s.range ? 0 : E_CODER);
 }
 
 // ---- block assembly plan (k_assemble; doFqzEncode@0x42d2d0) ----------------

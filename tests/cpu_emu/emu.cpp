@@ -169,43 +169,44 @@ int main(int argc, char** argv)
     if (!plan_batch(blocks, totals, bp)) { std::printf("FAIL plan\n"); return 1; }
 
     // ---- emit ----
-    std::vector<uint32_t> sk(bp.seq.total, SORT_PAD), sv(bp.seq.total), ak(bp.aux.total, SORT_PAD), av(bp.aux.total);
-    std::vector<uint8_t> asym(bp.aux.total);
+    const size_t stot = bp.seq.total + 64, atot = bp.aux.total + 64;   // slack as the engine
+    std::vector<uint32_t> sk(stot, SORT_PAD), sv(stot), ak(atot, SORT_PAD), av(atot);
     for (uint32_t r = 0; r < nr; r++)
         err |= emit_read(bv, r, counts.data(), name_p.data(), name_s.data(), maxlen.data(), sk.data(), sv.data(),
-                         ak.data(), av.data(), asym.data());
+                         ak.data(), av.data());
     if (err) { std::printf("FAIL emit error bits %x\n", err); return 1; }
 
     // ---- stable sort per segment (what k_sort_* computes) ----
-    auto sort_space = [](std::vector<uint32_t>& K, std::vector<uint32_t>& V, const SortPlan& p) {
+    auto sort_space = [](std::vector<uint32_t>& K, std::vector<uint32_t>& V, const SortPlan& p, int lo) {
         for (const SortSeg& g : p.segs) {
             const size_t n = (size_t)g.ntiles * SORT_TILE;
             std::vector<uint32_t> idx(n);
             std::iota(idx.begin(), idx.end(), 0u);
-            std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return K[g.base + a] < K[g.base + b]; });
+            std::stable_sort(idx.begin(), idx.end(),
+                             [&](uint32_t a, uint32_t b) { return (K[g.base + a] >> lo) < (K[g.base + b] >> lo); });
             std::vector<uint32_t> k2(n), v2(n);
             for (size_t i = 0; i < n; i++) { k2[i] = K[g.base + idx[i]]; v2[i] = V[g.base + idx[i]]; }
             std::copy(k2.begin(), k2.end(), K.begin() + (long)g.base);
             std::copy(v2.begin(), v2.end(), V.begin() + (long)g.base);
         }
     };
-    sort_space(sk, sv, bp.seq);
-    sort_space(ak, av, bp.aux);
+    sort_space(sk, sv, bp.seq, 0);
+    sort_space(ak, av, bp.aux, AUX_SYM_BITS);
 
     // ---- replays ----
     std::vector<uint64_t> recip(65536, 0);
     for (uint32_t t = 2; t < 65536; t++) recip[t] = ~0ull / t + 1;
-    std::vector<Rec> rs(bp.seq.total), ra(bp.aux.total);
-    std::vector<uint32_t> F(261);
+    std::vector<Rec> rs(stot), ra(atot);
+    std::vector<uint32_t> F(256);
     for (const SortSeg& g : bp.seq.segs)
         for (size_t i = g.base; i < g.base + g.count; i++)
             if (i == g.base || sk[i - 1] != sk[i])
-                replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], rs.data() + g.base, recip.data());
+                replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], rs.data() + g.base);
     for (const SortSeg& g : bp.aux.segs)
         for (size_t i = g.base; i < g.base + g.count; i++)
-            if (i == g.base || ak[i - 1] != ak[i])
-                err |= replay_simple_run(ak.data(), av.data(), asym.data() + g.base, i, g.base + g.count, ak[i],
-                                         ra.data() + g.base, recip.data(), F.data());
+            if (i == g.base || (ak[i - 1] >> AUX_SYM_BITS) != (ak[i] >> AUX_SYM_BITS))
+                err |= replay_simple_run(ak.data(), av.data(), i, g.base + g.count, ak[i] >> AUX_SYM_BITS,
+                                         ra.data() + g.base, F.data());
     if (err) { std::printf("FAIL replay error bits %x\n", err); return 1; }
 
     // ---- coders, md5, assembly ----
@@ -214,7 +215,7 @@ int main(int argc, char** argv)
     for (size_t t = 0; t < bp.tasks.size(); t++) {
         const CoderTask& tk = bp.tasks[t];
         const Rec* R = (tk.space ? ra.data() : rs.data()) + tk.rec_base;
-        err |= code_stream(R, tk.n, payload.data() + tk.out_base, tk.out_cap, out_len[t]);
+        err |= code_stream(R, tk.n, recip.data(), payload.data() + tk.out_base, tk.out_cap, out_len[t]);
     }
     if (err) { std::printf("FAIL coder error bits %x\n", err); return 1; }
     std::vector<uint32_t> digests((size_t)nb * 12);
