@@ -9,6 +9,7 @@ Reference interface mirrored (SeqArc-1.6, cited by address in the binary):
   cut_se / cut_pe    SeqArcRead::doReadJob@0x432a80 / doReadPEJob@0x432d10
   parse_se / parse_pe AlignEncodeSEJob::getBlockRead@0x411b60 / getBlockReadPE@0x412920
   analyze_ids        IDProcess::analysisIDBinType@0x4310a0
+  Encoder.code_records  the inlined RangeCoder (encode_seq@0x422010-0x422085)
 """
 from __future__ import annotations
 
@@ -67,6 +68,7 @@ def load_library(path: str | None = None):
         "sa_cut_se": ([P, U64, U64, P, U64], I64), "sa_cut_pe": ([P, U64, P, U64, U64, P, P, U64], I64),
         "sa_parse_se": ([P, U64, P, P, P, P, P], I64), "sa_parse_pe": ([P, U64, P, U64, P, P, P, P, P], I64),
         "sa_analyze_ids": ([P, I32, P], I32),
+        "sa_code_records": ([P, I32, P, P, P, P, P, U64, P], I32), "sa_coder_restarts": ([P], C.c_uint32),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -197,7 +199,7 @@ def blocks_from_fastq(t1, t2=None, block_size: int = BLOCK_SIZE) -> list[Block]:
 class Encoder:
     """A gfx950 device context of libseqarc_amd (one per device / host thread)."""
 
-    PHASES = 10
+    PHASES = 11
 
     def __init__(self, device: int = 0):
         self._lib = load_library()
@@ -252,6 +254,26 @@ class Encoder:
         self.stage(blocks)
         self.run(cfg)
         return self.fetch()
+
+    def code_records(self, streams) -> list[bytes]:
+        """Range-code pre-modelled streams [(cum, freq, tot) uint16 arrays] on the GPU."""
+        lens = np.array([len(c) for c, _, _ in streams], dtype=np.uint32)
+        cat = [np.ascontiguousarray(np.concatenate([s[k] for s in streams]) if streams else np.zeros(0), dtype=np.uint16)
+               for k in range(3)]
+        cap = int(2 * lens.sum() + 64 * len(streams) + 16)
+        out = np.empty(cap, dtype=np.uint8)
+        ol = np.zeros(max(1, len(streams)), dtype=np.uint64)
+        if self._lib.sa_code_records(self._ctx, len(streams), _ptr(lens), _ptr(cat[0]), _ptr(cat[1]), _ptr(cat[2]),
+                                     _ptr(out), cap, _ptr(ol)) != 0:
+            self._err("sa_code_records")
+        res, o = [], 0
+        for i in range(len(streams)):
+            res.append(out[o:o + int(ol[i])].tobytes())
+            o += int(ol[i])
+        return res
+
+    def coder_restarts(self) -> int:
+        return int(self._lib.sa_coder_restarts(self._ctx))
 
     def phase_times(self) -> dict[str, float]:
         names = (C.c_char_p * self.PHASES)()

@@ -278,19 +278,25 @@ SA_HD bool name_mid(const uint8_t* name, int len, int p, int s, Last last, Emit 
     return true;
 }
 
-// ---- range coder reciprocal ------------------------------------------------
-// q = floor(R / t) for R < 2^32, 2 <= t < 2^32, with M = ceil(2^64 / t):
-//   q = hi32( M_hi * R + mulhi(M_lo, R) )   (Lemire, Kaser & Kurz 2019)
-SA_HD uint64_t recip64(uint32_t t)
-{
-    return ~0ull / t + 1;   // ceil(2^64 / t) = floor((2^64 - 1) / t) + 1, t >= 2
-}
+// ---- range coder records ----------------------------------------------------
+// Pass-R record of one coded symbol: reciprocal m = ceil(2^32 / tot) and
+// tot | freq << 16.  q0 = mulhi(range, m) is q or q + 1 and q0 * tot never
+// wraps (DESIGN.md "Coder"), so one borrow corrects it.
+struct alignas(8) PRec {
+    uint32_t m;
+    uint32_t tf;
+};
 
-// One symbol's coder record (written by the model replay, read by the coder):
-// cum | freq << 16 and the model total; the coder divides via recip64(tot).
-struct alignas(8) Rec {
-    uint32_t cumfreq;
-    uint32_t tot;
+// Coder segment: symbols per range checkpoint (DESIGN.md "Coder").
+constexpr uint32_t SEG_SYMS = 64;
+
+// Affine effect of a run of symbols on the coder's low word:
+// low -> (low << s) + B  (s in bits, saturated at 64 meaning "all shifted out"),
+// plus the number of bytes the run emits.
+struct LowMap {
+    uint64_t B;
+    uint32_t s;
+    uint32_t nbytes;
 };
 
 // AUX sort keys carry the symbol in the low 8 bits (not sorted on):

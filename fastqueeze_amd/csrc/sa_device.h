@@ -74,13 +74,49 @@ struct LongRun {
     uint32_t model, pad_;
 };
 
+// One range-coder stream (block, stream) and its segments (SEG_SYMS symbols
+// each; at least one, so that an empty stream still flushes its 8 bytes).
 struct CoderTask {
-    uint64_t rec_base;   // first record (element offset into the space's record array)
+    uint64_t rec_base;   // first record (element offset into the space's record arrays)
     uint64_t out_base;   // byte offset into the payload arena
+    uint64_t seg_base;   // first global segment
     uint32_t n;          // symbols
     uint32_t out_cap;    // payload capacity in bytes
     uint32_t space;      // 0 = SEQ records, 1 = AUX records
+    uint32_t nseg;
+};
+
+// Where a (re)started stream begins: segment, range, low and output offset there.
+struct CoderRun {
+    uint64_t low0;
+    uint32_t r0;
+    uint32_t start_seg;
+    uint32_t off0;
     uint32_t pad_;
+};
+
+// The streams of one coder launch: ids into the task table, per listed task
+// the prefix of its segment counts from start_seg, and its start state.
+struct TaskList {
+    const uint32_t* ids;
+    const uint64_t* gbase;   // count + 1 entries
+    const CoderRun* run;
+    uint32_t count;
+    uint32_t pad_;
+    uint64_t total_segs;
+};
+
+struct CoderView {
+    const CoderTask* tasks;
+    const PRec* prs[2];        // [space]
+    const uint16_t* cum[2];
+    uint8_t* out;              // payload arena
+    uint32_t* ck_r;            // per segment: range at its first symbol (pass R)
+    LowMap* maps;              // per segment: L1 map; end state of a squeezed segment (L3)
+    uint64_t* low_at;          // per segment: low at its first symbol (L2)
+    uint32_t* off_at;          // per segment: output offset of its first byte (L2)
+    uint32_t* out_len;         // per task
+    uint32_t* first_sq;        // per task: first segment whose exact coding squeezed
 };
 
 struct Md5Task {

@@ -42,8 +42,8 @@ struct DBuf {
 };
 
 const char* kPhaseNames[] = {"prep+scan", "emit", "sort_seq", "sort_aux", "replay_seq", "replay_aux",
-                             "coder", "md5", "assemble", "total"};
-enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX, PH_CODER, PH_MD5,
+                             "coder_r", "coder_l", "md5", "assemble", "total"};
+enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX, PH_CODER_R, PH_CODER_L, PH_MD5,
        PH_ASM, PH_TOTAL, PH_N };
 
 }  // namespace
@@ -53,6 +53,7 @@ struct sa_ctx {
     hipStream_t st = nullptr, st2 = nullptr;
     std::string err;
     bool timing = false;
+    uint32_t coder_restarts = 0;
     hipEvent_t ev_beg[PH_N], ev_end[PH_N];
     float ph_ms[PH_N];
 
@@ -66,10 +67,11 @@ struct sa_ctx {
 
     // work
     DBuf d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
-    DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_rec_seq, d_rec_aux;
+    DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
-    DBuf d_recip, d_longs, d_nlong;
+    DBuf d_rtab, d_longs, d_nlong;
+    DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq, d_list_ids, d_list_gbase, d_list_run;
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
 
     // last run
@@ -81,10 +83,11 @@ struct sa_ctx {
         DBuf* all[] = {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off,
                        &d_seq_len, &d_blocks, &d_counts, &d_totals, &d_name_p, &d_name_s, &d_maxlen, &d_err,
                        &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
-                       &d_aux_v[0], &d_aux_v[1], &d_rec_seq, &d_rec_aux, &d_hist_seq,
+                       &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
                        &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
-                       &d_final_len, &d_recip, &d_longs, &d_nlong};
+                       &d_final_len, &d_rtab, &d_longs, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                       &d_first_sq, &d_list_ids, &d_list_gbase, &d_list_run};
         for (DBuf* b : all) b->release();
         for (int i = 0; i < PH_N; i++) {
             if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
@@ -134,6 +137,98 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     return 0;
 }
 
+void ev_begin(sa_ctx* c, int ph, hipStream_t st);
+void ev_finish(sa_ctx* c, int ph, hipStream_t st);
+
+// Range-codes every task (DESIGN.md "Coder"): pass R, L1, L2, L3, then
+// restarts the streams whose exact coding squeezed before their last segment,
+// from the state L3 computed, until none does.  cv: tasks/records/out/out_len set
+// by the caller; the segment arrays are this context's.
+int coder_run(sa_ctx* c, hipStream_t st, const std::vector<CoderTask>& tasks, uint64_t total_segs, CoderView cv)
+{
+    if (tasks.empty()) return 0;
+    const uint64_t nsegs = std::max<uint64_t>(total_segs, 1);
+    SA_CHECK(c, c->d_ck.ensure(nsegs * 4));
+    SA_CHECK(c, c->d_maps.ensure(nsegs * sizeof(LowMap)));
+    SA_CHECK(c, c->d_low_at.ensure(nsegs * 8));
+    SA_CHECK(c, c->d_off_at.ensure(nsegs * 4));
+    SA_CHECK(c, c->d_first_sq.ensure(4 * tasks.size()));
+    SA_CHECK(c, c->d_list_ids.ensure(4 * tasks.size()));
+    SA_CHECK(c, c->d_list_gbase.ensure(8 * (tasks.size() + 1)));
+    SA_CHECK(c, c->d_list_run.ensure(sizeof(CoderRun) * tasks.size()));
+    cv.ck_r = c->d_ck.as<uint32_t>();
+    cv.maps = c->d_maps.as<LowMap>();
+    cv.low_at = c->d_low_at.as<uint64_t>();
+    cv.off_at = c->d_off_at.as<uint32_t>();
+    cv.first_sq = c->d_first_sq.as<uint32_t>();
+    SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
+    std::vector<uint32_t> ids(tasks.size());
+    std::vector<CoderRun> runs(tasks.size());
+    std::vector<uint64_t> gbase(tasks.size() + 1);
+    for (size_t i = 0; i < tasks.size(); i++) {
+        ids[i] = (uint32_t)i;
+        runs[i] = CoderRun{0ull, 0xffffffffu, 0u, 0u, 0u};
+    }
+    std::vector<uint32_t> first_sq(tasks.size()), out_len(tasks.size());
+    c->coder_restarts = 0;
+    for (int round = 0;; round++) {
+        const size_t cnt = ids.size();
+        gbase[0] = 0;
+        for (size_t i = 0; i < cnt; i++) gbase[i + 1] = gbase[i] + (tasks[ids[i]].nseg - runs[i].start_seg);
+        SA_CHECK(c, hipMemcpyAsync(c->d_list_ids.p, ids.data(), 4 * cnt, hipMemcpyHostToDevice, st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_list_gbase.p, gbase.data(), 8 * (cnt + 1), hipMemcpyHostToDevice, st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_list_run.p, runs.data(), sizeof(CoderRun) * cnt, hipMemcpyHostToDevice, st));
+        TaskList tl{c->d_list_ids.as<uint32_t>(), c->d_list_gbase.as<uint64_t>(), c->d_list_run.as<CoderRun>(),
+                    (uint32_t)cnt, 0u, gbase[cnt]};
+        const uint32_t lgrid = (uint32_t)((gbase[cnt] + 255) / 256);
+        if (round == 0) ev_begin(c, PH_CODER_R, st);
+        hipLaunchKernelGGL(k_coder_r, dim3((uint32_t)cnt), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r);
+        if (round == 0) ev_finish(c, PH_CODER_R, st);
+        if (round == 0) ev_begin(c, PH_CODER_L, st);
+        hipLaunchKernelGGL(k_coder_l1, dim3(lgrid), dim3(256), 0, st, cv, tl);
+        hipLaunchKernelGGL(k_coder_l2, dim3((uint32_t)cnt), dim3(L2_THREADS), 0, st, cv, tl);
+        hipLaunchKernelGGL(k_coder_l3, dim3(lgrid), dim3(256), 0, st, cv, tl);
+        if (round == 0) ev_finish(c, PH_CODER_L, st);
+        SA_CHECK(c, hipGetLastError());
+        SA_CHECK(c, hipMemcpyAsync(first_sq.data(), c->d_first_sq.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(out_len.data(), c->d_out_len.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipStreamSynchronize(st));
+        // streams whose first squeeze is not in their last segment restart after it
+        std::vector<uint32_t> nids;
+        std::vector<CoderRun> nruns;
+        for (size_t t = 0; t < tasks.size(); t++) {
+            const uint32_t k = first_sq[t];
+            if (k == 0xffffffffu || k + 1 >= tasks[t].nseg) continue;
+            LowMap endst;
+            uint32_t off;
+            SA_CHECK(c, hipMemcpy(&endst, c->d_maps.as<LowMap>() + tasks[t].seg_base + k, sizeof endst,
+                                  hipMemcpyDeviceToHost));
+            SA_CHECK(c, hipMemcpy(&off, c->d_off_at.as<uint32_t>() + tasks[t].seg_base + k, 4, hipMemcpyDeviceToHost));
+            nids.push_back((uint32_t)t);
+            nruns.push_back(CoderRun{endst.B, endst.s, k + 1, off + endst.nbytes, 0u});
+            const uint32_t none = 0xffffffffu;
+            SA_CHECK(c, hipMemcpy(c->d_first_sq.as<uint32_t>() + t, &none, 4, hipMemcpyHostToDevice));
+        }
+        if (nids.empty()) {
+            for (size_t t = 0; t < tasks.size(); t++)
+                if (out_len[t] > tasks[t].out_cap) {
+                    c->err = "range coder output overflowed its buffer";
+                    return -1;
+                }
+            break;
+        }
+        if (round > 1000) {
+            c->err = "range coder: too many restarts";
+            return -1;
+        }
+        c->coder_restarts += (uint32_t)nids.size();
+        ids.swap(nids);
+        runs.swap(nruns);
+    }
+
+    return 0;
+}
+
 void ev_begin(sa_ctx* c, int ph, hipStream_t st)
 {
     if (c->timing) (void)hipEventRecord(c->ev_beg[ph], st);
@@ -175,11 +270,11 @@ sa_ctx* sa_create(int device)
             return nullptr;
         }
     }
-    // reciprocal table M = ceil(2^64 / t), t < 65536 (tot of any model <= 0xffe0)
-    std::vector<uint64_t> recip(65536, 0);
-    for (uint32_t t = 2; t < 65536; t++) recip[t] = ~0ull / t + 1;
-    if (c->d_recip.ensure(recip.size() * 8) != hipSuccess ||
-        hipMemcpy(c->d_recip.p, recip.data(), recip.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+    // reciprocal table m = ceil(2^32 / t), t < 65536 (tot of any model <= 0xffe0)
+    std::vector<uint32_t> rtab(65536, 0);
+    for (uint32_t t = 1; t < 65536; t++) rtab[t] = recip32(t);
+    if (c->d_rtab.ensure(rtab.size() * 4) != hipSuccess ||
+        hipMemcpy(c->d_rtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -408,16 +503,19 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     }
 
     // ---- device buffers ----
-    // slack: the replay and coder loops read up to 2 chunks past a run's end
-    const uint64_t stot = ps.total + 64, atot = pa.total + 64;
+    // slack: the replay loops read up to 2 chunks past a run's end, pass R one
+    // 16-record chunk past a stream's last full segment
+    const uint64_t stot = ps.total + 128, atot = pa.total + 128;
     for (int i = 0; i < 2; i++) {
         SA_CHECK(c, c->d_seq_k[i].ensure(stot * 4));
         SA_CHECK(c, c->d_seq_v[i].ensure(stot * 4));
         SA_CHECK(c, c->d_aux_k[i].ensure(atot * 4));
         SA_CHECK(c, c->d_aux_v[i].ensure(atot * 4));
     }
-    SA_CHECK(c, c->d_rec_seq.ensure(stot * sizeof(Rec)));
-    SA_CHECK(c, c->d_rec_aux.ensure(atot * sizeof(Rec)));
+    SA_CHECK(c, c->d_prs_seq.ensure(stot * sizeof(PRec)));
+    SA_CHECK(c, c->d_prs_aux.ensure(atot * sizeof(PRec)));
+    SA_CHECK(c, c->d_cum_seq.ensure(stot * 2));
+    SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
     const uint64_t max_long = pa.total / LONG_RUN + 1;
     SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
     SA_CHECK(c, c->d_nlong.ensure(4));
@@ -496,11 +594,13 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
                  ps.total, (uint32_t)ps.tile_seg.size(), nbk};
     SortView sva{c->d_segs_aux.as<SortSeg>(), c->d_tile_aux.as<uint32_t>(), c->d_hist_aux.as<uint32_t>(),
                  pa.total, (uint32_t)pa.tile_seg.size(), nbk};
+    const SymSink sink_seq{c->d_prs_seq.as<PRec>(), c->d_cum_seq.as<uint16_t>(), c->d_rtab.as<uint32_t>()};
+    const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>(), c->d_rtab.as<uint32_t>()};
     ev_begin(c, PH_REPLAY_SEQ, st);
     if (ps.total)
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)((ps.total + 255) / 256)), dim3(256), 0, st, svs,
                            c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
-                           c->d_rec_seq.as<Rec>());
+                           sink_seq);
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_REPLAY_AUX, st);
     if (pa.total) {
@@ -508,21 +608,24 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
         const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();
         const uint32_t* av = c->d_aux_v[c->aux_sorted_buf].as<uint32_t>();
         hipLaunchKernelGGL(k_replay_aux_short, dim3((uint32_t)((pa.total + RP_THREADS - 1) / RP_THREADS)),
-                           dim3(RP_THREADS), 0, st, sva, ak, av, c->d_rec_aux.as<Rec>(), c->d_longs.as<LongRun>(),
+                           dim3(RP_THREADS), 0, st, sva, ak, av, sink_aux, c->d_longs.as<LongRun>(),
                            c->d_nlong.as<uint32_t>(), d_err);
         hipLaunchKernelGGL(k_replay_aux_long, dim3((uint32_t)max_long), dim3(64), 0, st, c->d_longs.as<LongRun>(),
-                           c->d_nlong.as<uint32_t>(), ak, av, c->d_rec_aux.as<Rec>(), d_err);
+                           c->d_nlong.as<uint32_t>(), ak, av, sink_aux, d_err);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_AUX, st);
 
     // ---- range coders ----
-    ev_begin(c, PH_CODER, st);
-    hipLaunchKernelGGL(k_coder, dim3((uint32_t)tasks.size()), dim3(64), 0, st, c->d_tasks.as<CoderTask>(),
-                       (uint32_t)tasks.size(), c->d_rec_seq.as<Rec>(), c->d_rec_aux.as<Rec>(),
-                       c->d_recip.as<uint64_t>(), c->d_payload.as<uint8_t>(), c->d_out_len.as<uint32_t>(), d_err);
-    SA_CHECK(c, hipGetLastError());
-    ev_finish(c, PH_CODER, st);
+    CoderView cv{};
+    cv.tasks = c->d_tasks.as<CoderTask>();
+    cv.prs[0] = c->d_prs_seq.as<PRec>();
+    cv.prs[1] = c->d_prs_aux.as<PRec>();
+    cv.cum[0] = c->d_cum_seq.as<uint16_t>();
+    cv.cum[1] = c->d_cum_aux.as<uint16_t>();
+    cv.out = c->d_payload.as<uint8_t>();
+    cv.out_len = c->d_out_len.as<uint32_t>();
+    if (coder_run(c, st, tasks, bp.total_segs, cv)) return -1;
 
     // ---- assembly ----
     if (cfg->md5) {
@@ -593,6 +696,80 @@ int sa_fetch(sa_ctx* c, sa_out* out, int n)
     SA_CHECK(c, hipStreamSynchronize(c->st));
     return 0;
 }
+
+int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_t* cum, const uint16_t* freq,
+                    const uint16_t* tot, uint8_t* out, uint64_t out_cap, uint64_t* out_lens)
+{
+    if (!c || nstreams < 0 || (nstreams && (!lens || !out || !out_lens))) return -1;
+    SA_CHECK(c, hipSetDevice(c->device));
+    std::vector<CoderTask> tasks((size_t)nstreams);
+    uint64_t nsym = 0, payload = 0, segs = 0;
+    for (int s = 0; s < nstreams; s++) {
+        CoderTask& tk = tasks[(size_t)s];
+        tk.rec_base = nsym;
+        tk.n = lens[s];
+        tk.space = 0;
+        tk.nseg = tk.n ? (tk.n + SEG_SYMS - 1) / SEG_SYMS : 1;
+        tk.seg_base = segs;
+        tk.out_base = payload;
+        const uint64_t cap = 2ull * tk.n + 64;
+        if (cap > 0xffffffffull) {
+            c->err = "sa_code_records: stream too long";
+            return -1;
+        }
+        tk.out_cap = (uint32_t)cap;
+        nsym += tk.n;
+        segs += tk.nseg;
+        payload = align_up(payload + cap, 16);
+    }
+    std::vector<PRec> prs(nsym + 128, PRec{0, 0});
+    std::vector<uint16_t> cm(nsym + 128, 0);
+    for (uint64_t i = 0; i < nsym; i++) {
+        const uint32_t t = tot[i], f = freq[i], cu = cum[i];
+        if (t < 2 || f < 1 || cu + f > t) {
+            c->err = "sa_code_records: invalid (cum, freq, tot)";   // the reference abort()s
+            return -1;
+        }
+        prs[i] = PRec{recip32(t), t | (f << 16)};
+        cm[i] = (uint16_t)cu;
+    }
+    hipStream_t st = c->st;
+    SA_CHECK(c, c->d_prs_seq.ensure(prs.size() * sizeof(PRec)));
+    SA_CHECK(c, c->d_cum_seq.ensure(cm.size() * 2));
+    SA_CHECK(c, c->d_tasks.ensure(sizeof(CoderTask) * std::max<size_t>(tasks.size(), 1)));
+    SA_CHECK(c, c->d_out_len.ensure(4 * std::max<size_t>(tasks.size(), 1)));
+    SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
+    SA_CHECK(c, hipMemcpyAsync(c->d_prs_seq.p, prs.data(), prs.size() * sizeof(PRec), hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_cum_seq.p, cm.data(), cm.size() * 2, hipMemcpyHostToDevice, st));
+    if (!tasks.empty())
+        SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice, st));
+    CoderView cv{};
+    cv.tasks = c->d_tasks.as<CoderTask>();
+    cv.prs[0] = cv.prs[1] = c->d_prs_seq.as<PRec>();
+    cv.cum[0] = cv.cum[1] = c->d_cum_seq.as<uint16_t>();
+    cv.out = c->d_payload.as<uint8_t>();
+    cv.out_len = c->d_out_len.as<uint32_t>();
+    c->have_output = false;
+    if (coder_run(c, st, tasks, segs, cv)) return -1;
+    std::vector<uint32_t> ol(tasks.size());
+    if (!tasks.empty())
+        SA_CHECK(c, hipMemcpyAsync(ol.data(), c->d_out_len.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipStreamSynchronize(st));
+    uint64_t o = 0;
+    for (size_t s = 0; s < tasks.size(); s++) {
+        if (o + ol[s] > out_cap) {
+            c->err = "sa_code_records: output buffer too small";
+            return -1;
+        }
+        SA_CHECK(c, hipMemcpyAsync(out + o, c->d_payload.as<uint8_t>() + tasks[s].out_base, ol[s], hipMemcpyDeviceToHost, st));
+        out_lens[s] = ol[s];
+        o += ol[s];
+    }
+    SA_CHECK(c, hipStreamSynchronize(st));
+    return 0;
+}
+
+uint32_t sa_coder_restarts(const sa_ctx* c) { return c ? c->coder_restarts : 0; }
 
 int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, sa_out* out)
 {

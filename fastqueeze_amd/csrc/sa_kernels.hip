@@ -256,7 +256,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 // it walks the segment and writes the coder record of every base.
 // ---------------------------------------------------------------------------
 __global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ keys,
-                             const uint32_t* __restrict__ vals, Rec* __restrict__ rec)
+                             const uint32_t* __restrict__ vals, const SymSink rec)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= sv.total) return;
@@ -264,7 +264,7 @@ __global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ key
     const uint32_t key = keys[i];
     if (key == SORT_PAD) return;
     if (i != sg.base && keys[i - 1] == key) return;
-    replay_seq_run(keys, vals, i, sg.base + sg.count, key, rec + sg.base);
+    replay_seq_run(keys, vals, i, sg.base + sg.count, key, SymSink{rec.prs + sg.base, rec.cum + sg.base, rec.rtab});
 }
 
 // ---------------------------------------------------------------------------
@@ -283,7 +283,7 @@ constexpr uint32_t LONG_RUN = 2048;
 
 __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView sv, const uint32_t* __restrict__ keys,
                                                                  const uint32_t* __restrict__ vals,
-                                                                 Rec* __restrict__ rec, LongRun* __restrict__ longs,
+                                                                 const SymSink rec, LongRun* __restrict__ longs,
                                                                  uint32_t* __restrict__ nlong,
                                                                  uint32_t* __restrict__ err)
 {
@@ -302,21 +302,22 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView 
         return;
     }
     uint32_t* F = lds + threadIdx.x * RP_STRIDE;
-    const uint32_t e = replay_simple_run(keys, vals, i, end, model, rec + sg.base, F);
+    const uint32_t e =
+        replay_simple_run(keys, vals, i, end, model, SymSink{rec.prs + sg.base, rec.cum + sg.base, rec.rtab}, F);
     if (e) atomicOr(err, e);
 }
 
 __global__ __launch_bounds__(64) void k_replay_aux_long(const LongRun* __restrict__ longs,
                                                         const uint32_t* __restrict__ nlong,
                                                         const uint32_t* __restrict__ keys,
-                                                        const uint32_t* __restrict__ vals, Rec* __restrict__ rec_all,
+                                                        const uint32_t* __restrict__ vals, const SymSink rec_all,
                                                         uint32_t* __restrict__ err)
 {
     __shared__ uint32_t F[256];
     if (blockIdx.x >= *nlong) return;
     const LongRun lr = longs[blockIdx.x];
     const uint32_t lane = threadIdx.x;
-    Rec* rec = rec_all + lr.rec_base;
+    const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base, rec_all.rtab};
     SModel m;
     sm_init(m, model_nsym(lr.model), F, lane, 64);
     __syncthreads();
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(64) void k_replay_aux_long(const LongRun* __restric
             if (lane == 0) atomicOr(err, (uint32_t)E_CODER);
             return;
         }
-        if (lane < cnt) rec[v0] = Rec{cfb, tb};
+        if (lane < cnt) sink_put(rec, v0, cfb & 0xffff, cfb >> 16, tb);
         if (cnt < 64) break;
         k0 = k1;
         v0 = v1;
@@ -365,97 +366,197 @@ __global__ __launch_bounds__(64) void k_replay_aux_long(const LongRun* __restric
 }
 
 // ---------------------------------------------------------------------------
-// Range coder: one wave per (block, stream) task.  Carry-less 64-bit coder of
-// encode_seq@0x422010-0x422085, finish = 8 x (low>>56) @0x424a1c.
-// q = range / tot via the per-symbol reciprocal M = ceil(2^64 / tot).
-// The wave loads the records (and gathers their reciprocals) 64 at a time,
-// one and two steps ahead; the serial coder runs on wave-uniform values and
-// writes its bytes into an LDS ring that the wave flushes 4 KiB at a time.
+// Range coder, decomposed (sa_logic.h "decomposed range coder").
+//
+// k_coder_r: pass R, one wave per stream.  The range chain runs on the scalar
+// unit: 16 records (32 dwords) per s_load chunk, double-buffered so the next
+// chunk's s_load is in flight while the current one is coded; the chain step is
+// hand-scheduled (10 SALU instructions).  One range checkpoint per segment is
+// collected in a VGPR (lane = segment mod 64) and stored 64 at a time.
 // ---------------------------------------------------------------------------
-constexpr uint32_t CODER_RING = 8192;
-constexpr uint32_t CODER_HALF = CODER_RING / 2;
-
-struct RingPut {
-    uint8_t* ring;
-    uint32_t op;
-    __device__ void operator()(uint8_t b)
-    {
-        ring[op & (CODER_RING - 1)] = b;   // every lane writes the same byte
-        op++;
-    }
+struct PChunk {
+    uint32_t w[32];   // 16 PRec
 };
 
-// Copy ring bytes [from, to) (to - from <= CODER_RING) to o, bytes >= cap dropped.
-__device__ inline void ring_flush(const uint8_t* ring, uint8_t* o, uint32_t from, uint32_t to, uint32_t cap,
-                                  uint32_t lane)
+__device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t tf)
 {
-    __syncthreads();
-    if (to - from == CODER_HALF && (from & (CODER_HALF - 1)) == 0 && to <= cap) {
-        const uint4* src = reinterpret_cast<const uint4*>(ring + (from & (CODER_RING - 1)));
-        uint4* dst = reinterpret_cast<uint4*>(o + from);
-#pragma unroll
-        for (uint32_t w = 0; w < CODER_HALF / 16 / 64; w++) dst[w * 64 + lane] = src[w * 64 + lane];
-    } else {
-        for (uint32_t p = from + lane; p < to; p += 64)
-            if (p < cap) o[p] = ring[p & (CODER_RING - 1)];
-    }
-    __syncthreads();
+    uint32_t t, f, q, p;
+    asm volatile(
+        "s_and_b32 %1, %5, 0xffff\n\t"
+        "s_lshr_b32 %2, %5, 16\n\t"
+        "s_mul_hi_u32 %3, %0, %6\n\t"
+        "s_mul_i32 %4, %3, %1\n\t"
+        "s_cmp_lt_u32 %0, %4\n\t"
+        "s_subb_u32 %3, %3, 0\n\t"
+        "s_mul_i32 %3, %3, %2\n\t"
+        "s_flbit_i32_b32 %4, %3\n\t"
+        "s_and_b32 %4, %4, 24\n\t"
+        "s_lshl_b32 %0, %3, %4"
+        : "+s"(r), "=&s"(t), "=&s"(f), "=&s"(q), "=&s"(p)
+        : "s"(tf), "s"(m)
+        : "scc");
 }
 
-__global__ __launch_bounds__(64) void k_coder(const CoderTask* __restrict__ tasks, uint32_t ntasks,
-                                              const Rec* __restrict__ rec_seq, const Rec* __restrict__ rec_aux,
-                                              const uint64_t* __restrict__ recip, uint8_t* __restrict__ out,
-                                              uint32_t* __restrict__ out_len, uint32_t* __restrict__ err)
+#define SA_CHUNK_STEPS(X, j0)                                                         \
+    _Pragma("unroll") for (int j = (j0); j < 16; j++) rc_range_salu(r, X.w[2 * j], X.w[2 * j + 1])
+
+__global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ tasks, const TaskList tl,
+                                                const PRec* __restrict__ prs0, const PRec* __restrict__ prs1,
+                                                uint32_t* __restrict__ ck_r)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[CODER_RING];
-    const uint32_t t = blockIdx.x;
-    if (t >= ntasks) return;
+    const uint32_t li = blockIdx.x;
     const uint32_t lane = threadIdx.x;
+    const uint32_t t = tl.ids[li];
     const CoderTask tk = tasks[t];
-    const Rec* R = (tk.space ? rec_aux : rec_seq) + tk.rec_base;
-    uint8_t* o = out + tk.out_base;
-    const uint32_t n = tk.n;
-    auto load = [&](uint32_t base) -> Rec { return base + lane < n ? R[base + lane] : Rec{0x10000u, 2u}; };
-    RCState s{0, 0xffffffffu};
-    RingPut put{ring, 0};
-    uint32_t flushed = 0;
-    Rec r0 = load(0), r1 = load(64);
-    uint64_t m0 = recip[r0.tot & 0xffff];
-    for (uint32_t base = 0; base < n; base += 64) {
-        const Rec r2 = load(base + 128);
-        const uint64_t m1 = recip[r1.tot & 0xffff];
-        const uint32_t cum_v = r0.cumfreq & 0xffff, f_v = r0.cumfreq >> 16;
-        const uint32_t mlo_v = (uint32_t)m0, mhi_v = (uint32_t)(m0 >> 32);
-        const uint32_t cnt = min(64u, n - base);
-        if (cnt == 64) {
-#pragma unroll 16
-            for (int q = 0; q < 64; q++)
-                rc_step(s, __builtin_amdgcn_readlane(cum_v, q), __builtin_amdgcn_readlane(f_v, q),
-                        __builtin_amdgcn_readlane(mlo_v, q), __builtin_amdgcn_readlane(mhi_v, q), put);
-        } else {
-            for (uint32_t q = 0; q < cnt; q++)
-                rc_step(s, __builtin_amdgcn_readlane(cum_v, q), __builtin_amdgcn_readlane(f_v, q),
-                        __builtin_amdgcn_readlane(mlo_v, q), __builtin_amdgcn_readlane(mhi_v, q), put);
+    const CoderRun run = tl.run[li];
+    const PRec* P = (tk.space ? prs1 : prs0) + tk.rec_base;
+    uint32_t* ck = ck_r + tk.seg_base;
+    const uint32_t first = run.start_seg, last = tk.nseg - 1;
+    uint32_t r = run.r0;
+    uint32_t g = first;
+    uint32_t kv = 0;
+    if (g < last) {
+        const PChunk* C = reinterpret_cast<const PChunk*>(P + (size_t)g * SEG_SYMS);
+        PChunk A = C[0], B;
+        for (; g < last; g++, C += 4) {
+            kv = lane == (g & 63) ? r : kv;
+            if ((g & 63) == 63) {
+                const uint32_t s = g - 63 + lane;
+                if (s >= first) ck[s] = kv;
+            }
+            rc_range_salu(r, A.w[0], A.w[1]);
+            __builtin_amdgcn_sched_barrier(0);
+            B = C[1];
+            __builtin_amdgcn_sched_barrier(0);
+            SA_CHUNK_STEPS(A, 1);
+            rc_range_salu(r, B.w[0], B.w[1]);
+            __builtin_amdgcn_sched_barrier(0);
+            A = C[2];
+            __builtin_amdgcn_sched_barrier(0);
+            SA_CHUNK_STEPS(B, 1);
+            rc_range_salu(r, A.w[0], A.w[1]);
+            __builtin_amdgcn_sched_barrier(0);
+            B = C[3];
+            __builtin_amdgcn_sched_barrier(0);
+            SA_CHUNK_STEPS(A, 1);
+            rc_range_salu(r, B.w[0], B.w[1]);
+            __builtin_amdgcn_sched_barrier(0);
+            A = C[4];   // the next segment (the record arrays carry >= 64 records of slack)
+            __builtin_amdgcn_sched_barrier(0);
+            SA_CHUNK_STEPS(B, 1);
         }
-        // <= 3 bytes per symbol -> <= 192 per step: the ring never overruns
-        if (put.op - flushed >= CODER_HALF) {
-            ring_flush(ring, o, flushed, flushed + CODER_HALF, tk.out_cap, lane);
-            flushed += CODER_HALF;
+    }
+    kv = lane == (g & 63) ? r : kv;
+    const uint32_t s = (g & ~63u) + lane;
+    if (s >= first && s <= g) ck[s] = kv;
+}
+#undef SA_CHUNK_STEPS
+
+// Locate list entry and segment of global coder-lane gi (gbase ascending).
+__device__ inline uint32_t list_find(const TaskList& tl, uint64_t gi)
+{
+    uint32_t lo = 0, hi = tl.count;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tl.gbase[mid] <= gi) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// L1: one lane per segment -> its LowMap.
+__global__ __launch_bounds__(256) void k_coder_l1(const CoderView cv, const TaskList tl)
+{
+    const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= tl.total_segs) return;
+    const uint32_t li = list_find(tl, gi);
+    const CoderTask& tk = cv.tasks[tl.ids[li]];
+    const uint32_t g = tl.run[li].start_seg + (uint32_t)(gi - tl.gbase[li]);
+    const size_t at = tk.rec_base + (size_t)g * SEG_SYMS;
+    cv.maps[tk.seg_base + g] =
+        seg_lowmap(cv.prs[tk.space] + at, cv.cum[tk.space] + at, cv.ck_r[tk.seg_base + g], seg_count(tk.n, g));
+}
+
+// L2: one workgroup per listed stream: exclusive scan of the segment maps from
+// the stream's start state -> low and output offset at every segment.
+constexpr int L2_THREADS = 256;
+
+__device__ inline LowMap shfl_up_map(const LowMap& m, int d)
+{
+    LowMap o;
+    o.B = __shfl_up(m.B, d, 64);
+    o.s = __shfl_up(m.s, d, 64);
+    o.nbytes = __shfl_up(m.nbytes, d, 64);
+    return o;
+}
+
+__global__ __launch_bounds__(L2_THREADS) void k_coder_l2(const CoderView cv, const TaskList tl)
+{
+    __shared__ LowMap wtot[L2_THREADS / 64];
+    __shared__ uint64_t carry_low;
+    __shared__ uint32_t carry_off;
+    const uint32_t li = blockIdx.x;
+    const CoderTask tk = cv.tasks[tl.ids[li]];
+    const CoderRun run = tl.run[li];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        carry_low = run.low0;
+        carry_off = run.off0;
+    }
+    __syncthreads();
+    for (uint32_t base = run.start_seg; base < tk.nseg; base += L2_THREADS) {
+        const uint32_t g = base + threadIdx.x;
+        const bool in = g < tk.nseg;
+        LowMap x = in ? cv.maps[tk.seg_base + g] : LowMap{0ull, 0u, 0u};
+        // inclusive wave scan (compose: earlier then later)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const LowMap y = shfl_up_map(x, d);
+            if (lane >= (uint32_t)d) x = lowmap_compose(y, x);
         }
-        r0 = r1;
-        r1 = r2;
-        m0 = m1;
+        if (lane == 63) wtot[w] = x;
+        __syncthreads();
+        LowMap pre{0ull, 0u, 0u};
+        for (uint32_t k = 0; k < w; k++) pre = lowmap_compose(pre, wtot[k]);
+        LowMap ex = shfl_up_map(x, 1);
+        if (lane == 0) ex = LowMap{0ull, 0u, 0u};
+        ex = lowmap_compose(pre, ex);
+        const uint64_t cl = carry_low;
+        const uint32_t co = carry_off;
+        if (in) {
+            cv.low_at[tk.seg_base + g] = shl64(cl, ex.s) + ex.B;
+            cv.off_at[tk.seg_base + g] = co + ex.nbytes;
+        }
+        __syncthreads();
+        if (threadIdx.x == L2_THREADS - 1) {
+            const LowMap tot = lowmap_compose(pre, x);
+            carry_low = shl64(cl, tot.s) + tot.B;
+            carry_off = co + tot.nbytes;
+        }
+        __syncthreads();
     }
-    rc_finish(s, put);
-    while (put.op - flushed > CODER_HALF) {
-        ring_flush(ring, o, flushed, flushed + CODER_HALF, tk.out_cap, lane);
-        flushed += CODER_HALF;
-    }
-    ring_flush(ring, o, flushed, put.op, tk.out_cap, lane);
-    if (lane == 0) {
-        out_len[t] = put.op;
-        if (put.op > tk.out_cap) atomicOr(err, (uint32_t)E_OVERFLOW);
-        if (!s.range) atomicOr(err, (uint32_t)E_CODER);
+}
+
+// L3: one lane per segment: the exact coder from (range, low) at its offset.
+__global__ __launch_bounds__(256) void k_coder_l3(const CoderView cv, const TaskList tl)
+{
+    const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= tl.total_segs) return;
+    const uint32_t li = list_find(tl, gi);
+    const uint32_t t = tl.ids[li];
+    const CoderTask& tk = cv.tasks[t];
+    const uint32_t g = tl.run[li].start_seg + (uint32_t)(gi - tl.gbase[li]);
+    const size_t at = tk.rec_base + (size_t)g * SEG_SYMS;
+    const uint64_t sg = tk.seg_base + g;
+    const uint32_t off = cv.off_at[sg];
+    const bool last = g + 1 == tk.nseg;
+    const SegEnd e = seg_code(cv.prs[tk.space] + at, cv.cum[tk.space] + at, cv.ck_r[sg], cv.low_at[sg],
+                              seg_count(tk.n, g), cv.out + tk.out_base + off, tk.out_cap > off ? tk.out_cap - off : 0,
+                              last);
+    if (last) cv.out_len[t] = off + e.nbytes;
+    if (e.squeezed) {
+        cv.maps[sg] = LowMap{e.low, e.r, e.nbytes};
+        atomicMin(&cv.first_sq[t], g);
     }
 }
 

@@ -190,6 +190,16 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
     return e;
 }
 
+// ---- coder records written by the model replays ---------------------------
+// Per coded symbol, in stream order: the Pass-R record {ceil(2^32/tot),
+// tot | freq << 16} and cum (< 2^16: every model total is <= 0xffe0).
+struct SymSink {
+    PRec* prs;
+    uint16_t* cum;
+    const uint32_t* rtab;   // rtab[t] = ceil(2^32 / t)
+};
+SA_HD void sink_put(const SymSink& o, uint32_t pos, uint32_t cum, uint32_t f, uint32_t t);
+
 // ---- BASE_MODEL replay of one context run (k_replay_seq) -------------------
 // keys/vals: the block's sorted SEQ symbols (val = stream position << 2 | base);
 // the run of `key` starts at i.  rec: the block's SEQ records.  Keys and
@@ -197,7 +207,7 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
 constexpr int RP_CHUNK = 8;
 
 SA_HD void replay_seq_run(const uint32_t* keys, const uint32_t* vals, size_t i, size_t end, uint32_t key,
-                          Rec* rec)
+                          const SymSink& rec)
 {
     uint32_t st = 0x03030303u;
     uint32_t kk[RP_CHUNK], vv[RP_CHUNK];
@@ -216,7 +226,7 @@ SA_HD void replay_seq_run(const uint32_t* keys, const uint32_t* vals, size_t i, 
             const uint32_t below = b ? (st & (0xffffffffu >> (32 - 8 * b))) : 0u;
             const uint32_t cum = (below & 0xff) + ((below >> 8) & 0xff) + ((below >> 16) & 0xff);
             const uint32_t f = (st >> (8 * b)) & 0xff;
-            rec[pos] = Rec{cum | (f << 16), tot};
+            sink_put(rec, pos, cum, f, tot);
             st += 1u << (8 * b);
         }
         for (int c = 0; c < RP_CHUNK; c++) { kk[c] = kn[c]; vv[c] = vn[c]; }
@@ -320,7 +330,7 @@ SA_HD bool sm_code(SModel& m, uint32_t* F, uint32_t sym, uint32_t& cf, uint32_t&
 
 // Per-lane replay of one model run (short runs; k_replay_aux_short).
 SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, size_t i, size_t end, uint32_t model,
-                                 Rec* rec, uint32_t* F)
+                                 const SymSink& rec, uint32_t* F)
 {
     SModel m;
     sm_init(m, model_nsym(model), F, 0, 1);
@@ -329,66 +339,142 @@ SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, siz
         if ((key >> AUX_SYM_BITS) != model) break;
         uint32_t cf, t;
         if (!sm_code(m, F, key & 0xff, cf, t)) return E_CODER;
-        rec[vals[j]] = Rec{cf, t};
+        sink_put(rec, vals[j], cf & 0xffff, cf >> 16, t);
     }
     return 0;
 }
 
-// ---- carry-less range coder step (encode_seq@0x422010-0x422085) ------------
-// q = range / tot = hi32(M_hi * range + mulhi(M_lo, range)), M = recip64(tot).
-struct RCState {
-    uint64_t low;
-    uint32_t range;
-};
+// ---- decomposed range coder ------------------------------------------------
+// The carry-less coder of encode_seq@0x422010-0x422085 has two state words:
+// range (u32) and low (u64).  Apart from the rare "squeeze" (range forced to
+// the distance to the next 2^24 boundary when low and low+range straddle a
+// top-byte boundary, probability ~2^-32 per normalisation), range evolves
+// independently of low:
+//     q = range / tot;  rr = q * f;  n = clz(rr) / 8;  range = rr << 8n
+// and low evolves as an affine map of its previous value per symbol:
+//     low = (low + cum * q) << 8n    (mod 2^64; the shifted-out bytes are output)
+// So the coder is split into
+//   R  (serial, one wave per stream): the range chain only, on the scalar unit,
+//      keeping one range checkpoint per SEG_SYMS symbols;
+//   L1 (parallel, one lane per segment): re-run the segment's range chain from
+//      its checkpoint and reduce its effect on low to an affine map
+//      low -> (low << 8N) + D  plus its byte count N;
+//   L2 (per stream): exclusive scan of those maps -> low and output offset at
+//      every segment start;
+//   L3 (parallel, one lane per segment): the exact reference coder over the
+//      segment from (range, low), writing its bytes at the segment's offset and
+//      checking the squeeze condition exactly.  A squeeze voids the checkpoints
+//      after it: the stream restarts R/L1/L2/L3 after that segment from the exact
+//      state L3 computed (the host loops until no stream squeezes).
 
-template <class Put>
-SA_HD void rc_step(RCState& s, uint32_t cum, uint32_t f, uint32_t m_lo, uint32_t m_hi, Put& put)
+SA_HD uint32_t recip32(uint32_t t) { return (uint32_t)((0x100000000ull + t - 1) / t); }
+
+SA_HD void sink_put(const SymSink& o, uint32_t pos, uint32_t cum, uint32_t f, uint32_t t)
 {
-    const uint32_t t1 = (uint32_t)(((uint64_t)m_lo * s.range) >> 32);
-    const uint32_t q = (uint32_t)(((uint64_t)m_hi * s.range + t1) >> 32);
-    s.low += (uint32_t)(cum * q);
-    s.range = q * f;
-    while (s.range < (1u << 24)) {
-        if ((s.low ^ (s.low + s.range)) >> 56) s.range = ((uint32_t)s.low | 0xffffffu) - (uint32_t)s.low;
-        put((uint8_t)(s.low >> 56));
-        s.range <<= 8;
-        s.low <<= 8;
-        if (!s.range) break;   // only from a corrupt record (f == 0): never loop forever
-    }
+    o.prs[pos] = PRec{o.rtab[t], t | (f << 16)};
+    o.cum[pos] = (uint16_t)cum;
 }
 
-template <class Put>
-SA_HD void rc_finish(RCState& s, Put& put)
+SA_HD uint32_t clz32(uint32_t v)
 {
-    for (int k = 0; k < 8; k++) {
-        put((uint8_t)(s.low >> 56));
-        s.low <<= 8;
-    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__builtin_clz(v);
+#else
+    return v ? (uint32_t)__builtin_clz(v) : 32u;
+#endif
 }
 
-// Host-side (and reference-order) serial coder of one stream.
-struct BytePut {
-    uint8_t* o;
-    uint32_t cap, op;
-    SA_HD void operator()(uint8_t b)
-    {
-        if (op < cap) o[op] = b;
-        op++;
-    }
-};
+SA_HD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
-SA_HD uint32_t code_stream(const Rec* R, uint32_t n, const uint64_t* recip, uint8_t* o, uint32_t cap,
-                           uint32_t& out_len)
+// one symbol of the range chain; returns q, updates r, sets n (bytes shifted)
+SA_HD uint32_t range_step(uint32_t& r, const PRec p, uint32_t& n)
 {
-    RCState s{0, 0xffffffffu};
-    BytePut put{o, cap, 0};
+    const uint32_t t = p.tf & 0xffffu, f = p.tf >> 16;
+    uint32_t q = mulhi32(r, p.m);
+    q -= (r < q * t) ? 1u : 0u;
+    const uint32_t rr = q * f;
+    const uint32_t sh = clz32(rr) & 24u;
+    n = sh >> 3;
+    r = rr << sh;
+    return q;
+}
+
+SA_HD uint64_t shl64(uint64_t x, uint32_t s) { return s >= 64 ? 0ull : x << s; }
+
+// apply a then b
+SA_HD LowMap lowmap_compose(const LowMap& a, const LowMap& b)
+{
+    LowMap c;
+    c.B = shl64(a.B, b.s) + b.B;
+    c.s = a.s + b.s >= 64 ? 64u : a.s + b.s;
+    c.nbytes = a.nbytes + b.nbytes;
+    return c;
+}
+
+// L1: a segment's map from its range checkpoint.
+SA_HD LowMap seg_lowmap(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
+{
+    LowMap m{0ull, 0u, 0u};
+    uint64_t low = 0;
+    uint32_t sbits = 0;
     for (uint32_t i = 0; i < n; i++) {
-        const uint64_t m = recip[R[i].tot & 0xffff];
-        rc_step(s, R[i].cumfreq & 0xffff, R[i].cumfreq >> 16, (uint32_t)m, (uint32_t)(m >> 32), put);
+        uint32_t nb;
+        const uint32_t q = range_step(r, P[i], nb);
+        low = shl64(low + (uint64_t)cum[i] * q, 8 * nb);
+        sbits += 8 * nb;
+        m.nbytes += nb;
     }
-    rc_finish(s, put);
-    out_len = put.op;
-    return (put.op > cap ? E_OVERFLOW : 0) | (s.range ? 0 : E_CODER);
+    m.B = low;
+    m.s = sbits >= 64 ? 64u : sbits;
+    return m;
+}
+
+// L3: the exact coder over one segment from (r, low).  Writes the bytes to
+// o[0..) (bytes at or beyond cap are dropped) and returns how many it produced;
+// `squeezed` is set if the carry-less squeeze fired.  If `finish`, the 8 flush
+// bytes of low follow (rc finish @0x424a1c).
+struct SegEnd {
+    uint64_t low;
+    uint32_t r;
+    uint32_t nbytes;
+    uint32_t squeezed;
+};
+
+SA_HD uint32_t seg_count(uint32_t n, uint32_t seg) { return n - seg * SEG_SYMS < SEG_SYMS ? n - seg * SEG_SYMS : SEG_SYMS; }
+
+SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
+                      uint64_t cap, bool finish)
+{
+    SegEnd e{0, 0, 0, 0};
+    uint32_t op = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t t = P[i].tf & 0xffffu, f = P[i].tf >> 16;
+        uint32_t q = mulhi32(r, P[i].m);
+        q -= (r < q * t) ? 1u : 0u;
+        low += (uint64_t)cum[i] * q;
+        r = q * f;
+        while (r < (1u << 24)) {
+            if ((low ^ (low + r)) >> 56) {
+                r = ((uint32_t)low | 0xffffffu) - (uint32_t)low;
+                e.squeezed = 1;
+            }
+            if (op < cap) o[op] = (uint8_t)(low >> 56);
+            op++;
+            r <<= 8;
+            low <<= 8;
+        }
+    }
+    if (finish) {
+        for (int k = 0; k < 8; k++) {
+            if (op < cap) o[op] = (uint8_t)(low >> 56);
+            op++;
+            low <<= 8;
+        }
+    }
+    e.low = low;
+    e.r = r;
+    e.nbytes = op;
+    return e;
 }
 
 // ---- block assembly plan (k_assemble; doFqzEncode@0x42d2d0) ----------------

@@ -46,6 +46,7 @@ struct BatchPlan {
     std::vector<CoderTask> tasks;
     std::vector<uint64_t> task_out_base;
     std::vector<AsmBlock> asmb;
+    uint64_t total_segs = 0;
     uint64_t payload_bytes = 0;
     uint64_t final_bytes = 0;
 };
@@ -83,7 +84,7 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
     bp.tasks.clear();
     bp.task_out_base.clear();
     bp.asmb.assign(nbk, AsmBlock{});
-    uint64_t payload = 0, fin = 0;
+    uint64_t payload = 0, fin = 0, segs = 0;
     for (size_t b = 0; b < nbk; b++) {
         DevBlock& d = blocks[b];
         d.seq_sym_base = bp.seq.segs[b].base;
@@ -102,6 +103,9 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
             }
             // each symbol narrows the range by at most 2^16 (tot <= 0xffe0):
             // <= 2 output bytes per symbol, plus the 8-byte flush
+            tk.nseg = tk.n ? (tk.n + SEG_SYMS - 1) / SEG_SYMS : 1;
+            tk.seg_base = segs;
+            segs += tk.nseg;
             const uint64_t cap = 2ull * tk.n + 64;
             tk.out_cap = (uint32_t)std::min<uint64_t>(cap, 0xffffffffull);
             tk.out_base = payload;
@@ -116,6 +120,7 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
         bp.asmb[b].out_base = fin;
         fin = align_up(fin + blk_out, 16);
     }
+    bp.total_segs = segs;
     bp.payload_bytes = payload;
     bp.final_bytes = fin;
     return true;

@@ -72,6 +72,18 @@ int sa_fetch(sa_ctx *ctx, sa_out *out, int n);             /* D2H of the encaps 
 int sa_phase_times(const sa_ctx *ctx, const char **names, float *ms, int max);
 void sa_set_timing(sa_ctx *ctx, int on);
 
+/* ---- range coder over pre-modelled symbols ---------------------------- */
+/* The carry-less range coder inlined in every EncapFqzComp::encode_* (e.g.
+ * encode_seq@0x422010-0x422085, finish @0x424a1c), applied to nstreams streams
+ * of (cum, freq, tot) triples laid out back to back (stream s has lens[s]
+ * symbols).  Writes the streams' coded bytes back to back into out and their
+ * lengths into out_lens.  Rejects cum + freq > tot (the reference abort()s). */
+int sa_code_records(sa_ctx *ctx, int nstreams, const uint32_t *lens, const uint16_t *cum,
+                    const uint16_t *freq, const uint16_t *tot, uint8_t *out, uint64_t out_cap,
+                    uint64_t *out_lens);
+/* streams restarted after a carry-less squeeze in the last sa_run / sa_code_records */
+uint32_t sa_coder_restarts(const sa_ctx *ctx);
+
 /* ---- host-side mirrors of the reference's block plumbing -------------- */
 /* Block cut: SeqArcRead::doReadJob@0x432a80 / cultbuf@0x432530 / getEndPos@0x4320c0
  * (SE) and doReadPEJob@0x432d10 / cultPEbuf@0x432180 (PE).  Returns #blocks. */

@@ -63,6 +63,16 @@ static void rc_finish(rc_t *rc)
     }
 }
 
+int64_t orc_rc_encode(const uint16_t *cum, const uint16_t *freq, const uint16_t *tot, size_t n,
+                      uint8_t *out, size_t cap)
+{
+    rc_t rc;
+    rc_init(&rc, out, out + cap);
+    for (size_t i = 0; i < n && !rc.err; i++) rc_encode(&rc, cum[i], freq[i], tot[i]);
+    rc_finish(&rc);
+    return rc.err ? -1 : (int64_t)(rc.out - out);
+}
+
 /* ------------------------------------------------------------------------ */
 /* SIMPLE_MODEL<N>: layout {u32 TotFreq, u32 BubCnt, sentinel, F[N+1]}.      */
 /* Clearest inlined instance: kModelEncode@0x42ccb0; init @0x426f30.         */

@@ -66,6 +66,11 @@ int64_t orc_qual_payload(const orc_block *b, int qlevel, uint8_t *out, size_t ca
  * se = 1 for single-end input. Returns 0, or -1 if the reference would throw. */
 int orc_analyze_idbin(const orc_block *first, int se, uint8_t tmpl[512]);
 
+/* The bare range coder (encode_seq@0x422010-0x422085, finish @0x424a1c) over n
+ * given (cum, freq, tot) triples; returns bytes written or -1. */
+int64_t orc_rc_encode(const uint16_t *cum, const uint16_t *freq, const uint16_t *tot, size_t n,
+                      uint8_t *out, size_t cap);
+
 /* RFC1321 MD5 (the vendored RSA implementation, MDString@0x4058f0). */
 void orc_md5(const uint8_t *data, size_t len, uint8_t digest[16]);
 

@@ -37,6 +37,86 @@ static std::vector<uint8_t> slurp(const char* p)
     return v;
 }
 
+// The GPU coder decomposition (pass R, L1, L2, L3, restart after a squeeze)
+// run sequentially; returns the stream's byte count.
+static uint32_t code_decomposed(const PRec* P, const uint16_t* C, uint32_t n, uint8_t* o, uint32_t cap, int& restarts)
+{
+    const uint32_t nseg = n ? (n + SEG_SYMS - 1) / SEG_SYMS : 1;
+    std::vector<uint32_t> ck(nseg), offat(nseg);
+    std::vector<LowMap> mp(nseg);
+    std::vector<uint64_t> lowat(nseg);
+    uint32_t start = 0, r0 = 0xffffffffu, off0 = 0, out_len = 0;
+    uint64_t low0 = 0;
+    for (;;) {
+        uint32_t r = r0;
+        for (uint32_t g = start; g < nseg; g++) {
+            ck[g] = r;
+            if (g + 1 < nseg)
+                for (uint32_t i = 0; i < SEG_SYMS; i++) {
+                    uint32_t nb;
+                    range_step(r, P[g * SEG_SYMS + i], nb);
+                }
+        }
+        for (uint32_t g = start; g < nseg; g++)
+            mp[g] = seg_lowmap(P + g * SEG_SYMS, C + g * SEG_SYMS, ck[g], seg_count(n, g));
+        uint64_t low = low0;
+        uint32_t off = off0;
+        for (uint32_t g = start; g < nseg; g++) {
+            lowat[g] = low;
+            offat[g] = off;
+            low = shl64(low, mp[g].s) + mp[g].B;
+            off += mp[g].nbytes;
+        }
+        int64_t sq = -1;
+        SegEnd sqe{};
+        for (uint32_t g = start; g < nseg; g++) {
+            const uint64_t room = cap > offat[g] ? cap - offat[g] : 0;
+            SegEnd e = seg_code(P + g * SEG_SYMS, C + g * SEG_SYMS, ck[g], lowat[g], seg_count(n, g), o + offat[g], room,
+                                g + 1 == nseg);
+            if (g + 1 == nseg) out_len = offat[g] + e.nbytes;
+            if (e.squeezed && sq < 0) { sq = g; sqe = e; }
+        }
+        if (sq < 0 || sq + 1 == (int64_t)nseg) return out_len;
+        restarts++;
+        start = (uint32_t)sq + 1;
+        r0 = sqe.r;
+        low0 = sqe.low;
+        off0 = offat[(size_t)sq] + sqe.nbytes;
+    }
+}
+
+// Coder-only check on synthetic record streams, including streams built to hit
+// the carry-less squeeze (the same symbol at probability 1/2 drives low towards
+// all-ones): decomposed == serial, and the restart path is exercised.
+static int coder_selftest()
+{
+    uint32_t x = 99;
+    auto rnd = [&]() { x = x * 1664525u + 1013904223u; return x >> 8; };
+    int restarts = 0, fails = 0;
+    for (int tc = 0; tc < 400; tc++) {
+        const uint32_t n = tc < 8 ? (uint32_t)tc : 1 + rnd() % 20000;
+        std::vector<PRec> P(n + 1);
+        std::vector<uint16_t> C(n + 1);
+        const int kind = tc % 4;
+        for (uint32_t i = 0; i < n; i++) {
+            uint32_t t, f, c;
+            if (kind == 0) { t = 2; f = 1; c = 1; }                                  // squeeze generator
+            else if (kind == 1) { t = 2 + rnd() % 0xffdf; f = 1 + rnd() % t; if (f > t) f = t; c = rnd() % (t - f + 1); }
+            else if (kind == 2) { t = 0xffe0; f = (rnd() & 1) ? 0xffd0 : 1; c = f == 1 ? 0xffdf : 0; }
+            else { t = 12 + rnd() % 240; f = 1 + rnd() % (t - 1); c = rnd() % (t - f + 1); }
+            P[i] = PRec{recip32(t), t | (f << 16)};
+            C[i] = (uint16_t)c;
+        }
+        const uint32_t cap = 2 * n + 64;
+        std::vector<uint8_t> a(cap), b(cap);
+        uint32_t la = code_decomposed(P.data(), C.data(), n, a.data(), cap, restarts);
+        SegEnd e = seg_code(P.data(), C.data(), 0xffffffffu, 0, n, b.data(), cap, true);
+        if (la != e.nbytes || std::memcmp(a.data(), b.data(), la)) fails++;
+    }
+    std::printf("%s coder self-test: %d fails, %d restarts\n", fails || !restarts ? "FAIL" : "OK", fails, restarts);
+    return fails || !restarts ? 1 : 0;
+}
+
 struct HostBlock {
     std::vector<uint8_t> names, seq, qual;
     std::vector<uint16_t> nl;
@@ -55,6 +135,7 @@ int main(int argc, char** argv)
         else if (!std::strcmp(argv[i], "-q") && i + 1 < argc) qlevel = std::atoi(argv[++i]);
         else in.push_back(argv[i]);
     }
+    if (in.size() == 1 && !std::strcmp(in[0], "--coder")) return coder_selftest();
     if (in.empty()) return 2;
     std::vector<uint8_t> t1 = slurp(in[0]), t2 = in.size() > 1 ? slurp(in[1]) : std::vector<uint8_t>();
     const bool pe = in.size() > 1;
@@ -194,30 +275,41 @@ int main(int argc, char** argv)
     sort_space(ak, av, bp.aux, AUX_SYM_BITS);
 
     // ---- replays ----
-    std::vector<uint64_t> recip(65536, 0);
-    for (uint32_t t = 2; t < 65536; t++) recip[t] = ~0ull / t + 1;
-    std::vector<Rec> rs(stot), ra(atot);
+    std::vector<uint32_t> rtab(65536, 0);
+    for (uint32_t t = 1; t < 65536; t++) rtab[t] = recip32(t);
+    std::vector<PRec> ps(stot), pa(atot);
+    std::vector<uint16_t> cs(stot), ca(atot);
     std::vector<uint32_t> F(256);
-    for (const SortSeg& g : bp.seq.segs)
+    for (const SortSeg& g : bp.seq.segs) {
+        const SymSink sink{ps.data() + g.base, cs.data() + g.base, rtab.data()};
         for (size_t i = g.base; i < g.base + g.count; i++)
-            if (i == g.base || sk[i - 1] != sk[i])
-                replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], rs.data() + g.base);
-    for (const SortSeg& g : bp.aux.segs)
+            if (i == g.base || sk[i - 1] != sk[i]) replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], sink);
+    }
+    for (const SortSeg& g : bp.aux.segs) {
+        const SymSink sink{pa.data() + g.base, ca.data() + g.base, rtab.data()};
         for (size_t i = g.base; i < g.base + g.count; i++)
             if (i == g.base || (ak[i - 1] >> AUX_SYM_BITS) != (ak[i] >> AUX_SYM_BITS))
-                err |= replay_simple_run(ak.data(), av.data(), i, g.base + g.count, ak[i] >> AUX_SYM_BITS,
-                                         ra.data() + g.base, F.data());
+                err |= replay_simple_run(ak.data(), av.data(), i, g.base + g.count, ak[i] >> AUX_SYM_BITS, sink, F.data());
+    }
     if (err) { std::printf("FAIL replay error bits %x\n", err); return 1; }
 
-    // ---- coders, md5, assembly ----
+    // ---- coders: the decomposed coder, checked against the serial one ----
     std::vector<uint8_t> payload(bp.payload_bytes + 16);
     std::vector<uint32_t> out_len(bp.tasks.size());
+    int restarts = 0;
     for (size_t t = 0; t < bp.tasks.size(); t++) {
         const CoderTask& tk = bp.tasks[t];
-        const Rec* R = (tk.space ? ra.data() : rs.data()) + tk.rec_base;
-        err |= code_stream(R, tk.n, recip.data(), payload.data() + tk.out_base, tk.out_cap, out_len[t]);
+        const PRec* P = (tk.space ? pa.data() : ps.data()) + tk.rec_base;
+        const uint16_t* C = (tk.space ? ca.data() : cs.data()) + tk.rec_base;
+        uint8_t* o = payload.data() + tk.out_base;
+        out_len[t] = code_decomposed(P, C, tk.n, o, tk.out_cap, restarts);
+        std::vector<uint8_t> ser(tk.out_cap);
+        SegEnd e = seg_code(P, C, 0xffffffffu, 0, tk.n, ser.data(), tk.out_cap, true);
+        if (e.nbytes != out_len[t] || std::memcmp(ser.data(), o, e.nbytes)) {
+            std::printf("FAIL decomposed coder differs from the serial coder (task %zu)\n", t);
+            return 1;
+        }
     }
-    if (err) { std::printf("FAIL coder error bits %x\n", err); return 1; }
     std::vector<uint32_t> digests((size_t)nb * 12);
     for (int64_t b = 0; b < nb; b++) {
         const DevBlock& d = blocks[(size_t)b];
@@ -251,7 +343,7 @@ int main(int argc, char** argv)
         }
         total_out += L;
     }
-    std::printf("%s blocks %lld reads %u out %llu bin_mode %d\n", fails ? "FAIL" : "OK", (long long)nb, nr,
-                (unsigned long long)total_out, T[0]);
+    std::printf("%s blocks %lld reads %u out %llu bin_mode %d coder restarts %d\n", fails ? "FAIL" : "OK", (long long)nb,
+                nr, (unsigned long long)total_out, T[0], restarts);
     return fails ? 1 : 0;
 }

@@ -42,6 +42,8 @@ def lib():
         l.orc_encode_block.restype = C.c_int64
         l.orc_analyze_idbin.argtypes = [P, C.c_int, P]
         l.orc_analyze_idbin.restype = C.c_int
+        l.orc_rc_encode.argtypes = [P, P, P, C.c_size_t, P, C.c_size_t]
+        l.orc_rc_encode.restype = C.c_int64
         l.orc_md5.argtypes = [P, C.c_size_t, P]
         l.orc_md5.restype = None
         _lib = l
@@ -79,3 +81,37 @@ def md5(data: bytes) -> bytes:
     d = np.zeros(16, dtype=np.uint8)
     lib().orc_md5(_p(a), a.size, _p(d))
     return d.tobytes()
+
+
+def rc_encode(cum: np.ndarray, freq: np.ndarray, tot: np.ndarray) -> bytes:
+    """The bare range coder over (cum, freq, tot) triples (uint16 arrays)."""
+    cum, freq, tot = (np.ascontiguousarray(a, dtype=np.uint16) for a in (cum, freq, tot))
+    cap = 2 * cum.size + 64
+    out = np.empty(cap, dtype=np.uint8)
+    n = lib().orc_rc_encode(_p(cum), _p(freq), _p(tot), cum.size, _p(out), cap)
+    if n < 0:
+        raise RuntimeError("oracle range coder rejected the records")
+    return out[:n].tobytes()
+
+
+def squeeze_streams(seed: int = 7, count: int = 12):
+    """(cum, freq, tot) streams for the coder tests: random models plus streams
+    that drive low towards all-ones (the same symbol at probability 1/2), which
+    fire the carry-less squeeze of the reference coder."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        n = int(rng.integers(1, 30000)) if i > 1 else i * 5
+        kind = i % 3
+        if kind == 0:
+            t = np.full(n, 2, np.uint16); f = np.ones(n, np.uint16); c = np.ones(n, np.uint16)
+        elif kind == 1:
+            t = rng.integers(2, 0xffe0, n, dtype=np.uint32)
+            f = np.maximum(1, (rng.random(n) * t).astype(np.uint32))
+            c = (rng.random(n) * (t - f + 1)).astype(np.uint32)
+        else:
+            t = rng.integers(12, 253, n, dtype=np.uint32)
+            f = np.maximum(1, (rng.random(n) * (t - 1)).astype(np.uint32))
+            c = (rng.random(n) * (t - f + 1)).astype(np.uint32)
+        out.append((c.astype(np.uint16), f.astype(np.uint16), t.astype(np.uint16)))
+    return out

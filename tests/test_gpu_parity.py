@@ -98,3 +98,13 @@ def test_rejects_out_of_model_quality(enc):
     bad = fq.parse_se(b"@r\nACGT\n+\nII\x7fI\n")
     with pytest.raises(fq.SeqArcError):
         enc.encode([bad], fq.Config())
+
+
+def test_coder_records_with_squeezes(enc):
+    """Bare coder on streams that fire the carry-less squeeze: the GPU decomposition
+    restarts those streams and still matches the serial reference coder."""
+    streams = oracle_py.squeeze_streams()
+    got = enc.code_records(streams)
+    assert enc.coder_restarts() > 0
+    for i, (s, g) in enumerate(zip(streams, got)):
+        assert g == oracle_py.rc_encode(*s), f"stream {i}"

@@ -100,3 +100,21 @@ def test_cpu_decomposition(tmp_path):
     for args in runs:
         r = subprocess.run([str(exe)] + args, capture_output=True, text=True)
         assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
+
+
+def test_coder_decomposition_selftest(tmp_path):
+    """Decomposed coder (pass R / L1 / L2 / L3 + squeeze restarts) == serial coder on the host."""
+    exe = tmp_path / "emu"
+    src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
+                    os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c")], check=True)
+    r = subprocess.run([str(exe), "--coder"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout
+
+
+def test_oracle_rc_squeeze_streams():
+    """The oracle's bare coder accepts the squeeze streams the GPU coder test uses."""
+    for c, f, t in oracle_py.squeeze_streams():
+        out = oracle_py.rc_encode(c, f, t)
+        assert len(out) >= 8
