@@ -279,7 +279,7 @@ __global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ key
 // ---------------------------------------------------------------------------
 constexpr int RP_THREADS = 64;
 constexpr int RP_STRIDE = 253;   // >= 256 - RP_REG entries, odd -> conflict-free
-constexpr uint32_t LONG_RUN = 2048;
+constexpr uint32_t LONG_RUN = 512;
 
 __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView sv, const uint32_t* __restrict__ keys,
                                                                  const uint32_t* __restrict__ vals,
@@ -307,62 +307,165 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView 
     if (e) atomicOr(err, e);
 }
 
+// k_replay_aux_long: one wave per long model run, 64 symbols per step.
+// Within a step the symbol order of the model only changes by the bubble swaps
+// (every 16th update of the model) and the frequencies only by +8 per
+// occurrence (a halving is made to fall on a step's last update), so for lane i
+// holding symbol s_i at position p_i:
+//     freq_i = F[s_i] + 8 * #{j < i : s_j = s_i}
+//     cum_i  = Cpre[p_i] + 8 * #{j < i : p_j < p_i}   (+ bubble corrections)
+//     tot_i  = Tot + 8 i
+// The counts come from one ballot per distinct symbol of the step.  Each bubble
+// event inside the step swaps at most one adjacent pair (x ahead of y); lanes
+// after it that hold y gain freq_x, lanes that hold x lose freq_y.  Model state
+// (symbol at position, position of symbol, freq of symbol, prefix by position)
+// lives in LDS.
 __global__ __launch_bounds__(64) void k_replay_aux_long(const LongRun* __restrict__ longs,
                                                         const uint32_t* __restrict__ nlong,
                                                         const uint32_t* __restrict__ keys,
                                                         const uint32_t* __restrict__ vals, const SymSink rec_all,
                                                         uint32_t* __restrict__ err)
 {
-    __shared__ uint32_t F[256];
+    __shared__ uint32_t ent[256], posof[256], fr[256], cpre[256];
     if (blockIdx.x >= *nlong) return;
     const LongRun lr = longs[blockIdx.x];
     const uint32_t lane = threadIdx.x;
     const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base, rec_all.rtab};
-    SModel m;
-    sm_init(m, model_nsym(lr.model), F, lane, 64);
-    __syncthreads();
-    auto load = [&](size_t j, uint32_t& k, uint32_t& v) {
-        if (j + lane < lr.end) {
-            k = keys[j + lane];
-            v = vals[j + lane];
-        } else {
-            k = SORT_PAD;
-            v = 0;
-        }
-    };
-    uint32_t k0, v0;
-    load(lr.start, k0, v0);
-    for (size_t j = lr.start; j < lr.end; j += 64) {
-        uint32_t k1, v1;
-        load(j + 64, k1, v1);
-        // the run is contiguous in the sorted keys: its symbols in this step are a lane prefix
-        const uint32_t cnt = (uint32_t)__popcll(__ballot((k0 >> AUX_SYM_BITS) == lr.model));
-        const uint32_t sym_v = k0 & 0xff;
-        uint32_t cfb = 0, tb = 0;
-        bool ok = true;
-        if (cnt == 64) {
-#pragma unroll 16
-            for (int q = 0; q < 64; q++) {
-                uint32_t cf, t;
-                ok &= sm_code(m, F, __builtin_amdgcn_readlane(sym_v, q), cf, t);
-                if (lane == (uint32_t)q) { cfb = cf; tb = t; }
-            }
-        } else {
-            for (uint32_t q = 0; q < cnt; q++) {
-                uint32_t cf, t;
-                ok &= sm_code(m, F, __builtin_amdgcn_readlane(sym_v, q), cf, t);
-                if (lane == (uint32_t)q) { cfb = cf; tb = t; }
-            }
-        }
-        if (!ok) {
-            if (lane == 0) atomicOr(err, (uint32_t)E_CODER);
-            return;
-        }
-        if (lane < cnt) sink_put(rec, v0, cfb & 0xffff, cfb >> 16, tb);
-        if (cnt < 64) break;
-        k0 = k1;
-        v0 = v1;
+    const uint32_t N = model_nsym(lr.model);
+    for (uint32_t k = lane; k < 256; k += 64) {
+        ent[k] = k;
+        posof[k] = k;
+        fr[k] = k < N ? 1u : 0u;
+        cpre[k] = k < N ? k : N;
     }
+    __syncthreads();
+    const uint64_t before = (1ull << lane) - 1ull;
+    uint32_t tot = N, bub = 0;
+    bool bad = false;
+    for (size_t base = lr.start; base < lr.end;) {
+        uint32_t key = SORT_PAD, pos = 0;
+        if (base + lane < lr.end) {
+            key = keys[base + lane];
+            pos = vals[base + lane];
+        }
+        const bool in_run = (key >> AUX_SYM_BITS) == lr.model;
+        uint32_t c = (uint32_t)__popcll(__ballot(in_run));   // the run is a lane prefix
+        if (c == 0) break;
+        // cut the step so that a halving (tot > 0xffe0 after an update) falls on its last update
+        const uint32_t to_halve = (0xffe0u - tot) / 8u + 1u;
+        bool halve = false;
+        if (to_halve <= c) {
+            c = to_halve;
+            halve = true;
+        }
+        const bool act = lane < c;
+        const uint64_t amask = c == 64 ? ~0ull : ((1ull << c) - 1ull);
+        const uint32_t sym = key & 0xffu;
+        if (act && sym >= N) bad = true;
+        const uint32_t p = act ? posof[sym] : 0u;
+        const uint32_t f0 = act ? fr[sym] : 0u;
+        int32_t cum = act ? (int32_t)cpre[p] : 0;
+        uint32_t same = 0, less = 0;
+        // one ballot per distinct symbol of the step
+        uint64_t rem = amask;
+        while (rem) {
+            const uint32_t fl = (uint32_t)__builtin_ctzll(rem);
+            const uint32_t x = __builtin_amdgcn_readlane(sym, fl);
+            const uint32_t px = __builtin_amdgcn_readlane(p, fl);
+            const uint64_t m = __ballot(act && sym == x);
+            const uint32_t below = (uint32_t)__popcll(m & before);
+            if (sym == x) same = below;
+            else if (px < p) less += below;
+            rem &= ~m;
+        }
+        cum += (int32_t)(8u * less);
+        // bubble events inside the step (the one on its last update comes after the state update)
+        uint32_t b = 15u - (bub & 15u);
+        for (; b + 1 < c; b += 16) {
+            const uint32_t x = __builtin_amdgcn_readlane(sym, b);
+            const uint32_t P = posof[x];
+            if (P == 0) continue;
+            const uint32_t y = ent[P - 1];
+            const uint64_t mx = __ballot(act && sym == x), my = __ballot(act && sym == y);
+            const uint64_t upto = (2ull << b) - 1ull;
+            const uint32_t fx = fr[x] + 8u * (uint32_t)__popcll(mx & upto);
+            const uint32_t fy = fr[y] + 8u * (uint32_t)__popcll(my & upto);
+            if (fx > fy) {
+                __syncthreads();
+                if (lane == 0) {
+                    ent[P - 1] = x;
+                    ent[P] = y;
+                    posof[x] = P - 1;
+                    posof[y] = P;
+                }
+                __syncthreads();
+                if (lane > b) {
+                    if (sym == y) cum += (int32_t)(fr[x] + 8u * (uint32_t)__popcll(mx & before));
+                    else if (sym == x) cum -= (int32_t)(fr[y] + 8u * (uint32_t)__popcll(my & before));
+                }
+            }
+        }
+        if (act) {
+            const uint32_t f = f0 + 8u * same;
+            const uint32_t t = tot + 8u * lane;
+            if (cum < 0 || (uint32_t)cum + f > t || f == 0) bad = true;
+            sink_put(rec, pos, (uint32_t)cum & 0xffffu, f, t);
+        }
+        // state update: frequencies, total, bubble counter, halving
+        __syncthreads();
+        rem = amask;
+        while (rem) {
+            const uint32_t fl = (uint32_t)__builtin_ctzll(rem);
+            const uint32_t x = __builtin_amdgcn_readlane(sym, fl);
+            const uint64_t m = __ballot(act && sym == x);
+            if (lane == fl) fr[x] += 8u * (uint32_t)__popcll(m);
+            rem &= ~m;
+        }
+        __syncthreads();
+        tot += 8u * c;
+        bub += c;
+        if (halve) {
+            uint32_t part = 0;
+            for (uint32_t k = lane; k < N; k += 64) {
+                const uint32_t v = fr[k];
+                fr[k] = v - (v >> 1);
+                part += v - (v >> 1);
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
+            tot = part;
+        }
+        __syncthreads();
+        if ((bub & 15u) == 0) {   // the step's last update was a bubble event
+            const uint32_t x = __builtin_amdgcn_readlane(sym, c - 1);
+            const uint32_t P = posof[x];
+            if (P > 0) {
+                const uint32_t y = ent[P - 1];
+                if (fr[x] > fr[y]) {
+                    __syncthreads();
+                    if (lane == 0) {
+                        ent[P - 1] = x;
+                        ent[P] = y;
+                        posof[x] = P - 1;
+                        posof[y] = P;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // prefix of frequencies by position
+        uint32_t carry = 0;
+        for (uint32_t k0 = 0; k0 < N; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const uint32_t v = k < N ? fr[ent[k]] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (k < N) cpre[k] = carry + inc - v;
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+        __syncthreads();
+        base += c;
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(err, (uint32_t)E_CODER);
 }
 
 // ---------------------------------------------------------------------------
