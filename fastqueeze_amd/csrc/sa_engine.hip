@@ -41,8 +41,11 @@ struct DBuf {
     }
 };
 
-const char* kPhaseNames[] = {"prep+scan", "emit", "sort_seq", "sort_aux", "replay_seq", "replay_aux",
-                             "coder_r", "coder_l", "md5", "assemble", "total"};
+// Device time of each phase of the last sa_run, from HIP events on the stream
+// the phase runs on.  MD5 runs on its own stream concurrently with the
+// others; "total" is the wall time of the whole batch.
+const char* kPhaseNames[] = {"prep+scan", "emit", "sort_seq", "sort_aux", "replay_seq", "replay_aux", "coder_r",
+                             "coder_l", "md5", "assemble", "total"};
 enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX, PH_CODER_R, PH_CODER_L, PH_MD5,
        PH_ASM, PH_TOTAL, PH_N };
 
@@ -50,7 +53,8 @@ enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX,
 
 struct sa_ctx {
     int device = 0;
-    hipStream_t st = nullptr, st2 = nullptr;
+    hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;   // main/AUX, MD5, SEQ
+    hipEvent_t ev_fork = nullptr, ev_seq_done = nullptr, ev_md5_done = nullptr, ev_r[2] = {nullptr, nullptr};
     std::string err;
     bool timing = false;
     uint32_t coder_restarts = 0;
@@ -70,8 +74,9 @@ struct sa_ctx {
     DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
-    DBuf d_rtab, d_longs, d_nlong;
-    DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq, d_list_ids, d_list_gbase, d_list_run;
+    DBuf d_longs, d_nlong;
+    DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
+    DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
 
     // last run
@@ -86,15 +91,19 @@ struct sa_ctx {
                        &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
                        &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
-                       &d_final_len, &d_rtab, &d_longs, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                       &d_first_sq, &d_list_ids, &d_list_gbase, &d_list_run};
+                       &d_final_len, &d_longs, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                       &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
+                       &d_list_gbase[1], &d_list_run[1]};
         for (DBuf* b : all) b->release();
         for (int i = 0; i < PH_N; i++) {
             if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
             if (ev_end[i]) (void)hipEventDestroy(ev_end[i]);
         }
+        for (hipEvent_t e : {ev_fork, ev_seq_done, ev_md5_done, ev_r[0], ev_r[1]})
+            if (e) (void)hipEventDestroy(e);
         if (st) (void)hipStreamDestroy(st);
         if (st2) (void)hipStreamDestroy(st2);
+        if (st3) (void)hipStreamDestroy(st3);
     }
 };
 
@@ -140,92 +149,143 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
 void ev_begin(sa_ctx* c, int ph, hipStream_t st);
 void ev_finish(sa_ctx* c, int ph, hipStream_t st);
 
-// Range-codes every task (DESIGN.md "Coder"): pass R, L1, L2, L3, then
-// restarts the streams whose exact coding squeezed before their last segment,
-// from the state L3 computed, until none does.  cv: tasks/records/out/out_len set
-// by the caller; the segment arrays are this context's.
-int coder_run(sa_ctx* c, hipStream_t st, const std::vector<CoderTask>& tasks, uint64_t total_segs, CoderView cv)
+// Range coder driver (DESIGN.md "Coder").  A group = a contiguous range of
+// tasks coded on one stream: pass R, L1, L2, L3.  After all groups of a round
+// finish, the streams whose exact coding squeezed before their last segment
+// restart after that segment from the state L3 computed (on the first group's
+// stream), until none does.
+struct CoderGroup {
+    hipStream_t st;
+    uint32_t t0, t1;
+    int ph_r, ph_l;   // phase slots for the first round (-1: untimed)
+};
+
+int coder_buffers(sa_ctx* c, size_t ntasks, uint64_t total_segs, CoderView& cv)
 {
-    if (tasks.empty()) return 0;
     const uint64_t nsegs = std::max<uint64_t>(total_segs, 1);
     SA_CHECK(c, c->d_ck.ensure(nsegs * 4));
     SA_CHECK(c, c->d_maps.ensure(nsegs * sizeof(LowMap)));
     SA_CHECK(c, c->d_low_at.ensure(nsegs * 8));
     SA_CHECK(c, c->d_off_at.ensure(nsegs * 4));
-    SA_CHECK(c, c->d_first_sq.ensure(4 * tasks.size()));
-    SA_CHECK(c, c->d_list_ids.ensure(4 * tasks.size()));
-    SA_CHECK(c, c->d_list_gbase.ensure(8 * (tasks.size() + 1)));
-    SA_CHECK(c, c->d_list_run.ensure(sizeof(CoderRun) * tasks.size()));
+    SA_CHECK(c, c->d_first_sq.ensure(4 * std::max<size_t>(ntasks, 1)));
+    for (int g = 0; g < 2; g++) {
+        SA_CHECK(c, c->d_list_ids[g].ensure(4 * std::max<size_t>(ntasks, 1)));
+        SA_CHECK(c, c->d_list_gbase[g].ensure(8 * (ntasks + 1)));
+        SA_CHECK(c, c->d_list_run[g].ensure(sizeof(CoderRun) * std::max<size_t>(ntasks, 1)));
+    }
     cv.ck_r = c->d_ck.as<uint32_t>();
     cv.maps = c->d_maps.as<LowMap>();
     cv.low_at = c->d_low_at.as<uint64_t>();
     cv.off_at = c->d_off_at.as<uint32_t>();
     cv.first_sq = c->d_first_sq.as<uint32_t>();
-    SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
-    std::vector<uint32_t> ids(tasks.size());
-    std::vector<CoderRun> runs(tasks.size());
-    std::vector<uint64_t> gbase(tasks.size() + 1);
-    for (size_t i = 0; i < tasks.size(); i++) {
-        ids[i] = (uint32_t)i;
-        runs[i] = CoderRun{0ull, 0xffffffffu, 0u, 0u, 0u};
+    return 0;
+}
+
+// Uploads the list of one round (tasks ids + start states) into list slot `slot`.
+int coder_list(sa_ctx* c, hipStream_t st, int slot, const std::vector<CoderTask>& tasks,
+               const std::vector<uint32_t>& ids, const std::vector<CoderRun>& runs, std::vector<uint64_t>& gbase,
+               TaskList& tl)
+{
+    const size_t cnt = ids.size();
+    gbase.assign(cnt + 1, 0);
+    for (size_t i = 0; i < cnt; i++) gbase[i + 1] = gbase[i] + (tasks[ids[i]].nseg - runs[i].start_seg);
+    if (cnt) {
+        SA_CHECK(c, hipMemcpyAsync(c->d_list_ids[slot].p, ids.data(), 4 * cnt, hipMemcpyHostToDevice, st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_list_gbase[slot].p, gbase.data(), 8 * (cnt + 1), hipMemcpyHostToDevice, st));
+        SA_CHECK(c, hipMemcpyAsync(c->d_list_run[slot].p, runs.data(), sizeof(CoderRun) * cnt, hipMemcpyHostToDevice,
+                                   st));
     }
-    std::vector<uint32_t> first_sq(tasks.size()), out_len(tasks.size());
+    tl = TaskList{c->d_list_ids[slot].as<uint32_t>(), c->d_list_gbase[slot].as<uint64_t>(),
+                  c->d_list_run[slot].as<CoderRun>(), (uint32_t)cnt, 0u, gbase[cnt]};
+    return 0;
+}
+
+void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv, int ph)
+{
+    if (!tl.count) return;
+    if (ph >= 0) ev_begin(c, ph, st);
+    hipLaunchKernelGGL(k_coder_r, dim3(tl.count), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r);
+    if (ph >= 0) ev_finish(c, ph, st);
+}
+
+void coder_launch_l(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv, int ph)
+{
+    if (!tl.count) return;
+    const uint32_t lgrid = (uint32_t)((tl.total_segs + 255) / 256);
+    if (ph >= 0) ev_begin(c, ph, st);
+    hipLaunchKernelGGL(k_coder_l1, dim3(lgrid), dim3(256), 0, st, cv, tl);
+    hipLaunchKernelGGL(k_coder_l2, dim3(tl.count), dim3(L2_THREADS), 0, st, cv, tl);
+    hipLaunchKernelGGL(k_coder_l3, dim3(lgrid), dim3(256), 0, st, cv, tl);
+    if (ph >= 0) ev_finish(c, ph, st);
+}
+
+// Runs pass R of every group concurrently (each group's stream must already be
+// ordered after that group's records), then -- once every pass R is done, so
+// that the parallel L passes never share the GPU with a latency-bound chain --
+// the L passes of every group; then the restarts.  On return every stream of
+// every group is coded and all group streams are idle.
+int coder_run(sa_ctx* c, const std::vector<CoderTask>& tasks, const CoderView& cv, const CoderGroup* groups,
+              int ngroups)
+{
+    if (tasks.empty()) return 0;
     c->coder_restarts = 0;
-    for (int round = 0;; round++) {
-        const size_t cnt = ids.size();
-        gbase[0] = 0;
-        for (size_t i = 0; i < cnt; i++) gbase[i + 1] = gbase[i] + (tasks[ids[i]].nseg - runs[i].start_seg);
-        SA_CHECK(c, hipMemcpyAsync(c->d_list_ids.p, ids.data(), 4 * cnt, hipMemcpyHostToDevice, st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_list_gbase.p, gbase.data(), 8 * (cnt + 1), hipMemcpyHostToDevice, st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_list_run.p, runs.data(), sizeof(CoderRun) * cnt, hipMemcpyHostToDevice, st));
-        TaskList tl{c->d_list_ids.as<uint32_t>(), c->d_list_gbase.as<uint64_t>(), c->d_list_run.as<CoderRun>(),
-                    (uint32_t)cnt, 0u, gbase[cnt]};
-        const uint32_t lgrid = (uint32_t)((gbase[cnt] + 255) / 256);
-        if (round == 0) ev_begin(c, PH_CODER_R, st);
-        hipLaunchKernelGGL(k_coder_r, dim3((uint32_t)cnt), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r);
-        if (round == 0) ev_finish(c, PH_CODER_R, st);
-        if (round == 0) ev_begin(c, PH_CODER_L, st);
-        hipLaunchKernelGGL(k_coder_l1, dim3(lgrid), dim3(256), 0, st, cv, tl);
-        hipLaunchKernelGGL(k_coder_l2, dim3((uint32_t)cnt), dim3(L2_THREADS), 0, st, cv, tl);
-        hipLaunchKernelGGL(k_coder_l3, dim3(lgrid), dim3(256), 0, st, cv, tl);
-        if (round == 0) ev_finish(c, PH_CODER_L, st);
+    std::vector<uint64_t> gb[2];
+    TaskList tl[2];
+    for (int g = 0; g < ngroups; g++) {
+        std::vector<uint32_t> ids;
+        std::vector<CoderRun> runs;
+        for (uint32_t t = groups[g].t0; t < groups[g].t1; t++) ids.push_back(t);
+        // longest streams first: workgroups are dealt round-robin over the XCDs and
+        // their CUs, so the long chains get CUs of their own
+        std::stable_sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t b) { return tasks[a].n > tasks[b].n; });
+        runs.assign(ids.size(), CoderRun{0ull, 0xffffffffu, 0u, 0u, 0u});
+        if (coder_list(c, groups[g].st, g, tasks, ids, runs, gb[g], tl[g])) return -1;
+        coder_launch_r(c, groups[g].st, tl[g], cv, c->timing ? groups[g].ph_r : -1);
+        SA_CHECK(c, hipEventRecord(c->ev_r[g], groups[g].st));
+    }
+    for (int g = 0; g < ngroups; g++) {
+        for (int h = 0; h < ngroups; h++)
+            if (h != g) SA_CHECK(c, hipStreamWaitEvent(groups[g].st, c->ev_r[h], 0));
+        coder_launch_l(c, groups[g].st, tl[g], cv, c->timing ? groups[g].ph_l : -1);
         SA_CHECK(c, hipGetLastError());
-        SA_CHECK(c, hipMemcpyAsync(first_sq.data(), c->d_first_sq.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
-        SA_CHECK(c, hipMemcpyAsync(out_len.data(), c->d_out_len.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
+    }
+    for (int g = 0; g < ngroups; g++) SA_CHECK(c, hipStreamSynchronize(groups[g].st));
+    hipStream_t st = groups[0].st;
+    std::vector<uint32_t> first_sq(tasks.size()), out_len(tasks.size());
+    for (int round = 0;; round++) {
+        SA_CHECK(c, hipMemcpyAsync(first_sq.data(), cv.first_sq, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(out_len.data(), cv.out_len, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
         SA_CHECK(c, hipStreamSynchronize(st));
-        // streams whose first squeeze is not in their last segment restart after it
-        std::vector<uint32_t> nids;
-        std::vector<CoderRun> nruns;
+        std::vector<uint32_t> ids;
+        std::vector<CoderRun> runs;
         for (size_t t = 0; t < tasks.size(); t++) {
             const uint32_t k = first_sq[t];
             if (k == 0xffffffffu || k + 1 >= tasks[t].nseg) continue;
             LowMap endst;
             uint32_t off;
-            SA_CHECK(c, hipMemcpy(&endst, c->d_maps.as<LowMap>() + tasks[t].seg_base + k, sizeof endst,
-                                  hipMemcpyDeviceToHost));
-            SA_CHECK(c, hipMemcpy(&off, c->d_off_at.as<uint32_t>() + tasks[t].seg_base + k, 4, hipMemcpyDeviceToHost));
-            nids.push_back((uint32_t)t);
-            nruns.push_back(CoderRun{endst.B, endst.s, k + 1, off + endst.nbytes, 0u});
+            SA_CHECK(c, hipMemcpy(&endst, cv.maps + tasks[t].seg_base + k, sizeof endst, hipMemcpyDeviceToHost));
+            SA_CHECK(c, hipMemcpy(&off, cv.off_at + tasks[t].seg_base + k, 4, hipMemcpyDeviceToHost));
+            ids.push_back((uint32_t)t);
+            runs.push_back(CoderRun{endst.B, endst.s, k + 1, off + endst.nbytes, 0u});
             const uint32_t none = 0xffffffffu;
-            SA_CHECK(c, hipMemcpy(c->d_first_sq.as<uint32_t>() + t, &none, 4, hipMemcpyHostToDevice));
+            SA_CHECK(c, hipMemcpy(cv.first_sq + t, &none, 4, hipMemcpyHostToDevice));
         }
-        if (nids.empty()) {
-            for (size_t t = 0; t < tasks.size(); t++)
-                if (out_len[t] > tasks[t].out_cap) {
-                    c->err = "range coder output overflowed its buffer";
-                    return -1;
-                }
-            break;
-        }
+        if (ids.empty()) break;
         if (round > 1000) {
             c->err = "range coder: too many restarts";
             return -1;
         }
-        c->coder_restarts += (uint32_t)nids.size();
-        ids.swap(nids);
-        runs.swap(nruns);
+        c->coder_restarts += (uint32_t)ids.size();
+        if (coder_list(c, st, 0, tasks, ids, runs, gb[0], tl[0])) return -1;
+        coder_launch_r(c, st, tl[0], cv, -1);
+        coder_launch_l(c, st, tl[0], cv, -1);
+        SA_CHECK(c, hipGetLastError());
     }
-
+    for (size_t t = 0; t < tasks.size(); t++)
+        if (out_len[t] > tasks[t].out_cap) {
+            c->err = "range coder output overflowed its buffer";
+            return -1;
+        }
     return 0;
 }
 
@@ -260,7 +320,13 @@ sa_ctx* sa_create(int device)
     c->device = device;
     for (int i = 0; i < PH_N; i++) c->ev_beg[i] = c->ev_end[i] = nullptr;
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_seq_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_md5_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_r[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_r[1], hipEventDisableTiming) != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -269,14 +335,6 @@ sa_ctx* sa_create(int device)
             delete c;
             return nullptr;
         }
-    }
-    // reciprocal table m = ceil(2^32 / t), t < 65536 (tot of any model <= 0xffe0)
-    std::vector<uint32_t> rtab(65536, 0);
-    for (uint32_t t = 1; t < 65536; t++) rtab[t] = recip32(t);
-    if (c->d_rtab.ensure(rtab.size() * 4) != hipSuccess ||
-        hipMemcpy(c->d_rtab.p, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-        delete c;
-        return nullptr;
     }
     return c;
 }
@@ -450,6 +508,31 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     uint32_t* d_err = c->d_err.as<uint32_t>();
 
     ev_begin(c, PH_TOTAL, st);
+    // ---- MD5 of every block's IDs/bases/quals (calcBlockMd5@0x414d90) on st2,
+    //      concurrent with everything up to the assembly ----
+    std::vector<Md5Task> md5t;
+    for (uint32_t b = 0; b < nbk; b++) {
+        const DevBlock& d = c->blocks[b];
+        md5t.push_back(Md5Task{c->d_names.as<uint8_t>() + d.name_base, d.name_bytes});
+        md5t.push_back(Md5Task{c->d_seq.as<uint8_t>() + d.seq_base, d.seq_bytes});
+        md5t.push_back(Md5Task{c->d_qual.as<uint8_t>() + d.seq_base, d.seq_bytes});
+    }
+    if (cfg->md5) {
+        SA_CHECK(c, c->d_md5tasks.ensure(sizeof(Md5Task) * md5t.size()));
+        SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
+        SA_CHECK(c, hipEventRecord(c->ev_fork, st));
+        SA_CHECK(c, hipStreamWaitEvent(c->st2, c->ev_fork, 0));
+        SA_CHECK(c, hipMemcpyAsync(c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), hipMemcpyHostToDevice,
+                                   c->st2));
+        ev_begin(c, PH_MD5, c->st2);
+        hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(64), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
+                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>());
+        ev_finish(c, PH_MD5, c->st2);
+        SA_CHECK(c, hipGetLastError());
+        SA_CHECK(c, hipEventRecord(c->ev_md5_done, c->st2));
+    } else {
+        SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
+    }
     ev_begin(c, PH_PREP, st);
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
@@ -484,23 +567,8 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     const std::vector<uint64_t>& task_out_base = bp.task_out_base;
     const std::vector<AsmBlock>& asmb = bp.asmb;
     const uint64_t payload = bp.payload_bytes, final_bytes = bp.final_bytes;
-    std::vector<Md5Task> md5t;
     c->final_base.assign(nbk, 0);
-    for (uint32_t b = 0; b < nbk; b++) {
-        const DevBlock& d = c->blocks[b];
-        c->final_base[b] = asmb[b].out_base;
-        for (int f = 0; f < 3; f++) {
-            Md5Task m{};
-            if (f == 0) {
-                m.ptr = c->d_names.as<uint8_t>() + d.name_base;
-                m.len = d.name_bytes;
-            } else {
-                m.ptr = (f == 1 ? c->d_seq.as<uint8_t>() : c->d_qual.as<uint8_t>()) + d.seq_base;
-                m.len = d.seq_bytes;
-            }
-            md5t.push_back(m);
-        }
-    }
+    for (uint32_t b = 0; b < nbk; b++) c->final_base[b] = asmb[b].out_base;
 
     // ---- device buffers ----
     // slack: the replay loops read up to 2 chunks past a run's end, pass R one
@@ -528,8 +596,6 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     SA_CHECK(c, c->d_tasks.ensure(sizeof(CoderTask) * tasks.size()));
     SA_CHECK(c, c->d_out_len.ensure(4 * tasks.size()));
     SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
-    SA_CHECK(c, c->d_md5tasks.ensure(sizeof(Md5Task) * md5t.size()));
-    SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
     SA_CHECK(c, c->d_asm.ensure(sizeof(AsmBlock) * nbk));
     SA_CHECK(c, c->d_task_out_base.ensure(8 * task_out_base.size()));
     SA_CHECK(c, c->d_final.ensure(std::max<uint64_t>(final_bytes, 16)));
@@ -543,31 +609,27 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     if (!pa.tile_seg.empty())
         SA_CHECK(c, hipMemcpyAsync(c->d_tile_aux.p, pa.tile_seg.data(), pa.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
     SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), hipMemcpyHostToDevice, st));
     SA_CHECK(c, hipMemcpyAsync(c->d_asm.p, asmb.data(), sizeof(AsmBlock) * nbk, hipMemcpyHostToDevice, st));
     SA_CHECK(c, hipMemcpyAsync(c->d_task_out_base.p, task_out_base.data(), 8 * task_out_base.size(),
                                hipMemcpyHostToDevice, st));
 
-    // ---- MD5 on the second stream (inputs only) ----
-    if (cfg->md5) {
-        hipEvent_t ready;
-        SA_CHECK(c, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        SA_CHECK(c, hipEventRecord(ready, st));
-        SA_CHECK(c, hipStreamWaitEvent(c->st2, ready, 0));
-        (void)hipEventDestroy(ready);
-        ev_begin(c, PH_MD5, c->st2);
-        hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(64), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
-                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>());
-        ev_finish(c, PH_MD5, c->st2);
-        SA_CHECK(c, hipGetLastError());
-    }
+    CoderView cv{};
+    cv.tasks = c->d_tasks.as<CoderTask>();
+    cv.prs[0] = c->d_prs_seq.as<PRec>();
+    cv.prs[1] = c->d_prs_aux.as<PRec>();
+    cv.cum[0] = c->d_cum_seq.as<uint16_t>();
+    cv.cum[1] = c->d_cum_aux.as<uint16_t>();
+    cv.out = c->d_payload.as<uint8_t>();
+    cv.out_len = c->d_out_len.as<uint32_t>();
+    if (coder_buffers(c, tasks.size(), bp.total_segs, cv)) return -1;
 
-    // ---- emit ----
+    // ---- emit (main stream) ----
     ev_begin(c, PH_EMIT, st);
     SA_CHECK(c, hipMemsetAsync(c->d_seq_k[0].p, 0xff, stot * 4, st));
     SA_CHECK(c, hipMemsetAsync(c->d_aux_k[0].p, 0xff, atot * 4, st));
     SA_CHECK(c, hipMemsetAsync(c->d_seq_k[1].p, 0xff, stot * 4, st));
     SA_CHECK(c, hipMemsetAsync(c->d_aux_k[1].p, 0xff, atot * 4, st));
+    SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
     if (nr) {
         hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
                            c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), c->d_maxlen.as<uint16_t>(),
@@ -576,8 +638,15 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);
+    SortView svs{c->d_segs_seq.as<SortSeg>(), c->d_tile_seq.as<uint32_t>(), c->d_hist_seq.as<uint32_t>(),
+                 ps.total, (uint32_t)ps.tile_seg.size(), nbk};
+    SortView sva{c->d_segs_aux.as<SortSeg>(), c->d_tile_aux.as<uint32_t>(), c->d_hist_aux.as<uint32_t>(),
+                 pa.total, (uint32_t)pa.tile_seg.size(), nbk};
+    const SymSink sink_seq{c->d_prs_seq.as<PRec>(), c->d_cum_seq.as<uint16_t>()};
+    const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>()};
 
-    // ---- sorts ----
+    // ---- throughput phases, one after the other on st (each fills the GPU):
+    //      sorts, BASE_MODEL replay, short SIMPLE_MODEL runs ----
     ev_begin(c, PH_SORT_SEQ, st);
     if (run_sort(c, st, ps, c->d_segs_seq, c->d_tile_seq, c->d_hist_seq, c->d_seq_k, c->d_seq_v, 0,
                  ns > 1 ? seq_bits : 0, c->seq_sorted_buf))
@@ -588,14 +657,6 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
                  AUX_SYM_BITS + aux_bits, c->aux_sorted_buf))
         return -1;
     ev_finish(c, PH_SORT_AUX, st);
-
-    // ---- replays ----
-    SortView svs{c->d_segs_seq.as<SortSeg>(), c->d_tile_seq.as<uint32_t>(), c->d_hist_seq.as<uint32_t>(),
-                 ps.total, (uint32_t)ps.tile_seg.size(), nbk};
-    SortView sva{c->d_segs_aux.as<SortSeg>(), c->d_tile_aux.as<uint32_t>(), c->d_hist_aux.as<uint32_t>(),
-                 pa.total, (uint32_t)pa.tile_seg.size(), nbk};
-    const SymSink sink_seq{c->d_prs_seq.as<PRec>(), c->d_cum_seq.as<uint16_t>(), c->d_rtab.as<uint32_t>()};
-    const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>(), c->d_rtab.as<uint32_t>()};
     ev_begin(c, PH_REPLAY_SEQ, st);
     if (ps.total)
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)((ps.total + 255) / 256)), dim3(256), 0, st, svs,
@@ -603,41 +664,33 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
                            sink_seq);
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_REPLAY_AUX, st);
-    if (pa.total) {
-        SA_CHECK(c, hipMemsetAsync(c->d_nlong.p, 0, 4, st));
-        const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();
-        const uint32_t* av = c->d_aux_v[c->aux_sorted_buf].as<uint32_t>();
+    const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();
+    const uint32_t* av = c->d_aux_v[c->aux_sorted_buf].as<uint32_t>();
+    SA_CHECK(c, hipMemsetAsync(c->d_nlong.p, 0, 4, st));
+    if (pa.total)
         hipLaunchKernelGGL(k_replay_aux_short, dim3((uint32_t)((pa.total + RP_THREADS - 1) / RP_THREADS)),
                            dim3(RP_THREADS), 0, st, sva, ak, av, sink_aux, c->d_longs.as<LongRun>(),
                            c->d_nlong.as<uint32_t>(), d_err);
-        hipLaunchKernelGGL(k_replay_aux_long, dim3((uint32_t)max_long), dim3(64), 0, st, c->d_longs.as<LongRun>(),
+    // ---- latency-bound phases: long SIMPLE_MODEL runs, then every coder chain
+    //      in one launch (concurrent latency-bound launches land on shared SIMDs) ----
+    if (pa.total) {
+        hipLaunchKernelGGL(k_replay_aux_long, dim3((uint32_t)max_long), dim3(128), 0, st, c->d_longs.as<LongRun>(),
                            c->d_nlong.as<uint32_t>(), ak, av, sink_aux, d_err);
+        hipLaunchKernelGGL(k_fill_recip, dim3((uint32_t)((pa.total + 255) / 256)), dim3(256), 0, st, sva,
+                           c->d_prs_aux.as<PRec>());
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_AUX, st);
 
-    // ---- range coders ----
-    CoderView cv{};
-    cv.tasks = c->d_tasks.as<CoderTask>();
-    cv.prs[0] = c->d_prs_seq.as<PRec>();
-    cv.prs[1] = c->d_prs_aux.as<PRec>();
-    cv.cum[0] = c->d_cum_seq.as<uint16_t>();
-    cv.cum[1] = c->d_cum_aux.as<uint16_t>();
-    cv.out = c->d_payload.as<uint8_t>();
-    cv.out_len = c->d_out_len.as<uint32_t>();
-    if (coder_run(c, st, tasks, bp.total_segs, cv)) return -1;
+    // ---- range coders: SEQ tasks [0, nbk) on st3, AUX tasks on st ----
+    const CoderGroup group{st, 0u, (uint32_t)tasks.size(), PH_CODER_R, PH_CODER_L};
+    if (coder_run(c, tasks, cv, &group, 1)) return -1;
 
-    // ---- assembly ----
-    if (cfg->md5) {
-        hipEvent_t done;
-        SA_CHECK(c, hipEventCreateWithFlags(&done, hipEventDisableTiming));
-        SA_CHECK(c, hipEventRecord(done, c->st2));
-        SA_CHECK(c, hipStreamWaitEvent(st, done, 0));
-        (void)hipEventDestroy(done);
-    }
+    // ---- assembly (after MD5) ----
+    if (cfg->md5) SA_CHECK(c, hipStreamWaitEvent(st, c->ev_md5_done, 0));
     ev_begin(c, PH_ASM, st);
-    AsmView av{c->d_asm.as<AsmBlock>(), c->d_task_out_base.as<uint64_t>()};
-    hipLaunchKernelGGL(k_assemble, dim3(nbk), dim3(256), 0, st, bv, av, c->d_payload.as<uint8_t>(),
+    AsmView asv{c->d_asm.as<AsmBlock>(), c->d_task_out_base.as<uint64_t>()};
+    hipLaunchKernelGGL(k_assemble, dim3(nbk), dim3(256), 0, st, bv, asv, c->d_payload.as<uint8_t>(),
                        c->d_out_len.as<uint32_t>(), c->d_digests.as<uint32_t>(), c->d_final.as<uint8_t>(),
                        c->d_final_len.as<uint64_t>());
     SA_CHECK(c, hipGetLastError());
@@ -750,7 +803,10 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
     cv.out = c->d_payload.as<uint8_t>();
     cv.out_len = c->d_out_len.as<uint32_t>();
     c->have_output = false;
-    if (coder_run(c, st, tasks, segs, cv)) return -1;
+    if (coder_buffers(c, tasks.size(), segs, cv)) return -1;
+    SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * std::max<size_t>(tasks.size(), 1), st));
+    const CoderGroup group{st, 0u, (uint32_t)tasks.size(), -1, -1};
+    if (coder_run(c, tasks, cv, &group, 1)) return -1;
     std::vector<uint32_t> ol(tasks.size());
     if (!tasks.empty())
         SA_CHECK(c, hipMemcpyAsync(ol.data(), c->d_out_len.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));

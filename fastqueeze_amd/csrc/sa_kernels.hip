@@ -33,6 +33,19 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v)
     return v;
 }
 
+// inclusive add-scan of a wave64 on DPP (row shifts, then row broadcasts 15/31):
+// register-to-register, no LDS round trip
+__device__ inline uint32_t wave_incl_scan_dpp(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
 // exclusive scan across a 1024-thread workgroup; returns the workgroup total
 __device__ inline uint32_t wg1024_excl_scan(uint32_t v, uint32_t& excl, uint32_t* sh /*16*/)
 {
@@ -264,7 +277,7 @@ __global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ key
     const uint32_t key = keys[i];
     if (key == SORT_PAD) return;
     if (i != sg.base && keys[i - 1] == key) return;
-    replay_seq_run(keys, vals, i, sg.base + sg.count, key, SymSink{rec.prs + sg.base, rec.cum + sg.base, rec.rtab});
+    replay_seq_run(keys, vals, i, sg.base + sg.count, key, SymSink{rec.prs + sg.base, rec.cum + sg.base});
 }
 
 // ---------------------------------------------------------------------------
@@ -303,7 +316,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView 
     }
     uint32_t* F = lds + threadIdx.x * RP_STRIDE;
     const uint32_t e =
-        replay_simple_run(keys, vals, i, end, model, SymSink{rec.prs + sg.base, rec.cum + sg.base, rec.rtab}, F);
+        replay_simple_run(keys, vals, i, end, model, SymSink{rec.prs + sg.base, rec.cum + sg.base}, F);
     if (e) atomicOr(err, e);
 }
 
@@ -313,159 +326,356 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView 
 // occurrence (a halving is made to fall on a step's last update), so for lane i
 // holding symbol s_i at position p_i:
 //     freq_i = F[s_i] + 8 * #{j < i : s_j = s_i}
-//     cum_i  = Cpre[p_i] + 8 * #{j < i : p_j < p_i}   (+ bubble corrections)
+//     cum_i  = C[s_i] + 8 * #{j < i : p_j < p_i}   (+ bubble corrections)
 //     tot_i  = Tot + 8 i
-// The counts come from one ballot per distinct symbol of the step.  Each bubble
-// event inside the step swaps at most one adjacent pair (x ahead of y); lanes
-// after it that hold y gain freq_x, lanes that hold x lose freq_y.  Model state
-// (symbol at position, position of symbol, freq of symbol, prefix by position)
-// lives in LDS.
-__global__ __launch_bounds__(64) void k_replay_aux_long(const LongRun* __restrict__ longs,
-                                                        const uint32_t* __restrict__ nlong,
-                                                        const uint32_t* __restrict__ keys,
-                                                        const uint32_t* __restrict__ vals, const SymSink rec_all,
-                                                        uint32_t* __restrict__ err)
+// One pass over the distinct symbols of the step (one ballot each) gives the
+// counts; the frequency increments are LDS atomics by position.  A bubble event
+// swaps at most one adjacent pair (x ahead of y); lanes after it that hold y
+// gain freq_x, lanes that hold x lose freq_y.  Only events whose symbol is not
+// already in front are visited.  Model state (RunModel) lives in LDS; the
+// prefix of the freqs by position is a DPP scan.  Records are written without
+// the reciprocal (k_fill_recip adds it).
+
+// Orders this wave's LDS accesses for the compiler only: one wave's LDS
+// operations are performed in issue order, so no s_waitcnt is needed (a
+// workgroup fence would also wait for the outstanding global loads and stores).
+__device__ inline void lds_order() { asm volatile("" ::: "memory"); }
+
+__device__ inline uint32_t lanes_below(uint64_t m)   // popc(m & ((1 << lane) - 1))
 {
-    __shared__ uint32_t ent[256], posof[256], fr[256], cpre[256];
-    if (blockIdx.x >= *nlong) return;
-    const LongRun lr = longs[blockIdx.x];
-    const uint32_t lane = threadIdx.x;
-    const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base, rec_all.rtab};
-    const uint32_t N = model_nsym(lr.model);
-    for (uint32_t k = lane; k < 256; k += 64) {
-        ent[k] = k;
-        posof[k] = k;
-        fr[k] = k < N ? 1u : 0u;
-        cpre[k] = k < N ? k : N;
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// LDS ring of a long run's sorted (key, value) pairs, filled ahead of the
+// replaying wave by a loader wave of the same workgroup.
+constexpr uint32_t RING_WIN = 32;                 // windows of 64 pairs
+constexpr uint32_t RING_LEN = RING_WIN * 64;
+constexpr uint32_t RING_BATCH = 8;                // windows per loader batch
+struct RunRing {
+    uint32_t key[RING_LEN];
+    uint32_t val[RING_LEN];
+    uint32_t filled;     // windows published by the loader
+    uint32_t consumed;   // first window the replaying wave still needs
+    uint32_t done;       // replaying wave finished
+};
+
+// Relaxed workgroup-scope atomics keep these on the LDS path (a volatile access
+// through the reference becomes a flat access that waits for every outstanding
+// global store), and readfirstlane tells the compiler the polled value is
+// uniform (a loop exit on a "divergent" LDS load makes the whole step loop
+// divergent: waterfalled, exec-masked code).
+__device__ inline uint32_t lds_poll(const uint32_t* p)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ inline void lds_publish(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Loader wave: windows w = 0, 1, ... of [lr.start, lr.end) into the ring, a
+// batch of RING_BATCH windows per round trip, until the batch after the one
+// that leaves the run (or the block's end) is published -- the replaying wave
+// reads up to 63 pairs past its position -- or the replaying wave is done.
+__device__ void run_loader(const LongRun& lr, const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                           RunRing& rg)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    bool last = false;
+    for (uint32_t w = 0;; w += RING_BATCH) {
+        uint32_t spins = 0;
+        while (w + RING_BATCH > lds_poll(&rg.consumed) + RING_WIN) {
+            if (lds_poll(&rg.done) || ++spins > (1u << 24)) return;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        uint32_t k[RING_BATCH], v[RING_BATCH];
+#pragma unroll
+        for (uint32_t j = 0; j < RING_BATCH; j++) {
+            const size_t at = lr.start + (size_t)(w + j) * 64 + lane;
+            k[j] = SORT_PAD;
+            v[j] = 0;
+            if (at < lr.end) {
+                k[j] = keys[at];
+                v[j] = vals[at];
+            }
+        }
+        bool out = false;
+#pragma unroll
+        for (uint32_t j = 0; j < RING_BATCH; j++) {
+            const uint32_t slot = ((w + j) % RING_WIN) * 64 + lane;
+            rg.key[slot] = k[j];
+            rg.val[slot] = v[j];
+            out |= (k[j] >> AUX_SYM_BITS) != lr.model;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the windows are in LDS
+        lds_order();
+        if (lane == 0) lds_publish(&rg.filled, w + RING_BATCH);
+        if (last) return;
+        last = __ballot(out) != 0;
     }
-    __syncthreads();
-    const uint64_t before = (1ull << lane) - 1ull;
+}
+
+#ifdef SA_PROF   // scripts/micro/replay_long.hip: per-section cycle counts of one run
+__device__ unsigned long long g_prof[8];
+#define PROF_T(i) const uint64_t pt##i = __builtin_amdgcn_s_memtime()
+#define PROF_ACC(k, a, b) acc[k] += pt##b - pt##a
+#else
+#define PROF_T(i)
+#define PROF_ACC(k, a, b)
+#endif
+
+// The model state of one long run, in LDS (N <= 256 entries).
+struct RunModel {
+    uint32_t ent[256];    // symbol at position
+    uint32_t posr[256];   // position of symbol
+    uint32_t fpos[256];   // freq of the entry at position
+    uint32_t cpos[256];   // exclusive prefix of fpos
+};
+
+__device__ inline uint32_t uread(const uint32_t* p)   // wave-uniform LDS read
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)*p);
+}
+
+template <int NR>
+__device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink& rec, uint32_t* __restrict__ err,
+                                                RunModel& md, RunRing& rg)
+{
+#ifdef SA_PROF
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    const uint32_t lane = threadIdx.x;
+    const uint32_t N = model_nsym(lr.model);
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+        const uint32_t k = 64u * j + lane;
+        md.ent[k] = k;
+        md.posr[k] = k;
+        md.fpos[k] = k < N ? 1u : 0u;
+        md.cpos[k] = k < N ? k : N;
+    }
+    lds_order();
     uint32_t tot = N, bub = 0;
     bool bad = false;
-    for (size_t base = lr.start; base < lr.end;) {
-        uint32_t key = SORT_PAD, pos = 0;
-        if (base + lane < lr.end) {
-            key = keys[base + lane];
-            pos = vals[base + lane];
+    size_t base = lr.start;
+    uint32_t avail = 0;                                          // windows known published
+    uint32_t nxt_rel = 0xffffffffu, nxt_key = 0, nxt_pos = 0;   // next window, read ahead
+    auto swap_at = [&](uint32_t P, uint32_t x, uint32_t y) __attribute__((always_inline)) {
+        // x at P moves ahead of y at P - 1 (the freqs travel with the symbols)
+        if (lane == 0) {
+            const uint32_t fx = md.fpos[P], fy = md.fpos[P - 1];
+            md.ent[P - 1] = x;
+            md.ent[P] = y;
+            md.fpos[P - 1] = fx;
+            md.fpos[P] = fy;
+            md.posr[x] = P - 1;
+            md.posr[y] = P;
+        }
+        lds_order();
+    };
+    for (;;) {
+        PROF_T(0);
+        const uint32_t rel = (uint32_t)(base - lr.start);
+        const uint32_t need = (rel + 63) / 64 + 1;   // windows that must be published
+        if (avail < need) {
+            uint32_t spins = 0;   // bounded: a stalled loader fails the batch instead of hanging
+            while ((avail = lds_poll(&rg.filled)) < need && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(1);
+            if (spins >= (1u << 24)) {
+                bad = true;
+                break;
+            }
+            lds_order();
+            nxt_rel = 0xffffffffu;
+        }
+        PROF_T(1);
+        uint32_t key, pos;
+        if (nxt_rel == rel) {
+            key = nxt_key;
+            pos = nxt_pos;
+        } else {
+            const uint32_t slot = (rel + lane) % RING_LEN;
+            key = rg.key[slot];
+            pos = rg.val[slot];
+        }
+        // read the following window ahead when it is published (a step takes 64
+        // symbols except at a halving cut)
+        nxt_rel = 0xffffffffu;
+        if ((rel + 127) / 64 < avail) {
+            const uint32_t slot = (rel + 64 + lane) % RING_LEN;
+            nxt_key = rg.key[slot];
+            nxt_pos = rg.val[slot];
+            nxt_rel = rel + 64;
         }
         const bool in_run = (key >> AUX_SYM_BITS) == lr.model;
-        uint32_t c = (uint32_t)__popcll(__ballot(in_run));   // the run is a lane prefix
+        // symbols of the run in this window: the leading in-run lanes
+        const uint64_t outm = ~__ballot(in_run);
+        uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(outm ? (int)__builtin_ctzll(outm) : 64);
         if (c == 0) break;
-        // cut the step so that a halving (tot > 0xffe0 after an update) falls on its last update
+        tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)tot);
         const uint32_t to_halve = (0xffe0u - tot) / 8u + 1u;
         bool halve = false;
-        if (to_halve <= c) {
+        if (to_halve <= c) {   // cut the step so that a halving falls on its last update
             c = to_halve;
             halve = true;
         }
         const bool act = lane < c;
         const uint64_t amask = c == 64 ? ~0ull : ((1ull << c) - 1ull);
-        const uint32_t sym = key & 0xffu;
+        const uint32_t sym = act ? (key & 0xffu) : 0u;
         if (act && sym >= N) bad = true;
-        const uint32_t p = act ? posof[sym] : 0u;
-        const uint32_t f0 = act ? fr[sym] : 0u;
-        int32_t cum = act ? (int32_t)cpre[p] : 0;
+        uint32_t p = md.posr[sym];
+        const uint32_t f0 = md.fpos[p], c0 = md.cpos[p];
+        // the entry in front of each lane's symbol (bubble events)
+        uint32_t fprev = p ? md.fpos[p - 1] : 0u, yprev = p ? md.ent[p - 1] : 0u;
+        // counts: one ballot per distinct symbol of the step
         uint32_t same = 0, less = 0;
-        // one ballot per distinct symbol of the step
         uint64_t rem = amask;
         while (rem) {
-            const uint32_t fl = (uint32_t)__builtin_ctzll(rem);
-            const uint32_t x = __builtin_amdgcn_readlane(sym, fl);
-            const uint32_t px = __builtin_amdgcn_readlane(p, fl);
+            const int fl = (int)__builtin_ctzll(rem);
+            const uint32_t x = __builtin_amdgcn_readlane(sym, fl), px = __builtin_amdgcn_readlane(p, fl);
             const uint64_t m = __ballot(act && sym == x);
-            const uint32_t below = (uint32_t)__popcll(m & before);
+            const uint32_t below = lanes_below(m);
             if (sym == x) same = below;
-            else if (px < p) less += below;
+            less += px < p ? below : 0u;
             rem &= ~m;
         }
-        cum += (int32_t)(8u * less);
-        // bubble events inside the step (the one on its last update comes after the state update)
-        uint32_t b = 15u - (bub & 15u);
-        for (; b + 1 < c; b += 16) {
-            const uint32_t x = __builtin_amdgcn_readlane(sym, b);
-            const uint32_t P = posof[x];
-            if (P == 0) continue;
-            const uint32_t y = ent[P - 1];
-            const uint64_t mx = __ballot(act && sym == x), my = __ballot(act && sym == y);
+        int32_t cum = (int32_t)(c0 + 8u * less);
+        PROF_T(2);
+        // bubble events inside the step whose symbol is not in front
+        // updates b0, b0 + 16, ... before the last one (that one comes after the
+        // state update)
+        const uint32_t b0 = 15u - (bub & 15u);
+        const uint64_t emask = (0x0001000100010001ull << b0) & ((1ull << (c - 1)) - 1ull);
+        uint64_t cand = __ballot(p != 0) & emask;
+        // (LDS fpos holds the step-start freqs until the increments below; the
+        // per-lane copies p / fprev / yprev are refreshed after a swap)
+        while (cand) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(cand);
+            cand &= cand - 1;
+            const uint32_t x = __builtin_amdgcn_readlane(sym, (int)b);
+            const uint32_t P = __builtin_amdgcn_readlane(p, (int)b);
+            const uint32_t y = __builtin_amdgcn_readlane(yprev, (int)b);
+            const uint32_t fx0 = __builtin_amdgcn_readlane(f0, (int)b), fy0 = __builtin_amdgcn_readlane(fprev, (int)b);
             const uint64_t upto = (2ull << b) - 1ull;
-            const uint32_t fx = fr[x] + 8u * (uint32_t)__popcll(mx & upto);
-            const uint32_t fy = fr[y] + 8u * (uint32_t)__popcll(my & upto);
-            if (fx > fy) {
-                __syncthreads();
-                if (lane == 0) {
-                    ent[P - 1] = x;
-                    ent[P] = y;
-                    posof[x] = P - 1;
-                    posof[y] = P;
-                }
-                __syncthreads();
+            const uint64_t mx = __ballot(act && sym == x), my = __ballot(act && sym == y);
+            if (fx0 + 8u * (uint32_t)__popcll(mx & upto) > fy0 + 8u * (uint32_t)__popcll(my & upto)) {
+                swap_at(P, x, y);
                 if (lane > b) {
-                    if (sym == y) cum += (int32_t)(fr[x] + 8u * (uint32_t)__popcll(mx & before));
-                    else if (sym == x) cum -= (int32_t)(fr[y] + 8u * (uint32_t)__popcll(my & before));
+                    const uint32_t bx = lanes_below(mx), by = lanes_below(my);
+                    if (sym == y) cum += (int32_t)(fx0 + 8u * bx);
+                    else if (sym == x) cum -= (int32_t)(fy0 + 8u * by);
                 }
+                p = md.posr[sym];
+                fprev = p ? md.fpos[p - 1] : 0u;
+                yprev = p ? md.ent[p - 1] : 0u;
+                cand = __ballot(p != 0) & emask & ~upto;
             }
         }
+        // frequency increments, at the symbols' current positions
+        if (act) __hip_atomic_fetch_add(&md.fpos[p], 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_order();
+        PROF_T(3);
         if (act) {
             const uint32_t f = f0 + 8u * same;
             const uint32_t t = tot + 8u * lane;
             if (cum < 0 || (uint32_t)cum + f > t || f == 0) bad = true;
-            sink_put(rec, pos, (uint32_t)cum & 0xffffu, f, t);
+            rec.prs[pos] = PRec{0u, t | (f << 16)};
+            rec.cum[pos] = (uint16_t)cum;
         }
-        // state update: frequencies, total, bubble counter, halving
-        __syncthreads();
-        rem = amask;
-        while (rem) {
-            const uint32_t fl = (uint32_t)__builtin_ctzll(rem);
-            const uint32_t x = __builtin_amdgcn_readlane(sym, fl);
-            const uint64_t m = __ballot(act && sym == x);
-            if (lane == fl) fr[x] += 8u * (uint32_t)__popcll(m);
-            rem &= ~m;
-        }
-        __syncthreads();
+        PROF_T(4);
         tot += 8u * c;
         bub += c;
+        uint32_t fv[NR];
+#pragma unroll
+        for (int j = 0; j < NR; j++) fv[j] = md.fpos[64u * j + lane];
         if (halve) {
             uint32_t part = 0;
-            for (uint32_t k = lane; k < N; k += 64) {
-                const uint32_t v = fr[k];
-                fr[k] = v - (v >> 1);
-                part += v - (v >> 1);
-            }
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d, 64);
-            tot = part;
+            for (int j = 0; j < NR; j++) {
+                fv[j] -= fv[j] >> 1;
+                md.fpos[64u * j + lane] = fv[j];
+                part += fv[j];
+            }
+            tot = __builtin_amdgcn_readlane(wave_incl_scan_dpp(part), 63);
+            lds_order();
         }
-        __syncthreads();
         if ((bub & 15u) == 0) {   // the step's last update was a bubble event
-            const uint32_t x = __builtin_amdgcn_readlane(sym, c - 1);
-            const uint32_t P = posof[x];
-            if (P > 0) {
-                const uint32_t y = ent[P - 1];
-                if (fr[x] > fr[y]) {
-                    __syncthreads();
-                    if (lane == 0) {
-                        ent[P - 1] = x;
-                        ent[P] = y;
-                        posof[x] = P - 1;
-                        posof[y] = P;
-                    }
-                }
+            const uint32_t x = __builtin_amdgcn_readlane(sym, (int)(c - 1));
+            const uint32_t P = uread(&md.posr[x]);
+            if (P > 0 && uread(&md.fpos[P]) > uread(&md.fpos[P - 1])) {
+                swap_at(P, x, uread(&md.ent[P - 1]));
+#pragma unroll
+                for (int j = 0; j < NR; j++) fv[j] = md.fpos[64u * j + lane];
             }
         }
-        __syncthreads();
-        // prefix of frequencies by position
+        // prefix of the freqs by position
         uint32_t carry = 0;
-        for (uint32_t k0 = 0; k0 < N; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            const uint32_t v = k < N ? fr[ent[k]] : 0u;
-            const uint32_t inc = wave_incl_scan(v);
-            if (k < N) cpre[k] = carry + inc - v;
+#pragma unroll
+        for (int j = 0; j < NR; j++) {
+            const uint32_t inc = wave_incl_scan_dpp(fv[j]);
+            md.cpos[64u * j + lane] = carry + inc - fv[j];
             carry += __builtin_amdgcn_readlane(inc, 63);
         }
-        __syncthreads();
         base += c;
+        if (lane == 0) lds_publish(&rg.consumed, (uint32_t)(base - lr.start) / 64);
+        lds_order();
+        PROF_T(5);
+        PROF_ACC(0, 0, 1);
+        PROF_ACC(1, 1, 2);
+        PROF_ACC(2, 2, 3);
+        PROF_ACC(3, 3, 4);
+        PROF_ACC(4, 4, 5);
     }
+    if (lane == 0) lds_publish(&rg.done, 1u);
     if (__ballot(bad) && lane == 0) atomicOr(err, (uint32_t)E_CODER);
+#ifdef SA_PROF
+    if (lane == 0 && blockIdx.x == 0)
+        for (int k = 0; k < 5; k++) g_prof[k] = acc[k];
+#endif
+}
+
+// One workgroup of two waves per long run: wave 0 replays, wave 1 loads.  The
+// grid covers the largest possible number of long runs; the list is filled by
+// k_replay_aux_short, so workgroups beyond its length exit at once.
+__global__ __launch_bounds__(128) void k_replay_aux_long(const LongRun* __restrict__ longs,
+                                                         const uint32_t* __restrict__ nlong,
+                                                         const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals, const SymSink rec_all,
+                                                         uint32_t* __restrict__ err)
+{
+    __shared__ RunModel md;
+    __shared__ RunRing rg;
+    if (blockIdx.x >= *nlong) return;
+    const LongRun lr = longs[blockIdx.x];
+    if (threadIdx.x == 0) {
+        rg.filled = 0;
+        rg.consumed = 0;
+        rg.done = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) {
+        run_loader(lr, keys, vals, rg);
+        return;
+    }
+    const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base};
+    const uint32_t N = model_nsym(lr.model);
+    if (N <= 64) replay_long_run<1>(lr, rec, err, md, rg);
+    else if (N <= 128) replay_long_run<2>(lr, rec, err, md, rg);
+    else replay_long_run<4>(lr, rec, err, md, rg);
+}
+
+// Reciprocal of every AUX record written without one: m = ceil(2^32 / tot).
+__global__ __launch_bounds__(256) void k_fill_recip(const SortView sv, PRec* __restrict__ prs)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= sv.total) return;
+    const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
+    if (i >= sg.base + sg.count) return;
+    PRec r = prs[i];
+    if (r.m == 0u) {
+        r.m = recip32(r.tf & 0xffffu);
+        prs[i] = r;
+    }
 }
 
 // ---------------------------------------------------------------------------

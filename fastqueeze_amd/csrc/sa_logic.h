@@ -196,7 +196,6 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
 struct SymSink {
     PRec* prs;
     uint16_t* cum;
-    const uint32_t* rtab;   // rtab[t] = ceil(2^32 / t)
 };
 SA_HD void sink_put(const SymSink& o, uint32_t pos, uint32_t cum, uint32_t f, uint32_t t);
 
@@ -367,11 +366,12 @@ SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, siz
 //      after it: the stream restarts R/L1/L2/L3 after that segment from the exact
 //      state L3 computed (the host loops until no stream squeezes).
 
-SA_HD uint32_t recip32(uint32_t t) { return (uint32_t)((0x100000000ull + t - 1) / t); }
+// ceil(2^32 / t) for 2 <= t < 2^32 (t = 2^32 = a t + b: b > 0 -> a + 1; b = 0 -> a)
+SA_HD uint32_t recip32(uint32_t t) { return 0xffffffffu / t + 1u; }
 
 SA_HD void sink_put(const SymSink& o, uint32_t pos, uint32_t cum, uint32_t f, uint32_t t)
 {
-    o.prs[pos] = PRec{o.rtab[t], t | (f << 16)};
+    o.prs[pos] = PRec{recip32(t), t | (f << 16)};
     o.cum[pos] = (uint16_t)cum;
 }
 

@@ -85,37 +85,46 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
     bp.task_out_base.clear();
     bp.asmb.assign(nbk, AsmBlock{});
     uint64_t payload = 0, fin = 0, segs = 0;
+    // coder tasks: every block's SEQ stream first (tasks [0, nbk)), then the AUX
+    // streams (tasks [nbk, 9 nbk)), so the two groups can be coded on two streams
+    auto add_task = [&](size_t b, int s) {
+        const DevBlock& d = blocks[b];
+        CoderTask tk{};
+        if (s == ST_SEQ) {
+            tk.space = 0;
+            tk.rec_base = d.seq_sym_base;
+            tk.n = d.n_seq;
+        } else {
+            tk.space = 1;
+            tk.rec_base = d.aux_sym_base + d.sbase[s];
+            tk.n = d.scount[s];
+        }
+        tk.nseg = tk.n ? (tk.n + SEG_SYMS - 1) / SEG_SYMS : 1;
+        tk.seg_base = segs;
+        segs += tk.nseg;
+        // each symbol narrows the range by at most 2^16 (tot <= 0xffe0):
+        // <= 2 output bytes per symbol, plus the 8-byte flush
+        const uint64_t cap = 2ull * tk.n + 64;
+        tk.out_cap = (uint32_t)std::min<uint64_t>(cap, 0xffffffffull);
+        tk.out_base = payload;
+        payload = align_up(payload + tk.out_cap, 16);
+        bp.asmb[b].task[s] = (uint32_t)bp.tasks.size();
+        bp.tasks.push_back(tk);
+        bp.task_out_base.push_back(tk.out_base);
+    };
     for (size_t b = 0; b < nbk; b++) {
         DevBlock& d = blocks[b];
         d.seq_sym_base = bp.seq.segs[b].base;
         d.aux_sym_base = bp.aux.segs[b].base;
-        uint64_t blk_out = 64;
-        for (int s = 0; s < NSTREAM; s++) {
-            CoderTask tk{};
-            if (s == ST_SEQ) {
-                tk.space = 0;
-                tk.rec_base = d.seq_sym_base;
-                tk.n = d.n_seq;
-            } else {
-                tk.space = 1;
-                tk.rec_base = d.aux_sym_base + d.sbase[s];
-                tk.n = d.scount[s];
-            }
-            // each symbol narrows the range by at most 2^16 (tot <= 0xffe0):
-            // <= 2 output bytes per symbol, plus the 8-byte flush
-            tk.nseg = tk.n ? (tk.n + SEG_SYMS - 1) / SEG_SYMS : 1;
-            tk.seg_base = segs;
-            segs += tk.nseg;
-            const uint64_t cap = 2ull * tk.n + 64;
-            tk.out_cap = (uint32_t)std::min<uint64_t>(cap, 0xffffffffull);
-            tk.out_base = payload;
-            payload = align_up(payload + tk.out_cap, 16);
-            bp.asmb[b].task[s] = (uint32_t)bp.tasks.size();
-            bp.tasks.push_back(tk);
-            bp.task_out_base.push_back(tk.out_base);
-            blk_out += tk.out_cap + 32;
-        }
-        blk_out += 2 + d.name_bytes;   // ID-bin payload (first ID) + MD5s within the 64
+        add_task(b, ST_SEQ);
+    }
+    for (size_t b = 0; b < nbk; b++)
+        for (int s = 0; s < NSTREAM; s++)
+            if (s != ST_SEQ) add_task(b, s);
+    for (size_t b = 0; b < nbk; b++) {
+        const DevBlock& d = blocks[b];
+        uint64_t blk_out = 64 + 2 + d.name_bytes;   // headers, MD5s, ID-bin payload (first ID)
+        for (int s = 0; s < NSTREAM; s++) blk_out += bp.tasks[bp.asmb[b].task[s]].out_cap + 32;
         for (int f = 0; f < 3; f++) bp.asmb[b].md5_task[f] = (uint32_t)(3 * b + f);
         bp.asmb[b].out_base = fin;
         fin = align_up(fin + blk_out, 16);

@@ -275,18 +275,16 @@ int main(int argc, char** argv)
     sort_space(ak, av, bp.aux, AUX_SYM_BITS);
 
     // ---- replays ----
-    std::vector<uint32_t> rtab(65536, 0);
-    for (uint32_t t = 1; t < 65536; t++) rtab[t] = recip32(t);
     std::vector<PRec> ps(stot), pa(atot);
     std::vector<uint16_t> cs(stot), ca(atot);
     std::vector<uint32_t> F(256);
     for (const SortSeg& g : bp.seq.segs) {
-        const SymSink sink{ps.data() + g.base, cs.data() + g.base, rtab.data()};
+        const SymSink sink{ps.data() + g.base, cs.data() + g.base};
         for (size_t i = g.base; i < g.base + g.count; i++)
             if (i == g.base || sk[i - 1] != sk[i]) replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], sink);
     }
     for (const SortSeg& g : bp.aux.segs) {
-        const SymSink sink{pa.data() + g.base, ca.data() + g.base, rtab.data()};
+        const SymSink sink{pa.data() + g.base, ca.data() + g.base};
         for (size_t i = g.base; i < g.base + g.count; i++)
             if (i == g.base || (ak[i - 1] >> AUX_SYM_BITS) != (ak[i] >> AUX_SYM_BITS))
                 err |= replay_simple_run(ak.data(), av.data(), i, g.base + g.count, ak[i] >> AUX_SYM_BITS, sink, F.data());
