@@ -74,7 +74,7 @@ struct sa_ctx {
     DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
-    DBuf d_longs, d_nlong;
+    DBuf d_longs, d_nlong, d_seq_longs, d_nseq_long;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
@@ -91,7 +91,7 @@ struct sa_ctx {
                        &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
                        &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
-                       &d_final_len, &d_longs, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                       &d_final_len, &d_longs, &d_nlong, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
                        &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
                        &d_list_gbase[1], &d_list_run[1]};
         for (DBuf* b : all) b->release();
@@ -586,6 +586,9 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
     const uint64_t max_long = pa.total / LONG_RUN + 1;
     SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
+    const uint64_t max_seq_long = ps.total / (SEQ_HALVE_J + 1) + 1;
+    SA_CHECK(c, c->d_seq_longs.ensure(max_seq_long * 8));
+    SA_CHECK(c, c->d_nseq_long.ensure(4));
     SA_CHECK(c, c->d_nlong.ensure(4));
     SA_CHECK(c, c->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
     SA_CHECK(c, c->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
@@ -658,10 +661,15 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
         return -1;
     ev_finish(c, PH_SORT_AUX, st);
     ev_begin(c, PH_REPLAY_SEQ, st);
-    if (ps.total)
-        hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)((ps.total + 255) / 256)), dim3(256), 0, st, svs,
+    if (ps.total) {
+        SA_CHECK(c, hipMemsetAsync(c->d_nseq_long.p, 0, 4, st));
+        hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,
                            c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
-                           sink_seq);
+                           sink_seq, c->d_seq_longs.as<uint64_t>(), c->d_nseq_long.as<uint32_t>());
+        hipLaunchKernelGGL(k_replay_seq_long, dim3((uint32_t)((max_seq_long + 63) / 64)), dim3(64), 0, st, svs,
+                           c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
+                           sink_seq, c->d_seq_longs.as<uint64_t>(), c->d_nseq_long.as<uint32_t>());
+    }
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_REPLAY_AUX, st);
     const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();

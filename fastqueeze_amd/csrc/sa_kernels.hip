@@ -264,20 +264,140 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 }
 
 // ---------------------------------------------------------------------------
-// Sequence model replay: BASE_MODEL<u8> of encode_seq@0x421f30.  Thread i
-// starts a segment when its key differs from the previous key of the block;
-// it walks the segment and writes the coder record of every base.
+// Sequence model replay: BASE_MODEL<u8> of encode_seq@0x421f30.
+// Before the j-th symbol of a context run the model's counts are 3 + the
+// occurrences of each base among the run's first j symbols, as long as no
+// halving happened; the first halving comes at j = 242 (total 12 + j > 253).
+// k_replay_seq: one workgroup per sort tile (4096 sorted symbols, 16 per
+// thread): a segmented exclusive scan of one-hot packed counts (4 x 8 bit)
+// gives every symbol's model state directly.  The run that continues from the
+// previous tile gets its counts from a backwards scan by the first wave.  A
+// run reaching j = 242 is queued (its symbol j = 242 appends it) and replayed
+// from its start by one lane in k_replay_seq_long.
 // ---------------------------------------------------------------------------
-__global__ void k_replay_seq(const SortView sv, const uint32_t* __restrict__ keys,
-                             const uint32_t* __restrict__ vals, const SymSink rec)
+constexpr uint32_t SEQ_HALVE_J = 242;   // first in-run index that can halve
+
+// Packed counts: 4 x 16 bit (a run can hold more than 255 of one base; only
+// in-run indices < SEQ_HALVE_J are coded here, but the sums must not wrap).
+struct SegCnt {   // segmented-scan element
+    uint64_t cnt;
+    uint32_t head;
+};
+__device__ inline SegCnt segcnt_op(const SegCnt& a, const SegCnt& b)   // a then b
 {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= sv.total) return;
+    return SegCnt{b.head ? b.cnt : a.cnt + b.cnt, a.head | b.head};
+}
+__device__ inline uint64_t onehot16(uint32_t b) { return 1ull << (16 * b); }
+__device__ inline uint32_t sum16(uint64_t c)
+{
+    return (uint32_t)(c & 0xffff) + (uint32_t)((c >> 16) & 0xffff) + (uint32_t)((c >> 32) & 0xffff) +
+           (uint32_t)(c >> 48);
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, const uint32_t* __restrict__ keys,
+                                                             const uint32_t* __restrict__ vals, const SymSink rec,
+                                                             uint64_t* __restrict__ long_runs,
+                                                             uint32_t* __restrict__ nlong)
+{
+    __shared__ SegCnt part[SORT_THREADS];
+    __shared__ uint64_t carry_cnt;
+    __shared__ uint32_t last_key[SORT_THREADS];
+    const uint32_t t = blockIdx.x;
+    const SortSeg& sg = sv.segs[sv.tile_seg[t]];
+    const uint32_t lt = t - sg.tile0;
+    const size_t tile0 = sg.base + (size_t)lt * SORT_TILE;
+    const uint32_t tid = threadIdx.x;
+    const size_t i0 = tile0 + (size_t)tid * SORT_ITEMS;
+    uint32_t k[SORT_ITEMS], v[SORT_ITEMS];
+    {
+        const uint4* K4 = reinterpret_cast<const uint4*>(keys + i0);
+        const uint4* V4 = reinterpret_cast<const uint4*>(vals + i0);
+#pragma unroll
+        for (int q = 0; q < SORT_ITEMS / 4; q++) {
+            const uint4 a = K4[q], b = V4[q];
+            k[4 * q] = a.x; k[4 * q + 1] = a.y; k[4 * q + 2] = a.z; k[4 * q + 3] = a.w;
+            v[4 * q] = b.x; v[4 * q + 1] = b.y; v[4 * q + 2] = b.z; v[4 * q + 3] = b.w;
+        }
+    }
+    last_key[tid] = k[SORT_ITEMS - 1];
+    const uint32_t before_tile = lt > 0 ? keys[tile0 - 1] : SORT_PAD;
+    // counts of the run continued from the previous tile; only its first
+    // SEQ_HALVE_J + 64 symbols are counted (later ones are not coded here)
+    if (tid < 64) {
+        uint64_t cc = 0;
+        const uint32_t key0 = keys[tile0];
+        if (lt > 0 && before_tile == key0 && key0 != SORT_PAD) {
+            for (uint32_t back = 0; back < SEQ_HALVE_J + 64; back += 64) {
+                const size_t at = tile0 - 1 - back - tid;
+                const bool ok = at >= sg.base && at < tile0 && keys[at] == key0;
+                const uint64_t miss = ~__ballot(ok);
+                const uint64_t lead = miss ? ((1ull << __builtin_ctzll(miss)) - 1ull) : ~0ull;
+                if ((lead >> tid) & 1ull) cc += onehot16(vals[at] & 3u);
+                if (miss) break;
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) cc += __shfl_xor(cc, d, 64);
+        }
+        if (tid == 0) carry_cnt = cc;
+    }
+    __syncthreads();
+    const uint32_t prev_key = tid ? last_key[tid - 1] : before_tile;
+    // per-thread segmented reduction, then a block-wide scan of the aggregates
+    SegCnt acc{0ull, 0u};
+    uint32_t pk = prev_key;
+#pragma unroll
+    for (int e = 0; e < SORT_ITEMS; e++) {
+        if (k[e] != pk) {
+            acc.cnt = 0;
+            acc.head = 1;
+        }
+        if (k[e] != SORT_PAD) acc.cnt += onehot16(v[e] & 3u);
+        pk = k[e];
+    }
+    part[tid] = acc;
+    __syncthreads();
+    for (uint32_t d = 1; d < SORT_THREADS; d <<= 1) {
+        SegCnt x = part[tid];
+        if (tid >= d) x = segcnt_op(part[tid - d], x);
+        __syncthreads();
+        part[tid] = x;
+        __syncthreads();
+    }
+    SegCnt run = tid ? part[tid - 1] : SegCnt{0ull, 0u};
+    if (!run.head) run.cnt += carry_cnt;   // still inside the run continued from the previous tile
+    uint64_t cnt = run.cnt;
+    pk = prev_key;
+    const SymSink out{rec.prs + sg.base, rec.cum + sg.base};
+#pragma unroll
+    for (int e = 0; e < SORT_ITEMS; e++) {
+        if (k[e] != pk) cnt = 0;
+        pk = k[e];
+        if (k[e] == SORT_PAD) continue;
+        const uint32_t b = v[e] & 3u, pos = v[e] >> 2;
+        const uint32_t j = sum16(cnt);
+        if (j < SEQ_HALVE_J) {
+            const uint32_t c0 = 3u + (uint32_t)(cnt & 0xffff), c1 = 3u + (uint32_t)((cnt >> 16) & 0xffff);
+            const uint32_t c2 = 3u + (uint32_t)((cnt >> 32) & 0xffff), c3 = 3u + (uint32_t)(cnt >> 48);
+            const uint32_t cum = (b > 0 ? c0 : 0u) + (b > 1 ? c1 : 0u) + (b > 2 ? c2 : 0u);
+            const uint32_t f = b == 0 ? c0 : b == 1 ? c1 : b == 2 ? c2 : c3;
+            sink_put(out, pos, cum, f, j + 12u);
+        } else if (j == SEQ_HALVE_J) {
+            long_runs[atomicAdd(nlong, 1u)] = i0 + e - SEQ_HALVE_J;   // the run's first symbol
+        }
+        cnt += onehot16(b);
+    }
+}
+
+// Context runs that reach the first halving: one lane replays the whole run.
+__global__ void k_replay_seq_long(const SortView sv, const uint32_t* __restrict__ keys,
+                                  const uint32_t* __restrict__ vals, const SymSink rec,
+                                  const uint64_t* __restrict__ long_runs, const uint32_t* __restrict__ nlong)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= *nlong) return;
+    const size_t i = long_runs[r];
     const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
-    const uint32_t key = keys[i];
-    if (key == SORT_PAD) return;
-    if (i != sg.base && keys[i - 1] == key) return;
-    replay_seq_run(keys, vals, i, sg.base + sg.count, key, SymSink{rec.prs + sg.base, rec.cum + sg.base});
+    replay_seq_run(keys, vals, i, sg.base + sg.count, keys[i], SymSink{rec.prs + sg.base, rec.cum + sg.base});
 }
 
 // ---------------------------------------------------------------------------

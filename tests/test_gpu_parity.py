@@ -108,3 +108,24 @@ def test_coder_records_with_squeezes(enc):
     assert enc.coder_restarts() > 0
     for i, (s, g) in enumerate(zip(streams, got)):
         assert g == oracle_py.rc_encode(*s), f"stream {i}"
+
+
+def test_low_complexity_context_runs(enc):
+    """Poly-A / dinucleotide / triplet repeats: BASE_MODEL context runs far longer
+    than the first halving (in-run index 242) and runs that cross sort tiles."""
+    rng = np.random.default_rng(17)
+    recs = []
+    motifs = [b"A", b"AC", b"CAG", b"GATTACA"]
+    for i in range(3000):
+        m = motifs[i % len(motifs)]
+        s = (m * 200)[: 100 + (i % 51)]
+        if i % 7 == 0:   # sprinkle random bases and an N
+            arr = bytearray(s)
+            for p in rng.integers(0, len(arr), 3):
+                arr[int(p)] = b"ACGTN"[int(rng.integers(0, 5))]
+            s = bytes(arr)
+        q = bytes(rng.choice(np.frombuffer(b"F:,#", np.uint8), size=len(s), p=[0.7, 0.2, 0.08, 0.02]))
+        recs.append(b"@lc%d\n%s\n+\n%s\n" % (i, s, q))
+    blocks = fq.blocks_from_fastq(b"".join(recs))
+    for slevel in (3, 1):
+        _check(enc, blocks, fq.Config(slevel=slevel))
