@@ -666,9 +666,10 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,
                            c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
                            sink_seq, c->d_seq_longs.as<uint64_t>(), c->d_nseq_long.as<uint32_t>());
-        hipLaunchKernelGGL(k_replay_seq_long, dim3((uint32_t)((max_seq_long + 63) / 64)), dim3(64), 0, st, svs,
-                           c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
-                           sink_seq, c->d_seq_longs.as<uint64_t>(), c->d_nseq_long.as<uint32_t>());
+        hipLaunchKernelGGL(k_replay_seq_long, dim3((uint32_t)std::min<uint64_t>(max_seq_long, 2048)), dim3(128), 0,
+                           st, svs, c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(),
+                           c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(), sink_seq, c->d_seq_longs.as<uint64_t>(),
+                           c->d_nseq_long.as<uint32_t>(), d_err);
     }
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_REPLAY_AUX, st);

@@ -388,18 +388,6 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
     }
 }
 
-// Context runs that reach the first halving: one lane replays the whole run.
-__global__ void k_replay_seq_long(const SortView sv, const uint32_t* __restrict__ keys,
-                                  const uint32_t* __restrict__ vals, const SymSink rec,
-                                  const uint64_t* __restrict__ long_runs, const uint32_t* __restrict__ nlong)
-{
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= *nlong) return;
-    const size_t i = long_runs[r];
-    const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
-    replay_seq_run(keys, vals, i, sg.base + sg.count, keys[i], SymSink{rec.prs + sg.base, rec.cum + sg.base});
-}
-
 // ---------------------------------------------------------------------------
 // AUX model replay: SIMPLE_MODEL<N> (kModelEncode@0x42ccb0 and every inlined
 // copy), one model run = the symbols of one (block, model) in stream order.
@@ -498,8 +486,9 @@ __device__ inline void lds_publish(uint32_t* p, uint32_t v)
 // batch of RING_BATCH windows per round trip, until the batch after the one
 // that leaves the run (or the block's end) is published -- the replaying wave
 // reads up to 63 pairs past its position -- or the replaying wave is done.
+// `shift`: a pair belongs to the run while key >> shift == lr.model.
 __device__ void run_loader(const LongRun& lr, const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                           RunRing& rg)
+                           RunRing& rg, uint32_t shift)
 {
     const uint32_t lane = threadIdx.x & 63;
     bool last = false;
@@ -526,7 +515,7 @@ __device__ void run_loader(const LongRun& lr, const uint32_t* __restrict__ keys,
             const uint32_t slot = ((w + j) % RING_WIN) * 64 + lane;
             rg.key[slot] = k[j];
             rg.val[slot] = v[j];
-            out |= (k[j] >> AUX_SYM_BITS) != lr.model;
+            out |= (k[j] >> shift) != lr.model;
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the windows are in LDS
         lds_order();
@@ -774,7 +763,7 @@ __global__ __launch_bounds__(128) void k_replay_aux_long(const LongRun* __restri
     }
     __syncthreads();
     if (threadIdx.x >= 64) {
-        run_loader(lr, keys, vals, rg);
+        run_loader(lr, keys, vals, rg, AUX_SYM_BITS);
         return;
     }
     const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base};
@@ -782,6 +771,97 @@ __global__ __launch_bounds__(128) void k_replay_aux_long(const LongRun* __restri
     if (N <= 64) replay_long_run<1>(lr, rec, err, md, rg);
     else if (N <= 128) replay_long_run<2>(lr, rec, err, md, rg);
     else replay_long_run<4>(lr, rec, err, md, rg);
+}
+
+// ---------------------------------------------------------------------------
+// k_replay_seq_long: BASE_MODEL context runs that reach the first halving
+// (queued by k_replay_seq), one wave per run, 64 symbols per step.  Within a
+// step the four counts only grow by one per occurrence, so lane i's counts are
+// the step-start counts plus the occurrences in lanes below it (one ballot per
+// base).  A step is cut so that it ends right before the symbol whose total
+// exceeds 253 (that symbol halves first, at the start of the next step).  Only
+// the in-run indices >= SEQ_HALVE_J are written (k_replay_seq wrote the rest).
+// ---------------------------------------------------------------------------
+__device__ void replay_seq_long_run(const LongRun& lr, const SymSink& rec, RunRing& rg, bool& bad)
+{
+    const uint32_t lane = threadIdx.x;
+    uint32_t c0 = 3, c1 = 3, c2 = 3, c3 = 3;   // wave-uniform model state
+    size_t base = lr.start;
+    uint32_t avail = 0;
+    for (;;) {
+        const uint32_t rel = (uint32_t)(base - lr.start);
+        const uint32_t need = (rel + 63) / 64 + 1;   // windows that must be published
+        if (avail < need) {
+            uint32_t spins = 0;   // bounded: a stalled loader fails the batch instead of hanging
+            while ((avail = lds_poll(&rg.filled)) < need && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(1);
+            if (spins >= (1u << 24)) {
+                bad = true;
+                break;
+            }
+            lds_order();
+        }
+        const uint32_t slot = (rel + lane) % RING_LEN;
+        const uint32_t key = rg.key[slot], val = rg.val[slot];
+        const uint64_t outm = ~__ballot(key == lr.model);
+        uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(outm ? (int)__builtin_ctzll(outm) : 64);
+        if (c == 0) break;
+        uint32_t T = c0 + c1 + c2 + c3;
+        if (T > 253u) {
+            c0 -= c0 >> 1;
+            c1 -= c1 >> 1;
+            c2 -= c2 >> 1;
+            c3 -= c3 >> 1;
+            T = c0 + c1 + c2 + c3;
+        }
+        if (c > 254u - T) c = 254u - T;
+        const bool act = lane < c;
+        const uint32_t b = val & 3u;
+        const uint64_t m0 = __ballot(act && b == 0), m1 = __ballot(act && b == 1), m2 = __ballot(act && b == 2),
+                       m3 = __ballot(act && b == 3);
+        const uint32_t n0 = c0 + lanes_below(m0), n1 = c1 + lanes_below(m1), n2 = c2 + lanes_below(m2),
+                       n3 = c3 + lanes_below(m3);
+        if (act && rel + lane >= SEQ_HALVE_J) {
+            const uint32_t cum = (b > 0 ? n0 : 0u) + (b > 1 ? n1 : 0u) + (b > 2 ? n2 : 0u);
+            const uint32_t f = b == 0 ? n0 : b == 1 ? n1 : b == 2 ? n2 : n3;
+            sink_put(rec, val >> 2, cum, f, T + lane);
+        }
+        c0 += (uint32_t)__popcll(m0);
+        c1 += (uint32_t)__popcll(m1);
+        c2 += (uint32_t)__popcll(m2);
+        c3 += (uint32_t)__popcll(m3);
+        base += c;
+        if (lane == 0) lds_publish(&rg.consumed, (uint32_t)(base - lr.start) / 64);
+        lds_order();
+    }
+    if (lane == 0) lds_publish(&rg.done, 1u);
+}
+
+// A grid of workgroups (wave 0 replays, wave 1 loads) strides over the queued
+// runs (the count is only known on the device).
+__global__ __launch_bounds__(128) void k_replay_seq_long(const SortView sv, const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals, const SymSink rec_all,
+                                                         const uint64_t* __restrict__ long_runs,
+                                                         const uint32_t* __restrict__ nlong,
+                                                         uint32_t* __restrict__ err)
+{
+    __shared__ RunRing rg;
+    const uint32_t n = *nlong;
+    bool bad = false;
+    for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const size_t i = long_runs[r];
+        const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
+        const LongRun lr{i, sg.base + sg.count, sg.base, keys[i], 0};
+        if (threadIdx.x == 0) {
+            rg.filled = 0;
+            rg.consumed = 0;
+            rg.done = 0;
+        }
+        __syncthreads();
+        if (threadIdx.x >= 64) run_loader(lr, keys, vals, rg, 0);
+        else replay_seq_long_run(lr, SymSink{rec_all.prs + sg.base, rec_all.cum + sg.base}, rg, bad);
+        __syncthreads();
+    }
+    if (threadIdx.x < 64 && __ballot(bad) && threadIdx.x == 0) atomicOr(err, (uint32_t)E_CODER);
 }
 
 // Reciprocal of every AUX record written without one: m = ceil(2^32 / tot).
