@@ -635,9 +635,12 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
     if (nr) {
         hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                           c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), c->d_maxlen.as<uint16_t>(),
-                           c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(), c->d_aux_k[0].as<uint32_t>(),
-                           c->d_aux_v[0].as<uint32_t>(), d_err);
+                           c->d_totals.as<uint32_t>(), c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(),
+                           c->d_maxlen.as<uint16_t>(), c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(),
+                           c->d_aux_k[0].as<uint32_t>(), c->d_aux_v[0].as<uint32_t>(), d_err);
+        hipLaunchKernelGGL(k_emit_sq, dim3((nr + EMIT_WAVES - 1) / EMIT_WAVES), dim3(64 * EMIT_WAVES), 0, st, bv,
+                           c->d_counts.as<uint32_t>(), c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(),
+                           c->d_aux_k[0].as<uint32_t>(), c->d_aux_v[0].as<uint32_t>());
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);

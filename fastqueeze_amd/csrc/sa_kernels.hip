@@ -35,6 +35,11 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v)
 
 // inclusive add-scan of a wave64 on DPP (row shifts, then row broadcasts 15/31):
 // register-to-register, no LDS round trip
+__device__ inline uint32_t lanes_below(uint64_t m)   // popc(m & ((1 << lane) - 1))
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ inline uint32_t wave_incl_scan_dpp(uint32_t v)
 {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
@@ -137,9 +142,11 @@ __global__ __launch_bounds__(1024) void k_scan_reads(const BatchView bv, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// k_emit: one thread per read; writes every symbol of the read.
+// k_emit: one thread per read; the length, name and degenerate-base symbols
+// (the serial per-read tokenizers).  k_emit_sq: one wave per read; the SEQ and
+// QUAL symbols, 64 positions per step, written coalesced.
 // ---------------------------------------------------------------------------
-__global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts,
+__global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
                        const int16_t* __restrict__ name_p, const int16_t* __restrict__ name_s,
                        const uint16_t* __restrict__ name_maxlen,
                        uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
@@ -148,9 +155,123 @@ __global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts,
 {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= bv.nreads_total) return;
-    const uint32_t e = emit_read(bv, r, counts, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key,
-                                 aux_val);
+    const uint32_t e = emit_read(bv, r, counts, totals, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key,
+                                 aux_val, false);
     if (e) atomicOr(err, e);
+}
+
+__device__ inline uint32_t shfl_up0(uint32_t v, uint32_t d)   // lane - d's value, 0 below lane d
+{
+    const uint32_t x = (uint32_t)__shfl_up((int)v, d, 64);
+    return lane_id() >= d ? x : 0u;
+}
+
+constexpr uint32_t EMIT_WAVES = 4;
+
+// SEQ (encode_seq@0x421f30): the context of an ACGT base is the seed
+// 0x7616c7 shifted by two bits per earlier ACGT base of the read, plus those
+// bases' codes, masked -- i.e. the packed codes of the up to 16 previous ACGT
+// bases over the seed.  The step's ACGT bases are compacted (LDS, only when a
+// step holds another character), then a shuffle ladder packs 1, 2, 4, 8, 16
+// previous codes.  QUAL (encode_qual@0x422180): the context after symbol i
+// depends on symbols i-1, i-2 and the running sum delta of the drops, an
+// inclusive scan.
+__global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv, const uint32_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ seq_key,
+                                                              uint32_t* __restrict__ seq_val,
+                                                              uint32_t* __restrict__ aux_key,
+                                                              uint32_t* __restrict__ aux_val)
+{
+    __shared__ uint32_t comp[EMIT_WAVES][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t r = blockIdx.x * EMIT_WAVES + w;
+    if (r >= bv.nreads_total) return;   // wave-uniform
+    const uint32_t b = bv.read_block[r];
+    const DevBlock& blk = bv.blocks[b];
+    const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
+    const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
+    const uint32_t len = bv.seq_len[r];
+    const uint32_t* off = counts + (size_t)r * NCOL;
+    {
+        uint32_t* K = seq_key + blk.seq_sym_base;
+        uint32_t* V = seq_val + blk.seq_sym_base;
+        uint32_t d = off[C_SEQ];
+        const uint32_t mask = bv.seq_mask;
+        uint32_t carry = 0x7616c7u & mask;   // the context after the previous step
+        for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint32_t cd = i < len ? base_code(s[i]) : 4u;
+            const uint64_t vm = __ballot(cd <= 3);
+            const uint32_t nv = (uint32_t)__popcll(vm);
+            const uint32_t in_step = len - i0 < 64 ? len - i0 : 64;
+            uint32_t c = cd;
+            if (vm != (in_step == 64 ? ~0ull : (1ull << in_step) - 1ull)) {   // compact the ACGT codes
+                if (cd <= 3) comp[w][lanes_below(vm)] = cd;
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                c = lane < nv ? comp[w][lane] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+            }
+            uint32_t x = shfl_up0(c, 1);
+            x |= shfl_up0(x, 1) << 2;
+            x |= shfl_up0(x, 2) << 4;
+            x |= shfl_up0(x, 4) << 8;
+            x |= shfl_up0(x, 8) << 16;
+            const uint32_t ctx = ((lane < 16 ? carry << (2 * lane) : 0u) | x) & mask;
+            if (lane < nv) {
+                K[d + lane] = ctx;
+                V[d + lane] = ((d + lane) << 2) | c;
+            }
+            if (nv) carry = __builtin_amdgcn_readlane(((ctx << 2) + c) & mask, (int)nv - 1);
+            d += nv;
+        }
+    }
+    {
+        // trailing '#' are not coded (qual_nonhash); one symbol 94 marks them
+        uint32_t n = 0;
+        for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint64_t nz = __ballot(i < len && q[i] != '#');
+            if (nz) n = i0 + 64 - (uint32_t)__builtin_clzll(nz);
+        }
+        uint32_t* K = aux_key + blk.aux_sym_base;
+        uint32_t* V = aux_val + blk.aux_sym_base;
+        const uint32_t pos0 = blk.sbase[ST_QUAL] + off[C_QUAL];
+        const int ql = bv.qlevel;
+        uint32_t p1 = 0, p2 = 0, ctx_c = 0;   // sym i0-1, sym i0-2, the context after i0-1
+        int delta_c = 5;
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint32_t sym = i < n ? (uint32_t)(uint8_t)(q[i] - 33) : 0u;
+            const uint32_t u1 = (uint32_t)__shfl_up((int)sym, 1, 64), u2 = (uint32_t)__shfl_up((int)sym, 2, 64);
+            const uint32_t q1 = lane >= 1 ? u1 : p1;
+            const uint32_t q2 = lane >= 2 ? u2 : lane == 1 ? p1 : p2;
+            const uint32_t drop = i < n && q1 > sym ? q1 - sym : 0u;
+            const int delta = delta_c + (int)wave_incl_scan_dpp(drop);
+            uint32_t ctx = (((q1 > q2 ? q1 : q2) << 6) + sym) & 0xfffu;
+            if (ql > 1) {
+                ctx += q1 == q2 ? 0x1000u : 0u;
+                ctx += (uint32_t)(((delta <= 56 ? delta : 56) & 0xf8) << 10);
+                if (ql > 2) ctx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
+            }
+            const uint32_t uc = (uint32_t)__shfl_up((int)ctx, 1, 64);
+            const uint32_t last = lane >= 1 ? uc : ctx_c;
+            if (i < n) {
+                K[pos0 + i] = ((M_QUAL + last) << AUX_SYM_BITS) | sym;
+                V[pos0 + i] = pos0 + i;
+            }
+            const int tail = (int)(n - i0 < 64 ? n - i0 : 64) - 1;   // last lane of the step
+            p1 = __builtin_amdgcn_readlane(sym, tail);
+            p2 = __builtin_amdgcn_readlane(sym, tail >= 1 ? tail - 1 : 0);
+            delta_c = __builtin_amdgcn_readlane(delta, tail);
+            ctx_c = __builtin_amdgcn_readlane(ctx, tail);
+        }
+        if (n != len && lane == 0) {
+            K[pos0 + n] = ((M_QUAL + ctx_c) << AUX_SYM_BITS) | 94u;
+            V[pos0 + n] = pos0 + n;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -449,10 +570,6 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView 
 // workgroup fence would also wait for the outstanding global loads and stores).
 __device__ inline void lds_order() { asm volatile("" ::: "memory"); }
 
-__device__ inline uint32_t lanes_below(uint64_t m)   // popc(m & ((1 << lane) - 1))
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
 // LDS ring of a long run's sorted (key, value) pairs, filled ahead of the
 // replaying wave by a loader wave of the same workgroup.

@@ -79,9 +79,23 @@ SA_HD void emit_kmodel(AuxEmit& em, uint32_t v)
     for (int i = 0; i < nb; i++) em(M_KBIT0 + (uint32_t)i, (v >> i) & 1);
 }
 
-SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts, const int16_t* name_p,
-                         const int16_t* name_s, const uint16_t* name_maxlen, uint32_t* seq_key,
-                         uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val)
+// Symbols of column `col` of read r: the difference of the exclusive offsets
+// k_scan_reads left in `counts` (the block total after its last read).
+SA_HD uint32_t read_col_count(const BatchView& bv, const uint32_t* counts, const uint32_t* totals, uint32_t r,
+                              int col)
+{
+    const uint32_t b = bv.read_block[r];
+    const DevBlock& blk = bv.blocks[b];
+    const uint32_t next = r + 1 < blk.read0 + blk.nreads ? counts[(size_t)(r + 1) * NCOL + col]
+                                                          : totals[(size_t)b * NCOL + col];
+    return next - counts[(size_t)r * NCOL + col];
+}
+
+// Every symbol of read r.  bulk = false leaves out the SEQ and QUAL symbols
+// (k_emit_sq writes those one wave per read).
+SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts, const uint32_t* totals,
+                         const int16_t* name_p, const int16_t* name_s, const uint16_t* name_maxlen,
+                         uint32_t* seq_key, uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val, bool bulk)
 {
     uint32_t e = 0;
     const uint32_t b = bv.read_block[r];
@@ -93,7 +107,7 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
     const uint32_t* off = counts + (size_t)r * NCOL;
 
     // sequence: BASE_MODEL contexts (encode_seq@0x421f30)
-    {
+    if (bulk) {
         uint32_t* K = seq_key + blk.seq_sym_base;
         uint32_t* V = seq_val + blk.seq_sym_base;
         uint32_t d = off[C_SEQ];
@@ -147,7 +161,7 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
         if (!name_mid(nm, nl, p, sf, last, emid)) e |= E_NAME;
     }
     // qualities (encode_qual@0x422180)
-    {
+    if (bulk) {
         em.pos = blk.sbase[ST_QUAL] + off[C_QUAL];
         const uint32_t n = qual_nonhash(q, len);
         QualCtx qc{0, 0, 5};
@@ -162,9 +176,10 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
     // degenerate-base side streams (DegeInfoProcess@0x433a10)
     {
         em.pos = blk.sbase[ST_TIP] + off[C_TIP];
-        SeqStat st = seq_stat(s, q, len);
-        em(M_TIP, st.nch ? 1u : 0u);
-        if (st.nch) {
+        const uint32_t nch = read_col_count(bv, counts, totals, r, C_CH);   // from k_prep
+        em(M_TIP, nch ? 1u : 0u);
+        if (nch) {
+            const SeqStat st = seq_stat(s, q, len);
             em.pos = blk.sbase[ST_CH] + off[C_CH];
             for (uint32_t i = 0; i < len; i++) {
                 uint32_t cd = base_code(s[i]);
@@ -412,18 +427,42 @@ SA_HD LowMap lowmap_compose(const LowMap& a, const LowMap& b)
 }
 
 // L1: a segment's map from its range checkpoint.
+// The records of a segment, RC_CHUNK at a time: a chunk's loads are issued
+// back to back before it is coded (on the GPU one lane walks one segment, so
+// its cache lines must not be evicted between dependent steps).  The last
+// chunk re-reads record n - 1 instead of reading past the segment.
+constexpr uint32_t RC_CHUNK = 16;
+
+template <class Fn>
+SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
+{
+    for (uint32_t b = 0; b < n; b += RC_CHUNK) {
+        PRec p[RC_CHUNK];
+        uint32_t c[RC_CHUNK];
+#pragma unroll
+        for (uint32_t k = 0; k < RC_CHUNK; k++) {
+            const uint32_t i = b + k < n ? b + k : n - 1;
+            p[k] = P[i];
+            c[k] = cum[i];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < RC_CHUNK; k++)
+            if (b + k < n) fn(p[k], c[k]);
+    }
+}
+
 SA_HD LowMap seg_lowmap(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
 {
     LowMap m{0ull, 0u, 0u};
     uint64_t low = 0;
     uint32_t sbits = 0;
-    for (uint32_t i = 0; i < n; i++) {
+    seg_for_each(P, cum, n, [&](const PRec pr, uint32_t c) {
         uint32_t nb;
-        const uint32_t q = range_step(r, P[i], nb);
-        low = shl64(low + (uint64_t)cum[i] * q, 8 * nb);
+        const uint32_t q = range_step(r, pr, nb);
+        low = shl64(low + (uint64_t)c * q, 8 * nb);
         sbits += 8 * nb;
         m.nbytes += nb;
-    }
+    });
     m.B = low;
     m.s = sbits >= 64 ? 64u : sbits;
     return m;
@@ -447,11 +486,11 @@ SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t l
 {
     SegEnd e{0, 0, 0, 0};
     uint32_t op = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t t = P[i].tf & 0xffffu, f = P[i].tf >> 16;
-        uint32_t q = mulhi32(r, P[i].m);
+    seg_for_each(P, cum, n, [&](const PRec pr, uint32_t c) {
+        const uint32_t t = pr.tf & 0xffffu, f = pr.tf >> 16;
+        uint32_t q = mulhi32(r, pr.m);
         q -= (r < q * t) ? 1u : 0u;
-        low += (uint64_t)cum[i] * q;
+        low += (uint64_t)c * q;
         r = q * f;
         while (r < (1u << 24)) {
             if ((low ^ (low + r)) >> 56) {
@@ -463,7 +502,7 @@ SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t l
             r <<= 8;
             low <<= 8;
         }
-    }
+    });
     if (finish) {
         for (int k = 0; k < 8; k++) {
             if (op < cap) o[op] = (uint8_t)(low >> 56);

@@ -253,8 +253,8 @@ int main(int argc, char** argv)
     const size_t stot = bp.seq.total + 64, atot = bp.aux.total + 64;   // slack as the engine
     std::vector<uint32_t> sk(stot, SORT_PAD), sv(stot), ak(atot, SORT_PAD), av(atot);
     for (uint32_t r = 0; r < nr; r++)
-        err |= emit_read(bv, r, counts.data(), name_p.data(), name_s.data(), maxlen.data(), sk.data(), sv.data(),
-                         ak.data(), av.data());
+        err |= emit_read(bv, r, counts.data(), totals.data(), name_p.data(), name_s.data(), maxlen.data(), sk.data(),
+                         sv.data(), ak.data(), av.data(), true);
     if (err) { std::printf("FAIL emit error bits %x\n", err); return 1; }
 
     // ---- stable sort per segment (what k_sort_* computes) ----
@@ -274,6 +274,26 @@ int main(int argc, char** argv)
     sort_space(sk, sv, bp.seq, 0);
     sort_space(ak, av, bp.aux, AUX_SYM_BITS);
 
+    // EMU_RUNS=1: the longest model runs per space (what bounds the replay kernels)
+    if (std::getenv("EMU_RUNS")) {
+        auto runs = [](const std::vector<uint32_t>& K, const SortPlan& p, int lo, const char* name) {
+            std::vector<std::pair<size_t, uint32_t>> r;
+            for (const SortSeg& g : p.segs)
+                for (size_t i = g.base, s = g.base; i <= g.base + g.count; i++)
+                    if (i == g.base + g.count || (K[i] >> lo) != (K[s] >> lo)) {
+                        r.push_back({i - s, K[s] >> lo});
+                        s = i;
+                    }
+            std::sort(r.begin(), r.end(), std::greater<>());
+            size_t n512 = 0, tot = 0;
+            for (auto& x : r) { if (x.first >= 512) { n512++; tot += x.first; } }
+            std::printf("%s: %zu runs, %zu >= 512 holding %zu symbols; longest:", name, r.size(), n512, tot);
+            for (size_t i = 0; i < r.size() && i < 12; i++) std::printf(" %zu(m%x)", r[i].first, r[i].second);
+            std::printf("\n");
+        };
+        runs(sk, bp.seq, 0, "seq");
+        runs(ak, bp.aux, AUX_SYM_BITS, "aux");
+    }
     // ---- replays ----
     std::vector<PRec> ps(stot), pa(atot);
     std::vector<uint16_t> cs(stot), ca(atot);

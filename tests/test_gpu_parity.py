@@ -129,3 +129,34 @@ def test_low_complexity_context_runs(enc):
     blocks = fq.blocks_from_fastq(b"".join(recs))
     for slevel in (3, 1):
         _check(enc, blocks, fq.Config(slevel=slevel))
+
+
+def _long_read_fastq(seed, n):
+    """Reads whose lengths straddle the 64-position steps of k_emit_sq, with N /
+    IUPAC bases anywhere (so a step compacts its ACGT bases) and '#' runs that
+    end the read across step boundaries (qual_nonhash) or fill it."""
+    rng = np.random.default_rng(seed)
+    lens = [0, 1, 2, 16, 17, 63, 64, 65, 127, 128, 129, 150, 191, 192, 200, 300, 1000]
+    recs = []
+    for i in range(n):
+        L = lens[i % len(lens)]
+        s = bytearray(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=L))
+        rate = (0.0, 0.01, 0.2)[i % 3]
+        for p in np.nonzero(rng.random(L) < rate)[0]:
+            s[int(p)] = b"NNRYKMSWacgtn"[int(rng.integers(0, 13))]
+        q = bytearray(rng.integers(35, 75, size=L, dtype=np.uint8))
+        if L and i % 4 == 0:
+            tail = int(rng.integers(0, L + 1))
+            q[L - tail:] = b"#" * tail
+        if L and i % 5 == 1:
+            for p in np.nonzero(rng.random(L) < 0.1)[0]:
+                q[int(p)] = ord("#")
+        recs.append(b"@lr%d\n%s\n+\n%s\n" % (i, bytes(s), bytes(q)))
+    return b"".join(recs)
+
+
+@pytest.mark.parametrize("slevel,qlevel", [(3, 2), (1, 3), (4, 1), (9, 2)])
+def test_long_reads_emit_steps(enc, slevel, qlevel):
+    """SEQ contexts and QUAL contexts carried across k_emit_sq's 64-position steps."""
+    blocks = fq.blocks_from_fastq(_long_read_fastq(5 + slevel, 700))
+    _check(enc, blocks, fq.Config(slevel=slevel, qlevel=qlevel))
