@@ -1,0 +1,135 @@
+// Microbenchmark 5: pass-R range chain, 2-dword records {m, t | f << 16}
+// (10 SALU / symbol) against 3-dword records {m, t, f} (8 SALU / symbol).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+template <int W> struct Chunk { uint32_t w[16 * W]; };
+
+__device__ __forceinline__ void step2(uint32_t& r, uint32_t m, uint32_t tf)
+{
+    uint32_t t, f, q, p;
+    asm volatile(
+        "s_and_b32 %1, %5, 0xffff\n\t"
+        "s_lshr_b32 %2, %5, 16\n\t"
+        "s_mul_hi_u32 %3, %0, %6\n\t"
+        "s_mul_i32 %4, %3, %1\n\t"
+        "s_cmp_lt_u32 %0, %4\n\t"
+        "s_subb_u32 %3, %3, 0\n\t"
+        "s_mul_i32 %3, %3, %2\n\t"
+        "s_flbit_i32_b32 %4, %3\n\t"
+        "s_and_b32 %4, %4, 24\n\t"
+        "s_lshl_b32 %0, %3, %4"
+        : "+s"(r), "=&s"(t), "=&s"(f), "=&s"(q), "=&s"(p)
+        : "s"(tf), "s"(m)
+        : "scc");
+}
+
+__device__ __forceinline__ void step3(uint32_t& r, uint32_t m, uint32_t t, uint32_t f)
+{
+    uint32_t q, p;
+    asm volatile(
+        "s_mul_hi_u32 %1, %0, %3\n\t"
+        "s_mul_i32 %2, %1, %4\n\t"
+        "s_cmp_lt_u32 %0, %2\n\t"
+        "s_subb_u32 %1, %1, 0\n\t"
+        "s_mul_i32 %1, %1, %5\n\t"
+        "s_flbit_i32_b32 %2, %1\n\t"
+        "s_and_b32 %2, %2, 24\n\t"
+        "s_lshl_b32 %0, %1, %2"
+        : "+s"(r), "=&s"(q), "=&s"(p)
+        : "s"(m), "s"(t), "s"(f)
+        : "scc");
+}
+
+template <int W>
+__device__ __forceinline__ void steps(uint32_t& r, const Chunk<W>& A, int j0)
+{
+#pragma unroll
+    for (int j = j0; j < 16; j++) {
+        if constexpr (W == 2) step2(r, A.w[2 * j], A.w[2 * j + 1]);
+        else step3(r, A.w[3 * j], A.w[3 * j + 1], A.w[3 * j + 2]);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void k_passr(const Chunk<W>* __restrict__ chunks, uint32_t nchunks,
+                                              uint32_t* __restrict__ ckpt, uint32_t* res)
+{
+    const uint32_t lane = threadIdx.x;
+    const Chunk<W>* C = chunks + (size_t)blockIdx.x * (nchunks + 4);
+    uint32_t* K = ckpt + (size_t)blockIdx.x * (nchunks / 4 + 64);
+    uint32_t r = 0xffffffffu, kv = 0;
+    Chunk<W> A = C[0], B;
+    for (uint32_t c = 0; c < nchunks; c += 2) {
+        steps<W>(r, A, 0);   // placeholder for the first step; B requested after it
+        __builtin_amdgcn_sched_barrier(0);
+        B = C[c + 1];
+        __builtin_amdgcn_sched_barrier(0);
+        steps<W>(r, B, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        A = C[c + 2];
+        __builtin_amdgcn_sched_barrier(0);
+        if ((c & 3) == 2) {
+            const uint32_t slot = (c >> 2) & 63;
+            kv = lane == slot ? r : kv;
+            if (slot == 63) K[(c >> 2) - 63 + lane] = kv;
+        }
+    }
+    if (lane == 0) res[blockIdx.x] = r;
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+template <int W>
+int run(const char* name)
+{
+    const uint32_t nchunks = 65536;   // 1M symbols per stream
+    const int NS = 128;
+    std::vector<Chunk<W>> h((size_t)(nchunks + 4) * NS);
+    std::vector<uint32_t> tt((size_t)(nchunks + 4) * 16 * NS), ff(tt.size());
+    uint32_t x = 777;
+    for (size_t i = 0; i < h.size(); i++)
+        for (int j = 0; j < 16; j++) {
+            x = x * 1664525u + 1013904223u;
+            uint32_t t = 12 + (x >> 8) % 240, f = 1 + (x >> 20) % (t - 1);
+            uint32_t m = (uint32_t)((0x100000000ull + t - 1) / t);
+            if (W == 2) { h[i].w[2 * j] = m; h[i].w[2 * j + 1] = t | (f << 16); }
+            else { h[i].w[3 * j] = m; h[i].w[3 * j + 1] = t; h[i].w[3 * j + 2] = f; }
+            tt[i * 16 + j] = t; ff[i * 16 + j] = f;
+        }
+    Chunk<W>* d; uint32_t *dk, *dres;
+    CK(hipMalloc(&d, h.size() * sizeof(Chunk<W>)));
+    CK(hipMalloc(&dk, (size_t)NS * (nchunks / 4 + 64) * 4)); CK(hipMalloc(&dres, 4096 * 4));
+    CK(hipMemcpy(d, h.data(), h.size() * sizeof(Chunk<W>), hipMemcpyHostToDevice));
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    float ms;
+    for (int w : {1, 32, NS}) {
+        hipLaunchKernelGGL(k_passr<W>, dim3(w), dim3(64), 0, 0, d, nchunks, dk, dres);
+        CK(hipEventRecord(a)); hipLaunchKernelGGL(k_passr<W>, dim3(w), dim3(64), 0, 0, d, nchunks, dk, dres); CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
+        printf("%s streams=%3d : %.2f ns/sym/stream\n", name, w, ms * 1e6 / (nchunks * 16.0));
+    }
+    std::vector<uint32_t> res(NS);
+    CK(hipMemcpy(res.data(), dres, NS * 4, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (int s = 0; s < NS; s++) {
+        uint32_t r = 0xffffffffu;
+        for (size_t i = (size_t)s * (nchunks + 4) * 16; i < ((size_t)s * (nchunks + 4) + nchunks) * 16; i++) {
+            uint32_t q = r / tt[i], rr = q * ff[i];
+            r = rr << (__builtin_clz(rr) & 24);
+        }
+        bad += r != res[s];
+    }
+    printf("%s final range check: %zu of %d streams differ\n", name, bad, NS);
+    CK(hipFree(d)); CK(hipFree(dk)); CK(hipFree(dres));
+    return 0;
+}
+
+int main()
+{
+    if (run<2>("2-dword/10 SALU")) return 1;
+    if (run<3>("3-dword/8 SALU ")) return 1;
+    return 0;
+}
