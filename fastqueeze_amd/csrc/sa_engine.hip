@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -53,8 +54,12 @@ enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX,
 
 struct sa_ctx {
     int device = 0;
-    hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;   // main/AUX, MD5, SEQ
-    hipEvent_t ev_fork = nullptr, ev_seq_done = nullptr, ev_md5_done = nullptr, ev_r[2] = {nullptr, nullptr};
+    // main/AUX, MD5, SEQ path (CU-masked), long AUX runs (CU-masked, disjoint)
+    hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr, st4 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_fork_seq = nullptr, ev_md5_done = nullptr, ev_r[2] = {nullptr, nullptr};
+    hipEvent_t ev_seq_done = nullptr, ev_long_done = nullptr;
+    uint32_t long_lds = 0;
+    bool serial_seq = false;
     std::string err;
     bool timing = false;
     uint32_t coder_restarts = 0;
@@ -74,7 +79,7 @@ struct sa_ctx {
     DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
-    DBuf d_longs, d_nlong, d_seq_longs, d_nseq_long;
+    DBuf d_longs, d_huge_sorted, d_nlong, d_seq_longs, d_nseq_long, d_short_at;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
@@ -91,7 +96,7 @@ struct sa_ctx {
                        &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
                        &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
-                       &d_final_len, &d_longs, &d_nlong, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                       &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_short_at, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
                        &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
                        &d_list_gbase[1], &d_list_run[1]};
         for (DBuf* b : all) b->release();
@@ -99,11 +104,12 @@ struct sa_ctx {
             if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
             if (ev_end[i]) (void)hipEventDestroy(ev_end[i]);
         }
-        for (hipEvent_t e : {ev_fork, ev_seq_done, ev_md5_done, ev_r[0], ev_r[1]})
+        for (hipEvent_t e : {ev_fork, ev_fork_seq, ev_md5_done, ev_r[0], ev_r[1], ev_seq_done, ev_long_done})
             if (e) (void)hipEventDestroy(e);
         if (st) (void)hipStreamDestroy(st);
         if (st2) (void)hipStreamDestroy(st2);
         if (st3) (void)hipStreamDestroy(st3);
+        if (st4) (void)hipStreamDestroy(st4);
     }
 };
 
@@ -204,7 +210,8 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
 {
     if (!tl.count) return;
     if (ph >= 0) ev_begin(c, ph, st);
-    hipLaunchKernelGGL(k_coder_r, dim3(tl.count), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r);
+    hipLaunchKernelGGL(k_coder_r, dim3(tl.count), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r,
+                       c->d_err.as<uint32_t>());
     if (ph >= 0) ev_finish(c, ph, st);
 }
 
@@ -225,7 +232,7 @@ void coder_launch_l(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
 // the L passes of every group; then the restarts.  On return every stream of
 // every group is coded and all group streams are idle.
 int coder_run(sa_ctx* c, const std::vector<CoderTask>& tasks, const CoderView& cv, const CoderGroup* groups,
-              int ngroups)
+              int ngroups, hipEvent_t before_l = nullptr)
 {
     if (tasks.empty()) return 0;
     c->coder_restarts = 0;
@@ -246,6 +253,7 @@ int coder_run(sa_ctx* c, const std::vector<CoderTask>& tasks, const CoderView& c
     for (int g = 0; g < ngroups; g++) {
         for (int h = 0; h < ngroups; h++)
             if (h != g) SA_CHECK(c, hipStreamWaitEvent(groups[g].st, c->ev_r[h], 0));
+        if (before_l) SA_CHECK(c, hipStreamWaitEvent(groups[g].st, before_l, 0));
         coder_launch_l(c, groups[g].st, tl[g], cv, c->timing ? groups[g].ph_l : -1);
         SA_CHECK(c, hipGetLastError());
     }
@@ -319,11 +327,28 @@ sa_ctx* sa_create(int device)
     sa_ctx* c = new sa_ctx();
     c->device = device;
     for (int i = 0; i < PH_N; i++) c->ev_beg[i] = c->ev_end[i] = nullptr;
+    // st carries the critical path (AUX symbols -> QUAL coder chain).  While the
+    // long AUX model runs replay (latency-bound, st4: every 4th CU), the SEQ path
+    // (throughput, st3: the other CUs) runs beside them without sharing a SIMD.
+    // (SA_LONG_CU_EVERY / SA_LONG_LDS: tuning overrides of the split and of the
+    //  LDS per long-run workgroup, i.e. how many share a CU)
+    const char* ev = std::getenv("SA_LONG_CU_EVERY");
+    const int every = ev ? std::max(1, std::atoi(ev)) : 4;
+    const char* el = std::getenv("SA_LONG_LDS");
+    c->long_lds = el ? (uint32_t)std::atoi(el) : 0u;
+    c->serial_seq = std::getenv("SA_SERIAL_SEQ") != nullptr;
+    std::vector<uint32_t> m_long((prop.multiProcessorCount + 31) / 32, 0u), m_seq(m_long.size(), 0u);
+    for (int cu = 0; cu < prop.multiProcessorCount; cu++)
+        ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
+    if (every == 1) m_seq = m_long;   // (st3: the coder chains; st4: the long model runs)
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)prop.multiProcessorCount, m_seq.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)prop.multiProcessorCount, m_long.data()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_seq_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_long_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork_seq, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_md5_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r[1], hipEventDisableTiming) != hipSuccess) {
@@ -586,10 +611,14 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
     const uint64_t max_long = pa.total / LONG_RUN + 1;
     SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
+    SA_CHECK(c, c->d_huge_sorted.ensure((pa.total / HUGE_RUN + 1) * sizeof(LongRun)));
     const uint64_t max_seq_long = ps.total / (SEQ_HALVE_J + 1) + 1;
     SA_CHECK(c, c->d_seq_longs.ensure(max_seq_long * 8));
     SA_CHECK(c, c->d_nseq_long.ensure(4));
-    SA_CHECK(c, c->d_nlong.ensure(4));
+    SA_CHECK(c, c->d_nlong.ensure(16));   // RunLists counters: short, huge, long, queue
+    // at most one run per (block, model) and per symbol
+    const uint64_t max_short = std::max<uint64_t>(std::min<uint64_t>(pa.total, (uint64_t)nbk << aux_bits), 1);
+    SA_CHECK(c, c->d_short_at.ensure(max_short * 8));
     SA_CHECK(c, c->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
     SA_CHECK(c, c->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
     SA_CHECK(c, c->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
@@ -651,18 +680,17 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     const SymSink sink_seq{c->d_prs_seq.as<PRec>(), c->d_cum_seq.as<uint16_t>()};
     const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>()};
 
-    // ---- throughput phases, one after the other on st (each fills the GPU):
-    //      sorts, BASE_MODEL replay, short SIMPLE_MODEL runs ----
+    // ---- throughput phases on st (each fills the GPU): SEQ sort and BASE_MODEL
+    //      replay, AUX sort and short SIMPLE_MODEL runs.  Then the long SIMPLE_MODEL
+    //      runs (latency-bound, st4: CU set B) and pass R of every coder chain
+    //      (st3: the other CUs) start together: pass R waits per segment for
+    //      records the long runs have not written yet (k_coder_r) ----
+    SA_CHECK(c, hipMemsetAsync(c->d_prs_aux.p, 0, atot * sizeof(PRec), st));
     ev_begin(c, PH_SORT_SEQ, st);
     if (run_sort(c, st, ps, c->d_segs_seq, c->d_tile_seq, c->d_hist_seq, c->d_seq_k, c->d_seq_v, 0,
                  ns > 1 ? seq_bits : 0, c->seq_sorted_buf))
         return -1;
     ev_finish(c, PH_SORT_SEQ, st);
-    ev_begin(c, PH_SORT_AUX, st);
-    if (run_sort(c, st, pa, c->d_segs_aux, c->d_tile_aux, c->d_hist_aux, c->d_aux_k, c->d_aux_v, AUX_SYM_BITS,
-                 AUX_SYM_BITS + aux_bits, c->aux_sorted_buf))
-        return -1;
-    ev_finish(c, PH_SORT_AUX, st);
     ev_begin(c, PH_REPLAY_SEQ, st);
     if (ps.total) {
         SA_CHECK(c, hipMemsetAsync(c->d_nseq_long.p, 0, 4, st));
@@ -674,29 +702,44 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
                            c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(), sink_seq, c->d_seq_longs.as<uint64_t>(),
                            c->d_nseq_long.as<uint32_t>(), d_err);
     }
+    SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_SEQ, st);
+    ev_begin(c, PH_SORT_AUX, st);
+    if (run_sort(c, st, pa, c->d_segs_aux, c->d_tile_aux, c->d_hist_aux, c->d_aux_k, c->d_aux_v, AUX_SYM_BITS,
+                 AUX_SYM_BITS + aux_bits, c->aux_sorted_buf))
+        return -1;
+    ev_finish(c, PH_SORT_AUX, st);
     ev_begin(c, PH_REPLAY_AUX, st);
     const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();
     const uint32_t* av = c->d_aux_v[c->aux_sorted_buf].as<uint32_t>();
-    SA_CHECK(c, hipMemsetAsync(c->d_nlong.p, 0, 4, st));
-    if (pa.total)
-        hipLaunchKernelGGL(k_replay_aux_short, dim3((uint32_t)((pa.total + RP_THREADS - 1) / RP_THREADS)),
-                           dim3(RP_THREADS), 0, st, sva, ak, av, sink_aux, c->d_longs.as<LongRun>(),
-                           c->d_nlong.as<uint32_t>(), d_err);
-    // ---- latency-bound phases: long SIMPLE_MODEL runs, then every coder chain
-    //      in one launch (concurrent latency-bound launches land on shared SIMDs) ----
+    uint32_t* ctr = c->d_nlong.as<uint32_t>();
+    const RunLists rl{c->d_short_at.as<uint64_t>(), ctr, c->d_longs.as<LongRun>(), ctr + 1, ctr + 2, max_long, ctr + 3,
+                      c->d_huge_sorted.as<LongRun>()};
+    SA_CHECK(c, hipMemsetAsync(ctr, 0, 16, st));
     if (pa.total) {
-        hipLaunchKernelGGL(k_replay_aux_long, dim3((uint32_t)max_long), dim3(128), 0, st, c->d_longs.as<LongRun>(),
-                           c->d_nlong.as<uint32_t>(), ak, av, sink_aux, d_err);
-        hipLaunchKernelGGL(k_fill_recip, dim3((uint32_t)((pa.total + 255) / 256)), dim3(256), 0, st, sva,
-                           c->d_prs_aux.as<PRec>());
+        hipLaunchKernelGGL(k_find_runs, dim3((uint32_t)((pa.total / FIND_ITEMS + 255) / 256)), dim3(256), 0, st, sva,
+                           ak, rl);
+        hipLaunchKernelGGL(k_sort_huge, dim3(1), dim3(1024), 0, st, rl);
+        hipLaunchKernelGGL(k_replay_aux_short, dim3(SHORT_GRID), dim3(RP_THREADS), 0, st, sva, ak, av, sink_aux, rl,
+                           d_err);
     }
     SA_CHECK(c, hipGetLastError());
-    ev_finish(c, PH_REPLAY_AUX, st);
+    SA_CHECK(c, hipEventRecord(c->ev_fork_seq, st));
+    hipStream_t st3 = c->st3, st4 = c->st4;
+    SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
+    if (pa.total)
+        hipLaunchKernelGGL(k_replay_aux_long, dim3(LONG_GRID), dim3(128), c->long_lds, st4, rl, ak, av, sink_aux,
+                           d_err);
+    SA_CHECK(c, hipGetLastError());
+    SA_CHECK(c, hipEventRecord(c->ev_long_done, st4));
+    ev_finish(c, PH_REPLAY_AUX, st4);
 
-    // ---- range coders: SEQ tasks [0, nbk) on st3, AUX tasks on st ----
-    const CoderGroup group{st, 0u, (uint32_t)tasks.size(), PH_CODER_R, PH_CODER_L};
-    if (coder_run(c, tasks, cv, &group, 1)) return -1;
+    // ---- range coders: every chain in one launch on st3, longest first
+    //      (concurrent latency-bound launches land on shared SIMDs); the L passes
+    //      after the long runs are done ----
+    SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
+    const CoderGroup group{st3, 0u, (uint32_t)tasks.size(), PH_CODER_R, PH_CODER_L};
+    if (coder_run(c, tasks, cv, &group, 1, c->ev_long_done)) return -1;
 
     // ---- assembly (after MD5) ----
     if (cfg->md5) SA_CHECK(c, hipStreamWaitEvent(st, c->ev_md5_done, 0));

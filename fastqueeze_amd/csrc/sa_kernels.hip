@@ -523,29 +523,116 @@ constexpr int RP_THREADS = 64;
 constexpr int RP_STRIDE = 253;   // >= 256 - RP_REG entries, odd -> conflict-free
 constexpr uint32_t LONG_RUN = 512;
 
+constexpr uint32_t HUGE_RUN = 1u << 16;   // long runs replayed first
+constexpr uint32_t FIND_ITEMS = 16;        // sorted keys per thread in k_find_runs
+
+// Run lists of the AUX space (RunLists in sa_device.h terms):
+//   short: run starts (< LONG_RUN symbols), replayed one lane each;
+//   long:  LongRun entries, the runs of >= HUGE_RUN symbols from the front of
+//          the array, the others from the back, so that the long-run kernel
+//          (a work queue) takes the longest first.
+struct RunLists {
+    uint64_t* short_at;
+    uint32_t* n_short;
+    LongRun* longs;
+    uint32_t* n_huge;
+    uint32_t* n_long;
+    uint64_t cap_long;
+    uint32_t* next;        // work-queue counter of k_replay_aux_long
+    LongRun* huge_sorted;  // the huge runs, longest first (k_sort_huge)
+};
+
+__global__ __launch_bounds__(256) void k_find_runs(const SortView sv, const uint32_t* __restrict__ keys,
+                                                   const RunLists rl)
+{
+    const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * FIND_ITEMS;
+    if (i0 >= sv.total) return;
+    const SortSeg& sg = sv.segs[sv.tile_seg[i0 / SORT_TILE]];   // FIND_ITEMS divides SORT_TILE
+    const size_t end = sg.base + sg.count;
+    uint32_t k[FIND_ITEMS];
+    const uint4* K4 = reinterpret_cast<const uint4*>(keys + i0);
+#pragma unroll
+    for (uint32_t q = 0; q < FIND_ITEMS / 4; q++) {
+        const uint4 a = K4[q];
+        k[4 * q] = a.x; k[4 * q + 1] = a.y; k[4 * q + 2] = a.z; k[4 * q + 3] = a.w;
+    }
+    uint32_t prev = i0 > sg.base ? keys[i0 - 1] >> AUX_SYM_BITS : 0xffffffffu;
+#pragma unroll
+    for (uint32_t e = 0; e < FIND_ITEMS; e++) {
+        const size_t i = i0 + e;
+        const uint32_t model = k[e] >> AUX_SYM_BITS;
+        const bool start = i < end && k[e] != SORT_PAD && model != prev;
+        prev = model;
+        if (!start) continue;
+        if (i + LONG_RUN <= end && (keys[i + LONG_RUN - 1] >> AUX_SYM_BITS) == model) {
+            // run end: galloping then binary search over the sorted keys
+            size_t lo = i + LONG_RUN - 1, step = LONG_RUN, hi;
+            for (;;) {
+                hi = lo + step;
+                if (hi >= end || (keys[hi] >> AUX_SYM_BITS) != model) break;
+                lo = hi;
+                step *= 2;
+            }
+            if (hi > end) hi = end;
+            while (hi - lo > 1) {   // keys[lo] in the run, hi past it (or end)
+                const size_t mid = lo + (hi - lo) / 2;
+                if ((keys[mid] >> AUX_SYM_BITS) == model) lo = mid;
+                else hi = mid;
+            }
+            const LongRun lr{i, hi, sg.base, model, 0};
+            if (hi - i >= HUGE_RUN) rl.longs[atomicAdd(rl.n_huge, 1u)] = lr;
+            else rl.longs[rl.cap_long - 1 - atomicAdd(rl.n_long, 1u)] = lr;
+        } else {
+            rl.short_at[atomicAdd(rl.n_short, 1u)] = i;
+        }
+    }
+}
+
+// The huge runs, longest first (ties by list position), into huge_sorted: one
+// workgroup, rank by counting (up to HUGE_SORT_MAX runs; beyond that the list is
+// copied unsorted).
+constexpr uint32_t HUGE_SORT_MAX = 4096;
+
+__global__ __launch_bounds__(1024) void k_sort_huge(const RunLists rl)
+{
+    __shared__ uint32_t len[HUGE_SORT_MAX];
+    const uint32_t n = *rl.n_huge;
+    if (n > HUGE_SORT_MAX) {
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) rl.huge_sorted[i] = rl.longs[i];
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) len[i] = (uint32_t)(rl.longs[i].end - rl.longs[i].start);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t li = len[i];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < n; j++) {
+            const uint32_t lj = len[j];
+            rank += (lj > li || (lj == li && j < i)) ? 1u : 0u;
+        }
+        rl.huge_sorted[rank] = rl.longs[i];
+    }
+}
+
+// Short runs: a grid of lanes strides over the list; model in LDS, one
+// RP_STRIDE region per lane.
+constexpr uint32_t SHORT_GRID = 1024;
+
 __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView sv, const uint32_t* __restrict__ keys,
                                                                  const uint32_t* __restrict__ vals,
-                                                                 const SymSink rec, LongRun* __restrict__ longs,
-                                                                 uint32_t* __restrict__ nlong,
+                                                                 const SymSink rec, const RunLists rl,
                                                                  uint32_t* __restrict__ err)
 {
     __shared__ uint32_t lds[RP_THREADS * RP_STRIDE];
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= sv.total) return;
-    const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
-    const uint32_t key = keys[i];
-    if (key == SORT_PAD) return;
-    const uint32_t model = key >> AUX_SYM_BITS;
-    if (i != sg.base && (keys[i - 1] >> AUX_SYM_BITS) == model) return;
-    const size_t end = sg.base + sg.count;
-    if (i + LONG_RUN <= end && (keys[i + LONG_RUN - 1] >> AUX_SYM_BITS) == model) {
-        const uint32_t slot = atomicAdd(nlong, 1u);
-        longs[slot] = LongRun{i, end, sg.base, model, 0};
-        return;
-    }
     uint32_t* F = lds + threadIdx.x * RP_STRIDE;
-    const uint32_t e =
-        replay_simple_run(keys, vals, i, end, model, SymSink{rec.prs + sg.base, rec.cum + sg.base}, F);
+    const uint32_t n = *rl.n_short;
+    uint32_t e = 0;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const size_t i = rl.short_at[k];
+        const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
+        e |= replay_simple_run(keys, vals, i, sg.base + sg.count, keys[i] >> AUX_SYM_BITS,
+                               SymSink{rec.prs + sg.base, rec.cum + sg.base}, F);
+    }
     if (e) atomicOr(err, e);
 }
 
@@ -664,6 +751,27 @@ __device__ inline uint32_t uread(const uint32_t* p)   // wave-uniform LDS read
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)*p);
 }
 
+__device__ inline uint32_t bytesum(uint32_t x) { return (x * 0x01010101u) >> 24; }   // sum < 256
+__device__ inline uint32_t bytes_below(uint32_t k) { return k ? 0xffffffffu >> (32 - 8 * k) : 0u; }   // k < 4
+
+// counts by position q < 8 packed one byte each in (lo, hi)
+__device__ inline uint32_t pos_count(uint32_t lo, uint32_t hi, uint32_t q)
+{
+    return q < 8 ? ((q < 4 ? lo : hi) >> (8 * (q & 3))) & 0xffu : 0u;
+}
+__device__ inline uint32_t pos_below(uint32_t lo, uint32_t hi, uint32_t q)   // sum of the counts below q < 8
+{
+    const uint32_t bm = bytes_below(q & 3);
+    return q < 4 ? bytesum(lo & bm) : bytesum(lo) + bytesum(hi & bm);
+}
+
+// One long SIMPLE_MODEL run, 64 symbols per step (see above).  Fast steps --
+// every symbol of the step at a position < 8, no bubble swap, no halving --
+// run on registers: the counts by position are packed bytes scanned over the
+// wave, the freqs and prefixes of positions < 8 live in lanes 0..7 (f8, c8;
+// written through to LDS), the prefixes of positions >= 8 are stored without
+// cadd, and the end-of-step bubble event is checked on registers.  Other steps
+// take the general path.
 template <int NR>
 __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink& rec, uint32_t* __restrict__ err,
                                                 RunModel& md, RunRing& rg)
@@ -682,11 +790,13 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
         md.cpos[k] = k < N ? k : N;
     }
     lds_order();
-    uint32_t tot = N, bub = 0;
+    uint32_t f8 = lane < 8 ? md.fpos[lane] : 0u, c8 = lane < 8 ? md.cpos[lane] : 0u;
+    uint32_t tot = N, bub = 0, cadd = 0;
     bool bad = false;
     size_t base = lr.start;
     uint32_t avail = 0;                                          // windows known published
     uint32_t nxt_rel = 0xffffffffu, nxt_key = 0, nxt_pos = 0;   // next window, read ahead
+    uint32_t tlo = 0, thi = 0;   // the step's counts by position (fast steps)
     auto swap_at = [&](uint32_t P, uint32_t x, uint32_t y) __attribute__((always_inline)) {
         // x at P moves ahead of y at P - 1 (the freqs travel with the symbols)
         if (lane == 0) {
@@ -750,20 +860,32 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
         const uint32_t sym = act ? (key & 0xffu) : 0u;
         if (act && sym >= N) bad = true;
         uint32_t p = md.posr[sym];
-        const uint32_t f0 = md.fpos[p], c0 = md.cpos[p];
-        // the entry in front of each lane's symbol (bubble events)
-        uint32_t fprev = p ? md.fpos[p - 1] : 0u, yprev = p ? md.ent[p - 1] : 0u;
-        // counts: one ballot per distinct symbol of the step
-        uint32_t same = 0, less = 0;
-        uint64_t rem = amask;
-        while (rem) {
-            const int fl = (int)__builtin_ctzll(rem);
-            const uint32_t x = __builtin_amdgcn_readlane(sym, fl), px = __builtin_amdgcn_readlane(p, fl);
-            const uint64_t m = __ballot(act && sym == x);
-            const uint32_t below = lanes_below(m);
-            if (sym == x) same = below;
-            less += px < p ? below : 0u;
-            rem &= ~m;
+        const uint32_t f0 = md.fpos[p], c0 = md.cpos[p] + (p >= 8 ? cadd : 0u);
+        uint32_t fprev = p ? md.fpos[p - 1] : 0u;
+        // Counts.  Fast: every symbol of the step sits at a position < 8 -- one
+        // byte counter per position, packed 4 to a dword, scanned over the wave.
+        // Otherwise one ballot per distinct symbol of the step.
+        const uint64_t hi8 = __ballot(act && p >= 8);
+        uint32_t same = 0, less = 0, inlo = 0, inhi = 0;
+        if (!hi8) {
+            const uint32_t ohlo = act && p < 4 ? 1u << (8 * p) : 0u;
+            const uint32_t ohhi = act && p >= 4 ? 1u << (8 * (p - 4)) : 0u;
+            inlo = wave_incl_scan_dpp(ohlo);
+            inhi = wave_incl_scan_dpp(ohhi);
+            const uint32_t exlo = inlo - ohlo, exhi = inhi - ohhi;
+            same = pos_count(exlo, exhi, p);
+            less = pos_below(exlo, exhi, p);
+        } else {
+            uint64_t rem = amask;
+            while (rem) {
+                const int fl = (int)__builtin_ctzll(rem);
+                const uint32_t x = __builtin_amdgcn_readlane(sym, fl), px = __builtin_amdgcn_readlane(p, fl);
+                const uint64_t m = __ballot(act && sym == x);
+                const uint32_t below = lanes_below(m);
+                if (sym == x) same = below;
+                less += px < p ? below : 0u;
+                rem &= ~m;
+            }
         }
         int32_t cum = (int32_t)(c0 + 8u * less);
         PROF_T(2);
@@ -773,8 +895,17 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
         const uint32_t b0 = 15u - (bub & 15u);
         const uint64_t emask = (0x0001000100010001ull << b0) & ((1ull << (c - 1)) - 1ull);
         uint64_t cand = __ballot(p != 0) & emask;
+        bool swapped = false;
+        if (cand && !hi8) {
+            // fast check of every event against the step-start order: x (this
+            // lane's symbol) after its update vs y (position p - 1) at that time
+            const bool sw = p != 0 && f0 + 8u * (same + 1u) > fprev + 8u * pos_count(inlo, inhi, p - 1u);
+            if (!(__ballot(sw) & cand)) cand = 0;
+        }
         // (LDS fpos holds the step-start freqs until the increments below; the
         // per-lane copies p / fprev / yprev are refreshed after a swap)
+        uint32_t yprev = 0;
+        if (cand) yprev = p ? md.ent[p - 1] : 0u;
         while (cand) {
             const uint32_t b = (uint32_t)__builtin_ctzll(cand);
             cand &= cand - 1;
@@ -786,6 +917,7 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
             const uint64_t mx = __ballot(act && sym == x), my = __ballot(act && sym == y);
             if (fx0 + 8u * (uint32_t)__popcll(mx & upto) > fy0 + 8u * (uint32_t)__popcll(my & upto)) {
                 swap_at(P, x, y);
+                swapped = true;
                 if (lane > b) {
                     const uint32_t bx = lanes_below(mx), by = lanes_below(my);
                     if (sym == y) cum += (int32_t)(fx0 + 8u * bx);
@@ -797,50 +929,75 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
                 cand = __ballot(p != 0) & emask & ~upto;
             }
         }
-        // frequency increments, at the symbols' current positions
-        if (act) __hip_atomic_fetch_add(&md.fpos[p], 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        lds_order();
         PROF_T(3);
         if (act) {
             const uint32_t f = f0 + 8u * same;
             const uint32_t t = tot + 8u * lane;
             if (cum < 0 || (uint32_t)cum + f > t || f == 0) bad = true;
-            rec.prs[pos] = PRec{0u, t | (f << 16)};
+            rec.prs[pos] = PRec{recip32(t), t | (f << 16)};
             rec.cum[pos] = (uint16_t)cum;
         }
         PROF_T(4);
+        // frequency increments: fast steps from the position counts (the prefixes
+        // of positions >= 8 via cadd), else at the symbols' current positions with
+        // a full prefix recompute below
+        bool full = hi8 || swapped;
+        if (!full) {
+            tlo = __builtin_amdgcn_readlane(inlo, (int)(c - 1));
+            thi = __builtin_amdgcn_readlane(inhi, (int)(c - 1));
+            if (lane < 8) {
+                f8 += 8u * pos_count(tlo, thi, lane);
+                c8 += 8u * pos_below(tlo, thi, lane);
+                md.fpos[lane] = f8;
+                md.cpos[lane] = c8;
+            }
+            cadd += 8u * c;
+        } else if (act) {
+            __hip_atomic_fetch_add(&md.fpos[p], 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        lds_order();
         tot += 8u * c;
         bub += c;
-        uint32_t fv[NR];
-#pragma unroll
-        for (int j = 0; j < NR; j++) fv[j] = md.fpos[64u * j + lane];
         if (halve) {
             uint32_t part = 0;
 #pragma unroll
             for (int j = 0; j < NR; j++) {
-                fv[j] -= fv[j] >> 1;
-                md.fpos[64u * j + lane] = fv[j];
-                part += fv[j];
+                const uint32_t v = md.fpos[64u * j + lane];
+                md.fpos[64u * j + lane] = v - (v >> 1);
+                part += v - (v >> 1);
             }
             tot = __builtin_amdgcn_readlane(wave_incl_scan_dpp(part), 63);
             lds_order();
+            full = true;
         }
         if ((bub & 15u) == 0) {   // the step's last update was a bubble event
             const uint32_t x = __builtin_amdgcn_readlane(sym, (int)(c - 1));
-            const uint32_t P = uread(&md.posr[x]);
-            if (P > 0 && uread(&md.fpos[P]) > uread(&md.fpos[P - 1])) {
-                swap_at(P, x, uread(&md.ent[P - 1]));
-#pragma unroll
-                for (int j = 0; j < NR; j++) fv[j] = md.fpos[64u * j + lane];
+            if (!full) {   // from registers: x after the step vs y after the step
+                const uint32_t P = __builtin_amdgcn_readlane(p, (int)(c - 1));
+                const uint32_t fx = __builtin_amdgcn_readlane(f0 + 8u * (same + 1u), (int)(c - 1));
+                const uint32_t fy = __builtin_amdgcn_readlane(fprev, (int)(c - 1)) + 8u * pos_count(tlo, thi, P - 1u);
+                if (P > 0 && fx > fy) {
+                    swap_at(P, x, uread(&md.ent[P - 1]));
+                    full = true;
+                }
+            } else {
+                const uint32_t P = uread(&md.posr[x]);
+                if (P > 0 && uread(&md.fpos[P]) > uread(&md.fpos[P - 1])) swap_at(P, x, uread(&md.ent[P - 1]));
             }
         }
-        // prefix of the freqs by position
-        uint32_t carry = 0;
+        if (full) {   // prefix of the freqs by position
+            uint32_t carry = 0;
 #pragma unroll
-        for (int j = 0; j < NR; j++) {
-            const uint32_t inc = wave_incl_scan_dpp(fv[j]);
-            md.cpos[64u * j + lane] = carry + inc - fv[j];
-            carry += __builtin_amdgcn_readlane(inc, 63);
+            for (int j = 0; j < NR; j++) {
+                const uint32_t fv = md.fpos[64u * j + lane];
+                const uint32_t inc = wave_incl_scan_dpp(fv);
+                md.cpos[64u * j + lane] = carry + inc - fv;
+                carry += __builtin_amdgcn_readlane(inc, 63);
+            }
+            lds_order();
+            cadd = 0;
+            f8 = lane < 8 ? md.fpos[lane] : 0u;
+            c8 = lane < 8 ? md.cpos[lane] : 0u;
         }
         base += c;
         if (lane == 0) lds_publish(&rg.consumed, (uint32_t)(base - lr.start) / 64);
@@ -860,34 +1017,40 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
 #endif
 }
 
-// One workgroup of two waves per long run: wave 0 replays, wave 1 loads.  The
-// grid covers the largest possible number of long runs; the list is filled by
-// k_replay_aux_short, so workgroups beyond its length exit at once.
-__global__ __launch_bounds__(128) void k_replay_aux_long(const LongRun* __restrict__ longs,
-                                                         const uint32_t* __restrict__ nlong,
-                                                         const uint32_t* __restrict__ keys,
+// Workgroups of two waves (wave 0 replays, wave 1 loads) take long runs from
+// a work queue, the runs of >= HUGE_RUN symbols first.
+constexpr uint32_t LONG_GRID = 2048;
+
+__global__ __launch_bounds__(128) void k_replay_aux_long(const RunLists rl, const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, const SymSink rec_all,
                                                          uint32_t* __restrict__ err)
 {
     __shared__ RunModel md;
     __shared__ RunRing rg;
-    if (blockIdx.x >= *nlong) return;
-    const LongRun lr = longs[blockIdx.x];
-    if (threadIdx.x == 0) {
-        rg.filled = 0;
-        rg.consumed = 0;
-        rg.done = 0;
+    __shared__ uint32_t job;
+    const uint32_t nh = *rl.n_huge, n = nh + *rl.n_long;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            job = atomicAdd(rl.next, 1u);
+            rg.filled = 0;
+            rg.consumed = 0;
+            rg.done = 0;
+        }
+        __syncthreads();
+        const uint32_t r = job;
+        if (r >= n) break;
+        const LongRun lr = r < nh ? rl.huge_sorted[r] : rl.longs[rl.cap_long - 1 - (r - nh)];
+        if (threadIdx.x >= 64) {
+            run_loader(lr, keys, vals, rg, AUX_SYM_BITS);
+        } else {
+            const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base};
+            const uint32_t N = model_nsym(lr.model);
+            if (N <= 64) replay_long_run<1>(lr, rec, err, md, rg);
+            else if (N <= 128) replay_long_run<2>(lr, rec, err, md, rg);
+            else replay_long_run<4>(lr, rec, err, md, rg);
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x >= 64) {
-        run_loader(lr, keys, vals, rg, AUX_SYM_BITS);
-        return;
-    }
-    const SymSink rec{rec_all.prs + lr.rec_base, rec_all.cum + lr.rec_base};
-    const uint32_t N = model_nsym(lr.model);
-    if (N <= 64) replay_long_run<1>(lr, rec, err, md, rg);
-    else if (N <= 128) replay_long_run<2>(lr, rec, err, md, rg);
-    else replay_long_run<4>(lr, rec, err, md, rg);
 }
 
 // ---------------------------------------------------------------------------
@@ -1030,9 +1193,33 @@ __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t 
 #define SA_CHUNK_STEPS(X, j0)                                                         \
     _Pragma("unroll") for (int j = (j0); j < 16; j++) rc_range_salu(r, X.w[2 * j], X.w[2 * j + 1])
 
+// Pass R may start before the model replays have written every record (the
+// long runs are replayed concurrently): the record arrays are zeroed first, a
+// written record has m >= 1, and an unwritten one (m = 0) sends the range to 0,
+// where it stays -- a range chain never reaches 0 otherwise (q >= 1, f >= 1).
+// So a segment that ends with r == 0 is re-coded from its start once its
+// records are in, read through L2 (the scalar cache may hold the zeros).
+__device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t& bad)
+{
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+        const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(P + lane), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t m = (uint32_t)v, tf = (uint32_t)(v >> 32);
+        uint32_t r = r0;
+#pragma unroll 8
+        for (int k = 0; k < 64; k++)
+            rc_range_salu(r, __builtin_amdgcn_readlane(m, k), __builtin_amdgcn_readlane(tf, k));
+        if (r != 0) return r;
+        __builtin_amdgcn_s_sleep(32);
+    }
+    bad = 1;
+    return r0;
+}
+
 __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ tasks, const TaskList tl,
                                                 const PRec* __restrict__ prs0, const PRec* __restrict__ prs1,
-                                                uint32_t* __restrict__ ck_r)
+                                                uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err)
 {
     const uint32_t li = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -1048,12 +1235,14 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
     if (g < last) {
         const PChunk* C = reinterpret_cast<const PChunk*>(P + (size_t)g * SEG_SYMS);
         PChunk A = C[0], B;
+        uint32_t bad = 0;
         for (; g < last; g++, C += 4) {
             kv = lane == (g & 63) ? r : kv;
             if ((g & 63) == 63) {
                 const uint32_t s = g - 63 + lane;
                 if (s >= first) ck[s] = kv;
             }
+            const uint32_t r_seg = r;
             rc_range_salu(r, A.w[0], A.w[1]);
             __builtin_amdgcn_sched_barrier(0);
             B = C[1];
@@ -1074,7 +1263,9 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
             A = C[4];   // the next segment (the record arrays carry >= 64 records of slack)
             __builtin_amdgcn_sched_barrier(0);
             SA_CHUNK_STEPS(B, 1);
+            if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, bad);
         }
+        if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
     }
     kv = lane == (g & 63) ? r : kv;
     const uint32_t s = (g & ~63u) + lane;
