@@ -598,7 +598,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     // ---- device buffers ----
     // slack: the replay loops read up to 2 chunks past a run's end, pass R one
     // 16-record chunk past a stream's last full segment
-    const uint64_t stot = ps.total + 128, atot = pa.total + 128;
+    const uint64_t stot = ps.total + KEY_SLACK, atot = pa.total + KEY_SLACK;
     for (int i = 0; i < 2; i++) {
         SA_CHECK(c, c->d_seq_k[i].ensure(stot * 4));
         SA_CHECK(c, c->d_seq_v[i].ensure(stot * 4));
@@ -607,7 +607,6 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     }
     SA_CHECK(c, c->d_prs_seq.ensure(stot * sizeof(PRec)));
     SA_CHECK(c, c->d_prs_aux.ensure(atot * sizeof(PRec)));
-    SA_CHECK(c, c->d_cum_seq.ensure(stot * 2));
     SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
     const uint64_t max_long = pa.total / LONG_RUN + 1;
     SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
@@ -649,7 +648,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     cv.tasks = c->d_tasks.as<CoderTask>();
     cv.prs[0] = c->d_prs_seq.as<PRec>();
     cv.prs[1] = c->d_prs_aux.as<PRec>();
-    cv.cum[0] = c->d_cum_seq.as<uint16_t>();
+    cv.cum[0] = nullptr;   // packed SEQ records
     cv.cum[1] = c->d_cum_aux.as<uint16_t>();
     cv.out = c->d_payload.as<uint8_t>();
     cv.out_len = c->d_out_len.as<uint32_t>();
@@ -657,10 +656,15 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
 
     // ---- emit (main stream) ----
     ev_begin(c, PH_EMIT, st);
-    SA_CHECK(c, hipMemsetAsync(c->d_seq_k[0].p, 0xff, stot * 4, st));
-    SA_CHECK(c, hipMemsetAsync(c->d_aux_k[0].p, 0xff, atot * 4, st));
-    SA_CHECK(c, hipMemsetAsync(c->d_seq_k[1].p, 0xff, stot * 4, st));
-    SA_CHECK(c, hipMemsetAsync(c->d_aux_k[1].p, 0xff, atot * 4, st));
+    {
+        const SortView pv_s{c->d_segs_seq.as<SortSeg>(), nullptr, nullptr, ps.total, 0u, nbk};
+        const SortView pv_a{c->d_segs_aux.as<SortSeg>(), nullptr, nullptr, pa.total, 0u, nbk};
+        const uint32_t pgrid = (uint32_t)(((uint64_t)(nbk + 1) * SORT_TILE + 255) / 256);
+        hipLaunchKernelGGL(k_pad_keys, dim3(pgrid), dim3(256), 0, st, pv_s, c->d_seq_k[0].as<uint32_t>(),
+                           c->d_seq_k[1].as<uint32_t>());
+        hipLaunchKernelGGL(k_pad_keys, dim3(pgrid), dim3(256), 0, st, pv_a, c->d_aux_k[0].as<uint32_t>(),
+                           c->d_aux_k[1].as<uint32_t>());
+    }
     SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
     if (nr) {
         hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
@@ -677,7 +681,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
                  ps.total, (uint32_t)ps.tile_seg.size(), nbk};
     SortView sva{c->d_segs_aux.as<SortSeg>(), c->d_tile_aux.as<uint32_t>(), c->d_hist_aux.as<uint32_t>(),
                  pa.total, (uint32_t)pa.tile_seg.size(), nbk};
-    const SymSink sink_seq{c->d_prs_seq.as<PRec>(), c->d_cum_seq.as<uint16_t>()};
+    const SymSink sink_seq{c->d_prs_seq.as<PRec>(), nullptr};   // packed
     const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>()};
 
     // ---- throughput phases on st (each fills the GPU): SEQ sort and BASE_MODEL
@@ -816,7 +820,7 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
         CoderTask& tk = tasks[(size_t)s];
         tk.rec_base = nsym;
         tk.n = lens[s];
-        tk.space = 0;
+        tk.space = 1;   // wide records
         tk.nseg = tk.n ? (tk.n + SEG_SYMS - 1) / SEG_SYMS : 1;
         tk.seg_base = segs;
         tk.out_base = payload;

@@ -33,13 +33,13 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v)
     return v;
 }
 
-// inclusive add-scan of a wave64 on DPP (row shifts, then row broadcasts 15/31):
-// register-to-register, no LDS round trip
 __device__ inline uint32_t lanes_below(uint64_t m)   // popc(m & ((1 << lane) - 1))
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// inclusive add-scan of a wave64 on DPP (row shifts, then row broadcasts 15/31):
+// register-to-register, no LDS round trip
 __device__ inline uint32_t wave_incl_scan_dpp(uint32_t v)
 {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
@@ -69,6 +69,19 @@ __device__ inline uint32_t wg1024_excl_scan(uint32_t v, uint32_t& excl, uint32_t
     excl = wpre + inc - v;
     __syncthreads();
     return total;
+}
+
+// exclusive scan across a 256-thread workgroup (called once per kernel: sh is
+// not reset)
+__device__ inline void wg256_excl_scan(uint32_t v, uint32_t& excl, uint32_t* sh /*4*/)
+{
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan_dpp(v);
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (uint32_t k = 0; k < w; k++) wpre += sh[k];
+    excl = wpre + inc - v;
 }
 
 // ---------------------------------------------------------------------------
@@ -274,12 +287,34 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
     }
 }
 
+// SORT_PAD into the key slots no symbol is written to: each segment's tail up to
+// its last tile (ping buffer), and the slack slots past the space (both buffers;
+// the replays read past a run's end).
+constexpr uint32_t KEY_SLACK = 128;
+
+__global__ __launch_bounds__(256) void k_pad_keys(const SortView sv, uint32_t* __restrict__ k0,
+                                                  uint32_t* __restrict__ k1)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t seg = i / SORT_TILE, off = i % SORT_TILE;
+    if (seg < sv.nsegs) {
+        const SortSeg& g = sv.segs[seg];
+        const uint64_t pos = g.base + g.count + off;
+        if (pos < g.base + (uint64_t)g.ntiles * SORT_TILE) k0[pos] = SORT_PAD;
+    } else if (seg == sv.nsegs && off < KEY_SLACK) {
+        k0[sv.total + off] = SORT_PAD;
+        k1[sv.total + off] = SORT_PAD;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Segmented stable LSD radix sort (8-bit digits).
 // A segment is one block's symbol space, padded with key 0xffffffff to a whole
 // number of tiles.  Tile = 256 threads x 16 keys; each wave owns 1024
 // consecutive keys processed in 16 rounds of 64, ranked with an 8-ballot
-// match (the wavefront "multi-split"), so the scatter is stable.
+// match (the wavefront "multi-split"), so the scatter is stable.  The scatter
+// stages the tile in digit order in LDS and writes each digit's run with
+// consecutive threads.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, const uint32_t* __restrict__ keys,
                                                             uint32_t shift)
@@ -336,6 +371,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
                                                                uint32_t* __restrict__ vout, uint32_t shift)
 {
     __shared__ uint32_t wc[SORT_THREADS / 64][256];
+    __shared__ uint32_t lstart[256], gstart[256], dsum[SORT_THREADS / 64];
+    __shared__ uint32_t sk[SORT_TILE], svl[SORT_TILE];
     const uint32_t t = blockIdx.x;
     const SortSeg& sg = sv.segs[sv.tile_seg[t]];
     const uint32_t lt = t - sg.tile0;
@@ -365,22 +402,40 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     }
     __syncthreads();
     {
+        // per digit: the tile's count, each wave's start within the tile's run of
+        // that digit, the run's start in the tile (scan over digits) and in the
+        // output (the scanned histogram)
         const uint32_t d = threadIdx.x;   // SORT_THREADS == 256 digits
-        uint32_t acc = sv.hist[sg.hist_base + (size_t)d * sg.ntiles + lt];
+        uint32_t acc = 0;
 #pragma unroll
         for (int ww = 0; ww < SORT_THREADS / 64; ww++) {
-            uint32_t tcount = wc[ww][d];
+            const uint32_t tcount = wc[ww][d];
             wc[ww][d] = acc;
             acc += tcount;
         }
+        uint32_t ex;
+        wg256_excl_scan(acc, ex, dsum);
+        lstart[d] = ex;
+        gstart[d] = sv.hist[sg.hist_base + (size_t)d * sg.ntiles + lt] - ex;
+    }
+    __syncthreads();
+    // stage the tile in digit order in LDS, then write it out: consecutive
+    // threads write consecutive slots of one digit's run (coalesced)
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+        const uint32_t d = (k[r] >> shift) & 255;
+        const uint32_t at = lstart[d] + wc[w][d] + rk[r];
+        sk[at] = k[r];
+        svl[at] = v[r];
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t d = (k[r] >> shift) & 255;
-        const size_t dst = sg.base + wc[w][d] + rk[r];
-        kout[dst] = k[r];
-        vout[dst] = v[r];
+        const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
+        const uint32_t kk = sk[i];
+        const size_t dst = sg.base + gstart[(kk >> shift) & 255] + i;
+        kout[dst] = kk;
+        vout[dst] = svl[i];
     }
 }
 
@@ -488,7 +543,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
     if (!run.head) run.cnt += carry_cnt;   // still inside the run continued from the previous tile
     uint64_t cnt = run.cnt;
     pk = prev_key;
-    const SymSink out{rec.prs + sg.base, rec.cum + sg.base};
+    const SymSink out{rec.prs + sg.base, nullptr};   // packed SEQ records
 #pragma unroll
     for (int e = 0; e < SORT_ITEMS; e++) {
         if (k[e] != pk) cnt = 0;
@@ -649,8 +704,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_replay_aux_short(const SortView 
 // swaps at most one adjacent pair (x ahead of y); lanes after it that hold y
 // gain freq_x, lanes that hold x lose freq_y.  Only events whose symbol is not
 // already in front are visited.  Model state (RunModel) lives in LDS; the
-// prefix of the freqs by position is a DPP scan.  Records are written without
-// the reciprocal (k_fill_recip adds it).
+// prefix of the freqs by position is a DPP scan.
 
 // Orders this wave's LDS accesses for the compiler only: one wave's LDS
 // operations are performed in issue order, so no s_waitcnt is needed (a
@@ -1138,24 +1192,10 @@ __global__ __launch_bounds__(128) void k_replay_seq_long(const SortView sv, cons
         }
         __syncthreads();
         if (threadIdx.x >= 64) run_loader(lr, keys, vals, rg, 0);
-        else replay_seq_long_run(lr, SymSink{rec_all.prs + sg.base, rec_all.cum + sg.base}, rg, bad);
+        else replay_seq_long_run(lr, SymSink{rec_all.prs + sg.base, nullptr}, rg, bad);
         __syncthreads();
     }
     if (threadIdx.x < 64 && __ballot(bad) && threadIdx.x == 0) atomicOr(err, (uint32_t)E_CODER);
-}
-
-// Reciprocal of every AUX record written without one: m = ceil(2^32 / tot).
-__global__ __launch_bounds__(256) void k_fill_recip(const SortView sv, PRec* __restrict__ prs)
-{
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= sv.total) return;
-    const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
-    if (i >= sg.base + sg.count) return;
-    PRec r = prs[i];
-    if (r.m == 0u) {
-        r.m = recip32(r.tf & 0xffffu);
-        prs[i] = r;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1171,11 +1211,11 @@ struct PChunk {
     uint32_t w[32];   // 16 PRec
 };
 
-__device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t tf)
+__device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t tf, uint32_t tmask)
 {
     uint32_t t, f, q, p;
     asm volatile(
-        "s_and_b32 %1, %5, 0xffff\n\t"
+        "s_and_b32 %1, %5, %7\n\t"
         "s_lshr_b32 %2, %5, 16\n\t"
         "s_mul_hi_u32 %3, %0, %6\n\t"
         "s_mul_i32 %4, %3, %1\n\t"
@@ -1186,12 +1226,12 @@ __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t 
         "s_and_b32 %4, %4, 24\n\t"
         "s_lshl_b32 %0, %3, %4"
         : "+s"(r), "=&s"(t), "=&s"(f), "=&s"(q), "=&s"(p)
-        : "s"(tf), "s"(m)
+        : "s"(tf), "s"(m), "s"(tmask)
         : "scc");
 }
 
 #define SA_CHUNK_STEPS(X, j0)                                                         \
-    _Pragma("unroll") for (int j = (j0); j < 16; j++) rc_range_salu(r, X.w[2 * j], X.w[2 * j + 1])
+    _Pragma("unroll") for (int j = (j0); j < 16; j++) rc_range_salu(r, X.w[2 * j], X.w[2 * j + 1], tmask)
 
 // Pass R may start before the model replays have written every record (the
 // long runs are replayed concurrently): the record arrays are zeroed first, a
@@ -1199,7 +1239,7 @@ __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t 
 // where it stays -- a range chain never reaches 0 otherwise (q >= 1, f >= 1).
 // So a segment that ends with r == 0 is re-coded from its start once its
 // records are in, read through L2 (the scalar cache may hold the zeros).
-__device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t& bad)
+__device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t tmask, uint32_t& bad)
 {
     const uint32_t lane = threadIdx.x;
     for (uint32_t spin = 0; spin < (1u << 22); spin++) {
@@ -1209,7 +1249,7 @@ __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t&
         uint32_t r = r0;
 #pragma unroll 8
         for (int k = 0; k < 64; k++)
-            rc_range_salu(r, __builtin_amdgcn_readlane(m, k), __builtin_amdgcn_readlane(tf, k));
+            rc_range_salu(r, __builtin_amdgcn_readlane(m, k), __builtin_amdgcn_readlane(tf, k), tmask);
         if (r != 0) return r;
         __builtin_amdgcn_s_sleep(32);
     }
@@ -1227,6 +1267,7 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
     const CoderTask tk = tasks[t];
     const CoderRun run = tl.run[li];
     const PRec* P = (tk.space ? prs1 : prs0) + tk.rec_base;
+    const uint32_t tmask = tk.space ? 0xffffu : 0xffu;   // wide AUX / packed SEQ records
     uint32_t* ck = ck_r + tk.seg_base;
     const uint32_t first = run.start_seg, last = tk.nseg - 1;
     uint32_t r = run.r0;
@@ -1243,27 +1284,27 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
                 if (s >= first) ck[s] = kv;
             }
             const uint32_t r_seg = r;
-            rc_range_salu(r, A.w[0], A.w[1]);
+            rc_range_salu(r, A.w[0], A.w[1], tmask);
             __builtin_amdgcn_sched_barrier(0);
             B = C[1];
             __builtin_amdgcn_sched_barrier(0);
             SA_CHUNK_STEPS(A, 1);
-            rc_range_salu(r, B.w[0], B.w[1]);
+            rc_range_salu(r, B.w[0], B.w[1], tmask);
             __builtin_amdgcn_sched_barrier(0);
             A = C[2];
             __builtin_amdgcn_sched_barrier(0);
             SA_CHUNK_STEPS(B, 1);
-            rc_range_salu(r, A.w[0], A.w[1]);
+            rc_range_salu(r, A.w[0], A.w[1], tmask);
             __builtin_amdgcn_sched_barrier(0);
             B = C[3];
             __builtin_amdgcn_sched_barrier(0);
             SA_CHUNK_STEPS(A, 1);
-            rc_range_salu(r, B.w[0], B.w[1]);
+            rc_range_salu(r, B.w[0], B.w[1], tmask);
             __builtin_amdgcn_sched_barrier(0);
             A = C[4];   // the next segment (the record arrays carry >= 64 records of slack)
             __builtin_amdgcn_sched_barrier(0);
             SA_CHUNK_STEPS(B, 1);
-            if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, bad);
+            if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
         }
         if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
     }
@@ -1295,7 +1336,8 @@ __global__ __launch_bounds__(256) void k_coder_l1(const CoderView cv, const Task
     const uint32_t g = tl.run[li].start_seg + (uint32_t)(gi - tl.gbase[li]);
     const size_t at = tk.rec_base + (size_t)g * SEG_SYMS;
     cv.maps[tk.seg_base + g] =
-        seg_lowmap(cv.prs[tk.space] + at, cv.cum[tk.space] + at, cv.ck_r[tk.seg_base + g], seg_count(tk.n, g));
+        seg_lowmap(cv.prs[tk.space] + at, cv.cum[tk.space] ? cv.cum[tk.space] + at : nullptr,
+                   cv.ck_r[tk.seg_base + g], seg_count(tk.n, g));
 }
 
 // L2: one workgroup per listed stream: exclusive scan of the segment maps from
@@ -1371,7 +1413,8 @@ __global__ __launch_bounds__(256) void k_coder_l3(const CoderView cv, const Task
     const uint64_t sg = tk.seg_base + g;
     const uint32_t off = cv.off_at[sg];
     const bool last = g + 1 == tk.nseg;
-    const SegEnd e = seg_code(cv.prs[tk.space] + at, cv.cum[tk.space] + at, cv.ck_r[sg], cv.low_at[sg],
+    const SegEnd e = seg_code(cv.prs[tk.space] + at, cv.cum[tk.space] ? cv.cum[tk.space] + at : nullptr,
+                              cv.ck_r[sg], cv.low_at[sg],
                               seg_count(tk.n, g), cv.out + tk.out_base + off, tk.out_cap > off ? tk.out_cap - off : 0,
                               last);
     if (last) cv.out_len[t] = off + e.nbytes;

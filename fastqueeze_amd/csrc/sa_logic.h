@@ -384,11 +384,21 @@ SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, siz
 // ceil(2^32 / t) for 2 <= t < 2^32 (t = 2^32 = a t + b: b > 0 -> a + 1; b = 0 -> a)
 SA_HD uint32_t recip32(uint32_t t) { return 0xffffffffu / t + 1u; }
 
+// Two record formats.  Wide (AUX, SIMPLE_MODEL totals up to 0xffe0):
+// tf = t | f << 16, cum in its own array.  Packed (SEQ, BASE_MODEL: t <= 253):
+// tf = t | cum << 8 | f << 16 and no cum array (SymSink::cum == nullptr), one
+// scattered store per symbol instead of two.
 SA_HD void sink_put(const SymSink& o, uint32_t pos, uint32_t cum, uint32_t f, uint32_t t)
 {
-    o.prs[pos] = PRec{recip32(t), t | (f << 16)};
-    o.cum[pos] = (uint16_t)cum;
+    if (!o.cum) {
+        o.prs[pos] = PRec{recip32(t), t | (cum << 8) | (f << 16)};
+    } else {
+        o.prs[pos] = PRec{recip32(t), t | (f << 16)};
+        o.cum[pos] = (uint16_t)cum;
+    }
 }
+
+SA_HD uint32_t rec_tmask(const uint16_t* cum) { return cum ? 0xffffu : 0xffu; }
 
 SA_HD uint32_t clz32(uint32_t v)
 {
@@ -402,9 +412,9 @@ SA_HD uint32_t clz32(uint32_t v)
 SA_HD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
 // one symbol of the range chain; returns q, updates r, sets n (bytes shifted)
-SA_HD uint32_t range_step(uint32_t& r, const PRec p, uint32_t& n)
+SA_HD uint32_t range_step(uint32_t& r, const PRec p, uint32_t tmask, uint32_t& n)
 {
-    const uint32_t t = p.tf & 0xffffu, f = p.tf >> 16;
+    const uint32_t t = p.tf & tmask, f = p.tf >> 16;
     uint32_t q = mulhi32(r, p.m);
     q -= (r < q * t) ? 1u : 0u;
     const uint32_t rr = q * f;
@@ -433,7 +443,7 @@ SA_HD LowMap lowmap_compose(const LowMap& a, const LowMap& b)
 // chunk re-reads record n - 1 instead of reading past the segment.
 constexpr uint32_t RC_CHUNK = 16;
 
-template <class Fn>
+template <bool PACKED, class Fn>
 SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
 {
     for (uint32_t b = 0; b < n; b += RC_CHUNK) {
@@ -443,7 +453,8 @@ SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
         for (uint32_t k = 0; k < RC_CHUNK; k++) {
             const uint32_t i = b + k < n ? b + k : n - 1;
             p[k] = P[i];
-            c[k] = cum[i];
+            if constexpr (PACKED) c[k] = (p[k].tf >> 8) & 0xffu;
+            else c[k] = cum[i];
         }
 #pragma unroll
         for (uint32_t k = 0; k < RC_CHUNK; k++)
@@ -451,14 +462,16 @@ SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
     }
 }
 
-SA_HD LowMap seg_lowmap(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
+template <bool PACKED>
+SA_HD LowMap seg_lowmap_t(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
 {
     LowMap m{0ull, 0u, 0u};
     uint64_t low = 0;
     uint32_t sbits = 0;
-    seg_for_each(P, cum, n, [&](const PRec pr, uint32_t c) {
+    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
+    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t c) {
         uint32_t nb;
-        const uint32_t q = range_step(r, pr, nb);
+        const uint32_t q = range_step(r, pr, tmask, nb);
         low = shl64(low + (uint64_t)c * q, 8 * nb);
         sbits += 8 * nb;
         m.nbytes += nb;
@@ -481,13 +494,15 @@ struct SegEnd {
 
 SA_HD uint32_t seg_count(uint32_t n, uint32_t seg) { return n - seg * SEG_SYMS < SEG_SYMS ? n - seg * SEG_SYMS : SEG_SYMS; }
 
-SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
-                      uint64_t cap, bool finish)
+template <bool PACKED>
+SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
+                        uint64_t cap, bool finish)
 {
     SegEnd e{0, 0, 0, 0};
     uint32_t op = 0;
-    seg_for_each(P, cum, n, [&](const PRec pr, uint32_t c) {
-        const uint32_t t = pr.tf & 0xffffu, f = pr.tf >> 16;
+    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
+    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t c) {
+        const uint32_t t = pr.tf & tmask, f = pr.tf >> 16;
         uint32_t q = mulhi32(r, pr.m);
         q -= (r < q * t) ? 1u : 0u;
         low += (uint64_t)c * q;
@@ -514,6 +529,17 @@ SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t l
     e.r = r;
     e.nbytes = op;
     return e;
+}
+
+// cum == nullptr: packed (SEQ) records
+SA_HD LowMap seg_lowmap(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
+{
+    return cum ? seg_lowmap_t<false>(P, cum, r, n) : seg_lowmap_t<true>(P, cum, r, n);
+}
+SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
+                      uint64_t cap, bool finish)
+{
+    return cum ? seg_code_t<false>(P, cum, r, low, n, o, cap, finish) : seg_code_t<true>(P, cum, r, low, n, o, cap, finish);
 }
 
 // ---- block assembly plan (k_assemble; doFqzEncode@0x42d2d0) ----------------

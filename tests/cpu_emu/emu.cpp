@@ -54,11 +54,11 @@ static uint32_t code_decomposed(const PRec* P, const uint16_t* C, uint32_t n, ui
             if (g + 1 < nseg)
                 for (uint32_t i = 0; i < SEG_SYMS; i++) {
                     uint32_t nb;
-                    range_step(r, P[g * SEG_SYMS + i], nb);
+                    range_step(r, P[g * SEG_SYMS + i], rec_tmask(C), nb);
                 }
         }
         for (uint32_t g = start; g < nseg; g++)
-            mp[g] = seg_lowmap(P + g * SEG_SYMS, C + g * SEG_SYMS, ck[g], seg_count(n, g));
+            mp[g] = seg_lowmap(P + g * SEG_SYMS, C ? C + g * SEG_SYMS : nullptr, ck[g], seg_count(n, g));
         uint64_t low = low0;
         uint32_t off = off0;
         for (uint32_t g = start; g < nseg; g++) {
@@ -71,7 +71,8 @@ static uint32_t code_decomposed(const PRec* P, const uint16_t* C, uint32_t n, ui
         SegEnd sqe{};
         for (uint32_t g = start; g < nseg; g++) {
             const uint64_t room = cap > offat[g] ? cap - offat[g] : 0;
-            SegEnd e = seg_code(P + g * SEG_SYMS, C + g * SEG_SYMS, ck[g], lowat[g], seg_count(n, g), o + offat[g], room,
+            SegEnd e = seg_code(P + g * SEG_SYMS, C ? C + g * SEG_SYMS : nullptr, ck[g], lowat[g], seg_count(n, g),
+                                o + offat[g], room,
                                 g + 1 == nseg);
             if (g + 1 == nseg) out_len = offat[g] + e.nbytes;
             if (e.squeezed && sq < 0) { sq = g; sqe = e; }
@@ -299,7 +300,7 @@ int main(int argc, char** argv)
     std::vector<uint16_t> cs(stot), ca(atot);
     std::vector<uint32_t> F(256);
     for (const SortSeg& g : bp.seq.segs) {
-        const SymSink sink{ps.data() + g.base, cs.data() + g.base};
+        const SymSink sink{ps.data() + g.base, nullptr};   // packed SEQ records
         for (size_t i = g.base; i < g.base + g.count; i++)
             if (i == g.base || sk[i - 1] != sk[i]) replay_seq_run(sk.data(), sv.data(), i, g.base + g.count, sk[i], sink);
     }
@@ -318,7 +319,7 @@ int main(int argc, char** argv)
     for (size_t t = 0; t < bp.tasks.size(); t++) {
         const CoderTask& tk = bp.tasks[t];
         const PRec* P = (tk.space ? pa.data() : ps.data()) + tk.rec_base;
-        const uint16_t* C = (tk.space ? ca.data() : cs.data()) + tk.rec_base;
+        const uint16_t* C = tk.space ? ca.data() + tk.rec_base : nullptr;   // SEQ: packed records
         uint8_t* o = payload.data() + tk.out_base;
         out_len[t] = code_decomposed(P, C, tk.n, o, tk.out_cap, restarts);
         std::vector<uint8_t> ser(tk.out_cap);
