@@ -211,7 +211,8 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
     if (!tl.count) return;
     if (ph >= 0) ev_begin(c, ph, st);
     hipLaunchKernelGGL(k_coder_r, dim3(tl.count), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r,
-                       c->d_err.as<uint32_t>());
+                       c->d_err.as<uint32_t>(), reinterpret_cast<const uint2*>(cv.prs[0]),
+                       reinterpret_cast<const uint2*>(cv.prs[1]));
     if (ph >= 0) ev_finish(c, ph, st);
 }
 

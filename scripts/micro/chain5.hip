@@ -60,14 +60,17 @@ __device__ __forceinline__ void first(uint32_t& r, const Chunk<W>& A)
     else step3(r, A.w[0], A.w[1], A.w[2]);
 }
 
-template <int W>
+template <int W, int PF = 0>
 __global__ __launch_bounds__(64) void k_passr(const Chunk<W>* __restrict__ chunks, uint32_t nchunks,
-                                              uint32_t* __restrict__ ckpt, uint32_t* res)
+                                              uint32_t* __restrict__ ckpt, uint32_t* res,
+                                              const uint32_t* __restrict__ pfp = nullptr)
 {
+    uint32_t pf_acc = 0, pf_prev = 0;
     const uint32_t lane = threadIdx.x;
     const Chunk<W>* C = chunks + (size_t)blockIdx.x * (nchunks + 4);
     uint32_t* K = ckpt + (size_t)blockIdx.x * (nchunks / 4 + 64);
     uint32_t r = 0xffffffffu, kv = 0;
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), t0 = __builtin_amdgcn_s_memrealtime();
     Chunk<W> A = C[0], B;
     for (uint32_t c = 0; c < nchunks; c += 2) {
         first<W>(r, A);   // waits for A; then B is requested while A is coded
@@ -80,13 +83,23 @@ __global__ __launch_bounds__(64) void k_passr(const Chunk<W>* __restrict__ chunk
         A = C[c + 2];
         __builtin_amdgcn_sched_barrier(0);
         steps<W>(r, B, 1);
+        if (PF > 0 && c + PF + 2 <= nchunks) {   // touch the records PF chunks ahead (lane-parallel: 2 chunks) into L2
+            pf_acc += pf_prev;
+            pf_prev = pfp[(size_t)blockIdx.x * (nchunks + 4) * (16 * W) + (size_t)(c + PF) * (16 * W) + lane];
+        }
         if ((c & 3) == 2) {
             const uint32_t slot = (c >> 2) & 63;
             kv = lane == slot ? r : kv;
             if (slot == 63) K[(c >> 2) - 63 + lane] = kv;
         }
     }
-    if (lane == 0) res[blockIdx.x] = r;
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), t1 = __builtin_amdgcn_s_memrealtime();
+    if (pf_acc + pf_prev == 0x12345678u) res[8000] = 1;   // keeps the prefetch loads
+    if (lane == 0) {
+        res[blockIdx.x] = r;
+        res[4096 + 2 * blockIdx.x] = (uint32_t)(c1 - c0);
+        res[4096 + 2 * blockIdx.x + 1] = (uint32_t)(t1 - t0);
+    }
 }
 
 // 3-dword records, 8 per chunk, three chunks in flight (SGPR budget: 72 of 102)
@@ -132,7 +145,7 @@ template <int W>
 int run(const char* name)
 {
     const uint32_t nchunks = 65536;   // 1M symbols per stream
-    const int NS = 128;
+    const int NS = 256;
     std::vector<Chunk<W>> h((size_t)(nchunks + 4) * NS);
     std::vector<uint32_t> tt((size_t)(nchunks + 4) * 16 * NS), ff(tt.size());
     uint32_t x = 777;
@@ -147,16 +160,59 @@ int run(const char* name)
         }
     Chunk<W>* d; uint32_t *dk, *dres;
     CK(hipMalloc(&d, h.size() * sizeof(Chunk<W>)));
-    CK(hipMalloc(&dk, (size_t)NS * (nchunks / 4 + 64) * 4)); CK(hipMalloc(&dres, 4096 * 4));
+    CK(hipMalloc(&dk, (size_t)NS * (nchunks / 4 + 64) * 4)); CK(hipMalloc(&dres, 3 * 4096 * 4));
     CK(hipMemcpy(d, h.data(), h.size() * sizeof(Chunk<W>), hipMemcpyHostToDevice));
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     float ms;
-    for (int lds : {0, 96 * 1024})
-    for (int w : {1, 32, NS}) {
+    for (int pfv : {0, 8, 32}) {
+        for (int w : {32, 64, 128}) {
+            auto kern = pfv == 0 ? k_passr<W, 0> : pfv == 8 ? k_passr<W, 8> : k_passr<W, 32>;
+            hipLaunchKernelGGL(kern, dim3(w), dim3(64), 0, 0, d, nchunks, dk, dres, (const uint32_t*)d);
+            CK(hipEventRecord(a)); hipLaunchKernelGGL(kern, dim3(w), dim3(64), 0, 0, d, nchunks, dk, dres, (const uint32_t*)d); CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
+            printf("%s prefetch %2d chunks ahead, streams=%3d : %.2f ns/sym\n", name, pfv, w, ms * 1e6 / (nchunks * 16.0));
+        }
+    }
+    for (int lds : {0})
+    for (int w : {1}) {
         hipLaunchKernelGGL(k_passr<W>, dim3(w), dim3(64), lds, 0, d, nchunks, dk, dres);
         CK(hipEventRecord(a)); hipLaunchKernelGGL(k_passr<W>, dim3(w), dim3(64), lds, 0, d, nchunks, dk, dres); CK(hipEventRecord(b));
         CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
-        printf("%s streams=%3d lds=%6d : %.2f ns/sym/stream\n", name, w, lds, ms * 1e6 / (nchunks * 16.0));
+        std::vector<uint32_t> cr(2 * w);
+        CK(hipMemcpy(cr.data(), dres + 4096, 8 * w, hipMemcpyDeviceToHost));
+        double cyc = 0, rt = 0;
+        for (int i = 0; i < w; i++) { cyc += cr[2 * i]; rt += cr[2 * i + 1]; }
+        printf("%s streams=%3d lds=%6d : %.2f ns/sym/stream, %.1f cycles/sym, clock %.0f MHz (memtime / memrealtime at 100 MHz)\n",
+               name, w, lds, ms * 1e6 / (nchunks * 16.0), cyc / w / (nchunks * 16.0), cyc / rt * 100.0);
+    }
+    {
+        hipDeviceProp_t prop;
+        CK(hipGetDeviceProperties(&prop, 0));
+        const int ncu = prop.multiProcessorCount;
+        for (int every : {2, 4}) {
+            for (int phase = 0; phase < 2; phase++) {
+                std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+                for (int cu = 0; cu < ncu; cu++)
+                    if (cu % every == phase) m[cu / 32] |= 1u << (cu % 32);
+                hipStream_t sm;
+                CK(hipExtStreamCreateWithCUMask(&sm, (uint32_t)ncu, m.data()));
+                for (int w : {32, 64, 128}) {
+                    hipLaunchKernelGGL(k_passr<W>, dim3(w), dim3(64), 0, sm, d, nchunks, dk, dres);
+                    CK(hipEventRecord(a, sm));
+                    hipLaunchKernelGGL(k_passr<W>, dim3(w), dim3(64), 0, sm, d, nchunks, dk, dres);
+                    CK(hipEventRecord(b, sm));
+                    CK(hipEventSynchronize(b));
+                    CK(hipEventElapsedTime(&ms, a, b));
+                    std::vector<uint32_t> cr(2 * w);
+                    CK(hipMemcpy(cr.data(), dres + 4096, 8 * w, hipMemcpyDeviceToHost));
+                    double cyc = 0;
+                    for (int i = 0; i < w; i++) cyc += cr[2 * i];
+                    printf("%s CU mask cu%%%d==%d streams=%3d : %.2f ns/sym, %.1f cycles/sym\n", name, every, phase, w,
+                           ms * 1e6 / (nchunks * 16.0), cyc / w / (nchunks * 16.0));
+                }
+                CK(hipStreamDestroy(sm));
+            }
+        }
     }
     std::vector<uint32_t> res(NS);
     CK(hipMemcpy(res.data(), dres, NS * 4, hipMemcpyDeviceToHost));
