@@ -30,6 +30,11 @@ import torch.distributed as dist  # noqa: E402
 import fastqueeze_amd as fq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Dependency-chain bound of pass R: one wave issues at most one
+# instruction per 4 cycles and a range-coder step is 10 SALU instructions, so a
+# stream of L symbols needs >= L * 40 cycles at 2.4 GHz.
+R_SALU_PER_SYMBOL = 10
+R_NS_PER_SYMBOL = R_SALU_PER_SYMBOL * 4 / 2.4
 
 
 def log(*a):
@@ -46,6 +51,9 @@ def main():
     ap.add_argument("--block-size", type=int, default=fq.BLOCK_SIZE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM bytes of the dominant kernel from the PMC passes "
+                         "(scripts/gpu_pmc.sh + scripts/pmc_traffic.py) of this tree")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -99,6 +107,7 @@ def main():
     else:
         total_in = float(in_bytes)
 
+    max_syms, all_syms = enc.stream_stats()
     outs = enc.fetch()
     out_bytes = sum(len(o) for o in outs)
     if not args.no_verify and rank == 0:
@@ -115,6 +124,10 @@ def main():
     dom = max(kern, key=kern.get)
     algo_bytes = in_bytes + out_bytes           # FASTQ in + encoded out
     achieved = algo_bytes / (kern[dom] / 1e3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get(dom)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -153,7 +166,11 @@ def main():
                    "parallelism": f"block-shard x{world}"},
         "ratio": round(in_bytes / out_bytes, 3),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
+        "chain_bound": {"kernel": "coder_r", "longest_stream_symbols": max_syms, "all_stream_symbols": all_syms,
+                        "salu_per_symbol": R_SALU_PER_SYMBOL, "bound_ms": round(max_syms * R_NS_PER_SYMBOL / 1e6, 2),
+                        "achieved_ms": round(ph.get("coder_r", 0.0), 2),
+                        "frac": round(max_syms * R_NS_PER_SYMBOL / 1e6 / max(ph.get("coder_r", 1e-9), 1e-9), 3)},
         "phase_ms": {k: round(v, 2) for k, v in ph.items()},
         "cpu_baseline": cpu,
     }

@@ -69,6 +69,7 @@ def load_library(path: str | None = None):
         "sa_parse_se": ([P, U64, P, P, P, P, P], I64), "sa_parse_pe": ([P, U64, P, U64, P, P, P, P, P], I64),
         "sa_analyze_ids": ([P, I32, P], I32),
         "sa_code_records": ([P, I32, P, P, P, P, P, U64, P], I32), "sa_coder_restarts": ([P], C.c_uint32),
+        "sa_stream_stats": ([P, P, P], None),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -274,6 +275,12 @@ class Encoder:
 
     def coder_restarts(self) -> int:
         return int(self._lib.sa_coder_restarts(self._ctx))
+
+    def stream_stats(self) -> tuple[int, int]:
+        """(symbols of the longest coder stream, symbols of all streams) of the last run."""
+        mx, tot = C.c_uint64(0), C.c_uint64(0)
+        self._lib.sa_stream_stats(self._ctx, C.byref(mx), C.byref(tot))
+        return int(mx.value), int(tot.value)
 
     def phase_times(self) -> dict[str, float]:
         names = (C.c_char_p * self.PHASES)()

@@ -63,6 +63,7 @@ struct sa_ctx {
     std::string err;
     bool timing = false;
     uint32_t coder_restarts = 0;
+    uint64_t max_stream_syms = 0, total_stream_syms = 0;
     hipEvent_t ev_beg[PH_N], ev_end[PH_N];
     float ph_ms[PH_N];
 
@@ -590,6 +591,11 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     const SortPlan& ps = bp.seq;
     const SortPlan& pa = bp.aux;
     const std::vector<CoderTask>& tasks = bp.tasks;
+    c->max_stream_syms = c->total_stream_syms = 0;
+    for (const CoderTask& tk : tasks) {
+        c->max_stream_syms = std::max<uint64_t>(c->max_stream_syms, tk.n);
+        c->total_stream_syms += tk.n;
+    }
     const std::vector<uint64_t>& task_out_base = bp.task_out_base;
     const std::vector<AsmBlock>& asmb = bp.asmb;
     const uint64_t payload = bp.payload_bytes, final_bytes = bp.final_bytes;
@@ -886,6 +892,12 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
 }
 
 uint32_t sa_coder_restarts(const sa_ctx* c) { return c ? c->coder_restarts : 0; }
+
+void sa_stream_stats(const sa_ctx* c, uint64_t* max_symbols, uint64_t* total_symbols)
+{
+    if (max_symbols) *max_symbols = c ? c->max_stream_syms : 0;
+    if (total_symbols) *total_symbols = c ? c->total_stream_syms : 0;
+}
 
 int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, sa_out* out)
 {

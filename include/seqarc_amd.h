@@ -83,6 +83,9 @@ int sa_code_records(sa_ctx *ctx, int nstreams, const uint32_t *lens, const uint1
                     uint64_t *out_lens);
 /* streams restarted after a carry-less squeeze in the last sa_run / sa_code_records */
 uint32_t sa_coder_restarts(const sa_ctx *ctx);
+/* symbols of the longest coder stream and of all streams in the last sa_run
+ * (the serial range chain of the longest stream bounds the batch) */
+void sa_stream_stats(const sa_ctx *ctx, uint64_t *max_symbols, uint64_t *total_symbols);
 
 /* ---- host-side mirrors of the reference's block plumbing -------------- */
 /* Block cut: SeqArcRead::doReadJob@0x432a80 / cultbuf@0x432530 / getEndPos@0x4320c0
