@@ -565,6 +565,8 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     if (nr) {
         hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
                            c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
+        hipLaunchKernelGGL(k_prep_sq, dim3((nr + EMIT_WAVES - 1) / EMIT_WAVES), dim3(64 * EMIT_WAVES), 0, st, bv,
+                           c->d_counts.as<uint32_t>(), d_err);
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
                        c->d_totals.as<uint32_t>(), c->d_maxlen.as<uint16_t>());

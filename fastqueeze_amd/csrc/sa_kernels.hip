@@ -85,7 +85,8 @@ __device__ inline void wg256_excl_scan(uint32_t v, uint32_t& excl, uint32_t* sh 
 }
 
 // ---------------------------------------------------------------------------
-// k_prep: one thread per read
+// k_prep: one thread per read (name prefix / suffix, length and tip columns);
+// k_prep_sq: one wave per read (SEQ, QUAL and N-IUPAC columns, input checks).
 // ---------------------------------------------------------------------------
 __global__ void k_prep(const BatchView bv, uint32_t* __restrict__ counts,
                        int16_t* __restrict__ name_p, int16_t* __restrict__ name_s,
@@ -93,8 +94,108 @@ __global__ void k_prep(const BatchView bv, uint32_t* __restrict__ counts,
 {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= bv.nreads_total) return;
-    const uint32_t e = prep_read(bv, r, counts, name_p, name_s);
+    const uint32_t e = prep_read(bv, r, counts, name_p, name_s, false);
     if (e) atomicOr(err, e);
+}
+
+constexpr uint32_t EMIT_WAVES = 4;
+constexpr uint32_t EMIT_STAGE = 256;   // bases / quals of a read staged in LDS up front
+
+// Stages the first EMIT_STAGE bases and quals of a read in LDS: every load is
+// issued before any is used (one memory latency per read instead of one per
+// step and loop).
+__device__ __forceinline__ void stage_read(const uint8_t* s, const uint8_t* q, uint32_t len,
+                                           uint8_t (&st)[2][EMIT_STAGE])
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t pre = len < EMIT_STAGE ? len : EMIT_STAGE;
+    uint32_t sb[EMIT_STAGE / 64], qb[EMIT_STAGE / 64];
+#pragma unroll
+    for (uint32_t k = 0; k < EMIT_STAGE / 64; k++) {
+        const uint32_t i = 64 * k + lane;
+        sb[k] = i < pre ? s[i] : 0u;
+        qb[k] = i < pre ? q[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < EMIT_STAGE / 64; k++) {
+        st[0][64 * k + lane] = (uint8_t)sb[k];
+        st[1][64 * k + lane] = (uint8_t)qb[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ inline int wave_max_i32(int v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// seq_stat + qual_nonhash + the quality range check of one read (sa_common.h),
+// 64 positions per step; the gap statistics of reads with an N/IUPAC base run
+// on one lane over the staged bytes.
+__global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv, uint32_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ err)
+{
+    __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t r = blockIdx.x * EMIT_WAVES + w;
+    if (r >= bv.nreads_total) return;   // wave-uniform
+    const uint32_t b = bv.read_block[r];
+    const DevBlock& blk = bv.blocks[b];
+    const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
+    const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
+    const uint32_t len = bv.seq_len[r];
+    stage_read(s, q, len, stage[w]);
+    auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][0][i] : s[i]; };
+    auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][1][i] : q[i]; };
+    uint32_t valid = 0, nch = 0, n = 0;
+    int maxq = 0;
+    bool nonascii = false;
+    for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool in = i < len;
+        const uint32_t c = in ? S(i) : (uint32_t)'A', qq = in ? Q(i) : (uint32_t)'#';
+        const uint32_t cd = base_code((uint8_t)c);
+        nonascii |= __ballot(in && c >= 0x80) != 0;
+        const uint64_t vm = __ballot(in && cd <= 3), nm = __ballot(in && cd > 3);
+        valid += (uint32_t)__popcll(vm);
+        nch += (uint32_t)__popcll(nm);
+        if (nm) {
+            const int m = wave_max_i32(in && cd > 3 ? (int)(int8_t)qq : 0);
+            maxq = m > maxq ? m : maxq;
+        }
+        const uint64_t nz = __ballot(in && qq != '#');
+        if (nz) n = i0 + 64 - (uint32_t)__builtin_clzll(nz);
+    }
+    bool qbad = false;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t qq = i < n ? Q(i) : 33u;
+        qbad |= __ballot(qq < 33 || qq > 126) != 0;
+    }
+    SeqStat st{valid, nch, (uint32_t)maxq & 0xffu, 0u, 0u, nonascii ? (uint32_t)E_NONASCII : 0u};
+    if (nch && lane == 0) {   // seq_stat's second loop
+        uint32_t gap = 0;
+        for (uint32_t i = 0; i < len; i++) {
+            if ((int)st.maxq < (int)(int8_t)Q(i)) continue;
+            if (base_code(S(i)) > 3) {
+                gap++;
+            } else {
+                st.exc++;
+                st.npos_syms += 1 + (uint32_t)nbits_u32(gap);
+                gap = 0;
+            }
+        }
+    }
+    if (lane == 0) {
+        const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, n, st, qbad);
+        if (e) atomicOr(err, e);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -179,8 +280,6 @@ __device__ inline uint32_t shfl_up0(uint32_t v, uint32_t d)   // lane - d's valu
     return lane_id() >= d ? x : 0u;
 }
 
-constexpr uint32_t EMIT_WAVES = 4;
-
 // SEQ (encode_seq@0x421f30): the context of an ACGT base is the seed
 // 0x7616c7 shifted by two bits per earlier ACGT base of the read, plus those
 // bases' codes, masked -- i.e. the packed codes of the up to 16 previous ACGT
@@ -196,6 +295,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
                                                               uint32_t* __restrict__ aux_val)
 {
     __shared__ uint32_t comp[EMIT_WAVES][64];
+    __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t r = blockIdx.x * EMIT_WAVES + w;
     if (r >= bv.nreads_total) return;   // wave-uniform
@@ -205,6 +305,9 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
     const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
     const uint32_t len = bv.seq_len[r];
     const uint32_t* off = counts + (size_t)r * NCOL;
+    stage_read(s, q, len, stage[w]);
+    auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][0][i] : s[i]; };
+    auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][1][i] : q[i]; };
     {
         uint32_t* K = seq_key + blk.seq_sym_base;
         uint32_t* V = seq_val + blk.seq_sym_base;
@@ -213,7 +316,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
         uint32_t carry = 0x7616c7u & mask;   // the context after the previous step
         for (uint32_t i0 = 0; i0 < len; i0 += 64) {
             const uint32_t i = i0 + lane;
-            const uint32_t cd = i < len ? base_code(s[i]) : 4u;
+            const uint32_t cd = i < len ? base_code(S(i)) : 4u;
             const uint64_t vm = __ballot(cd <= 3);
             const uint32_t nv = (uint32_t)__popcll(vm);
             const uint32_t in_step = len - i0 < 64 ? len - i0 : 64;
@@ -245,7 +348,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
         uint32_t n = 0;
         for (uint32_t i0 = 0; i0 < len; i0 += 64) {
             const uint32_t i = i0 + lane;
-            const uint64_t nz = __ballot(i < len && q[i] != '#');
+            const uint64_t nz = __ballot(i < len && Q(i) != '#');
             if (nz) n = i0 + 64 - (uint32_t)__builtin_clzll(nz);
         }
         uint32_t* K = aux_key + blk.aux_sym_base;
@@ -256,7 +359,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
         int delta_c = 5;
         for (uint32_t i0 = 0; i0 < n; i0 += 64) {
             const uint32_t i = i0 + lane;
-            const uint32_t sym = i < n ? (uint32_t)(uint8_t)(q[i] - 33) : 0u;
+            const uint32_t sym = i < n ? (uint32_t)(uint8_t)(Q(i) - 33) : 0u;
             const uint32_t u1 = (uint32_t)__shfl_up((int)sym, 1, 64), u2 = (uint32_t)__shfl_up((int)sym, 2, 64);
             const uint32_t q1 = lane >= 1 ? u1 : p1;
             const uint32_t q2 = lane >= 2 ? u2 : lane == 1 ? p1 : p2;

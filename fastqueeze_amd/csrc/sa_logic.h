@@ -9,7 +9,29 @@
 namespace sa {
 
 // ---- per-read counts (k_prep) ----------------------------------------------
-SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int16_t* name_p, int16_t* name_s)
+// The columns of a read's SEQ / QUAL / N-IUPAC side streams (and their input
+// checks) from its seq_stat and trimmed quality length.
+SA_HD uint32_t prep_sq_cols(uint32_t* c, uint32_t len, uint32_t nq, const SeqStat& st, bool qual_bad)
+{
+    uint32_t e = st.err;
+    c[C_SEQ] = st.valid;
+    if (len > 0xffff) e |= E_LONGREAD;
+    c[C_QUAL] = nq + (nq != len ? 1 : 0);
+    if (qual_bad) e |= E_QUALRANGE;
+    c[C_CH] = st.nch;
+    const uint32_t has = st.nch ? 1 : 0;
+    c[C_MAXQ] = has;
+    if (has && (st.maxq < 33 || st.maxq > 127)) e |= E_QUALRANGE;
+    c[C_NCNT] = has ? 1 + (uint32_t)nbits_u32(st.exc) : 0;
+    c[C_NPOS] = has ? st.npos_syms : 0;
+    c[C_NPOSV] = has ? st.exc : 0;
+    return e;
+}
+
+// Every column of read r; bulk = false leaves out the SEQ / QUAL / N-IUPAC
+// columns (k_prep_sq computes those one wave per read).
+SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int16_t* name_p, int16_t* name_s,
+                         bool bulk)
 {
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
@@ -19,24 +41,17 @@ SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int1
     const uint32_t len = bv.seq_len[r];
     uint32_t e = 0;
 
-    SeqStat st = seq_stat(s, q, len);
-    e |= st.err;
     uint32_t* c = counts + (size_t)r * NCOL;
-    c[C_SEQ] = st.valid;
-    if (len > 0xffff) e |= E_LONGREAD;
+    if (bulk) {
+        const SeqStat st = seq_stat(s, q, len);
+        const uint32_t n = qual_nonhash(q, len);
+        bool qbad = false;
+        for (uint32_t i = 0; i < n; i++)
+            if (q[i] < 33 || q[i] > 126) { qbad = true; break; }
+        e |= prep_sq_cols(c, len, n, st, qbad);
+    }
     c[C_LEN] = len == 0 ? 1 : 3;
-    uint32_t n = qual_nonhash(q, len);
-    c[C_QUAL] = n + (n != len ? 1 : 0);
-    for (uint32_t i = 0; i < n; i++)
-        if (q[i] < 33 || q[i] > 126) { e |= E_QUALRANGE; break; }
     c[C_TIP] = 1;
-    c[C_CH] = st.nch;
-    const uint32_t has = st.nch ? 1 : 0;
-    c[C_MAXQ] = has;
-    if (has && (st.maxq < 33 || st.maxq > 127)) e |= E_QUALRANGE;
-    c[C_NCNT] = has ? 1 + (uint32_t)nbits_u32(st.exc) : 0;
-    c[C_NPOS] = has ? st.npos_syms : 0;
-    c[C_NPOSV] = has ? st.exc : 0;
 
     if (bv.bin_mode) {
         c[C_NAME] = 0;

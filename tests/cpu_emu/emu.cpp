@@ -232,7 +232,7 @@ int main(int argc, char** argv)
     std::vector<int16_t> name_p(nr), name_s(nr);
     std::vector<uint16_t> maxlen(nr);
     uint32_t err = 0;
-    for (uint32_t r = 0; r < nr; r++) err |= prep_read(bv, r, counts.data(), name_p.data(), name_s.data());
+    for (uint32_t r = 0; r < nr; r++) err |= prep_read(bv, r, counts.data(), name_p.data(), name_s.data(), true);
     if (err) { std::printf("FAIL prep error bits %x\n", err); return 1; }
     std::vector<uint32_t> totals((size_t)nb * NCOL);
     for (int64_t b = 0; b < nb; b++) {
