@@ -133,6 +133,9 @@ struct AsmBlock {
 struct AsmView {
     const AsmBlock* blocks;
     const uint64_t* task_out_base;
+    uint32_t* copies;   // per block: count, then (dst offset, source task, length) x ASM_MAX_COPIES
 };
+constexpr uint32_t ASM_MAX_COPIES = 16;
+constexpr uint32_t ASM_COPY_WORDS = 1 + 3 * ASM_MAX_COPIES;
 
 }  // namespace sa

@@ -79,7 +79,7 @@ struct sa_ctx {
     DBuf d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
     DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
-    DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_task_out_base, d_final, d_final_len;
+    DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_asm_copies, d_task_out_base, d_final, d_final_len;
     DBuf d_longs, d_huge_sorted, d_nlong, d_seq_longs, d_nseq_long, d_short_at;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
@@ -96,7 +96,7 @@ struct sa_ctx {
                        &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
                        &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
-                       &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_task_out_base, &d_final,
+                       &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base, &d_final,
                        &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_short_at, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
                        &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
                        &d_list_gbase[1], &d_list_run[1]};
@@ -637,6 +637,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     SA_CHECK(c, c->d_out_len.ensure(4 * tasks.size()));
     SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
     SA_CHECK(c, c->d_asm.ensure(sizeof(AsmBlock) * nbk));
+    SA_CHECK(c, c->d_asm_copies.ensure(4ull * ASM_COPY_WORDS * nbk));
     SA_CHECK(c, c->d_task_out_base.ensure(8 * task_out_base.size()));
     SA_CHECK(c, c->d_final.ensure(std::max<uint64_t>(final_bytes, 16)));
     SA_CHECK(c, c->d_final_len.ensure(8 * nbk));
@@ -757,10 +758,11 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     // ---- assembly (after MD5) ----
     if (cfg->md5) SA_CHECK(c, hipStreamWaitEvent(st, c->ev_md5_done, 0));
     ev_begin(c, PH_ASM, st);
-    AsmView asv{c->d_asm.as<AsmBlock>(), c->d_task_out_base.as<uint64_t>()};
-    hipLaunchKernelGGL(k_assemble, dim3(nbk), dim3(256), 0, st, bv, asv, c->d_payload.as<uint8_t>(),
-                       c->d_out_len.as<uint32_t>(), c->d_digests.as<uint32_t>(), c->d_final.as<uint8_t>(),
-                       c->d_final_len.as<uint64_t>());
+    AsmView asv{c->d_asm.as<AsmBlock>(), c->d_task_out_base.as<uint64_t>(), c->d_asm_copies.as<uint32_t>()};
+    hipLaunchKernelGGL(k_assemble, dim3((nbk + 63) / 64), dim3(64), 0, st, bv, asv, c->d_out_len.as<uint32_t>(),
+                       c->d_digests.as<uint32_t>(), c->d_final.as<uint8_t>(), c->d_final_len.as<uint64_t>());
+    hipLaunchKernelGGL(k_assemble_copy, dim3(nbk * ASM_SLICES), dim3(256), 0, st, asv, c->d_payload.as<uint8_t>(),
+                       c->d_final.as<uint8_t>());
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_ASM, st);
     ev_finish(c, PH_TOTAL, st);

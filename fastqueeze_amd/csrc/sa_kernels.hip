@@ -1667,29 +1667,40 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Task* __restrict__ tasks, u
 // ---------------------------------------------------------------------------
 // Block assembly (doFqzEncode@0x42d2d0): one workgroup per block.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_assemble(const BatchView bv, const AsmView av,
-                                                  const uint8_t* __restrict__ payload,
-                                                  const uint32_t* __restrict__ out_len,
-                                                  const uint32_t* __restrict__ digests,
-                                                  uint8_t* __restrict__ final_out,
-                                                  uint64_t* __restrict__ final_len)
+__global__ __launch_bounds__(64) void k_assemble(const BatchView bv, const AsmView av,
+                                                 const uint32_t* __restrict__ out_len,
+                                                 const uint32_t* __restrict__ digests,
+                                                 uint8_t* __restrict__ final_out,
+                                                 uint64_t* __restrict__ final_len)
 {
-    __shared__ uint32_t seg_dst[16], seg_src_task[16], seg_len[16];
-    __shared__ uint32_t nseg;
-    const uint32_t b = blockIdx.x;
+    // one lane per block: headers, MD5s, ID-bin payload and the list of coder
+    // payloads to copy (k_assemble_copy)
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= bv.nblocks) return;
     const AsmBlock& ab = av.blocks[b];
-    uint8_t* o = final_out + ab.out_base;
-    if (threadIdx.x == 0) {
-        uint32_t ns = 0;
-        final_len[b] = assemble_plan(bv, b, ab, out_len, digests, o, seg_dst, seg_src_task, seg_len, ns);
-        nseg = ns;
-    }
-    __syncthreads();
-    for (uint32_t sgi = 0; sgi < nseg; sgi++) {
-        const uint8_t* src = payload + av.task_out_base[seg_src_task[sgi]];
-        uint8_t* dst = o + seg_dst[sgi];
-        const uint32_t L = seg_len[sgi];
-        for (uint32_t k = threadIdx.x; k < L; k += blockDim.x) dst[k] = src[k];
+    uint32_t* cp = av.copies + (size_t)b * ASM_COPY_WORDS;
+    uint32_t ns = 0;
+    final_len[b] = assemble_plan(bv, b, ab, out_len, digests, final_out + ab.out_base, cp + 1,
+                                 cp + 1 + ASM_MAX_COPIES, cp + 1 + 2 * ASM_MAX_COPIES, ns);
+    cp[0] = ns;
+}
+
+// Coder payloads into place: ASM_SLICES workgroups per block, consecutive threads
+// copy consecutive bytes.
+constexpr uint32_t ASM_SLICES = 32;
+
+__global__ __launch_bounds__(256) void k_assemble_copy(const AsmView av, const uint8_t* __restrict__ payload,
+                                                       uint8_t* __restrict__ final_out)
+{
+    const uint32_t b = blockIdx.x / ASM_SLICES, slice = blockIdx.x % ASM_SLICES;
+    const uint32_t* cp = av.copies + (size_t)b * ASM_COPY_WORDS;
+    const uint32_t ns = cp[0];
+    uint8_t* o = final_out + av.blocks[b].out_base;
+    for (uint32_t sgi = 0; sgi < ns; sgi++) {
+        const uint8_t* src = payload + av.task_out_base[cp[1 + ASM_MAX_COPIES + sgi]];
+        uint8_t* dst = o + cp[1 + sgi];
+        const uint32_t L = cp[1 + 2 * ASM_MAX_COPIES + sgi];
+        for (uint32_t k = slice * blockDim.x + threadIdx.x; k < L; k += ASM_SLICES * blockDim.x) dst[k] = src[k];
     }
 }
 
