@@ -344,7 +344,7 @@ sa_ctx* sa_create(int device)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
     if (every == 1) m_seq = m_long;   // (st3: the coder chains; st4: the long model runs)
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)prop.multiProcessorCount, m_long.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)prop.multiProcessorCount, m_seq.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)prop.multiProcessorCount, m_long.data()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_seq_done, hipEventDisableTiming) != hipSuccess ||
