@@ -116,7 +116,13 @@ def main():
             b = blocks[i]
             if outs[i] != oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode):
                 raise SystemExit(f"bench output of block {i} differs from the CPU restatement")
-        log("[rank 0] spot-check: first and last block bit-identical to the oracle")
+            if not cfg.bin_mode:   # round trip: decode (CPU) back to the block, MD5s verified
+                nm, nl, sq, sl, ql, ok = oracle_py.decode_block(outs[i], b.nreads, b.names.size, b.seq.size,
+                                                               cfg.slevel, cfg.qlevel, cfg.md5)
+                if not (ok and np.array_equal(sq, b.seq) and np.array_equal(ql, b.qual)
+                        and np.array_equal(nm, b.names)):
+                    raise SystemExit(f"bench output of block {i} does not decode back to its input")
+        log("[rank 0] spot-check: first and last block bit-identical to the oracle and decode back to the input")
 
     # dominant kernel phase (device time from HIP events on its own stream)
     ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}

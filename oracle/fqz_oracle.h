@@ -71,6 +71,24 @@ int orc_analyze_idbin(const orc_block *first, int se, uint8_t tmpl[512]);
 int64_t orc_rc_encode(const uint16_t *cum, const uint16_t *freq, const uint16_t *tot, size_t n,
                       uint8_t *out, size_t cap);
 
+/* Decoded block (caller-owned arrays; see fqz_decode.c). */
+typedef struct {
+    uint8_t  *names;      /* >= name_cap bytes */
+    uint16_t *name_lens;  /* >= max_reads      */
+    uint8_t  *seq;        /* >= seq_cap bytes  */
+    int32_t  *seq_lens;   /* >= max_reads      */
+    uint8_t  *qual;       /* >= seq_cap bytes  */
+    size_t    name_cap, seq_cap;
+    uint32_t  max_reads;
+    uint32_t  nreads;     /* out */
+    int       md5_ok;     /* out: 1 if every stored digest matches (or MD5 off) */
+} orc_decoded;
+
+/* Decode one block written by orc_encode_block / the GPU encoder (the inverse
+ * of doFqzEncode@0x42d2d0; the reference's decoder is doFqzDecode@0x42c680).
+ * Returns nreads, -1 on malformed input, -2 for the ID-bin mode. */
+int64_t orc_decode_block(const uint8_t *in, size_t len, const orc_cfg *cfg, orc_decoded *out);
+
 /* RFC1321 MD5 (the vendored RSA implementation, MDString@0x4058f0). */
 void orc_md5(const uint8_t *data, size_t len, uint8_t digest[16]);
 

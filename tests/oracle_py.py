@@ -33,7 +33,7 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fqz_oracle.c", "fqz_oracle.h", "orc_cli.c")]
+        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fqz_oracle.c", "fqz_decode.c", "fqz_oracle.h", "orc_cli.c")]
         if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
             build()
         l = C.CDLL(LIB)
@@ -46,6 +46,8 @@ def lib():
         l.orc_rc_encode.restype = C.c_int64
         l.orc_md5.argtypes = [P, C.c_size_t, P]
         l.orc_md5.restype = None
+        l.orc_decode_block.argtypes = [P, C.c_size_t, P, P]
+        l.orc_decode_block.restype = C.c_int64
         _lib = l
     return _lib
 
@@ -66,6 +68,32 @@ def encode_block(b, slevel=3, qlevel=2, md5=True, bin_mode=0) -> bytes:
     if n < 0:
         raise RuntimeError("oracle encode failed")
     return out[:n].tobytes()
+
+
+class _Dec(C.Structure):
+    _fields_ = [("names", C.c_void_p), ("name_lens", C.c_void_p), ("seq", C.c_void_p),
+                ("seq_lens", C.c_void_p), ("qual", C.c_void_p), ("name_cap", C.c_size_t),
+                ("seq_cap", C.c_size_t), ("max_reads", C.c_uint32), ("nreads", C.c_uint32),
+                ("md5_ok", C.c_int)]
+
+
+def decode_block(data: bytes, max_reads: int, name_cap: int, seq_cap: int, slevel=3, qlevel=2, md5=True):
+    """CPU decode of one encoded block (oracle/fqz_decode.c) -> (names, name_lens,
+    seq, seq_lens, qual, md5_ok)."""
+    names = np.empty(max(name_cap, 1), np.uint8)
+    nl = np.empty(max(max_reads, 1), np.uint16)
+    seq = np.empty(max(seq_cap, 1), np.uint8)
+    sl = np.empty(max(max_reads, 1), np.int32)
+    qual = np.empty(max(seq_cap, 1), np.uint8)
+    d = _Dec(_p(names), _p(nl), _p(seq), _p(sl), _p(qual), name_cap, seq_cap, max_reads, 0, 0)
+    src = np.frombuffer(data, np.uint8)
+    cc = _Cfg(slevel, qlevel, 1 if md5 else 0, 0)
+    n = lib().orc_decode_block(_p(src), src.size, C.byref(cc), C.byref(d))
+    if n < 0:
+        raise RuntimeError(f"oracle decode failed ({n})")
+    n = int(n)
+    ln, ls = int(nl[:n].astype(np.int64).sum()), int(sl[:n].astype(np.int64).sum())
+    return names[:ln], nl[:n], seq[:ls], sl[:n], qual[:ls], bool(d.md5_ok)
 
 
 def analyze_ids(b, single_end: bool) -> np.ndarray:

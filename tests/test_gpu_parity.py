@@ -79,11 +79,17 @@ def test_many_blocks_one_batch(enc):
 
 
 def test_full_size_block(enc):
-    """One full 50 MiB block (146,716 x 150 bp reads) -- the bench's unit of work."""
+    """One full 50 MiB block (146,716 x 150 bp reads) -- the bench's unit of work --
+    equal to the oracle, and decoding back to the input (CPU decoder, MD5s match)."""
     a, _ = synth.generate(150_000, seed=5)
     blocks = fq.blocks_from_fastq(a)
     assert blocks[0].text_bytes > 50_000_000
-    _check(enc, blocks[:1], fq.Config())
+    got = _check(enc, blocks[:1], fq.Config())
+    b = blocks[0]
+    names, nl, seq, sl, qual, ok = oracle_py.decode_block(got[0], b.nreads, b.names.size, b.seq.size)
+    assert ok
+    assert np.array_equal(names, b.names) and np.array_equal(nl, b.name_lens)
+    assert np.array_equal(seq, b.seq) and np.array_equal(sl, b.seq_lens) and np.array_equal(qual, b.qual)
 
 
 def test_deterministic_rerun(enc):

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_py
+import synth
 from conftest import GOLDEN, ROOT, TEST1, TEST2
 
 import fastqueeze_amd as fq
@@ -118,3 +119,53 @@ def test_oracle_rc_squeeze_streams():
     for c, f, t in oracle_py.squeeze_streams():
         out = oracle_py.rc_encode(c, f, t)
         assert len(out) >= 8
+
+
+_IUPAC = b"MRYKSWHBVD"
+
+
+def _norm_seq(seq: np.ndarray) -> np.ndarray:
+    """What a decoder can return for stored bases: ACGT / IUPAC upper-cased,
+    anything else 'N' (the encoder keeps base codes, seq_val_table@0x44b800)."""
+    up = seq.copy()
+    low = (up >= ord("a")) & (up <= ord("z"))
+    up[low] -= 32
+    keep = np.isin(up, np.frombuffer(b"ACGT" + _IUPAC, np.uint8))
+    up[~keep] = ord("N")
+    return up
+
+
+def _roundtrip(b, slevel, qlevel, md5=True):
+    import oracle_py as ob
+    enc = ob.encode_block(b, slevel, qlevel, md5, 0)
+    names, nl, seq, sl, qual, ok = ob.decode_block(enc, b.nreads, b.names.size, b.seq.size, slevel, qlevel, md5)
+    assert np.array_equal(nl, b.name_lens) and np.array_equal(names, b.names)
+    assert np.array_equal(sl, b.seq_lens)
+    assert np.array_equal(qual, b.qual)
+    assert np.array_equal(seq, _norm_seq(b.seq))
+    return ok
+
+
+@pytest.mark.parametrize("slevel,qlevel", [(3, 2), (1, 1), (4, 3), (9, 2)])
+def test_decoder_round_trip_synthetic(slevel, qlevel):
+    """encode -> decode (oracle/fqz_decode.c) gives the block back, MD5s match."""
+    import fastqueeze_amd as fq
+    text1, text2 = synth.generate(3000, paired=True, seed=40 + slevel)
+    for b in fq.blocks_from_fastq(text1, text2, 400_000):
+        assert _roundtrip(b, slevel, qlevel)
+
+
+def test_decoder_round_trip_edge_cases():
+    """N / IUPAC / lowercase bases, '#' runs, empty reads: the decoded block is the
+    input with bases normalised; the MD5 check flags the lowercase input."""
+    import fastqueeze_amd as fq
+    b = fq.blocks_from_fastq(synth.edge_cases())[0]
+    ok = _roundtrip(b, 3, 2)
+    assert ok == bool(np.array_equal(_norm_seq(b.seq), b.seq))
+
+
+def test_decoder_round_trip_reference_pair(test_pair):
+    import fastqueeze_amd as fq
+    t1, t2 = test_pair
+    for b in fq.blocks_from_fastq(t1, t2):
+        assert _roundtrip(b, 3, 2)
