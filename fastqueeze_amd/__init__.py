@@ -39,7 +39,8 @@ class _SaBlock(C.Structure):
 
 
 class _SaCfg(C.Structure):
-    _fields_ = [("slevel", C.c_int32), ("qlevel", C.c_int32), ("md5", C.c_int32), ("bin_mode", C.c_int32)]
+    _fields_ = [("slevel", C.c_int32), ("qlevel", C.c_int32), ("md5", C.c_int32), ("bin_mode", C.c_int32),
+                ("lossy", C.c_double)]
 
 
 class _SaOut(C.Structure):
@@ -109,9 +110,10 @@ class Config:
     qlevel: int = 2
     md5: bool = True
     bin_mode: int = 0
+    lossy: float = 0.0     # -l R (R-Block lossy qualities, rblock@0x426c10); 0 = lossless
 
     def _c(self) -> _SaCfg:
-        return _SaCfg(self.slevel, self.qlevel, 1 if self.md5 else 0, 1 if self.bin_mode else 0)
+        return _SaCfg(self.slevel, self.qlevel, 1 if self.md5 else 0, 1 if self.bin_mode else 0, float(self.lossy))
 
 
 def _as_u8(text) -> np.ndarray:

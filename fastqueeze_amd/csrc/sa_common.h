@@ -65,6 +65,8 @@ constexpr uint32_t M_CH = 4;              // SIMPLE_MODEL<11>
 constexpr uint32_t M_MAXQ = 5;            // SIMPLE_MODEL<95>
 constexpr uint32_t M_KBITS = 6;           // kModel SIMPLE_MODEL<64> @+0x15c0
 constexpr uint32_t M_KBIT0 = 7;           // 64 x SIMPLE_MODEL<2> (vector @+0x15a8)
+constexpr uint32_t M_LEN_B2 = 71;         // SIMPLE_MODEL<256> @+0x828 (compressLen_long@0x423710)
+constexpr uint32_t M_LEN_B3 = 72;         // SIMPLE_MODEL<256> @+0xc38
 constexpr uint32_t M_NAME_PRE = 128;      // 256 x SIMPLE_MODEL<256> @+0x1068
 constexpr uint32_t M_NAME_SUF = 384;      // 256 x SIMPLE_MODEL<256> @+0x1070
 constexpr uint32_t M_NAME_LEN = 640;      // 256 x SIMPLE_MODEL<256> @+0x1078
@@ -76,6 +78,7 @@ SA_HD uint32_t model_nsym(uint32_t id)
     if (id >= M_QUAL) return 95;
     if (id >= M_NAME_MID) return 128;
     if (id >= M_NAME_PRE) return 256;
+    if (id == M_LEN_B2 || id == M_LEN_B3) return 256;
     if (id >= M_KBIT0) return 2;
     switch (id) {
     case M_LEN_SAME: return 2;
@@ -93,7 +96,7 @@ enum Err : uint32_t {
     E_NONASCII = 1u,     // sequence byte >= 0x80 (reference behaviour undefined)
     E_QUALRANGE = 2u,    // quality byte outside '!'..'~' (outside SIMPLE_MODEL<95>)
     E_NAME = 4u,         // name > 255 bytes or out-of-range model index
-    E_LONGREAD = 8u,     // read > 65535 bp (compressLen_long, not implemented)
+    E_LONGREAD = 8u,     // (unused: reads > 65535 bp take compressLen_long@0x423710)
     E_OVERFLOW = 16u,    // a range coder output overflowed its buffer
     E_CODER = 32u,       // cum + freq > tot (reference: abort())
 };

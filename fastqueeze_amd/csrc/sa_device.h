@@ -28,6 +28,8 @@ struct DevBlock {
     uint32_t vcount[NSTREAM];  // value counts written in the dege encaps
     uint32_t n_seq;
     uint32_t n_aux;
+    uint32_t len_long;         // a read > 0xffff bp: compressLen_long@0x423710 (SeqArcMemBuf+0x2)
+    uint32_t pad_;
 };
 
 struct BatchView {
@@ -38,6 +40,7 @@ struct BatchView {
     const uint8_t* names;
     const uint8_t* seq;
     const uint8_t* qual;
+    const uint8_t* qual_q;        // qualities the QUAL stream codes: qual, or the rblock output (-l)
     const uint32_t* name_off;     // within the block
     const uint16_t* name_len;
     const uint32_t* seq_off;      // within the block
@@ -46,6 +49,21 @@ struct BatchView {
     int32_t qlevel;
     int32_t bin_mode;
     int32_t md5;
+    int32_t lossy;                // -l: QUAL codes qual_q, no quality MD5 (compressQual@0x426eca)
+};
+
+// R-Block lossy pre-pass (rblock@0x426c10): a block's quality bytes are cut
+// into RB_CHUNK-byte chunks (the last one of a block may be shorter).
+struct RbChunk {
+    uint64_t base;       // byte offset of the chunk in BatchView::qual
+    uint32_t len;
+    uint32_t flags;      // RB_FIRST: the block's first chunk, RB_LAST: its last
+};
+constexpr uint32_t RB_FIRST = 1u, RB_LAST = 2u;
+// one open run of rblock: start position (byte offset in BatchView::qual), min, max
+struct RbRun {
+    uint64_t start;
+    uint32_t mn, mx;
 };
 
 // A sort segment = one block's symbol space.

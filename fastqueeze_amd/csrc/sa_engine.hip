@@ -83,6 +83,7 @@ struct sa_ctx {
     DBuf d_longs, d_huge_sorted, d_nlong, d_seq_longs, d_nseq_long, d_short_at;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
+    DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry;   // -l (rblock)
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
 
     // last run
@@ -98,6 +99,7 @@ struct sa_ctx {
                        &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
                        &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base, &d_final,
                        &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_short_at, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                       &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry,
                        &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
                        &d_list_gbase[1], &d_list_run[1]};
         for (DBuf* b : all) b->release();
@@ -155,6 +157,46 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
 
 void ev_begin(sa_ctx* c, int ph, hipStream_t st);
 void ev_finish(sa_ctx* c, int ph, hipStream_t st);
+
+// -l R: the R-Block pre-pass (rblock@0x426c10) of every block's qualities into
+// d_qual_q, which the QUAL stream then codes (speculative chunks, one carry
+// lane per block, chunk replay; sa_logic.h).  The staged qualities stay
+// untouched: the N/IUPAC side streams use them, and the batch can be re-run.
+int run_rblock(sa_ctx* c, double ratio, BatchView& bv)
+{
+    hipStream_t st = c->st;
+    std::vector<RbChunk> ck;
+    std::vector<uint32_t> ck0;
+    for (const DevBlock& d : c->blocks) {
+        ck0.push_back((uint32_t)ck.size());
+        for (uint64_t o = 0; o < d.seq_bytes; o += RB_CHUNK) {
+            const uint32_t len = (uint32_t)std::min<uint64_t>(RB_CHUNK, d.seq_bytes - o);
+            uint32_t fl = (o == 0 ? RB_FIRST : 0u) | (o + len == d.seq_bytes ? RB_LAST : 0u);
+            ck.push_back(RbChunk{d.seq_base + o, len, fl});
+        }
+    }
+    ck0.push_back((uint32_t)ck.size());
+    const uint32_t nck = (uint32_t)ck.size(), nbk = (uint32_t)c->blocks.size();
+    SA_CHECK(c, c->d_qual_q.ensure(c->seq_bytes + 16));
+    bv.qual_q = c->d_qual_q.as<uint8_t>();
+    if (!nck) return 0;
+    SA_CHECK(c, c->d_rb_chunks.ensure(sizeof(RbChunk) * nck));
+    SA_CHECK(c, c->d_rb_ck0.ensure(4ull * (nbk + 1)));
+    SA_CHECK(c, c->d_rb_opens.ensure(4ull * RB_WORDS * nck));
+    SA_CHECK(c, c->d_rb_spec.ensure(sizeof(RbRun) * nck));
+    SA_CHECK(c, c->d_rb_entry.ensure(sizeof(RbRun) * nck));
+    SA_CHECK(c, hipMemcpyAsync(c->d_rb_chunks.p, ck.data(), sizeof(RbChunk) * nck, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_rb_ck0.p, ck0.data(), 4ull * (nbk + 1), hipMemcpyHostToDevice, st));
+    const RbChunk* dck = c->d_rb_chunks.as<RbChunk>();
+    hipLaunchKernelGGL(k_rb_spec, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, dck, nck, ratio,
+                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>());
+    hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk,
+                       ratio, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_entry.as<RbRun>());
+    hipLaunchKernelGGL(k_rb_apply, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck, nck,
+                       ratio, c->d_rb_entry.as<RbRun>());
+    SA_CHECK(c, hipGetLastError());
+    return 0;
+}
 
 // Range coder driver (DESIGN.md "Coder").  A group = a contiguous range of
 // tasks coded on one stream: pass R, L1, L2, L3.  After all groups of a round
@@ -416,6 +458,7 @@ int sa_stage(sa_ctx* c, const sa_block* in, int n)
             }
             ln += in[b].name_lens[r];
             ls += (uint64_t)in[b].seq_lens[r];
+            if (in[b].seq_lens[r] > 0xffff) d.len_long = 1;   // getBlockRead@0x411d2a
         }
         if (ls >= (1ull << 30) || ln >= (1ull << 32)) {
             c->err = "block too large (a reference block is 50 MiB of FASTQ)";
@@ -499,6 +542,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
         c->err = "unsupported slevel/qlevel";
         return -1;
     }
+    const bool lossy = cfg->lossy > 0.0;   // -l R: param+0x1870 / +0x1878
     const int k = cfg->slevel + 7;
     const uint32_t ns = 1u << ((2 * k) & 31);
     const int seq_bits = (2 * k) & 31;   // NS = 1 << seq_bits (x86 shl masks the count)
@@ -524,6 +568,8 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     bv.names = c->d_names.as<uint8_t>();
     bv.seq = c->d_seq.as<uint8_t>();
     bv.qual = c->d_qual.as<uint8_t>();
+    bv.qual_q = bv.qual;
+    bv.lossy = lossy ? 1 : 0;
     bv.name_off = c->d_name_off.as<uint32_t>();
     bv.name_len = c->d_name_len.as<uint16_t>();
     bv.seq_off = c->d_seq_off.as<uint32_t>();
@@ -561,6 +607,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
         SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
     }
     ev_begin(c, PH_PREP, st);
+    if (lossy && run_rblock(c, cfg->lossy, bv)) return -1;
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
         hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),

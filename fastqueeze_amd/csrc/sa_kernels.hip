@@ -150,6 +150,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv,
     const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
     const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
     const uint32_t len = bv.seq_len[r];
+    const uint8_t* qv = bv.qual_q + blk.seq_base + bv.seq_off[r];   // QUAL stream (rblock output with -l)
     stage_read(s, q, len, stage[w]);
     auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][0][i] : s[i]; };
     auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][1][i] : q[i]; };
@@ -169,13 +170,14 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv,
             const int m = wave_max_i32(in && cd > 3 ? (int)(int8_t)qq : 0);
             maxq = m > maxq ? m : maxq;
         }
-        const uint64_t nz = __ballot(in && qq != '#');
+        const uint32_t qc = bv.lossy ? (in ? (uint32_t)qv[i] : (uint32_t)'#') : qq;   // the QUAL stream's byte
+        const uint64_t nz = __ballot(in && qc != '#');
         if (nz) n = i0 + 64 - (uint32_t)__builtin_clzll(nz);
     }
     bool qbad = false;
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
-        const uint32_t qq = i < n ? Q(i) : 33u;
+        const uint32_t qq = i < n ? (bv.lossy ? (uint32_t)qv[i] : Q(i)) : 33u;
         qbad |= __ballot(qq < 33 || qq > 126) != 0;
     }
     SeqStat st{valid, nch, (uint32_t)maxq & 0xffu, 0u, 0u, nonascii ? (uint32_t)E_NONASCII : 0u};
@@ -196,6 +198,45 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv,
         const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, n, st, qbad);
         if (e) atomicOr(err, e);
     }
+}
+
+// ---------------------------------------------------------------------------
+// R-Block lossy pre-pass (rblock@0x426c10; sa_logic.h): speculative chunk
+// passes, one carry lane per block, chunk replay writing every run once.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_rb_spec(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
+                                                uint32_t nck, double R, uint32_t* __restrict__ opens,
+                                                RbRun* __restrict__ spec_exit)
+{
+    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= nck) return;
+    spec_exit[c] = rb_spec(q, ck[c], R, opens + (size_t)c * RB_WORDS);
+}
+
+__global__ __launch_bounds__(64) void k_rb_fix(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
+                                               const uint32_t* __restrict__ ck0, uint32_t nblk, double R,
+                                               const uint32_t* __restrict__ opens,
+                                               const RbRun* __restrict__ spec_exit, RbRun* __restrict__ entry)
+{
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= nblk) return;
+    const uint32_t c0 = ck0[b], c1 = ck0[b + 1];
+    if (c0 == c1) return;
+    RbRun cur = spec_exit[c0];
+    for (uint32_t c = c0 + 1; c < c1; c++) {
+        entry[c] = cur;
+        cur = rb_carry(q, ck[c], cur, R, opens + (size_t)c * RB_WORDS, spec_exit[c]);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_rb_apply(const uint8_t* __restrict__ q, uint8_t* __restrict__ out,
+                                                 const RbChunk* __restrict__ ck, uint32_t nck, double R,
+                                                 const RbRun* __restrict__ entry)
+{
+    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= nck) return;
+    const RbChunk k = ck[c];
+    rb_apply(q, out, k, (k.flags & RB_FIRST) ? RbRun{k.base, 0u, 0u} : entry[c], R);
 }
 
 // ---------------------------------------------------------------------------
@@ -302,7 +343,7 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
     const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
-    const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
+    const uint8_t* q = bv.qual_q + blk.seq_base + bv.seq_off[r];   // QUAL stream only (rblock output with -l)
     const uint32_t len = bv.seq_len[r];
     const uint32_t* off = counts + (size_t)r * NCOL;
     stage_read(s, q, len, stage[w]);

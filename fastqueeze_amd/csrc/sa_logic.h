@@ -15,7 +15,6 @@ SA_HD uint32_t prep_sq_cols(uint32_t* c, uint32_t len, uint32_t nq, const SeqSta
 {
     uint32_t e = st.err;
     c[C_SEQ] = st.valid;
-    if (len > 0xffff) e |= E_LONGREAD;
     c[C_QUAL] = nq + (nq != len ? 1 : 0);
     if (qual_bad) e |= E_QUALRANGE;
     c[C_CH] = st.nch;
@@ -43,14 +42,15 @@ SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int1
 
     uint32_t* c = counts + (size_t)r * NCOL;
     if (bulk) {
-        const SeqStat st = seq_stat(s, q, len);
-        const uint32_t n = qual_nonhash(q, len);
+        const SeqStat st = seq_stat(s, q, len);   // N/IUPAC side info: original qualities
+        const uint8_t* qq = bv.qual_q + blk.seq_base + bv.seq_off[r];
+        const uint32_t n = qual_nonhash(qq, len);
         bool qbad = false;
         for (uint32_t i = 0; i < n; i++)
-            if (q[i] < 33 || q[i] > 126) { qbad = true; break; }
+            if (qq[i] < 33 || qq[i] > 126) { qbad = true; break; }
         e |= prep_sq_cols(c, len, n, st, qbad);
     }
-    c[C_LEN] = len == 0 ? 1 : 3;
+    c[C_LEN] = len == 0 ? 1 : (blk.len_long ? 5 : 3);
     c[C_TIP] = 1;
 
     if (bv.bin_mode) {
@@ -146,6 +146,10 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
         em(M_LEN_SAME, 0);
         em(M_LEN_LO, len & 0xff);
         em(M_LEN_HI, (len >> 8) & 0xff);
+        if (blk.len_long) {   // encode_len_long@0x422e70: bytes 2 and 3 as well
+            em(M_LEN_B2, (len >> 16) & 0xff);
+            em(M_LEN_B3, len >> 24);
+        }
     }
     // names (encode_name@0x421070)
     if (!bv.bin_mode) {
@@ -178,11 +182,12 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
     // qualities (encode_qual@0x422180)
     if (bulk) {
         em.pos = blk.sbase[ST_QUAL] + off[C_QUAL];
-        const uint32_t n = qual_nonhash(q, len);
+        const uint8_t* qq = bv.qual_q + blk.seq_base + bv.seq_off[r];
+        const uint32_t n = qual_nonhash(qq, len);
         QualCtx qc{0, 0, 5};
         uint32_t last = 0;
         for (uint32_t i = 0; i < n; i++) {
-            int sym = (uint8_t)(q[i] - 33);
+            int sym = (uint8_t)(qq[i] - 33);
             em(M_QUAL + last, (uint32_t)sym);
             last = qual_next_ctx(qc, sym, i, bv.qlevel);
         }
@@ -569,6 +574,103 @@ SA_HD void put_u32le(uint8_t* o, uint32_t v)
     o[0] = (uint8_t)v; o[1] = (uint8_t)(v >> 8); o[2] = (uint8_t)(v >> 16); o[3] = (uint8_t)(v >> 24);
 }
 
+// ---------------------------------------------------------------------------
+// R-Block lossy pre-pass, EncapFqzComp::rblock@0x426c10 (-l R).  One greedy
+// pass over a block's whole quality buffer: a run keeps its min and max; a new
+// character c in [min, max] extends it; c > max extends it iff R > g/min and
+// R > c/g, g = round(sqrt(c*min)) (@0x426cc0); c < min iff R > g/c and
+// R > max/g, g = round(sqrt(c*max)) (@0x426d48); otherwise the run is
+// overwritten with round(sqrt(min*max)) (@0x426c6d) and a new run opens at c.
+// The divisions are IEEE double as in the reference; round(sqrt(n)) of an
+// integer n is exact in integers (sqrt(n) is never within 2^-20 of k + 1/2).
+//
+// Parallel form: every chunk runs the greedy pass speculatively from a fresh
+// run at its first byte and records where its runs open (rb_spec); one lane
+// per block carries the true open run across the chunks, re-running a chunk
+// only until the true pass closes a run where the speculative one opened one
+// (from there both agree), else to the chunk's end (rb_fix); every chunk then
+// replays from its true entry run and writes the runs that close inside it
+// (rb_apply), so each byte is written exactly once.
+// ---------------------------------------------------------------------------
+SA_HD uint32_t rb_round_sqrt(uint32_t n)
+{
+    uint32_t g = 0;
+    for (uint32_t b = 1u << 15; b; b >>= 1)   // floor(sqrt(n)), n < 2^30
+        if ((g + b) * (g + b) <= n) g += b;
+    return n > g * g + g ? g + 1 : g;
+}
+
+// One character c of the open run; false: the run closes before c.
+SA_HD bool rb_extend(RbRun& s, uint32_t c, double R)
+{
+    if (s.mx >= c) {
+        if (s.mn <= c) return true;
+        const uint32_t g = rb_round_sqrt(c * s.mx);
+        if (R > (double)g / (double)c && R > (double)s.mx / (double)g) { s.mn = c; return true; }
+    } else {
+        const uint32_t g = rb_round_sqrt(c * s.mn);
+        if (R > (double)g / (double)s.mn && R > (double)c / (double)g) { s.mx = c; return true; }
+    }
+    return false;
+}
+
+constexpr uint32_t RB_CHUNK = 8192;
+constexpr uint32_t RB_WORDS = RB_CHUNK / 32;
+
+// Speculative pass over one chunk: bit i of opens = a run opens at byte i.
+SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, double R, uint32_t* opens)
+{
+    RbRun s{ck.base, q[ck.base], q[ck.base]};
+    uint32_t w = 1u;   // a run opens at the chunk's first byte
+    for (uint32_t i = 1; i < ck.len; i++) {
+        const uint32_t c = q[ck.base + i];
+        if (!rb_extend(s, c, R)) {
+            s = RbRun{ck.base + i, c, c};
+            w |= 1u << (i & 31);
+        }
+        if ((i & 31) == 31) { opens[i >> 5] = w; w = 0; }
+    }
+    if ((ck.len & 31) != 0) opens[(ck.len - 1) >> 5] = w;
+    for (uint32_t k = (ck.len + 31) >> 5; k < RB_WORDS; k++) opens[k] = 0;
+    return s;
+}
+
+// The true open run after chunk ck, given the true run open before it.
+SA_HD RbRun rb_carry(const uint8_t* q, const RbChunk& ck, RbRun s, double R, const uint32_t* opens, const RbRun& spec_exit)
+{
+    for (uint32_t i = 0; i < ck.len; i++) {
+        const uint32_t c = q[ck.base + i];
+        if (!rb_extend(s, c, R)) {
+            if ((opens[i >> 5] >> (i & 31)) & 1u) return spec_exit;   // converged
+            s = RbRun{ck.base + i, c, c};
+        }
+    }
+    return s;
+}
+
+// Writes every run that closes inside chunk ck (and, in the block's last
+// chunk, the final run); entry = the true run open before the chunk.
+SA_HD void rb_apply(const uint8_t* q, uint8_t* out, const RbChunk& ck, RbRun s, double R)
+{
+    uint32_t i = 0;
+    if (ck.flags & RB_FIRST) {
+        s = RbRun{ck.base, q[ck.base], q[ck.base]};
+        i = 1;
+    }
+    for (; i < ck.len; i++) {
+        const uint32_t c = q[ck.base + i];
+        if (!rb_extend(s, c, R)) {
+            const uint8_t g = (uint8_t)rb_round_sqrt(s.mn * s.mx);
+            for (uint64_t j = s.start; j < ck.base + i; j++) out[j] = g;
+            s = RbRun{ck.base + i, c, c};
+        }
+    }
+    if (ck.flags & RB_LAST) {
+        const uint8_t g = (uint8_t)rb_round_sqrt(s.mn * s.mx);
+        for (uint64_t j = s.start; j < ck.base + ck.len; j++) out[j] = g;
+    }
+}
+
 // Writes every header, MD5 and the ID-bin payload of block b into o, and lists
 // the coder payloads still to copy (destination offset, coder task, length).
 // Returns the block's total length.
@@ -615,7 +717,7 @@ SA_HD uint32_t assemble_plan(const BatchView& bv, uint32_t b, const AsmBlock& ab
         p += put_id(o + p, 7);
         uint32_t szp = p; p += 4;
         uint32_t h = 0;
-        if (md5) {
+        if (md5 && !bv.lossy) {   // compressQual@0x426eca: no quality MD5 with -l
             for (int k = 0; k < 4; k++) put_u32le(o + p + 4 * k, digests[(size_t)ab.md5_task[2] * 4 + k]);
             p += 16; h = 16;
         }

@@ -45,6 +45,8 @@ typedef struct {
     int32_t qlevel;    /* param+0x1b58 (default 2)                                */
     int32_t md5;       /* param+0x1880 (default 1): per-block MD5 of ID/seq/qual  */
     int32_t bin_mode;  /* param+0x18a4 (ID template byte 0, see sa_analyze_ids)   */
+    double lossy;      /* -l R (param+0x1878; param+0x1870 set iff R > 0): R-Block
+                          quality pre-pass rblock@0x426c10, no quality MD5; 0 = off */
 } sa_cfg;
 
 typedef struct {

@@ -308,7 +308,7 @@ int64_t orc_decode_block(const uint8_t *in, size_t in_len, const orc_cfg *cfg, o
         const uint32_t sz = take_size4(&c);
         if (c.err || (size_t)(c.end - c.p) < sz) goto out;
         const uint8_t *q = c.p;
-        if (cfg->md5) { memcpy(md5_qual, q, 16); q += 16; }
+        if (cfg->md5 && !(cfg->lossy > 0.0)) { memcpy(md5_qual, q, 16); q += 16; }
         const uint32_t nm = cfg->qlevel > 2 ? 0x100000u : 0x10000u;
         qm = (dmodel *)malloc((size_t)nm * sizeof(dmodel));
         if (!qm) goto out;
@@ -470,8 +470,10 @@ int64_t orc_decode_block(const uint8_t *in, size_t in_len, const orc_cfg *cfg, o
         uint8_t dg[16];
         orc_md5(o->names, (size_t)name_total, dg);
         if (memcmp(dg, md5_id, 16)) o->md5_ok = 0;
-        orc_md5(o->qual, (size_t)total, dg);
-        if (memcmp(dg, md5_qual, 16)) o->md5_ok = 0;
+        if (!(cfg->lossy > 0.0)) {   /* compressQual@0x426eca: no qual MD5 with -l */
+            orc_md5(o->qual, (size_t)total, dg);
+            if (memcmp(dg, md5_qual, 16)) o->md5_ok = 0;
+        }
         orc_md5(o->seq, (size_t)total, dg);
         if (memcmp(dg, md5_seq, 16)) o->md5_ok = 0;
     }

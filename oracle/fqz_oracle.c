@@ -10,6 +10,7 @@
  */
 #include "fqz_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -361,18 +362,72 @@ int64_t orc_qual_payload(const orc_block *b, int qlevel, uint8_t *out, size_t ca
     return qual_payload(b, qlevel, out, out + cap);
 }
 
+/* EncapFqzComp::rblock@0x426c10, restated from the disassembly.  One greedy
+ * pass over the block's whole quality buffer (runs cross read boundaries; the
+ * reference stops at the '\n' after the last quality).  A run keeps its min and
+ * max; a new character c inside [min, max] extends it; c > max extends it iff
+ * R > g/min and R > c/g with g = round(sqrt(c*min)) (@0x426cc0); c < min iff
+ * R > g/c and R > max/g with g = round(sqrt(c*max)) (@0x426d48); otherwise the
+ * run [start, i) is overwritten with round(sqrt(min*max)) (@0x426c6d) and a new
+ * run starts at i.  The last run is flushed at the terminator (@0x426dd0). */
+void orc_rblock(uint8_t *q, size_t n, double ratio)
+{
+    if (n == 0) return;
+    uint32_t start = 0;
+    uint32_t mx = q[0], mn = q[0];    /* r13d, edx */
+    for (uint32_t i = 1; i < (uint32_t)n; i++) {
+        const uint32_t c = q[i];
+        int ext;
+        if (mx >= c) {
+            if (mn <= c) continue;                       /* inside [min, max] */
+            uint32_t g = (uint32_t)(int64_t)round(sqrt((double)(uint64_t)(c * mx)));
+            ext = ratio > (double)g / (double)c && ratio > (double)mx / (double)g;
+            if (ext) { mn = c; continue; }
+        } else {
+            uint32_t g = (uint32_t)(int64_t)round(sqrt((double)(uint64_t)(c * mn)));
+            ext = ratio > (double)g / (double)mn && ratio > (double)c / (double)g;
+            if (ext) { mx = c; continue; }
+        }
+        const uint8_t g = (uint8_t)(int64_t)round(sqrt((double)(uint64_t)(mx * mn)));
+        for (uint32_t j = start; j < i; j++) q[j] = g;
+        mx = mn = c;
+        start = i;
+    }
+    const uint8_t g = (uint8_t)(int64_t)round(sqrt((double)(uint64_t)(mx * mn)));
+    for (uint32_t j = start; j < (uint32_t)n; j++) q[j] = g;
+}
+
+/* compressQual@0x426e80: the MD5 is written only when param+0x1880 is set and
+ * the lossy flag param+0x1870 is clear (@0x426eca-0x426ee4); with -l the block's
+ * quality buffer goes through rblock before encode_qual (@0x427142).  The
+ * N/IUPAC side streams keep the original qualities (DegeInfoProcess@0x433a10
+ * runs in doTask@0x433dd0 before doFqzEncode). */
 int64_t orc_encap_qual(const orc_block *b, const orc_cfg *cfg, uint8_t *out, size_t cap)
 {
     if (cap < 32) return -1;
     int n = encap_set_id(7, out);
     uint8_t *p = out + n + 4;
     int hdr = 0;
-    if (cfg->md5) {   /* lossy (-l) would omit it; lossy is not restated */
+    const int lossy = cfg->lossy > 0.0;
+    if (cfg->md5 && !lossy) {
         orc_md5(b->qual, (size_t)total_seq(b), p);
         p += 16;
         hdr = 16;
     }
-    int64_t pl = qual_payload(b, cfg->qlevel, p, out + cap);
+    int64_t pl;
+    if (lossy) {
+        const size_t nq = (size_t)total_seq(b);
+        uint8_t *lq = (uint8_t *)malloc(nq ? nq : 1);
+        if (!lq) return -1;
+        memcpy(lq, b->qual, nq);
+        orc_rblock(lq, nq, cfg->lossy);
+        orc_block lb = *b;
+        lb.qual = lq;
+        pl = qual_payload(&lb, cfg->qlevel, p, out + cap);
+        free(lq);
+    } else {
+        pl = qual_payload(b, cfg->qlevel, p, out + cap);
+    }
     if (pl < 0) return -1;
     encap_set_size((uint64_t)(hdr + pl), 4, out + n);
     return n + 4 + hdr + pl;
@@ -383,19 +438,25 @@ int64_t orc_encap_qual(const orc_block *b, const orc_cfg *cfg, uint8_t *out, siz
 /* encode_len_short@0x4239a0.  same_len SIMPLE_MODEL<2>, lo/hi <256>.        */
 /* last_len (+0x1060) is compared but never updated: always 0.               */
 /* ------------------------------------------------------------------------ */
+/* compressLen@0x424120 picks compressLen_long@0x423710 when the block's
+ * long-read flag (SeqArcMemBuf+0x2) is set: getBlockRead@0x411d2a (and the PE
+ * parse @0x412a76/0x412bb3) sets it for any read longer than 0xffff; it is
+ * cleared per block (clearCommonBuf@0x414b18).  encode_len_long@0x422e70 codes
+ * same_len, then all four length bytes, each with its own SIMPLE_MODEL<256>
+ * (+0x8, +0x418 -- the short path's lo/hi -- then +0x828, +0xc38). */
 int64_t orc_encap_len(const orc_block *b, uint8_t *out, size_t cap)
 {
     if (cap < 16) return -1;
+    int lng = 0;
     for (uint32_t r = 0; r < b->nreads; r++)
-        if (b->seq_lens[r] > 0xffff) return -1;   /* compressLen_long: not restated */
+        if (b->seq_lens[r] > 0xffff) lng = 1;
     int n = encap_set_id(4, out);
     uint8_t *p = out + n + 4;
-    smodel *m = (smodel *)malloc(3 * sizeof(smodel));
+    smodel *m = (smodel *)malloc(5 * sizeof(smodel));
     if (!m) return -1;
-    smodel *same = &m[0], *lo = &m[1], *hi = &m[2];
+    smodel *same = &m[0], *by = &m[1];
     sm_init(same, 2);
-    sm_init(lo, 256);
-    sm_init(hi, 256);
+    for (int k = 0; k < 4; k++) sm_init(&by[k], 256);
     rc_t rc;
     rc_init(&rc, p, out + cap);
     const int32_t last_len = 0;
@@ -405,8 +466,8 @@ int64_t orc_encap_len(const orc_block *b, uint8_t *out, size_t cap)
             sm_encode(same, &rc, 1);
         } else {
             sm_encode(same, &rc, 0);
-            sm_encode(lo, &rc, (uint16_t)(len & 0xff));
-            sm_encode(hi, &rc, (uint16_t)((len >> 8) & 0xff));
+            for (int k = 0; k < (lng ? 4 : 2); k++)
+                sm_encode(&by[k], &rc, (uint16_t)(((uint32_t)len >> (8 * k)) & 0xff));
         }
     }
     rc_finish(&rc);

@@ -32,6 +32,7 @@ typedef struct {
     int qlevel;        /* param+0x1b58, default 2                             */
     int md5;           /* param+0x1880, default 1                             */
     int bin_mode;      /* param+0x18a4 (ID template byte 0): encodeIDS path   */
+    double lossy;      /* -l R: param+0x1878 (R), param+0x1870 set iff R > 0  */
 } orc_cfg;
 
 /* One parsed block (SeqArcMemBuf SoA; PE reads interleaved r1,r2). */
@@ -88,6 +89,10 @@ typedef struct {
  * of doFqzEncode@0x42d2d0; the reference's decoder is doFqzDecode@0x42c680).
  * Returns nreads, -1 on malformed input, -2 for the ID-bin mode. */
 int64_t orc_decode_block(const uint8_t *in, size_t len, const orc_cfg *cfg, orc_decoded *out);
+
+/* R-Block lossy quality pre-pass over one block's concatenated qualities,
+ * EncapFqzComp::rblock@0x426c10 (in place; n = bytes before the buffer's '\n'). */
+void orc_rblock(uint8_t *q, size_t n, double ratio);
 
 /* RFC1321 MD5 (the vendored RSA implementation, MDString@0x4058f0). */
 void orc_md5(const uint8_t *data, size_t len, uint8_t digest[16]);

@@ -81,7 +81,7 @@ int main(int argc, char **argv)
         if (nr < 0) { fprintf(stderr, "parse failed in block %lld\n", (long long)b); return 1; }
         orc_block blk = {names, nl, seq, sl, qual, (uint32_t)nr};
         if (b == 0 && orc_analyze_idbin(&blk, nin == 1, T)) { fprintf(stderr, "ID analysis failed\n"); return 1; }
-        orc_cfg cfg = {slevel, qlevel, 1, T[0]};
+        orc_cfg cfg = {slevel, qlevel, 1, T[0], 0.0};
         size_t ocap = 2 * (l1 + l2) + 4096;
         uint8_t *out = (uint8_t *)malloc(ocap);
         double t0 = now();

@@ -129,11 +129,13 @@ int main(int argc, char** argv)
 {
     uint64_t bs = 50ull << 20;
     int slevel = 3, qlevel = 2;
+    double lossy = 0.0;
     std::vector<const char*> in;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "-b") && i + 1 < argc) bs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "-s") && i + 1 < argc) slevel = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "-q") && i + 1 < argc) qlevel = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "-l") && i + 1 < argc) lossy = std::atof(argv[++i]);
         else in.push_back(argv[i]);
     }
     if (in.size() == 1 && !std::strcmp(in[0], "--coder")) return coder_selftest();
@@ -185,7 +187,11 @@ int main(int argc, char** argv)
         d.nreads = h.nreads;
         d.read0 = nr;
         uint64_t ln = 0, ls = 0;
-        for (uint32_t r = 0; r < h.nreads; r++) { ln += h.nl[r]; ls += (uint64_t)h.sl[r]; }
+        for (uint32_t r = 0; r < h.nreads; r++) {
+            ln += h.nl[r];
+            ls += (uint64_t)h.sl[r];
+            if (h.sl[r] > 0xffff) d.len_long = 1;
+        }
         d.name_base = names.size();
         d.seq_base = seq.size();
         d.name_bytes = ln;
@@ -226,6 +232,39 @@ int main(int argc, char** argv)
     bv.qlevel = qlevel;
     bv.bin_mode = T[0];
     bv.md5 = 1;
+    bv.qual_q = qual.data();
+    bv.lossy = lossy > 0.0;
+    // -l: the chunked rblock (what k_rb_spec / k_rb_fix / k_rb_apply compute),
+    // checked against the oracle's serial restatement block by block
+    std::vector<uint8_t> qual_q;
+    if (lossy > 0.0) {
+        qual_q.assign(qual.size(), 0);
+        for (int64_t b = 0; b < nb; b++) {
+            const DevBlock& d = blocks[(size_t)b];
+            std::vector<RbChunk> ck;
+            for (uint64_t o = 0; o < d.seq_bytes; o += RB_CHUNK) {
+                const uint32_t len = (uint32_t)std::min<uint64_t>(RB_CHUNK, d.seq_bytes - o);
+                ck.push_back(RbChunk{d.seq_base + o, len, (o == 0 ? RB_FIRST : 0u) | (o + len == d.seq_bytes ? RB_LAST : 0u)});
+            }
+            if (ck.empty()) continue;
+            std::vector<uint32_t> opens(ck.size() * RB_WORDS);
+            std::vector<RbRun> spec(ck.size()), entry(ck.size());
+            for (size_t c = 0; c < ck.size(); c++) spec[c] = rb_spec(qual.data(), ck[c], lossy, &opens[c * RB_WORDS]);
+            RbRun cur = spec[0];
+            for (size_t c = 1; c < ck.size(); c++) {
+                entry[c] = cur;
+                cur = rb_carry(qual.data(), ck[c], cur, lossy, &opens[c * RB_WORDS], spec[c]);
+            }
+            for (size_t c = ck.size(); c-- > 0;) rb_apply(qual.data(), qual_q.data(), ck[c], entry[c], lossy);
+            std::vector<uint8_t> ref(qual.begin() + (long)d.seq_base, qual.begin() + (long)(d.seq_base + d.seq_bytes));
+            orc_rblock(ref.data(), ref.size(), lossy);
+            if (std::memcmp(ref.data(), qual_q.data() + d.seq_base, ref.size())) {
+                std::printf("FAIL chunked rblock differs from the oracle (block %lld)\n", (long long)b);
+                return 1;
+            }
+        }
+        bv.qual_q = qual_q.data();
+    }
 
     // ---- prep + scan ----
     std::vector<uint32_t> counts((size_t)nr * NCOL);
@@ -350,7 +389,7 @@ int main(int argc, char** argv)
         for (uint32_t s = 0; s < nseg; s++) std::memcpy(o.data() + dst[s], payload.data() + bp.task_out_base[tsk[s]], len[s]);
         HostBlock& h = hb[(size_t)b];
         orc_block ob{h.names.data(), h.nl.data(), h.seq.data(), h.sl.data(), h.qual.data(), h.nreads};
-        orc_cfg oc{slevel, qlevel, 1, T[0]};
+        orc_cfg oc{slevel, qlevel, 1, T[0], lossy};
         std::vector<uint8_t> ref(2 * (h.seq.size() + h.names.size()) + 4096);
         int64_t rl = orc_encode_block(&ob, &oc, ref.data(), ref.size());
         bool ok = rl == (int64_t)L && std::memcmp(ref.data(), o.data(), L) == 0;

@@ -23,7 +23,8 @@ class _Blk(C.Structure):
 
 
 class _Cfg(C.Structure):
-    _fields_ = [("slevel", C.c_int), ("qlevel", C.c_int), ("md5", C.c_int), ("bin_mode", C.c_int)]
+    _fields_ = [("slevel", C.c_int), ("qlevel", C.c_int), ("md5", C.c_int), ("bin_mode", C.c_int),
+                ("lossy", C.c_double)]
 
 
 def build():
@@ -48,6 +49,8 @@ def lib():
         l.orc_md5.restype = None
         l.orc_decode_block.argtypes = [P, C.c_size_t, P, P]
         l.orc_decode_block.restype = C.c_int64
+        l.orc_rblock.argtypes = [P, C.c_size_t, C.c_double]
+        l.orc_rblock.restype = None
         _lib = l
     return _lib
 
@@ -60,10 +63,10 @@ def _blk(b) -> _Blk:
     return _Blk(_p(b.names), _p(b.name_lens), _p(b.seq), _p(b.seq_lens), _p(b.qual), b.nreads)
 
 
-def encode_block(b, slevel=3, qlevel=2, md5=True, bin_mode=0) -> bytes:
+def encode_block(b, slevel=3, qlevel=2, md5=True, bin_mode=0, lossy=0.0) -> bytes:
     cap = 2 * (b.seq.size + b.names.size) + 16 * b.nreads + 4096
     out = np.empty(cap, dtype=np.uint8)
-    cb, cc = _blk(b), _Cfg(slevel, qlevel, 1 if md5 else 0, 1 if bin_mode else 0)
+    cb, cc = _blk(b), _Cfg(slevel, qlevel, 1 if md5 else 0, 1 if bin_mode else 0, float(lossy))
     n = lib().orc_encode_block(C.byref(cb), C.byref(cc), _p(out), cap)
     if n < 0:
         raise RuntimeError("oracle encode failed")
@@ -77,7 +80,8 @@ class _Dec(C.Structure):
                 ("md5_ok", C.c_int)]
 
 
-def decode_block(data: bytes, max_reads: int, name_cap: int, seq_cap: int, slevel=3, qlevel=2, md5=True):
+def decode_block(data: bytes, max_reads: int, name_cap: int, seq_cap: int, slevel=3, qlevel=2, md5=True,
+                 lossy=0.0):
     """CPU decode of one encoded block (oracle/fqz_decode.c) -> (names, name_lens,
     seq, seq_lens, qual, md5_ok)."""
     names = np.empty(max(name_cap, 1), np.uint8)
@@ -87,13 +91,20 @@ def decode_block(data: bytes, max_reads: int, name_cap: int, seq_cap: int, sleve
     qual = np.empty(max(seq_cap, 1), np.uint8)
     d = _Dec(_p(names), _p(nl), _p(seq), _p(sl), _p(qual), name_cap, seq_cap, max_reads, 0, 0)
     src = np.frombuffer(data, np.uint8)
-    cc = _Cfg(slevel, qlevel, 1 if md5 else 0, 0)
+    cc = _Cfg(slevel, qlevel, 1 if md5 else 0, 0, float(lossy))
     n = lib().orc_decode_block(_p(src), src.size, C.byref(cc), C.byref(d))
     if n < 0:
         raise RuntimeError(f"oracle decode failed ({n})")
     n = int(n)
     ln, ls = int(nl[:n].astype(np.int64).sum()), int(sl[:n].astype(np.int64).sum())
     return names[:ln], nl[:n], seq[:ls], sl[:n], qual[:ls], bool(d.md5_ok)
+
+
+def rblock(qual: np.ndarray, ratio: float) -> np.ndarray:
+    """R-Block lossy pre-pass (rblock@0x426c10) over one block's qualities."""
+    q = np.array(qual, dtype=np.uint8, copy=True)
+    lib().orc_rblock(_p(q), q.size, float(ratio))
+    return q
 
 
 def analyze_ids(b, single_end: bool) -> np.ndarray:

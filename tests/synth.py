@@ -54,7 +54,7 @@ def generate(n_reads: int, read_len: int = 150, paired: bool = False, seed: int 
     ar = np.arange(read_len)
     for s in range(0, n_reads, chunk):
         n = min(chunk, n_reads - s)
-        start = rng.integers(0, genome_len - 450, size=n)
+        start = rng.integers(0, genome_len - max(450, read_len), size=n)
         ins = rng.integers(250, 450, size=n)
         r1 = genome[start[:, None] + ar[None, :]]
         sub = rng.random((n, read_len)) < 0.002

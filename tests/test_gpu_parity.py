@@ -23,7 +23,7 @@ def enc():
 
 
 def _oracle_outs(blocks, cfg):
-    return [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode) for b in blocks]
+    return [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode, cfg.lossy) for b in blocks]
 
 
 def _check(enc, blocks, cfg):
@@ -166,3 +166,25 @@ def test_long_reads_emit_steps(enc, slevel, qlevel):
     """SEQ contexts and QUAL contexts carried across k_emit_sq's 64-position steps."""
     blocks = fq.blocks_from_fastq(_long_read_fastq(5 + slevel, 700))
     _check(enc, blocks, fq.Config(slevel=slevel, qlevel=qlevel))
+
+
+@pytest.mark.parametrize("ratio", [1.05, 1.15, 1.6])
+def test_lossy_rblock(enc, test_pair, ratio):
+    """-l R (rblock@0x426c10 + no quality MD5): GPU chunked R-Block == the oracle's serial pass,
+    incl. a block of long reads whose runs cross many 8 KiB chunks."""
+    blocks = fq.blocks_from_fastq(*test_pair)
+    tmpl = fq.analyze_ids(blocks[0], False)
+    _check(enc, blocks, fq.Config(bin_mode=int(tmpl[0]), lossy=ratio))
+    t1, _ = synth.generate(60, paired=False, seed=11, read_len=20000)
+    _check(enc, fq.blocks_from_fastq(t1), fq.Config(lossy=ratio))
+    _check(enc, fq.blocks_from_fastq(synth.edge_cases()), fq.Config(lossy=ratio, md5=False))
+
+
+def test_long_length_path(enc):
+    """Reads > 65535 bp switch the block to compressLen_long@0x423710 (four length
+    bytes); a block of short reads next to it keeps compressLen_short."""
+    t_long, _ = synth.generate(12, paired=False, seed=5, read_len=70000)
+    t_short, _ = synth.generate(300, paired=False, seed=6)
+    blocks = fq.blocks_from_fastq(t_long) + fq.blocks_from_fastq(t_short)
+    _check(enc, blocks, fq.Config())
+    _check(enc, blocks, fq.Config(lossy=1.15, slevel=4))

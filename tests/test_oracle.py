@@ -89,15 +89,19 @@ def test_cpu_decomposition(tmp_path):
     src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
                     os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
-                    os.path.join(ROOT, "oracle", "fqz_oracle.c")], check=True)
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), "-lm"], check=True)
     import synth
     pe1, pe2 = synth.generate(3000, paired=True, seed=3)
     (tmp_path / "a.fq").write_bytes(pe1)
     (tmp_path / "b.fq").write_bytes(pe2)
     (tmp_path / "e.fq").write_bytes(synth.edge_cases())
+    (tmp_path / "long.fq").write_bytes(synth.generate(12, read_len=70000, seed=5)[0])
     runs = [[TEST1, TEST2], [TEST1], ["-b", "600000", TEST1, TEST2], [str(tmp_path / "a.fq"), str(tmp_path / "b.fq")],
             ["-s", "4", "-b", "300000", str(tmp_path / "a.fq"), str(tmp_path / "b.fq")],
-            ["-q", "3", str(tmp_path / "a.fq")], [str(tmp_path / "e.fq")], ["-s", "9", str(tmp_path / "e.fq")]]
+            ["-q", "3", str(tmp_path / "a.fq")], [str(tmp_path / "e.fq")], ["-s", "9", str(tmp_path / "e.fq")],
+            ["-l", "1.15", TEST1, TEST2], ["-l", "1.3", "-b", "300000", str(tmp_path / "a.fq")],
+            ["-l", "1.05", str(tmp_path / "e.fq")], [str(tmp_path / "long.fq")],
+            ["-l", "1.6", str(tmp_path / "long.fq")]]
     for args in runs:
         r = subprocess.run([str(exe)] + args, capture_output=True, text=True)
         assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
@@ -109,7 +113,7 @@ def test_coder_decomposition_selftest(tmp_path):
     src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
                     os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
-                    os.path.join(ROOT, "oracle", "fqz_oracle.c")], check=True)
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), "-lm"], check=True)
     r = subprocess.run([str(exe), "--coder"], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout
 
