@@ -43,6 +43,15 @@ class _SaCfg(C.Structure):
                 ("lossy", C.c_double)]
 
 
+class _SaArcBlock(C.Structure):
+    _fields_ = [("size", C.c_uint32), ("long_reads", C.c_uint32), ("text1", C.c_uint64), ("text2", C.c_uint64)]
+
+
+class _SaArcInfo(C.Structure):
+    _fields_ = [("file1", C.c_char_p), ("file2", C.c_char_p), ("paired", C.c_int32), ("gz1", C.c_int32),
+                ("bare_plus", C.c_int32), ("md5", C.c_int32), ("lossy", C.c_int32), ("id_template", C.c_void_p)]
+
+
 class _SaOut(C.Structure):
     _fields_ = [("data", C.c_void_p), ("cap", C.c_uint64), ("size", C.c_uint64)]
 
@@ -71,6 +80,7 @@ def load_library(path: str | None = None):
         "sa_analyze_ids": ([P, I32, P], I32),
         "sa_code_records": ([P, I32, P, P, P, P, P, U64, P], I32), "sa_coder_restarts": ([P], C.c_uint32),
         "sa_stream_stats": ([P, P, P], None),
+        "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -93,6 +103,8 @@ class Block:
     seq_lens: np.ndarray    # int32
     qual: np.ndarray        # uint8
     text_bytes: int = 0     # FASTQ bytes this block was parsed from
+    text1: int = 0          # ... of them in input 1 (ReadBuf+0xc)
+    text2: int = 0          # ... in input 2 (ReadBuf+0x10)
 
     @property
     def nreads(self) -> int:
@@ -196,7 +208,12 @@ def blocks_from_fastq(t1, t2=None, block_size: int = BLOCK_SIZE) -> list[Block]:
         a = _as_u8(t1)
         return [parse_se(a[s:e]) for s, e in cut_se(a, block_size)]
     a, b = _as_u8(t1), _as_u8(t2)
-    return [parse_pe(a[s1:e1], b[s2:e2]) for (s1, e1), (s2, e2) in cut_pe(a, b, block_size)]
+    out = []
+    for (s1, e1), (s2, e2) in cut_pe(a, b, block_size):
+        blk = parse_pe(a[s1:e1], b[s2:e2])
+        blk.text1, blk.text2 = e1 - s1, e2 - s2
+        out.append(blk)
+    return out
 
 
 class Encoder:
@@ -289,3 +306,36 @@ class Encoder:
         ms = (C.c_float * self.PHASES)()
         n = self._lib.sa_phase_times(self._ctx, names, ms, self.PHASES)
         return {names[i].decode(): float(ms[i]) for i in range(n)}
+
+
+def bare_plus(text) -> int:
+    """1 if the first record's '+' line carries no ID (getFirstLine@0x431eb0)."""
+    t = _as_u8(text)
+    nl = np.flatnonzero(t[: 1 << 16] == 10)[:3]
+    if nl.size < 3:
+        return 1
+    return 0 if int(nl[2]) - int(nl[1]) > 2 else 1
+
+
+def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str | None = None,
+                template: np.ndarray | None = None, cfg: Config | None = None, gz1: bool = False,
+                plus_bare: int = 1) -> bytes:
+    """The .arc file around encoded blocks (header, blocks in input order, trailer):
+    SeqArcFile::writeFileInfo@0x4171b0 / writeParam@0x416450 / writeBlockLenArry (arc_file.cpp)."""
+    lib = load_library()
+    cfg = cfg or Config()
+    recs = (_SaArcBlock * max(1, len(encaps)))()
+    for i, (e, b) in enumerate(zip(encaps, blocks)):
+        lng = 1 if b.nreads and int(b.seq_lens.max()) > 0xffff else 0
+        recs[i] = _SaArcBlock(len(e), lng, b.text1 or b.text_bytes, b.text2)
+    tmpl = np.zeros(512, np.uint8) if template is None else np.ascontiguousarray(template, dtype=np.uint8)
+    info = _SaArcInfo(file1.encode(), (file2 or "").encode(), 1 if file2 else 0, 1 if gz1 else 0, int(plus_bare),
+                      1 if cfg.md5 else 0, 1 if cfg.lossy > 0 else 0, _ptr(tmpl))
+    cap = 4096 + 40 * len(encaps)
+    tr = np.empty(cap, np.uint8)
+    n = lib.sa_arc_trailer(C.byref(info), recs, len(encaps), _ptr(tr), cap)
+    if n < 0:
+        raise SeqArcError("sa_arc_trailer failed")
+    hdr = np.zeros(16, np.uint8)
+    lib.sa_arc_header(sum(map(len, encaps)), _ptr(hdr))
+    return hdr.tobytes() + b"".join(encaps) + tr[:n].tobytes()

@@ -10,8 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libseqarc_amd.so")
-SOURCES = ["sa_engine.hip", "fastq_host.cpp"]
-DEPS = SOURCES + ["sa_kernels.hip", "sa_common.h", "sa_device.h", "sa_logic.h", "sa_plan.h"]
+BIN_DIR = os.path.join(HERE, "bin")
+CLI = os.path.join(BIN_DIR, "seqarc_amd")
+SOURCES = ["sa_engine.hip", "fastq_host.cpp", "arc_file.cpp"]
+DEPS = SOURCES + ["seqarc_cli.cpp", "sa_kernels.hip", "sa_common.h", "sa_device.h", "sa_logic.h", "sa_plan.h"]
 
 
 def _hipcc() -> str:
@@ -26,6 +28,8 @@ def needs_build() -> bool:
         return True
     t = os.path.getmtime(LIB)
     inc = os.path.join(HERE, "..", "include", "seqarc_amd.h")
+    if not os.path.exists(CLI):
+        return True
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in DEPS) or os.path.getmtime(inc) > t
 
 
@@ -40,6 +44,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    # the SeqArc -c command line over the library (seqarc_cli.cpp)
+    os.makedirs(BIN_DIR, exist_ok=True)
+    cli = [_hipcc(), "-O2", "-std=c++17", "-Wall", "-o", CLI + ".tmp", os.path.join(CSRC, "seqarc_cli.cpp"),
+           "-L" + LIB_DIR, "-lseqarc_amd", "-lz", "-Wl,-rpath,$ORIGIN/../lib"]
+    if verbose:
+        print(" ".join(cli), file=sys.stderr)
+    subprocess.run(cli, check=True)
+    os.replace(CLI + ".tmp", CLI)
     return LIB
 
 

@@ -1,0 +1,213 @@
+// seqarc_amd -- the SeqArc -c command line over libseqarc_amd (host C++).
+//
+//   seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]
+//              [--slevel K] [--qlevel Q] [--device D] [--batch BLOCKS]
+//
+// Mirrors the reference's encode path (SeqArc-1.6 main@0x41fd40 ->
+// SeqArcContext::doReadAndEncode@0x41a4e0): the reader cuts 50 MiB blocks
+// (SeqArcRead::doReadJob@0x432a80 / doReadPEJob@0x432d10), the first block
+// decides the ID template (IDProcess::analysisIDBinType@0x4310a0), every block
+// is encoded (here on one gfx950 device, a batch of blocks per launch) and the
+// blocks are written after a 16-byte header in input order, followed by the
+// trailer (SeqArcFile::writeFileInfo@0x4171b0).  Output: PREFIX.arc.
+// -t is accepted for command-line compatibility (the GPU encodes a batch of
+// blocks concurrently); Slevel / Qlevel are the reference's developer options
+// (./seqarc.config), given here as --slevel / --qlevel.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/seqarc_amd.h"
+
+namespace {
+
+bool slurp(const char* path, std::vector<uint8_t>& out, bool& gz)
+{
+    FILE* f = fopen(path, "rb");
+    if (!f) return false;
+    unsigned char m[2] = {0, 0};
+    gz = fread(m, 1, 2, f) == 2 && m[0] == 0x1f && m[1] == 0x8b;   // getFileType@0x40d9f0
+    fclose(f);
+    gzFile g = gzopen(path, "rb");
+    if (!g) return false;
+    gzbuffer(g, 1 << 18);
+    out.clear();
+    std::vector<uint8_t> buf(1 << 22);
+    for (;;) {
+        const int n = gzread(g, buf.data(), (unsigned)buf.size());
+        if (n < 0) { gzclose(g); return false; }
+        if (n == 0) break;
+        out.insert(out.end(), buf.begin(), buf.begin() + n);
+    }
+    gzclose(g);
+    return true;
+}
+
+// getFirstLine@0x431eb0: the '+' line of the first record is bare ("+\n")
+int bare_plus(const std::vector<uint8_t>& t)
+{
+    size_t nl[3] = {0, 0, 0};
+    int k = 0;
+    for (size_t i = 0; i < t.size() && k < 3; i++)
+        if (t[i] == '\n') nl[k++] = i + 1;
+    if (k < 3) return 1;
+    return nl[2] - nl[1] > 2 ? 0 : 1;
+}
+
+struct Parsed {
+    std::vector<uint8_t> names, seq, qual;
+    std::vector<uint16_t> nl;
+    std::vector<int32_t> sl;
+    uint32_t nreads = 0;
+    uint64_t text1 = 0, text2 = 0;
+    sa_block view() const { return sa_block{names.data(), nl.data(), seq.data(), sl.data(), qual.data(), nreads}; }
+};
+
+int usage()
+{
+    fprintf(stderr,
+            "usage: seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]\n"
+            "                  [--slevel K] [--qlevel Q] [--device D] [--batch BLOCKS]\n");
+    return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    const char *f1 = nullptr, *f2 = nullptr, *outp = nullptr;
+    bool compress = false;
+    sa_cfg cfg{3, 2, 1, 0, 0.0};
+    int device = 0, batch = 16;
+    for (int i = 1; i < argc; i++) {
+        const char* a = argv[i];
+        auto val = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
+        if (!strcmp(a, "-c")) compress = true;
+        else if (!strcmp(a, "-1")) f1 = val();
+        else if (!strcmp(a, "-2")) f2 = val();
+        else if (!strcmp(a, "-o")) outp = val();
+        else if (!strcmp(a, "-n")) cfg.md5 = 0;
+        else if (!strcmp(a, "-l")) { const char* v = val(); if (!v) return usage(); cfg.lossy = atof(v); }
+        else if (!strcmp(a, "-t")) { if (!val()) return usage(); }
+        else if (!strcmp(a, "--slevel")) { const char* v = val(); if (!v) return usage(); cfg.slevel = atoi(v); }
+        else if (!strcmp(a, "--qlevel")) { const char* v = val(); if (!v) return usage(); cfg.qlevel = atoi(v); }
+        else if (!strcmp(a, "--device")) { const char* v = val(); if (!v) return usage(); device = atoi(v); }
+        else if (!strcmp(a, "--batch")) { const char* v = val(); if (!v) return usage(); batch = atoi(v) > 0 ? atoi(v) : 1; }
+        else if (!strcmp(a, "-d")) {
+            fprintf(stderr, "seqarc_amd: -d (decode) is not built yet; decode with SeqArc -d\n");
+            return 2;
+        } else return usage();
+    }
+    if (!compress || !f1 || !outp) return usage();
+    const bool pe = f2 && *f2;
+
+    std::vector<uint8_t> t1, t2;
+    bool gz1 = false, gz2 = false;
+    if (!slurp(f1, t1, gz1) || (pe && !slurp(f2, t2, gz2))) {
+        fprintf(stderr, "seqarc_amd: cannot read input\n");
+        return 1;
+    }
+    const uint64_t bs = 50ull << 20;   // BlockSize(M) 50 (param+0x1b78)
+    const uint64_t maxb = (t1.size() + t2.size()) / 1024 + 16;
+    std::vector<uint64_t> e1(maxb), e2(maxb);
+    const int64_t nb = pe ? sa_cut_pe(t1.data(), t1.size(), t2.data(), t2.size(), bs, e1.data(), e2.data(), maxb)
+                          : sa_cut_se(t1.data(), t1.size(), bs, e1.data(), maxb);
+    if (nb < 0) {
+        fprintf(stderr, "seqarc_amd: block cut failed\n");
+        return 1;
+    }
+    auto parse = [&](int64_t b, Parsed& p) -> bool {
+        const uint64_t s1 = b ? e1[b - 1] : 0, s2 = (pe && b) ? e2[b - 1] : 0;
+        const uint64_t l1 = e1[b] - s1, l2 = pe ? e2[b] - s2 : 0;
+        const uint64_t cap = l1 + l2 + 16;
+        p.names.resize(cap); p.seq.resize(cap); p.qual.resize(cap);
+        p.nl.resize(cap / 4 + 8); p.sl.resize(cap / 4 + 8);
+        const int64_t n = pe ? sa_parse_pe(t1.data() + s1, l1, t2.data() + s2, l2, p.names.data(), p.nl.data(),
+                                           p.seq.data(), p.sl.data(), p.qual.data())
+                             : sa_parse_se(t1.data() + s1, l1, p.names.data(), p.nl.data(), p.seq.data(), p.sl.data(),
+                                           p.qual.data());
+        if (n < 0) return false;
+        p.nreads = (uint32_t)n;
+        p.text1 = l1;
+        p.text2 = l2;
+        return true;
+    };
+
+    uint8_t tmpl[512] = {0};
+    if (nb > 0) {
+        Parsed first;
+        if (!parse(0, first)) { fprintf(stderr, "seqarc_amd: parse failed\n"); return 1; }
+        const sa_block fb = first.view();
+        if (sa_analyze_ids(&fb, pe ? 0 : 1, tmpl) != 0) {
+            fprintf(stderr, "seqarc_amd: ID analysis failed\n");
+            return 1;
+        }
+    }
+    cfg.bin_mode = tmpl[0];
+
+    sa_ctx* ctx = sa_create(device);
+    if (!ctx) {
+        fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", device);
+        return 1;
+    }
+    const std::string path = std::string(outp) + ".arc";
+    FILE* fo = fopen(path.c_str(), "wb");
+    if (!fo) { fprintf(stderr, "seqarc_amd: cannot write %s\n", path.c_str()); sa_destroy(ctx); return 1; }
+    uint8_t hdr[16] = {0};
+    fwrite(hdr, 1, 16, fo);   // patched at the end (createOutFile@0x417480 / writeFileInfo@0x4171b0)
+    std::vector<sa_arc_block> info;
+    uint64_t total = 0;
+    int rc = 0;
+    for (int64_t b0 = 0; b0 < nb && !rc; b0 += batch) {
+        const int64_t n = std::min<int64_t>(batch, nb - b0);
+        std::vector<Parsed> ps((size_t)n);
+        std::vector<sa_block> in((size_t)n);
+        std::vector<std::vector<uint8_t>> bufs((size_t)n);
+        std::vector<sa_out> outs((size_t)n);
+        for (int64_t i = 0; i < n && !rc; i++) {
+            if (!parse(b0 + i, ps[(size_t)i])) { rc = 1; break; }
+            in[(size_t)i] = ps[(size_t)i].view();
+            bufs[(size_t)i].resize(sa_output_bound(&in[(size_t)i]));
+            outs[(size_t)i] = sa_out{bufs[(size_t)i].data(), bufs[(size_t)i].size(), 0};
+        }
+        if (rc) { fprintf(stderr, "seqarc_amd: parse failed\n"); break; }
+        if (sa_encode_blocks(ctx, in.data(), (int)n, &cfg, outs.data()) != 0) {
+            fprintf(stderr, "seqarc_amd: encode failed: %s\n", sa_last_error(ctx));
+            rc = 1;
+            break;
+        }
+        for (int64_t i = 0; i < n; i++) {
+            const Parsed& p = ps[(size_t)i];
+            uint32_t lng = 0;
+            for (uint32_t r = 0; r < p.nreads; r++) lng |= p.sl[r] > 0xffff;
+            fwrite(outs[(size_t)i].data, 1, outs[(size_t)i].size, fo);
+            info.push_back(sa_arc_block{(uint32_t)outs[(size_t)i].size, lng, p.text1, p.text2});
+            total += outs[(size_t)i].size;
+        }
+    }
+    sa_destroy(ctx);
+    if (!rc) {
+        sa_arc_info ai{f1, pe ? f2 : nullptr, pe ? 1 : 0, gz1 ? 1 : 0, bare_plus(pe ? t2 : t1), cfg.md5,
+                       cfg.lossy > 0.0 ? 1 : 0, tmpl};
+        std::vector<uint8_t> tr(4096 + 40 * info.size());
+        const int64_t tl = sa_arc_trailer(&ai, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
+        if (tl < 0) { fprintf(stderr, "seqarc_amd: trailer failed\n"); rc = 1; }
+        else {
+            fwrite(tr.data(), 1, (size_t)tl, fo);
+            sa_arc_header(total, hdr);
+            fseek(fo, 0, SEEK_SET);
+            fwrite(hdr, 1, 16, fo);
+            fprintf(stderr, "seqarc_amd: %lld block(s), %llu -> %llu bytes (%.2fx)\n", (long long)nb,
+                    (unsigned long long)(t1.size() + t2.size()), (unsigned long long)(16 + total + tl),
+                    (double)(t1.size() + t2.size()) / (double)(16 + total + tl));
+        }
+    }
+    fclose(fo);
+    return rc;
+}

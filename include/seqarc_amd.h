@@ -108,6 +108,35 @@ int64_t sa_parse_pe(const uint8_t *t1, uint64_t len1, const uint8_t *t2, uint64_
  * area, caller zero-initialised; tmpl[0] is sa_cfg.bin_mode. */
 int sa_analyze_ids(const sa_block *first, int single_end, uint8_t tmpl[512]);
 
+/* ---- .arc container (SeqArcFile, host) ---------------------------------- */
+/* Archive = 16-byte header + the encoded blocks back to back (input order,
+ * the reference's -t 1 order) + trailer.  Restated from
+ * SeqArcFile::writeFileInfo@0x4171b0, writeParam@0x416450 and
+ * writeBlockLenArry{SE,PE}@0x416d60/0x416e90 (fastqueeze_amd/csrc/arc_file.cpp). */
+typedef struct {
+    uint32_t size;         /* encoded block bytes (sa_out.size of the block)           */
+    uint32_t long_reads;   /* a read > 65535 bp (SeqArcMemBuf+0x2; compressLen_long)   */
+    uint64_t text1;        /* FASTQ text bytes of the block in input 1 (ReadBuf+0xc)   */
+    uint64_t text2;        /* ... in input 2 (ReadBuf+0x10; 0 for single-end)          */
+} sa_arc_block;
+
+typedef struct {
+    const char *file1;             /* input paths as given (basename stored, ".gz" cut) */
+    const char *file2;             /* NULL / "" for single-end                          */
+    int32_t paired;
+    int32_t gz1;                   /* param+0x6: input 1 is gzip (getFileType@0x40d9f0)  */
+    int32_t bare_plus;             /* '+' lines carry no ID (getFirstLine@0x431eb0)      */
+    int32_t md5;                   /* param+0x1880                                       */
+    int32_t lossy;                 /* param+0x1870 (-l)                                  */
+    const uint8_t *id_template;    /* 512 B, param+0x18a4 (sa_analyze_ids)               */
+} sa_arc_info;
+
+/* 16-byte header; block_bytes = sum of the blocks' sizes. Returns 0. */
+int sa_arc_header(uint64_t block_bytes, uint8_t out[16]);
+/* Trailer bytes written to out (written at offset 16 + block_bytes), or -1. */
+int64_t sa_arc_trailer(const sa_arc_info *info, const sa_arc_block *blocks, uint32_t nblocks,
+                       uint8_t *out, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -188,3 +188,37 @@ def test_long_length_path(enc):
     blocks = fq.blocks_from_fastq(t_long) + fq.blocks_from_fastq(t_short)
     _check(enc, blocks, fq.Config())
     _check(enc, blocks, fq.Config(lossy=1.15, slevel=4))
+
+
+def test_cli_archive(tmp_path, test_pair):
+    """seqarc_amd -c (the SeqArc -c surface) writes the reference-sized archive:
+    the GPU blocks inside the restated container, plain and gzip inputs."""
+    import gzip
+    import shutil
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fastqueeze_amd", "bin",
+                       "seqarc_amd")
+    names = ["ERR2755197_test_1.fq", "ERR2755197_test_2.fq"]
+    paths = [str(tmp_path / n) for n in names]
+    for p, t in zip(paths, test_pair):
+        open(p, "wb").write(t)
+    blocks = fq.blocks_from_fastq(*test_pair)
+    tmpl = fq.analyze_ids(blocks[0], False)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    want = fq.arc_archive(_oracle_outs(blocks, cfg), blocks, names[0], names[1], tmpl, cfg)
+    r = subprocess.run([exe, "-c", "-t", "1", "-1", paths[0], "-2", paths[1], "-o", str(tmp_path / "pe")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = open(tmp_path / "pe.arc", "rb").read()
+    assert len(got) == 821500 and got == want
+    for p in paths:
+        with open(p, "rb") as f, gzip.open(p + ".gz", "wb") as g:
+            shutil.copyfileobj(f, g)
+    r = subprocess.run([exe, "-c", "-1", paths[0] + ".gz", "-2", paths[1] + ".gz", "-o", str(tmp_path / "gz")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    gz = open(tmp_path / "gz.arc", "rb").read()
+    assert len(gz) == len(want) and gz[:16 + len(got) - 700] == want[:16 + len(got) - 700]
+    r = subprocess.run([exe, "-c", "-1", paths[0], "-o", str(tmp_path / "se")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and os.path.getsize(tmp_path / "se.arc") == 379069, r.stderr
