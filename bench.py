@@ -51,9 +51,10 @@ def main():
     ap.add_argument("--block-size", type=int, default=fq.BLOCK_SIZE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
-                    help="per-launch HBM bytes of the dominant kernel from the PMC passes "
-                         "(scripts/gpu_pmc.sh + scripts/pmc_traffic.py) of this tree")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes per kernel from the two rocprofv3 --pmc passes "
+                         "(FETCH_SIZE x2 + WRITE_SIZE; scripts/gpu_r2.sh + scripts/pmc_traffic.py) of this "
+                         "tree's default bench, committed under profiles/")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -172,7 +173,8 @@ def main():
                    "parallelism": f"block-shard x{world}"},
         "ratio": round(in_bytes / out_bytes, 3),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 --pmc, profiles/traffic_latest.json)"},
         "chain_bound": {"kernel": "coder_r", "longest_stream_symbols": max_syms, "all_stream_symbols": all_syms,
                         "salu_per_symbol": R_SALU_PER_SYMBOL, "bound_ms": round(max_syms * R_NS_PER_SYMBOL / 1e6, 2),
                         "achieved_ms": round(ph.get("coder_r", 0.0), 2),
