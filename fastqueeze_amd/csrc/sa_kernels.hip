@@ -476,35 +476,71 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, c
         atomicAdd(&h[(k >> shift) & 255], 1u);
     }
     __syncthreads();
-    sv.hist[sg.hist_base + (size_t)threadIdx.x * sg.ntiles + lt] = h[threadIdx.x];
+    sv.hist[sg.hist_base + (size_t)lt * 256 + threadIdx.x] = h[threadIdx.x];   // tile-major: one coalesced row
 }
 
+// The segment's digit counts are tile-major (row t = tile t's 256 counts); the
+// output is, in place, each (tile, digit)'s start in the sorted segment:
+// base[d] + the counts of d in earlier tiles.  Four thread groups take a
+// quarter of the tiles each; a thread walks one digit column, reading rows
+// coalesced across the 256 digits.
 __global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
 {
-    __shared__ uint32_t sh[16];
+    __shared__ uint32_t part[4][256];
+    __shared__ uint32_t dsum[4];
     const SortSeg& sg = sv.segs[blockIdx.x];
     uint32_t* H = sv.hist + sg.hist_base;
-    const size_t n = (size_t)sg.ntiles * 256;
-    uint32_t carry = 0;
-    for (size_t base = 0; base < n; base += 4096) {
-        uint32_t v[4];
-        uint32_t loc = 0;
+    const uint32_t d = threadIdx.x & 255, g = threadIdx.x >> 8;
+    const uint32_t nt = sg.ntiles, q = (nt + 3) / 4;
+    const uint32_t t0 = g * q < nt ? g * q : nt, t1 = t0 + q < nt ? t0 + q : nt;
+    uint32_t sum = 0;
+    uint32_t t = t0;
+    for (; t + 8 <= t1; t += 8) {
+        uint32_t v[8];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            size_t i = base + (size_t)threadIdx.x * 4 + j;
-            v[j] = i < n ? H[i] : 0;
-            loc += v[j];
+        for (int j = 0; j < 8; j++) v[j] = H[(size_t)(t + j) * 256 + d];
+#pragma unroll
+        for (int j = 0; j < 8; j++) sum += v[j];
+    }
+    for (; t < t1; t++) sum += H[(size_t)t * 256 + d];
+    part[g][d] = sum;
+    __syncthreads();
+    // digit bases: exclusive scan of the digit totals by waves 0-3 (group 0);
+    // every thread reaches both barriers
+    uint32_t tot = 0, inc = 0;
+    if (g == 0) {
+        tot = part[0][d] + part[1][d] + part[2][d] + part[3][d];
+        inc = wave_incl_scan_dpp(tot);
+        if (lane_id() == 63) dsum[threadIdx.x >> 6] = inc;
+    }
+    __syncthreads();
+    if (g == 0) {
+        uint32_t acc = inc - tot;
+        for (uint32_t k = 0; k < (threadIdx.x >> 6); k++) acc += dsum[k];
+#pragma unroll
+        for (int gg = 0; gg < 4; gg++) {
+            const uint32_t p = part[gg][d];
+            part[gg][d] = acc;
+            acc += p;
         }
-        uint32_t ex;
-        uint32_t tot = wg1024_excl_scan(loc, ex, sh);
-        uint32_t run = carry + ex;
+    }
+    __syncthreads();
+    uint32_t run = part[g][d];
+    t = t0;
+    for (; t + 8 <= t1; t += 8) {
+        uint32_t v[8];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            size_t i = base + (size_t)threadIdx.x * 4 + j;
-            if (i < n) H[i] = run;
+        for (int j = 0; j < 8; j++) v[j] = H[(size_t)(t + j) * 256 + d];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            H[(size_t)(t + j) * 256 + d] = run;
             run += v[j];
         }
-        carry += tot;
+    }
+    for (; t < t1; t++) {
+        const uint32_t v = H[(size_t)t * 256 + d];
+        H[(size_t)t * 256 + d] = run;
+        run += v;
     }
 }
 
@@ -560,7 +596,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         uint32_t ex;
         wg256_excl_scan(acc, ex, dsum);
         lstart[d] = ex;
-        gstart[d] = sv.hist[sg.hist_base + (size_t)d * sg.ntiles + lt] - ex;
+        gstart[d] = sv.hist[sg.hist_base + (size_t)lt * 256 + d] - ex;
     }
     __syncthreads();
     // stage the tile in digit order in LDS, then write it out: consecutive
