@@ -52,6 +52,12 @@ class _SaArcInfo(C.Structure):
                 ("bare_plus", C.c_int32), ("md5", C.c_int32), ("lossy", C.c_int32), ("id_template", C.c_void_p)]
 
 
+class _SaDecoded(C.Structure):
+    _fields_ = [("names", C.c_void_p), ("name_lens", C.c_void_p), ("seq", C.c_void_p), ("seq_lens", C.c_void_p),
+                ("qual", C.c_void_p), ("name_cap", C.c_uint64), ("seq_cap", C.c_uint64), ("max_reads", C.c_uint32),
+                ("nreads", C.c_uint32), ("md5_ok", C.c_int32)]
+
+
 class _SaOut(C.Structure):
     _fields_ = [("data", C.c_void_p), ("cap", C.c_uint64), ("size", C.c_uint64)]
 
@@ -81,6 +87,7 @@ def load_library(path: str | None = None):
         "sa_code_records": ([P, I32, P, P, P, P, P, U64, P], I32), "sa_coder_restarts": ([P], C.c_uint32),
         "sa_stream_stats": ([P, P, P], None),
         "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
+        "sa_decode_block": ([P, U64, P, P, I32, P], I64),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -339,3 +346,27 @@ def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str
     hdr = np.zeros(16, np.uint8)
     lib.sa_arc_header(sum(map(len, encaps)), _ptr(hdr))
     return hdr.tobytes() + b"".join(encaps) + tr[:n].tobytes()
+
+
+def decode_block(data: bytes, text_bytes: int, cfg: Config | None = None, template: np.ndarray | None = None,
+                 long_reads: bool = False) -> tuple[Block, bool]:
+    """Host decode of one encoded block (sa_decode_block; doFqzDecode@0x42c680):
+    (the block's reads, stored MD5s match).  text_bytes bounds the arrays
+    (the block's FASTQ size, from the archive's block table)."""
+    lib = load_library()
+    cfg = cfg or Config()
+    cap = int(text_bytes) + 64
+    names, seq, qual = (np.empty(cap, np.uint8) for _ in range(3))
+    mr = cap // 4 + 8
+    nl, sl = np.empty(mr, np.uint16), np.empty(mr, np.int32)
+    d = _SaDecoded(_ptr(names), _ptr(nl), _ptr(seq), _ptr(sl), _ptr(qual), cap, cap, mr, 0, 0)
+    src = np.frombuffer(data, np.uint8)
+    tmpl = np.zeros(512, np.uint8) if template is None else np.ascontiguousarray(template, dtype=np.uint8)
+    c = cfg._c()
+    n = lib.sa_decode_block(_ptr(src), src.size, C.byref(c), _ptr(tmpl), 1 if long_reads else 0, C.byref(d))
+    if n < 0:
+        raise SeqArcError("sa_decode_block: malformed block")
+    n = int(n)
+    ln, ls = int(nl[:n].astype(np.int64).sum()), int(sl[:n].astype(np.int64).sum())
+    return Block(names[:ln].copy(), nl[:n].copy(), seq[:ls].copy(), sl[:n].copy(), qual[:ls].copy(), text_bytes), \
+        bool(d.md5_ok)

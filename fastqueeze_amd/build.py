@@ -12,7 +12,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libseqarc_amd.so")
 BIN_DIR = os.path.join(HERE, "bin")
 CLI = os.path.join(BIN_DIR, "seqarc_amd")
-SOURCES = ["sa_engine.hip", "fastq_host.cpp", "arc_file.cpp"]
+SOURCES = ["sa_engine.hip", "fastq_host.cpp", "arc_file.cpp", "arc_decode.cpp"]
 DEPS = SOURCES + ["seqarc_cli.cpp", "sa_kernels.hip", "sa_common.h", "sa_device.h", "sa_logic.h", "sa_plan.h"]
 
 

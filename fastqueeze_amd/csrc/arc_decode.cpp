@@ -1,0 +1,547 @@
+// arc_decode.cpp -- host decoder of one encoded block (SeqArc -d path).
+//
+// The inverse of the block layout doFqzEncode@0x42d2d0 writes; the reference's
+// decoder is EncapFqzComp::doFqzDecode@0x42c680 (decode_seq@0x4296b0,
+// decode_qual@0x42a750, decode_name@0x428380, the Dege decoders) and, in ID-bin
+// mode, IDProcess::decodeIDS@0x430610 + assembleNameS@0x4300a0.  Adaptive
+// decoding is a serial chain per stream (each symbol updates the model the next
+// one is read with), so blocks are decoded on host threads, one block each.
+#include <stdint.h>
+#include <string.h>
+
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/seqarc_amd.h"
+
+namespace {
+
+// ---- carry-less range decoder (Subbotin; the coder of encode_seq@0x422010) ----
+class RangeIn {
+public:
+    RangeIn(const uint8_t* p, const uint8_t* end) : p_(p), end_(end)
+    {
+        for (int i = 0; i < 8; i++) code_ = (code_ << 8) | byte();
+    }
+    // slot of the next symbol in [0, tot) and the scale range / tot
+    uint32_t slot(uint32_t tot, uint32_t& scale)
+    {
+        scale = range_ / tot;
+        const uint64_t v = (code_ - low_) / scale;
+        if (v >= tot) { bad = true; return tot - 1; }
+        return (uint32_t)v;
+    }
+    void consume(uint32_t scale, uint32_t cum, uint32_t freq)
+    {
+        low_ += (uint32_t)(cum * scale);
+        range_ = scale * freq;
+        while (range_ < (1u << 24)) {
+            if ((low_ ^ (low_ + range_)) >> 56) range_ = ((uint32_t)low_ | 0xffffffu) - (uint32_t)low_;
+            code_ = (code_ << 8) | byte();
+            range_ <<= 8;
+            low_ <<= 8;
+        }
+    }
+    bool bad = false;
+
+private:
+    uint8_t byte()
+    {
+        if (p_ < end_) return *p_++;
+        bad = true;
+        return 0;
+    }
+    const uint8_t *p_, *end_;
+    uint64_t low_ = 0, code_ = 0;
+    uint32_t range_ = 0xffffffffu;
+};
+
+// ---- SIMPLE_MODEL<N> (kModelEncode@0x42ccb0 layout): symbol list ordered by
+//      bubble swaps every 16th update, +8 per hit, halving above 0xffe0 ----
+class SModel {
+public:
+    void reset(int n)
+    {
+        n_ = n;
+        tot_ = (uint32_t)n;
+        bub_ = 0;
+        for (int i = 0; i < n; i++) { sym_[i] = (uint16_t)i; freq_[i] = 1; }
+    }
+    int decode(RangeIn& rc)
+    {
+        uint32_t scale;
+        const uint32_t v = rc.slot(tot_, scale);
+        uint32_t acc = 0;
+        int i = 0;
+        while (i < n_ && acc + freq_[i] <= v) acc += freq_[i++];
+        if (i >= n_) { rc.bad = true; return 0; }
+        const int s = sym_[i];
+        rc.consume(scale, acc, freq_[i]);
+        freq_[i] += 8;
+        tot_ += 8;
+        if (tot_ > 0xffe0) {
+            tot_ = 0;
+            for (int k = 0; k < n_; k++) { freq_[k] -= freq_[k] >> 1; tot_ += freq_[k]; }
+        }
+        if ((++bub_ & 15) == 0 && i > 0 && freq_[i] > freq_[i - 1]) {
+            std::swap(freq_[i], freq_[i - 1]);
+            std::swap(sym_[i], sym_[i - 1]);
+        }
+        return s;
+    }
+
+private:
+    int n_ = 0;
+    uint32_t tot_ = 0, bub_ = 0;
+    uint16_t sym_[256], freq_[256];
+};
+
+// kModel (kModelInit@0x42cbe0 / kModelEncode@0x42ccb0): bit count, then bits LSB first
+struct KModel {
+    SModel nbits, bits[64];
+    void reset()
+    {
+        nbits.reset(64);
+        for (auto& b : bits) b.reset(2);
+    }
+    uint64_t decode(RangeIn& rc)
+    {
+        const int nb = nbits.decode(rc);
+        uint64_t v = 0;
+        for (int i = 0; i < nb && i < 64; i++) v |= (uint64_t)bits[i].decode(rc) << i;
+        return v;
+    }
+};
+
+// ---- RFC 1321 MD5 (the block digests, calcBlockMd5@0x414d90) ----
+void md5(const uint8_t* data, size_t len, uint8_t out[16])
+{
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+    static const uint8_t S[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+    uint32_t h[4] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476};
+    auto block = [&](const uint8_t* p) {
+        uint32_t M[16];
+        for (int i = 0; i < 16; i++) M[i] = (uint32_t)p[4 * i] | (uint32_t)p[4 * i + 1] << 8 | (uint32_t)p[4 * i + 2] << 16 | (uint32_t)p[4 * i + 3] << 24;
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+        for (int i = 0; i < 64; i++) {
+            uint32_t f;
+            int g;
+            const int r = i >> 4;
+            if (r == 0) { f = (b & c) | (~b & d); g = i; }
+            else if (r == 1) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
+            else if (r == 2) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
+            else { f = c ^ (b | ~d); g = (7 * i) & 15; }
+            const uint32_t x = a + f + K[i] + M[g];
+            const int s = S[r][i & 3];
+            a = d; d = c; c = b;
+            b = b + ((x << s) | (x >> (32 - s)));
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+    };
+    size_t i = 0;
+    for (; i + 64 <= len; i += 64) block(data + i);
+    uint8_t tail[128] = {0};
+    const size_t r = len - i;
+    memcpy(tail, data + i, r);
+    tail[r] = 0x80;
+    const size_t tl = r < 56 ? 64 : 128;
+    const uint64_t bits = (uint64_t)len * 8;
+    for (int k = 0; k < 8; k++) tail[tl - 8 + k] = (uint8_t)(bits >> (8 * k));
+    block(tail);
+    if (tl == 128) block(tail + 64);
+    for (int k = 0; k < 16; k++) out[k] = (uint8_t)(h[k >> 2] >> (8 * (k & 3)));
+}
+
+// ---- encap walking (the one-byte IDs and 4-byte sizes of this layout) ----
+struct Cursor {
+    const uint8_t *p, *end;
+    bool bad = false;
+    bool id(int v)
+    {
+        if (p < end && *p == (uint8_t)(0x80 | v)) { p++; return true; }
+        return false;
+    }
+    uint32_t size4()
+    {
+        if (end - p < 4) { bad = true; return 0; }
+        const uint32_t v = ((uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]) & 0x0fffffffu;
+        p += 4;
+        if ((uint64_t)(end - p) < v) bad = true;
+        return v;
+    }
+};
+
+uint32_t le32(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+
+bool is_delim(uint8_t c) { return c == ' ' || (c >= '!' && c <= '/') || (c >= ':' && c <= '@') || (c >= '[' && c <= '`') || (c >= '{' && c <= '~'); }
+
+// encode_name@0x421070 inverse: prefix / suffix / length models keyed by the
+// previous name, middle characters keyed by the aligned previous-name byte.
+class NameDecoder {
+public:
+    NameDecoder() : m_(new SModel[768 + 8192])
+    {
+        for (int i = 0; i < 768; i++) m_[i].reset(256);
+        for (int i = 0; i < 8192; i++) m_[768 + i].reset(128);
+        buf_[0] = 0;   // the byte before the buffer (an alignment step can reach index -1)
+        memset(last_, ' ', 1024 + 1);
+    }
+    int decode(RangeIn& rc, uint8_t* name, int cap)
+    {
+        const int p = m_[last_p_].decode(rc), s = m_[256 + last_s_].decode(rc), len = m_[512 + last_len_].decode(rc);
+        if (rc.bad || len > cap || p + s > len || p > last_len_ || s > last_len_) return -1;
+        last_p_ = p;
+        last_s_ = s;
+        memcpy(name, last_, (size_t)p);
+        const int body = len - s;
+        int lc = p != 0, k = 0, j = p;
+        for (int i = p; i < body; i++) {
+            if (j > 1023) return -1;
+            const int ctx = (k * 64 + lc + 2 * ((int)(int8_t)last_[j] - 32)) % 8192;
+            if (ctx < 0) return -1;
+            const uint8_t c = (uint8_t)m_[768 + ctx].decode(rc);
+            name[i] = c;
+            bool reset = false;
+            if (c == ' ') {
+                if (last_[j] != ' ' && last_[j + 1] != ':') j++;
+                k = (k + 3) & ~3;
+                reset = j < 0;
+            } else {
+                uint8_t d = last_[j];
+                if (d == ' ') d = last_[--j];
+                if (c == ':') {
+                    j += d != ':';
+                    k = (k + 3) & ~3;
+                } else {
+                    j -= d == ':';
+                }
+                reset = j < 0;
+            }
+            if (reset) { j = 0; lc = 0; k++; }
+            else { lc = c == last_[j]; j++; k++; }
+        }
+        memcpy(name + body, last_ + last_len_ - s, (size_t)s);
+        memcpy(last_, name, (size_t)len);
+        last_len_ = len;
+        return rc.bad ? -1 : len;
+    }
+
+private:
+    std::unique_ptr<SModel[]> m_;
+    uint8_t buf_[1 + 1024 + 2];
+    uint8_t* const last_ = buf_ + 1;
+    int last_len_ = 0, last_p_ = 0, last_s_ = 0;
+};
+
+// ID-bin names: decodeIDS@0x430610 / assembleNameS@0x4300a0.  The block keeps
+// its first ID; token k of name i is template type T[k+2]: 0 the first ID's
+// token, 1 its number + i (+ i/2 for pairs), 3 the read length; mates per the
+// PE type T[1]: 1 the same name, 2 the last character '2', 3 the name up to
+// its last delimiter + the mate's length.
+bool bin_names(const uint8_t* first, int flen, const uint8_t T[512], const int32_t* lens, uint32_t n,
+               uint8_t* names, uint64_t cap, uint16_t* nl, uint64_t& used)
+{
+    std::vector<std::string> tok;
+    std::string delim;
+    int i = 0;
+    while (i < flen && is_delim(first[i])) i++;
+    while (i < flen) {
+        int j = i;
+        while (j < flen && !is_delim(first[j])) j++;
+        tok.emplace_back((const char*)first + i, (size_t)(j - i));
+        if (j < flen) delim.push_back((char)first[j]);
+        while (j < flen && is_delim(first[j])) j++;
+        i = j;
+    }
+    std::vector<uint64_t> val(tok.size(), 0);
+    for (size_t k = 0; k < tok.size(); k++)
+        if (k + 2 < 512 && T[k + 2] == 1) val[k] = strtoull(tok[k].c_str(), nullptr, 10);
+    const int pet = T[1];
+    used = 0;
+    auto put = [&](const std::string& s, uint32_t r) {
+        if (used + s.size() > cap || s.size() > 0xffff) return false;
+        memcpy(names + used, s.data(), s.size());
+        used += s.size();
+        nl[r] = (uint16_t)s.size();
+        return true;
+    };
+    auto assemble = [&](uint32_t idx) {
+        std::string s;
+        for (size_t k = 0; k < tok.size(); k++) {
+            const int ty = k + 2 < 512 ? T[k + 2] : 0;
+            if (ty == 1) s += std::to_string(val[k] + (pet ? idx / 2 : idx));
+            else if (ty == 3) s += std::to_string(lens[idx]);
+            else if (ty == 0) s += tok[k];
+            if (k + 1 < tok.size() && k < delim.size()) s += delim[k];
+        }
+        return s;
+    };
+    if (!pet) {
+        for (uint32_t r = 0; r < n; r++)
+            if (!put(assemble(r), r)) return false;
+        return true;
+    }
+    for (uint32_t r = 0; r < n; r += 2) {
+        const std::string a = assemble(r);
+        if (!put(a, r)) return false;
+        if (r + 1 >= n) break;
+        std::string b = a;
+        if (pet == 2 && !b.empty()) b.back() = '2';
+        else if (pet == 3) {
+            const char last = delim.empty() ? ' ' : delim.back();
+            const size_t at = a.rfind(last);
+            b = a.substr(0, at == std::string::npos ? 0 : at + 1) + std::to_string(lens[r + 1]);
+        }
+        if (!put(b, r + 1)) return false;
+    }
+    return true;
+}
+
+const char kIupac[] = "NMRYKSWHBVD";   // base codes 4..14 (seq_val_table@0x44b800)
+
+}  // namespace
+
+extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_cfg* cfg, const uint8_t tmpl[512],
+                                   int32_t long_reads, sa_decoded* o)
+{
+    if (!in || !cfg || !o) return -1;
+    Cursor c{in, in + in_len};
+    o->md5_ok = 1;
+    if (!c.id(1)) return -1;
+    const uint32_t bsize = c.size4();
+    if (c.bad) return -1;
+    c.end = c.p + bsize;
+    if (!c.id(1) || c.end - c.p < 5 || c.p[0] != 0x84) return -1;   // compressCount@0x422a00
+    const uint32_t n = le32(c.p + 1);
+    c.p += 5;
+    if (n > o->max_reads) return -1;
+    o->nreads = n;
+    std::vector<uint32_t> len(n);
+    const bool md5_q = cfg->md5 && !(cfg->lossy > 0.0);
+    uint8_t dg_id[16], dg_q[16], dg_s[16];
+
+    {   // lengths: compressLen_short@0x423f50 / compressLen_long@0x423710
+        if (!c.id(4)) return -1;
+        const uint32_t sz = c.size4();
+        if (c.bad) return -1;
+        SModel same, by[4];
+        same.reset(2);
+        for (auto& m : by) m.reset(256);
+        RangeIn rc(c.p, c.p + sz);
+        const int nbytes = long_reads ? 4 : 2;
+        for (uint32_t r = 0; r < n; r++) {
+            if (same.decode(rc)) { len[r] = 0; continue; }
+            uint32_t v = 0;
+            for (int k = 0; k < nbytes; k++) v |= (uint32_t)by[k].decode(rc) << (8 * k);
+            len[r] = v;
+        }
+        if (rc.bad) return -1;
+        c.p += sz;
+    }
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < n; r++) { o->seq_lens[r] = (int32_t)len[r]; total += len[r]; }
+    if (total > o->seq_cap) return -1;
+
+    uint64_t name_total = 0;
+    {   // IDs: compressID@0x4247c0
+        if (!c.id(5)) return -1;
+        const uint32_t sz = c.size4();
+        if (c.bad) return -1;
+        const uint8_t* q = c.p;
+        const uint8_t* qe = c.p + sz;
+        if (cfg->md5) { if (qe - q < 16) return -1; memcpy(dg_id, q, 16); q += 16; }
+        if (cfg->bin_mode) {
+            if (qe - q < 2) return -1;
+            const int fl = q[0] | q[1] << 8;
+            if (qe - q < 2 + fl) return -1;
+            if (!bin_names(q + 2, fl, tmpl, o->seq_lens, n, o->names, o->name_cap, o->name_lens, name_total)) return -1;
+        } else {
+            NameDecoder nd;
+            RangeIn rc(q, qe);
+            for (uint32_t r = 0; r < n; r++) {
+                const uint64_t room = o->name_cap - name_total;
+                const int l = nd.decode(rc, o->names + name_total, room > 255 ? 255 : (int)room);
+                if (l < 0) return -1;
+                o->name_lens[r] = (uint16_t)l;
+                name_total += (uint64_t)l;
+            }
+            if (rc.bad) return -1;
+        }
+        c.p += sz;
+    }
+
+    {   // qualities: compressQual@0x426e80 / encode_qual@0x422180
+        if (!c.id(7)) return -1;
+        const uint32_t sz = c.size4();
+        if (c.bad) return -1;
+        const uint8_t* q = c.p;
+        if (md5_q) { memcpy(dg_q, q, 16); q += 16; }
+        const uint32_t nm = cfg->qlevel > 2 ? 0x100000u : 0x10000u;
+        std::unique_ptr<SModel[]> qm(new SModel[nm]);
+        for (uint32_t i = 0; i < nm; i++) qm[i].reset(95);
+        RangeIn rc(q, c.p + sz);
+        uint8_t* Q = o->qual;
+        for (uint32_t r = 0; r < n && !rc.bad; r++) {
+            uint32_t last = 0;
+            int q1 = 0, q2 = 0, delta = 5;
+            for (uint32_t i = 0; i < len[r]; i++) {
+                const int s = qm[last].decode(rc);
+                if (s == 94) { memset(Q + i, '#', len[r] - i); break; }   // the stripped trailing '#' run
+                Q[i] = (uint8_t)(s + 33);
+                uint32_t ctx = ((uint32_t)((q1 > q2 ? q1 : q2) << 6) + (uint32_t)s) & 0xfffu;
+                if (cfg->qlevel > 1) {
+                    ctx += q1 == q2 ? 0x1000u : 0u;
+                    delta += q1 > s ? q1 - s : 0;
+                    ctx += (uint32_t)(((delta <= 56 ? delta : 56) & 0xf8) << 10);
+                    if (cfg->qlevel > 2) ctx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
+                }
+                q2 = q1;
+                q1 = s;
+                last = ctx;
+            }
+            Q += len[r];
+        }
+        if (rc.bad) return -1;
+        c.p += sz;
+    }
+
+    // N / IUPAC side streams (DegeInfoProcess@0x433a10): 23 tip, 14 chars,
+    // 24 max quality, 25 exception counts, 26 gaps (25 and 26 share one kModel)
+    std::vector<uint8_t> tip(n, 0), isn(total, 0), chs, maxq;
+    std::vector<uint64_t> exc, gaps;
+    {
+        KModel km;
+        km.reset();
+        uint32_t ntip = 0;
+        const int ids[5] = {23, 14, 24, 25, 26};
+        for (int s = 0; s < 5; s++) {
+            if (!c.id(ids[s])) continue;   // omitted when empty
+            const uint32_t sz = c.size4();
+            if (c.bad || sz < 4) return -1;
+            const uint32_t cnt = le32(c.p);
+            RangeIn rc(c.p + 4, c.p + sz);
+            if (ids[s] == 23) {
+                SModel m;
+                m.reset(2);
+                for (uint32_t i = 0; i < cnt && i < n; i++) ntip += tip[i] = (uint8_t)m.decode(rc);
+            } else if (ids[s] == 14 || ids[s] == 24) {
+                SModel m;
+                m.reset(ids[s] == 14 ? 11 : 95);
+                std::vector<uint8_t>& v = ids[s] == 14 ? chs : maxq;
+                v.resize(cnt);
+                for (uint32_t i = 0; i < cnt; i++) v[i] = (uint8_t)m.decode(rc);
+            } else {
+                std::vector<uint64_t>& v = ids[s] == 25 ? exc : gaps;
+                v.resize(cnt);
+                for (uint32_t i = 0; i < cnt; i++) v[i] = km.decode(rc);
+            }
+            if (rc.bad) return -1;
+            c.p += sz;
+        }
+        if (maxq.size() != ntip || exc.size() != ntip) return -1;
+        // a tip-1 read's candidate positions (quality <= its max) read
+        // N^g1 B N^g2 B ... N^gE B N...: gaps g, E = exception count.  With -l
+        // the candidates were chosen on the original qualities, which the
+        // archive no longer holds (the reference's decoder fails there, SURVEY
+        // section 5 ii): placement stops at the first inconsistency and the
+        // sequence MD5 reports it.
+        const bool lenient = cfg->lossy > 0.0;
+        size_t it = 0, ig = 0, ic = 0;
+        uint64_t at = 0;
+        const uint8_t* Q = o->qual;
+        for (uint32_t r = 0; r < n; r++) {
+            if (tip[r]) {
+                const int mq = (int)maxq[it] + 33;
+                const uint64_t E = exc[it++];
+                uint64_t e = 0;
+                uint64_t rem = ~0ull;
+                bool stop = false;
+                if (E) {
+                    if (ig >= gaps.size()) { if (!lenient) return -1; stop = true; }
+                    else rem = gaps[ig];
+                }
+                for (uint32_t i = 0; i < len[r] && !stop; i++) {
+                    if ((int)(int8_t)Q[i] > mq) continue;
+                    if (e < E && rem == 0) {
+                        e++;
+                        ig++;
+                        rem = ~0ull;
+                        if (e < E) {
+                            if (ig >= gaps.size()) { if (!lenient) return -1; stop = true; }
+                            else rem = gaps[ig];
+                        }
+                    } else {
+                        if (ic >= chs.size()) { if (!lenient) return -1; stop = true; break; }
+                        const uint8_t sc = chs[ic++];
+                        isn[at + i] = (uint8_t)kIupac[sc < 11 ? sc : 0];
+                        rem--;
+                    }
+                }
+            }
+            Q += len[r];
+            at += len[r];
+        }
+        if (ic != chs.size() && !lenient) return -1;
+    }
+
+    {   // bases: compressSeq@0x4248a0 / encode_seq@0x421f30 (BASE_MODEL, order k)
+        if (!c.id(6)) return -1;
+        const uint32_t sz = c.size4();
+        if (c.bad) return -1;
+        const uint8_t* q = c.p;
+        if (cfg->md5) { memcpy(dg_s, q, 16); q += 16; }
+        const int k = cfg->slevel + 7;
+        const uint32_t ns = 1u << ((2 * k) & 31), mask = ns - 1;
+        std::vector<uint8_t> tab((size_t)ns * 4, 3);
+        RangeIn rc(q, c.p + sz);
+        uint8_t* S = o->seq;
+        uint64_t at = 0;
+        for (uint32_t r = 0; r < n && !rc.bad; r++) {
+            uint32_t ctx = 0x7616c7u & mask;
+            for (uint32_t i = 0; i < len[r]; i++) {
+                if (isn[at + i]) { S[i] = isn[at + i]; continue; }
+                uint8_t* m = &tab[(size_t)ctx * 4];
+                uint32_t tot = (uint32_t)m[0] + m[1] + m[2] + m[3];
+                if (tot > 253) {
+                    for (int j = 0; j < 4; j++) m[j] = (uint8_t)(m[j] - (m[j] >> 1));
+                    tot = (uint32_t)m[0] + m[1] + m[2] + m[3];
+                }
+                uint32_t scale;
+                const uint32_t v = rc.slot(tot, scale);
+                uint32_t cum = 0, b = 0;
+                while (b < 3 && cum + m[b] <= v) cum += m[b++];
+                rc.consume(scale, cum, m[b]);
+                m[b]++;
+                S[i] = (uint8_t)"ACGT"[b];
+                ctx = ((ctx << 2) + b) & mask;
+            }
+            S += len[r];
+            at += len[r];
+        }
+        if (rc.bad) return -1;
+        c.p += sz;
+    }
+    if (c.p != c.end) return -1;
+    if (cfg->md5) {   // blockMd5Verify@0x414e00
+        uint8_t dg[16];
+        md5(o->names, name_total, dg);
+        if (memcmp(dg, dg_id, 16)) o->md5_ok = 0;
+        if (md5_q) {
+            md5(o->qual, total, dg);
+            if (memcmp(dg, dg_q, 16)) o->md5_ok = 0;
+        }
+        md5(o->seq, total, dg);
+        if (memcmp(dg, dg_s, 16)) o->md5_ok = 0;
+    }
+    return (int64_t)n;
+}

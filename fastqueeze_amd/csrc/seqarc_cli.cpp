@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/seqarc_amd.h"
@@ -73,8 +74,157 @@ int usage()
 {
     fprintf(stderr,
             "usage: seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]\n"
-            "                  [--slevel K] [--qlevel Q] [--device D] [--batch BLOCKS]\n");
+            "                  [--slevel K] [--qlevel Q] [--device D] [--batch BLOCKS]\n"
+            "       seqarc_amd -d [-t N] [--slevel K] [--qlevel Q] ARCHIVE.arc PREFIX\n");
     return 2;
+}
+
+uint64_t be(const uint8_t* p, int n)
+{
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+// EBML VINT (Encap::getValue@0x420680): value and width
+uint64_t vint(const uint8_t* p, const uint8_t* end, int& w)
+{
+    w = 1;
+    if (p >= end) { w = 0; return 0; }
+    while (w <= 8 && !(p[0] & (0x80 >> (w - 1)))) w++;
+    if (w > 8 || end - p < w) { w = 0; return 0; }
+    uint64_t v = p[0] & ((0x80u >> (w - 1)) - 1);
+    for (int i = 1; i < w; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+// SeqArc -d: SeqArcFile::readFileInfo@0x419660 (header, trailer params, block
+// table), one block per host thread (ISeqArcDecodeThread::doJob@0x435580),
+// FASTQ written in block order as PREFIX_1.fastq / PREFIX_2.fastq (PE,
+// .rodata +0x7b2) or PREFIX.fastq (SE).
+int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads)
+{
+    std::vector<uint8_t> a;
+    {
+        FILE* f = fopen(path, "rb");
+        if (!f) { fprintf(stderr, "seqarc_amd: cannot read %s\n", path); return 1; }
+        fseek(f, 0, SEEK_END);
+        a.resize((size_t)ftell(f));
+        fseek(f, 0, SEEK_SET);
+        if (fread(a.data(), 1, a.size(), f) != a.size()) { fclose(f); return 1; }
+        fclose(f);
+    }
+    if (a.size() < 16 || memcmp(a.data(), ".arc", 4) || a[7] != 0x82) {
+        fprintf(stderr, "seqarc_amd: %s is not a SeqArc 1.6 archive\n", path);
+        return 1;
+    }
+    const uint64_t region = be(a.data() + 8, 8) & ((1ull << 56) - 1);
+    if (16 + region > a.size()) return 1;
+    const uint8_t *t = a.data() + 16 + region, *end = a.data() + a.size();
+    int w;
+    if (vint(t, end, w) != 3 || !w) return 1;
+    t += w + 4;
+    // params encap (ID 1, 2-byte size): fields 1-18
+    if (vint(t, end, w) != 1 || !w) return 1;
+    t += w;
+    const uint64_t psz = be(t, 2) & 0x3fff;
+    t += 2;
+    const uint8_t* pend = t + psz;
+    uint8_t tmpl[512] = {0};
+    int bare = 1, paired = 0, lossy = 0, md5 = 1;
+    uint32_t nblocks = 0;
+    while (t < pend) {
+        const uint64_t id = vint(t, pend, w);
+        if (!w) return 1;
+        t += w;
+        const int sw = id == 15 ? 2 : 1;
+        const uint64_t ln = be(t, sw) & ((1ull << (7 * sw)) - 1);
+        t += sw;
+        if (t + ln > pend) return 1;
+        if (id == 2) bare = t[0];
+        else if (id == 11 && ln >= 4) nblocks = (uint32_t)(t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24);
+        else if (id == 14 && ln) paired = 1;
+        else if (id == 15 && ln == 512) memcpy(tmpl, t, 512);
+        else if (id == 16) lossy = t[0];
+        else if (id == 17) md5 = t[0];
+        t += ln;
+    }
+    if (vint(t, end, w) != 7 || !w) return 1;
+    t += w;
+    const uint64_t bt = be(t, 4) & 0x0fffffff;
+    t += 4;
+    const uint32_t rec = paired ? 40 : 32;
+    if (bt != (uint64_t)rec * nblocks || t + bt > end) return 1;
+    struct Blk { uint64_t off, size, text; uint32_t lng; };
+    std::vector<Blk> blks(nblocks);
+    for (uint32_t b = 0; b < nblocks; b++) {
+        const uint8_t* r = t + (size_t)rec * b;
+        const uint32_t s2 = r[0] | r[1] << 8 | r[2] << 16 | (uint32_t)r[3] << 24;
+        uint64_t off = 0;
+        for (int k = 7; k >= 0; k--) off = (off << 8) | r[0x10 + k];
+        const uint64_t text = paired ? (uint64_t)(r[4] | r[5] << 8 | r[6] << 16 | (uint32_t)r[7] << 24) +
+                                           (uint64_t)(r[8] | r[9] << 8 | r[10] << 16 | (uint32_t)r[11] << 24)
+                                     : (uint64_t)(r[8] | r[9] << 8 | r[10] << 16 | (uint32_t)r[11] << 24);
+        blks[b] = Blk{off, s2 >> 1, text, s2 & 1u};
+        if (off + blks[b].size > 16 + region) return 1;
+    }
+    cfg.md5 = md5;
+    cfg.lossy = lossy ? 1.0 : 0.0;
+    cfg.bin_mode = tmpl[0];
+    const std::string p1 = std::string(prefix) + (paired ? "_1.fastq" : ".fastq"), p2 = std::string(prefix) + "_2.fastq";
+    FILE* o1 = fopen(p1.c_str(), "wb");
+    FILE* o2 = paired ? fopen(p2.c_str(), "wb") : nullptr;
+    if (!o1 || (paired && !o2)) { fprintf(stderr, "seqarc_amd: cannot write %s\n", p1.c_str()); return 1; }
+    struct Dec {
+        std::vector<uint8_t> names, seq, qual;
+        std::vector<uint16_t> nl;
+        std::vector<int32_t> sl;
+        sa_decoded d{};
+        int64_t rc = -1;
+    };
+    int rc = 0, bad_md5 = 0;
+    const uint32_t nt = (uint32_t)std::max(1, threads);
+    for (uint32_t b0 = 0; b0 < nblocks && !rc; b0 += nt) {
+        const uint32_t n = std::min(nt, nblocks - b0);
+        std::vector<Dec> ds(n);
+        std::vector<std::thread> th;
+        for (uint32_t i = 0; i < n; i++)
+            th.emplace_back([&, i]() {
+                const Blk& bk = blks[b0 + i];
+                Dec& d = ds[i];
+                const uint64_t cap = bk.text + 64;   // names, bases, qualities each fit the FASTQ text
+                d.names.resize(cap); d.seq.resize(cap); d.qual.resize(cap);
+                d.nl.resize(cap / 4 + 8); d.sl.resize(cap / 4 + 8);
+                d.d = sa_decoded{d.names.data(), d.nl.data(), d.seq.data(), d.sl.data(), d.qual.data(), cap, cap,
+                                 (uint32_t)(cap / 4 + 8), 0, 0};
+                d.rc = sa_decode_block(a.data() + bk.off, bk.size, &cfg, tmpl, (int32_t)bk.lng, &d.d);
+            });
+        for (auto& x : th) x.join();
+        for (uint32_t i = 0; i < n && !rc; i++) {
+            Dec& d = ds[i];
+            if (d.rc < 0) { fprintf(stderr, "seqarc_amd: block %u does not decode\n", b0 + i); rc = 1; break; }
+            bad_md5 |= !d.d.md5_ok;
+            const uint8_t *nm = d.names.data(), *sq = d.seq.data(), *ql = d.qual.data();
+            for (uint32_t r = 0; r < d.d.nreads; r++) {
+                FILE* f = paired && (r & 1) ? o2 : o1;
+                const size_t L = (size_t)d.sl[r], N = d.nl[r];
+                fputc('@', f); fwrite(nm, 1, N, f); fputc('\n', f);
+                fwrite(sq, 1, L, f);
+                fputs("\n+", f);
+                if (!bare) fwrite(nm, 1, N, f);
+                fputc('\n', f);
+                fwrite(ql, 1, L, f); fputc('\n', f);
+                nm += N; sq += L; ql += L;
+            }
+        }
+    }
+    fclose(o1);
+    if (o2) fclose(o2);
+    if (bad_md5) {   // blockMd5Verify@0x414e00: "Name/Seq/Qual md5 unequal"
+        fprintf(stderr, "seqarc_amd: Name/Seq/Qual md5 unequal\n");
+        rc = rc ? rc : 3;
+    }
+    return rc;
 }
 
 }  // namespace
@@ -82,7 +232,9 @@ int usage()
 int main(int argc, char** argv)
 {
     const char *f1 = nullptr, *f2 = nullptr, *outp = nullptr;
-    bool compress = false;
+    bool compress = false, decompress = false;
+    const char* arc = nullptr;
+    int threads = 1;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
     int device = 0, batch = 16;
     for (int i = 1; i < argc; i++) {
@@ -94,15 +246,19 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "-o")) outp = val();
         else if (!strcmp(a, "-n")) cfg.md5 = 0;
         else if (!strcmp(a, "-l")) { const char* v = val(); if (!v) return usage(); cfg.lossy = atof(v); }
-        else if (!strcmp(a, "-t")) { if (!val()) return usage(); }
+        else if (!strcmp(a, "-t")) { const char* v = val(); if (!v) return usage(); threads = atoi(v) > 0 ? atoi(v) : 1; }
         else if (!strcmp(a, "--slevel")) { const char* v = val(); if (!v) return usage(); cfg.slevel = atoi(v); }
         else if (!strcmp(a, "--qlevel")) { const char* v = val(); if (!v) return usage(); cfg.qlevel = atoi(v); }
         else if (!strcmp(a, "--device")) { const char* v = val(); if (!v) return usage(); device = atoi(v); }
         else if (!strcmp(a, "--batch")) { const char* v = val(); if (!v) return usage(); batch = atoi(v) > 0 ? atoi(v) : 1; }
-        else if (!strcmp(a, "-d")) {
-            fprintf(stderr, "seqarc_amd: -d (decode) is not built yet; decode with SeqArc -d\n");
-            return 2;
-        } else return usage();
+        else if (!strcmp(a, "-d")) decompress = true;
+        else if (a[0] != '-' && decompress && !arc) arc = a;
+        else if (a[0] != '-' && decompress && !outp) outp = a;
+        else return usage();
+    }
+    if (decompress) {
+        if (!arc || !outp) return usage();
+        return decode_archive(arc, outp, cfg, threads);
     }
     if (!compress || !f1 || !outp) return usage();
     const bool pe = f2 && *f2;

@@ -131,6 +131,27 @@ typedef struct {
     const uint8_t *id_template;    /* 512 B, param+0x18a4 (sa_analyze_ids)               */
 } sa_arc_info;
 
+/* ---- block decoder (SeqArc -d; host) ------------------------------------ */
+/* The inverse of sa_encode_blocks for one block: EncapFqzComp::doFqzDecode@0x42c680
+ * and, in ID-bin mode, IDProcess::decodeIDS@0x430610 (fastqueeze_amd/csrc/arc_decode.cpp).
+ * Caller-owned arrays; PE reads come back interleaved r1, r2. */
+typedef struct {
+    uint8_t *names;        /* >= name_cap bytes     */
+    uint16_t *name_lens;   /* >= max_reads entries  */
+    uint8_t *seq;          /* >= seq_cap bytes      */
+    int32_t *seq_lens;     /* >= max_reads entries  */
+    uint8_t *qual;         /* >= seq_cap bytes      */
+    uint64_t name_cap, seq_cap;
+    uint32_t max_reads;
+    uint32_t nreads;       /* out */
+    int32_t md5_ok;        /* out: stored digests match (blockMd5Verify@0x414e00), 1 if MD5 off */
+} sa_decoded;
+/* Returns nreads, or -1 on a malformed block / too small arrays.  tmpl: the
+ * archive's 512-byte ID template (trailer field 15); long_reads: the block
+ * record's flag bit (compressLen_long). */
+int64_t sa_decode_block(const uint8_t *in, uint64_t len, const sa_cfg *cfg, const uint8_t tmpl[512],
+                        int32_t long_reads, sa_decoded *out);
+
 /* 16-byte header; block_bytes = sum of the blocks' sizes. Returns 0. */
 int sa_arc_header(uint64_t block_bytes, uint8_t out[16]);
 /* Trailer bytes written to out (written at offset 16 + block_bytes), or -1. */

@@ -1,0 +1,127 @@
+"""SeqArc -d path: the host block decoder (sa_decode_block, arc_decode.cpp)
+and `seqarc_amd -d` over an archive.  Blocks are produced by the CPU
+restatement (the GPU encoder is byte-identical to it, tests/test_gpu_parity.py),
+so these run without a GPU.  The reference's own round trip on its test files
+("-d reproduces the input MD5") is the bar: the decoded
+FASTQ equals the input byte for byte."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py
+import synth
+from conftest import GOLDEN
+from test_oracle import _norm_seq
+
+import fastqueeze_amd as fq
+
+T1 = os.path.join(GOLDEN, "ERR2755197_test_1.fq")
+T2 = os.path.join(GOLDEN, "ERR2755197_test_2.fq")
+CLI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fastqueeze_amd", "bin", "seqarc_amd")
+
+
+def _roundtrip(t1, t2=None, block_size=fq.BLOCK_SIZE, **kw):
+    blocks = fq.blocks_from_fastq(t1, t2, block_size) if t2 else fq.blocks_from_fastq(t1, block_size=block_size)
+    tmpl = fq.analyze_ids(blocks[0], t2 is None)
+    cfg = fq.Config(bin_mode=int(tmpl[0]), **kw)
+    out = []
+    for b in blocks:
+        enc = oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode, cfg.lossy)
+        lng = bool(b.nreads and int(b.seq_lens.max()) > 0xFFFF)
+        d, ok = fq.decode_block(enc, b.text_bytes or b.text1 + b.text2, cfg, tmpl, lng)
+        assert np.array_equal(d.name_lens, b.name_lens) and np.array_equal(d.seq_lens, b.seq_lens)
+        assert d.names.tobytes() == b.names.tobytes()
+        assert np.array_equal(d.seq, _norm_seq(b.seq))
+        want_q = oracle_py.rblock(b.qual, cfg.lossy) if cfg.lossy else b.qual
+        if not cfg.lossy or not (b.seq != _norm_seq(b.seq)).any():
+            assert d.qual.tobytes() == want_q.tobytes()
+        out.append(ok)
+    return out
+
+
+def test_reference_pair_bin_mode():
+    t1, t2 = open(T1, "rb").read(), open(T2, "rb").read()
+    assert all(_roundtrip(t1, t2))          # IDProcess::decodeIDS, PE type 1
+    assert all(_roundtrip(t1))              # SE bin mode
+
+
+@pytest.mark.parametrize("kw", [{}, {"slevel": 4, "qlevel": 3}, {"slevel": 9}, {"md5": False}, {"qlevel": 1}])
+def test_tokenizer_configs(kw):
+    a, b = synth.generate(2500, paired=True, seed=3)
+    assert all(_roundtrip(a, b, block_size=300_000, **kw))
+
+
+def test_edge_long_and_lossy():
+    e = synth.edge_cases()
+    oks = _roundtrip(e)
+    assert oks == [False]                   # lowercase / non-IUPAC bases come back normalised: MD5 differs
+    assert all(_roundtrip(synth.generate(12, read_len=70000, seed=5)[0]))   # compressLen_long
+    a, _ = synth.generate(2000, seed=8)
+    a = b"\n".join(l if i % 4 != 1 else l.replace(b"N", b"A") for i, l in enumerate(a.split(b"\n")))
+    assert all(_roundtrip(a, lossy=1.15))   # qualities come back as rblock output (no quality MD5)
+    a, _ = synth.generate(2000, seed=8)     # with N bases: placement uses lossy qualities (reference: fails)
+    blk = fq.blocks_from_fastq(a)[0]
+    d, ok = fq.decode_block(oracle_py.encode_block(blk, lossy=1.15), blk.text_bytes, fq.Config(lossy=1.15))
+    assert d.names.tobytes() == blk.names.tobytes() and d.nreads == blk.nreads
+
+
+def test_decoder_matches_oracle_decoder():
+    a, b = synth.generate(1500, paired=True, seed=9)
+    blk = fq.blocks_from_fastq(a, b)[0]
+    enc = oracle_py.encode_block(blk)
+    d, ok = fq.decode_block(enc, blk.text1 + blk.text2)
+    names, nl, seq, sl, qual, ok2 = oracle_py.decode_block(enc, blk.nreads, blk.names.size, blk.seq.size)
+    assert ok and ok2 and d.names.tobytes() == names.tobytes() and d.seq.tobytes() == seq.tobytes()
+    assert d.qual.tobytes() == qual.tobytes()
+
+
+def test_rejects_corrupt_block():
+    a, _ = synth.generate(500, seed=10)
+    blk = fq.blocks_from_fastq(a)[0]
+    enc = bytearray(oracle_py.encode_block(blk))
+    with pytest.raises(fq.SeqArcError):
+        fq.decode_block(bytes(enc[: len(enc) // 2]), blk.text_bytes)
+    enc[len(enc) // 2] ^= 0xFF
+    try:
+        _, ok = fq.decode_block(bytes(enc), blk.text_bytes)
+        assert not ok
+    except fq.SeqArcError:
+        pass
+
+
+def _write_archive(tmp_path, texts, names, block_size=fq.BLOCK_SIZE):
+    paths = []
+    for n, t in zip(names, texts):
+        p = tmp_path / n
+        p.write_bytes(t)
+        paths.append(p)
+    blocks = fq.blocks_from_fastq(*texts, block_size) if len(texts) == 2 else fq.blocks_from_fastq(texts[0], block_size=block_size)
+    tmpl = fq.analyze_ids(blocks[0], len(texts) == 1)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    enc = [oracle_py.encode_block(b, bin_mode=cfg.bin_mode) for b in blocks]
+    arc = fq.arc_archive(enc, blocks, names[0], names[1] if len(names) > 1 else None, tmpl, cfg,
+                         plus_bare=fq.bare_plus(texts[-1]))
+    ap = tmp_path / "in.arc"
+    ap.write_bytes(arc)
+    return ap
+
+
+def test_cli_decode_reference_pair(tmp_path):
+    texts = [open(T1, "rb").read(), open(T2, "rb").read()]
+    ap = _write_archive(tmp_path, texts, ["ERR2755197_test_1.fq", "ERR2755197_test_2.fq"])
+    r = subprocess.run([CLI, "-d", "-t", "2", str(ap), str(tmp_path / "out")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "out_1.fastq").read_bytes() == texts[0]
+    assert (tmp_path / "out_2.fastq").read_bytes() == texts[1]
+
+
+def test_cli_decode_multi_block_se(tmp_path):
+    t, _ = synth.generate(6000, seed=12)
+    ap = _write_archive(tmp_path, [t], ["s.fq"], block_size=400_000)
+    r = subprocess.run([CLI, "-d", "-t", "3", str(ap), str(tmp_path / "se")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "se.fastq").read_bytes() == t

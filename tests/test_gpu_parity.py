@@ -211,6 +211,11 @@ def test_cli_archive(tmp_path, test_pair):
     assert r.returncode == 0, r.stderr
     got = open(tmp_path / "pe.arc", "rb").read()
     assert len(got) == 821500 and got == want
+    r = subprocess.run([exe, "-d", "-t", "4", str(tmp_path / "pe.arc"), str(tmp_path / "back")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "back_1.fastq").read_bytes() == test_pair[0]
+    assert (tmp_path / "back_2.fastq").read_bytes() == test_pair[1]
     for p in paths:
         with open(p, "rb") as f, gzip.open(p + ".gz", "wb") as g:
             shutil.copyfileobj(f, g)
