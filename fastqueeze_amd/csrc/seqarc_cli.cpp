@@ -1,7 +1,13 @@
 // seqarc_amd -- the SeqArc -c command line over libseqarc_amd (host C++).
 //
 //   seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]
-//              [--slevel K] [--qlevel Q] [--device D] [--batch BLOCKS]
+//              [--slevel K] [--qlevel Q] [--device D] [--devices N] [--batch BLOCKS]
+//   seqarc_amd -d [-t N] ARCHIVE.arc PREFIX
+//
+// --devices N: batches of blocks are dealt to N gfx950 devices (one host
+// thread and sa_ctx each; blocks are independent, so there is no device-to-
+// device exchange) and gathered back in input order (--share-device: N
+// contexts on one device, for testing the scatter/gather on one GPU).
 //
 // Mirrors the reference's encode path (SeqArc-1.6 main@0x41fd40 ->
 // SeqArcContext::doReadAndEncode@0x41a4e0): the reader cuts 50 MiB blocks
@@ -20,6 +26,9 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -74,7 +83,8 @@ int usage()
 {
     fprintf(stderr,
             "usage: seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]\n"
-            "                  [--slevel K] [--qlevel Q] [--device D] [--batch BLOCKS]\n"
+            "                  [--slevel K] [--qlevel Q] [--device D] [--devices N] [--batch BLOCKS]\n"
+            "                  [--block-size MiB]\n"
             "       seqarc_amd -d [-t N] [--slevel K] [--qlevel Q] ARCHIVE.arc PREFIX\n");
     return 2;
 }
@@ -236,7 +246,8 @@ int main(int argc, char** argv)
     const char* arc = nullptr;
     int threads = 1;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
-    int device = 0, batch = 16;
+    int device = 0, batch = 16, devices = 1, block_mib = 50;
+    bool share_device = false;
     for (int i = 1; i < argc; i++) {
         const char* a = argv[i];
         auto val = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
@@ -250,6 +261,9 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--slevel")) { const char* v = val(); if (!v) return usage(); cfg.slevel = atoi(v); }
         else if (!strcmp(a, "--qlevel")) { const char* v = val(); if (!v) return usage(); cfg.qlevel = atoi(v); }
         else if (!strcmp(a, "--device")) { const char* v = val(); if (!v) return usage(); device = atoi(v); }
+        else if (!strcmp(a, "--devices")) { const char* v = val(); if (!v) return usage(); devices = atoi(v) > 0 ? atoi(v) : 1; }
+        else if (!strcmp(a, "--share-device")) share_device = true;
+        else if (!strcmp(a, "--block-size")) { const char* v = val(); if (!v) return usage(); block_mib = atoi(v) > 0 ? atoi(v) : 50; }
         else if (!strcmp(a, "--batch")) { const char* v = val(); if (!v) return usage(); batch = atoi(v) > 0 ? atoi(v) : 1; }
         else if (!strcmp(a, "-d")) decompress = true;
         else if (a[0] != '-' && decompress && !arc) arc = a;
@@ -269,7 +283,7 @@ int main(int argc, char** argv)
         fprintf(stderr, "seqarc_amd: cannot read input\n");
         return 1;
     }
-    const uint64_t bs = 50ull << 20;   // BlockSize(M) 50 (param+0x1b78)
+    const uint64_t bs = (uint64_t)block_mib << 20;   // BlockSize(M), default 50 (param+0x1b78)
     const uint64_t maxb = (t1.size() + t2.size()) / 1024 + 16;
     std::vector<uint64_t> e1(maxb), e2(maxb);
     const int64_t nb = pe ? sa_cut_pe(t1.data(), t1.size(), t2.data(), t2.size(), bs, e1.data(), e2.data(), maxb)
@@ -307,47 +321,110 @@ int main(int argc, char** argv)
     }
     cfg.bin_mode = tmpl[0];
 
-    sa_ctx* ctx = sa_create(device);
-    if (!ctx) {
-        fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", device);
-        return 1;
+    // one encoder context (and host thread) per device: batches of blocks are
+    // dealt to the devices in order, encoded independently (blocks share no
+    // model state), and gathered back in input order by this thread
+    std::vector<sa_ctx*> ctxs;
+    for (int d = 0; d < devices; d++) {
+        sa_ctx* c = sa_create(device + (share_device ? 0 : d));
+        if (!c) {
+            if (ctxs.empty()) { fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", device); return 1; }
+            break;   // fewer devices than asked for: use those present
+        }
+        ctxs.push_back(c);
     }
     const std::string path = std::string(outp) + ".arc";
     FILE* fo = fopen(path.c_str(), "wb");
-    if (!fo) { fprintf(stderr, "seqarc_amd: cannot write %s\n", path.c_str()); sa_destroy(ctx); return 1; }
+    if (!fo) {
+        fprintf(stderr, "seqarc_amd: cannot write %s\n", path.c_str());
+        for (sa_ctx* c : ctxs) sa_destroy(c);
+        return 1;
+    }
     uint8_t hdr[16] = {0};
     fwrite(hdr, 1, 16, fo);   // patched at the end (createOutFile@0x417480 / writeFileInfo@0x4171b0)
     std::vector<sa_arc_block> info;
     uint64_t total = 0;
     int rc = 0;
-    for (int64_t b0 = 0; b0 < nb && !rc; b0 += batch) {
-        const int64_t n = std::min<int64_t>(batch, nb - b0);
-        std::vector<Parsed> ps((size_t)n);
-        std::vector<sa_block> in((size_t)n);
-        std::vector<std::vector<uint8_t>> bufs((size_t)n);
-        std::vector<sa_out> outs((size_t)n);
-        for (int64_t i = 0; i < n && !rc; i++) {
-            if (!parse(b0 + i, ps[(size_t)i])) { rc = 1; break; }
-            in[(size_t)i] = ps[(size_t)i].view();
-            bufs[(size_t)i].resize(sa_output_bound(&in[(size_t)i]));
-            outs[(size_t)i] = sa_out{bufs[(size_t)i].data(), bufs[(size_t)i].size(), 0};
+    struct Batch {
+        std::vector<Parsed> ps;
+        std::vector<std::vector<uint8_t>> bufs;
+        std::vector<sa_out> outs;
+        int status = 0;   // 0 pending, 1 done, -1 failed
+        std::string err;
+    };
+    const int64_t nbatch = (nb + batch - 1) / batch;
+    std::vector<Batch> bt((size_t)nbatch);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<int64_t> next{0};
+    std::atomic<bool> stop{false};
+    const size_t max_ahead = 2 * ctxs.size();   // batches held in memory beyond the writer
+    int64_t written = 0;
+    auto worker = [&](sa_ctx* ctx) {
+        for (;;) {
+            int64_t k;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || next.load() < written + (int64_t)max_ahead || next.load() >= nbatch; });
+                if (stop || next.load() >= nbatch) return;
+                k = next++;
+            }
+            Batch& B = bt[(size_t)k];
+            const int64_t b0 = k * batch, n = std::min<int64_t>(batch, nb - b0);
+            B.ps.resize((size_t)n);
+            B.bufs.resize((size_t)n);
+            B.outs.resize((size_t)n);
+            std::vector<sa_block> in((size_t)n);
+            int st = 1;
+            for (int64_t i = 0; i < n; i++) {
+                if (!parse(b0 + i, B.ps[(size_t)i])) { st = -1; B.err = "parse failed"; break; }
+                in[(size_t)i] = B.ps[(size_t)i].view();
+                B.bufs[(size_t)i].resize(sa_output_bound(&in[(size_t)i]));
+                B.outs[(size_t)i] = sa_out{B.bufs[(size_t)i].data(), B.bufs[(size_t)i].size(), 0};
+            }
+            if (st > 0 && sa_encode_blocks(ctx, in.data(), (int)n, &cfg, B.outs.data()) != 0) {
+                st = -1;
+                B.err = std::string("encode failed: ") + sa_last_error(ctx);
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                B.status = st;
+            }
+            cv.notify_all();
         }
-        if (rc) { fprintf(stderr, "seqarc_amd: parse failed\n"); break; }
-        if (sa_encode_blocks(ctx, in.data(), (int)n, &cfg, outs.data()) != 0) {
-            fprintf(stderr, "seqarc_amd: encode failed: %s\n", sa_last_error(ctx));
-            rc = 1;
-            break;
+    };
+    std::vector<std::thread> th;
+    for (sa_ctx* c : ctxs) th.emplace_back(worker, c);
+    for (int64_t k = 0; k < nbatch && !rc; k++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return bt[(size_t)k].status != 0; });
         }
-        for (int64_t i = 0; i < n; i++) {
-            const Parsed& p = ps[(size_t)i];
+        Batch& B = bt[(size_t)k];
+        if (B.status < 0) { fprintf(stderr, "seqarc_amd: %s\n", B.err.c_str()); rc = 1; break; }
+        for (size_t i = 0; i < B.ps.size(); i++) {
+            const Parsed& p = B.ps[i];
             uint32_t lng = 0;
             for (uint32_t r = 0; r < p.nreads; r++) lng |= p.sl[r] > 0xffff;
-            fwrite(outs[(size_t)i].data, 1, outs[(size_t)i].size, fo);
-            info.push_back(sa_arc_block{(uint32_t)outs[(size_t)i].size, lng, p.text1, p.text2});
-            total += outs[(size_t)i].size;
+            fwrite(B.outs[i].data, 1, B.outs[i].size, fo);
+            info.push_back(sa_arc_block{(uint32_t)B.outs[i].size, lng, p.text1, p.text2});
+            total += B.outs[i].size;
         }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            B = Batch{};
+            B.status = 1;
+            written = k + 1;
+        }
+        cv.notify_all();
     }
-    sa_destroy(ctx);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+    }
+    cv.notify_all();
+    for (auto& x : th) x.join();
+    for (sa_ctx* c : ctxs) sa_destroy(c);
     if (!rc) {
         sa_arc_info ai{f1, pe ? f2 : nullptr, pe ? 1 : 0, gz1 ? 1 : 0, bare_plus(pe ? t2 : t1), cfg.md5,
                        cfg.lossy > 0.0 ? 1 : 0, tmpl};

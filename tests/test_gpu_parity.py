@@ -227,3 +227,27 @@ def test_cli_archive(tmp_path, test_pair):
     r = subprocess.run([exe, "-c", "-1", paths[0], "-o", str(tmp_path / "se")], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and os.path.getsize(tmp_path / "se.arc") == 379069, r.stderr
+
+
+def test_cli_multi_device_gather(tmp_path, test_pair):
+    """--devices: batches dealt to several encoder contexts (one host thread each)
+    and gathered in input order -- the same archive as one context.  On the
+    one-GPU test box the contexts share device 0 (--share-device)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fastqueeze_amd", "bin",
+                       "seqarc_amd")
+    paths = [str(tmp_path / n) for n in ("m_1.fq", "m_2.fq")]
+    for p, t in zip(paths, test_pair):
+        open(p, "wb").write(t)
+    base = [exe, "-c", "-1", paths[0], "-2", paths[1], "--block-size", "1", "--batch", "1"]
+    r1 = subprocess.run(base + ["-o", str(tmp_path / "one")], capture_output=True, text=True, timeout=120)
+    r3 = subprocess.run(base + ["--devices", "3", "--share-device", "-o", str(tmp_path / "three")],
+                        capture_output=True, text=True, timeout=120)
+    assert r1.returncode == 0 and r3.returncode == 0, (r1.stderr, r3.stderr)
+    one = open(tmp_path / "one.arc", "rb").read()
+    assert one == open(tmp_path / "three.arc", "rb").read()
+    blocks = fq.blocks_from_fastq(*test_pair, 1 << 20)
+    assert len(blocks) > 3
+    tmpl = fq.analyze_ids(blocks[0], False)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    assert one == fq.arc_archive(_oracle_outs(blocks, cfg), blocks, "m_1.fq", "m_2.fq", tmpl, cfg)
