@@ -136,7 +136,7 @@ def main():
         with open(args.traffic_json) as f:
             traffic = json.load(f).get(dom)
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         import oracle_py
         t0 = time.perf_counter()
@@ -151,6 +151,20 @@ def main():
         cpu = {"value": round(nbytes / ct / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
                "sample": f"{nb} of the bench's 50 MiB blocks ({nbytes/1e6:.0f} MB FASTQ) encoded by "
                          f"oracle/fqz_oracle.c (-O2, 1 thread) on this host"}
+        # the same restatement on the host cores this process may use, one block
+        # per thread (the reference's -t N shape: independent blocks per thread;
+        # ctypes releases the GIL during the C call)
+        from concurrent.futures import ThreadPoolExecutor
+        nt = max(1, min(16, len(os.sched_getaffinity(0))))
+        sample = blocks[: min(len(blocks), max(nt, int(nt * (nb / ct) * args.cpu_seconds / 2)))]   # ~half the budget
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nt) as ex:
+            list(ex.map(lambda b: oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode), sample))
+        ct2 = time.perf_counter() - t0
+        sb = sum(b.text_bytes for b in sample)
+        cpu_mt = {"value": round(sb / ct2 / 1e6, 2), "unit": "MB/s", "cores": nt, "kind": "port",
+                  "sample": f"{len(sample)} of the bench's 50 MiB blocks ({sb/1e6:.0f} MB FASTQ) encoded by "
+                            f"oracle/fqz_oracle.c on {nt} host threads, one block per thread"}
 
     step_ms = elapsed / args.steps * 1e3
     value = total_in * args.steps / elapsed / 1e6
@@ -181,6 +195,7 @@ def main():
                         "frac": round(max_syms * R_NS_PER_SYMBOL / 1e6 / max(ph.get("coder_r", 1e-9), 1e-9), 3)},
         "phase_ms": {k: round(v, 2) for k, v in ph.items()},
         "cpu_baseline": cpu,
+        "cpu_baseline_threads": cpu_mt,
     }
     if rank == 0:
         print(json.dumps(res), flush=True)
