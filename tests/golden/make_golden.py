@@ -24,6 +24,9 @@ CASES = {
     "synth_se_4k_q3": dict(synth=dict(n_reads=4000, seed=9), qlevel=3),
     "edge_se": dict(edge=True),
     "edge_se_s9": dict(edge=True, slevel=9),
+    "test_pe_lossy_115": dict(files=("ERR2755197_test_1.fq", "ERR2755197_test_2.fq"), lossy=1.15),
+    "synth_se_lossy_16": dict(synth=dict(n_reads=3000, seed=13), lossy=1.6),
+    "synth_long_70k": dict(synth=dict(n_reads=12, seed=5, read_len=70000)),
 }
 
 
@@ -40,7 +43,8 @@ def run_case(case):
     t1, t2 = inputs(case)
     blocks = fq.blocks_from_fastq(t1, t2, case.get("bs", fq.BLOCK_SIZE))
     tmpl = oracle_py.analyze_ids(blocks[0], t2 is None)
-    outs = [oracle_py.encode_block(b, case.get("slevel", 3), case.get("qlevel", 2), True, int(tmpl[0]))
+    outs = [oracle_py.encode_block(b, case.get("slevel", 3), case.get("qlevel", 2), True, int(tmpl[0]),
+                                   case.get("lossy", 0.0))
             for b in blocks]
     return blocks, tmpl, outs
 

@@ -49,7 +49,7 @@ def test_reference_test_pair(enc, test_pair):
 
 
 @pytest.mark.parametrize("name", ["test_pe_600k", "synth_pe_4k", "synth_pe_4k_s4", "synth_se_4k_q3", "edge_se",
-                                  "edge_se_s9"])
+                                  "edge_se_s9", "test_pe_lossy_115", "synth_se_lossy_16", "synth_long_70k"])
 def test_golden_cases(enc, name):
     import sys
     sys.path.insert(0, GOLDEN)
@@ -59,7 +59,8 @@ def test_golden_cases(enc, name):
     t1, t2 = make_golden.inputs(case)
     blocks = fq.blocks_from_fastq(t1, t2, case.get("bs", fq.BLOCK_SIZE))
     tmpl = fq.analyze_ids(blocks[0], t2 is None)
-    cfg = fq.Config(slevel=case.get("slevel", 3), qlevel=case.get("qlevel", 2), bin_mode=int(tmpl[0]))
+    cfg = fq.Config(slevel=case.get("slevel", 3), qlevel=case.get("qlevel", 2), bin_mode=int(tmpl[0]),
+                    lossy=case.get("lossy", 0.0))
     out = _check(enc, blocks, cfg)
     assert [len(o) for o in out] == g["blocks"]
 

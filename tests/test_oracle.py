@@ -74,7 +74,8 @@ def golden():
 
 
 @pytest.mark.parametrize("name", ["test_pe", "test_se", "test_pe_600k", "synth_pe_4k", "synth_pe_4k_s4",
-                                  "synth_se_4k_q3", "edge_se", "edge_se_s9"])
+                                  "synth_se_4k_q3", "edge_se", "edge_se_s9", "test_pe_lossy_115",
+                                  "synth_se_lossy_16", "synth_long_70k"])
 def test_oracle_golden(golden, name):
     mg, g = golden
     case = g[name]["case"]
