@@ -125,3 +125,35 @@ def test_cli_decode_multi_block_se(tmp_path):
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "se.fastq").read_bytes() == t
+
+
+@pytest.mark.parametrize("kind", [1, 2, 3])
+def test_bin_mode_pe_types(kind):
+    """ID-bin names of the three PE types (analysisPEType@0x430f50 / decodeIDS@0x430610):
+    1 identical mate IDs, 2 '/1' -> '/2', 3 '... length=' + the mate's own length."""
+    rng = np.random.default_rng(kind)
+
+    def rec(name, n):
+        s = rng.choice(np.frombuffer(b"ACGT", np.uint8), n).tobytes()
+        q = rng.choice(np.frombuffer(b"F:,", np.uint8), n).tobytes()
+        return b"@" + name + b"\n" + s + b"\n+\n" + q + b"\n"
+
+    r1, r2 = [], []
+    for i in range(500):
+        l1, l2 = 100 + i % 7, 90 + i % 5
+        if kind == 1:
+            n1 = n2 = b"SRR9.%d %d length=%d" % (i + 1, i + 1, l1)
+            l2 = l1
+        elif kind == 2:
+            n1, n2 = b"SRR9.%d %d/1" % (i + 1, i + 1), b"SRR9.%d %d/2" % (i + 1, i + 1)
+        else:
+            n1, n2 = b"SRR9.%d %d length=%d" % (i + 1, i + 1, l1), b"SRR9.%d %d length=%d" % (i + 1, i + 1, l2)
+        r1.append(rec(n1, l1))
+        r2.append(rec(n2, l2))
+    t1, t2 = b"".join(r1), b"".join(r2)
+    blk = fq.blocks_from_fastq(t1, t2)[0]
+    tmpl = fq.analyze_ids(blk, False)
+    assert (tmpl[0], tmpl[1]) == (1, kind)
+    cfg = fq.Config(bin_mode=1)
+    d, ok = fq.decode_block(oracle_py.encode_block(blk, bin_mode=1), blk.text1 + blk.text2, cfg, tmpl)
+    assert ok and d.names.tobytes() == blk.names.tobytes() and np.array_equal(d.name_lens, blk.name_lens)
