@@ -655,7 +655,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
                                                              uint64_t* __restrict__ long_runs,
                                                              uint32_t* __restrict__ nlong)
 {
-    __shared__ SegCnt part[SORT_THREADS];
+    __shared__ SegCnt part[SORT_THREADS / 64];
     __shared__ uint64_t carry_cnt;
     __shared__ uint32_t last_key[SORT_THREADS];
     const uint32_t t = blockIdx.x;
@@ -710,16 +710,23 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
         if (k[e] != SORT_PAD) acc.cnt += onehot16(v[e] & 3u);
         pk = k[e];
     }
-    part[tid] = acc;
-    __syncthreads();
-    for (uint32_t d = 1; d < SORT_THREADS; d <<= 1) {
-        SegCnt x = part[tid];
-        if (tid >= d) x = segcnt_op(part[tid - d], x);
-        __syncthreads();
-        part[tid] = x;
-        __syncthreads();
+    // block-wide exclusive segmented scan of the aggregates: a wave scan
+    // (shuffles), then the waves' totals through LDS
+    const uint32_t lane = tid & 63, w = tid >> 6;
+    SegCnt x = acc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const SegCnt y{__shfl_up(x.cnt, d, 64), __shfl_up(x.head, d, 64)};
+        if (lane >= (uint32_t)d) x = segcnt_op(y, x);
     }
-    SegCnt run = tid ? part[tid - 1] : SegCnt{0ull, 0u};
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    SegCnt run{0ull, 0u};
+    for (uint32_t k = 0; k < w; k++) run = segcnt_op(run, part[k]);
+    {
+        const SegCnt y{__shfl_up(x.cnt, 1, 64), __shfl_up(x.head, 1, 64)};
+        if (lane > 0) run = segcnt_op(run, y);
+    }
     if (!run.head) run.cnt += carry_cnt;   // still inside the run continued from the previous tile
     uint64_t cnt = run.cnt;
     pk = prev_key;
