@@ -142,7 +142,7 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     sv.nsegs = (uint32_t)plan.segs.size();
     int cur = 0;
     for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL(k_sort_hist, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,
+        hipLaunchKernelGGL(k_sort_hist, dim3((sv.ntiles + HIST_TILES - 1) / HIST_TILES), dim3(SORT_THREADS), 0, st, sv,
                            keys[cur].as<uint32_t>(), (uint32_t)shift);
         hipLaunchKernelGGL(k_sort_scan, dim3(sv.nsegs), dim3(1024), 0, st, sv);
         hipLaunchKernelGGL(k_sort_scatter, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,

@@ -460,23 +460,43 @@ __global__ __launch_bounds__(256) void k_pad_keys(const SortView sv, uint32_t* _
 // stages the tile in digit order in LDS and writes each digit's run with
 // consecutive threads.
 // ---------------------------------------------------------------------------
+constexpr uint32_t HIST_TILES = 2;
+
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, const uint32_t* __restrict__ keys,
                                                             uint32_t shift)
 {
-    __shared__ uint32_t h[256];
-    const uint32_t t = blockIdx.x;
-    const SortSeg& sg = sv.segs[sv.tile_seg[t]];
-    const uint32_t lt = t - sg.tile0;
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t* K = keys + sg.base + (size_t)lt * SORT_TILE;
+    // HIST_TILES consecutive tiles per workgroup (amortises the per-workgroup
+    // prologue; each tile's counts still go to its own row)
+    __shared__ uint32_t h[HIST_TILES][256];
+    uint32_t k[HIST_TILES][SORT_ITEMS];
+    const SortSeg* sgp[HIST_TILES];
+    uint32_t ltv[HIST_TILES];
 #pragma unroll
-    for (int i = 0; i < SORT_ITEMS; i++) {
-        uint32_t k = K[threadIdx.x + i * SORT_THREADS];
-        atomicAdd(&h[(k >> shift) & 255], 1u);
+    for (int j = 0; j < HIST_TILES; j++) {
+        const uint32_t t = blockIdx.x * HIST_TILES + j;
+        h[j][threadIdx.x] = 0;
+        sgp[j] = t < sv.ntiles ? &sv.segs[sv.tile_seg[t]] : nullptr;
+    }
+#pragma unroll
+    for (int j = 0; j < HIST_TILES; j++) {
+        if (!sgp[j]) continue;
+        const uint32_t t = blockIdx.x * HIST_TILES + j;
+        ltv[j] = t - sgp[j]->tile0;
+        const uint32_t* K = keys + sgp[j]->base + (size_t)ltv[j] * SORT_TILE;
+#pragma unroll
+        for (int i = 0; i < SORT_ITEMS; i++) k[j][i] = K[threadIdx.x + i * SORT_THREADS];
     }
     __syncthreads();
-    sv.hist[sg.hist_base + (size_t)lt * 256 + threadIdx.x] = h[threadIdx.x];   // tile-major: one coalesced row
+#pragma unroll
+    for (int j = 0; j < HIST_TILES; j++) {
+        if (!sgp[j]) continue;
+#pragma unroll
+        for (int i = 0; i < SORT_ITEMS; i++) atomicAdd(&h[j][(k[j][i] >> shift) & 255], 1u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < HIST_TILES; j++)   // tile-major: one coalesced row per tile
+        if (sgp[j]) sv.hist[sgp[j]->hist_base + (size_t)ltv[j] * 256 + threadIdx.x] = h[j][threadIdx.x];
 }
 
 // The segment's digit counts are tile-major (row t = tile t's 256 counts); the
