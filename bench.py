@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU shard")
     ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--paired", action="store_true",
+                    help="150 bp PE (configs[2] shape): --reads/2 mate pairs, r2 the reverse complement of "
+                         "the fragment end; same FASTQ volume per GPU as the SE default")
     ap.add_argument("--block-size", type=int, default=fq.BLOCK_SIZE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-verify", action="store_true")
@@ -72,15 +75,19 @@ def main():
         torch.cuda.synchronize(local)
 
     t0 = time.time()
-    text, _ = __import__("synth").generate(args.reads, read_len=args.read_len, seed=1000 + rank)
+    n_gen = args.reads // 2 if args.paired else args.reads
+    text, text2 = __import__("synth").generate(n_gen, read_len=args.read_len, paired=args.paired,
+                                               seed=1000 + rank)
     t_gen = time.time() - t0
     t0 = time.time()
-    blocks = fq.blocks_from_fastq(text, None, args.block_size)
+    blocks = fq.blocks_from_fastq(text, text2, args.block_size)
     t_parse = time.time() - t0
     in_bytes = sum(b.text_bytes for b in blocks)
-    tmpl = fq.analyze_ids(blocks[0], True)
+    gen_bytes = len(text) + (len(text2) if text2 is not None else 0)
+    del text, text2
+    tmpl = fq.analyze_ids(blocks[0], not args.paired)
     cfg = fq.Config(bin_mode=int(tmpl[0]))
-    log(f"[rank {rank}] generated {len(text)/1e9:.2f} GB in {t_gen:.1f}s, {len(blocks)} blocks parsed in "
+    log(f"[rank {rank}] generated {gen_bytes/1e9:.2f} GB in {t_gen:.1f}s, {len(blocks)} blocks parsed in "
         f"{t_parse:.1f}s, bin_mode={cfg.bin_mode}")
 
     enc = fq.Encoder(local)
@@ -181,7 +188,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SURVEY.md 8(d) generator, seed 1000+rank), inputs resident in HBM",
-        "config": {"workload": f"synthetic {args.reads/1e6:g}M x {args.read_len} bp SE per GPU, no-ref, "
+        "config": {"workload": f"synthetic {args.reads/1e6:g}M x {args.read_len} bp "
+                               f"{'PE (interleaved mate pairs)' if args.paired else 'SE'} per GPU, no-ref, "
                                f"Slevel 3 (order-10), Qlevel 2, 50 MiB blocks, MD5 on",
                    "blocks_per_gpu": len(blocks), "fastq_bytes_per_gpu": in_bytes,
                    "parallelism": f"block-shard x{world}"},
