@@ -77,7 +77,8 @@ def main():
     t0 = time.time()
     n_gen = args.reads // 2 if args.paired else args.reads
     text, text2 = __import__("synth").generate(n_gen, read_len=args.read_len, paired=args.paired,
-                                               seed=1000 + rank)
+                                               seed=1000 + rank,
+                                               progress=lambda k: log(f"[rank {rank}] generated {k} records"))
     t_gen = time.time() - t0
     t0 = time.time()
     blocks = fq.blocks_from_fastq(text, text2, args.block_size)

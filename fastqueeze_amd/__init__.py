@@ -277,6 +277,24 @@ class Encoder:
             self._err("sa_fetch")
         return [keep[i][: arr[i].size].tobytes() for i in range(len(outs))]
 
+    def encode_blocks(self, blocks: list[Block], cfg: Config) -> list[bytes]:
+        """One sa_encode_blocks call (the drop-in for doFqzEncode over a batch;
+        the library splits batches larger than its HBM cap into sub-batches)."""
+        ins = (_SaBlock * max(1, len(blocks)))(*[b._c() for b in blocks])
+        keep, outs = [], []
+        for b in blocks:
+            cb = b._c()
+            cap = int(self._lib.sa_output_bound(C.byref(cb)))
+            buf = np.empty(cap, dtype=np.uint8)
+            keep.append(buf)
+            outs.append(_SaOut(_ptr(buf), cap, 0))
+        arr = (_SaOut * max(1, len(outs)))(*outs)
+        c = cfg._c()
+        if self._lib.sa_encode_blocks(self._ctx, ins, len(blocks), C.byref(c), arr) != 0:
+            self._err("sa_encode_blocks")
+        self._staged = []
+        return [keep[i][: arr[i].size].tobytes() for i in range(len(outs))]
+
     def encode(self, blocks: list[Block], cfg: Config) -> list[bytes]:
         self.stage(blocks)
         self.run(cfg)

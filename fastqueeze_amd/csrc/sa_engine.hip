@@ -953,9 +953,34 @@ void sa_stream_stats(const sa_ctx* c, uint64_t* max_symbols, uint64_t* total_sym
 int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, sa_out* out)
 {
     if (!ctx || !cfg || (n > 0 && (!in || !out))) return -1;
-    if (sa_stage(ctx, in, n)) return -1;
-    if (sa_run(ctx, cfg)) return -1;
-    return sa_fetch(ctx, out, n);
+    // Blocks are independent, so a large batch is encoded as consecutive
+    // sub-batches of at most SA_BATCH_BASES bases: the symbol records and sort
+    // buffers of one sub-batch (~8 B per symbol, x2 for the sort) stay well
+    // inside 288 GB of HBM whatever the caller hands over.  SA_BATCH_BASES in
+    // the environment lowers the cap (tests split a small batch with it).
+    uint64_t cap_bases = 3ull << 30;
+    if (const char* e = std::getenv("SA_BATCH_BASES")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v > 0 && v < cap_bases) cap_bases = v;
+    }
+    if (n == 0) return 0;
+    int b0 = 0;
+    while (b0 < n) {
+        int b1 = b0;
+        uint64_t bases = 0;
+        while (b1 < n) {
+            uint64_t ls = 0;
+            for (uint32_t r = 0; r < in[b1].nreads; r++) ls += (uint64_t)std::max(in[b1].seq_lens[r], 0);
+            if (b1 > b0 && bases + ls > cap_bases) break;
+            bases += ls;
+            b1++;
+        }
+        if (sa_stage(ctx, in + b0, b1 - b0)) return -1;
+        if (sa_run(ctx, cfg)) return -1;
+        if (sa_fetch(ctx, out + b0, b1 - b0)) return -1;
+        b0 = b1;
+    }
+    return 0;
 }
 
 }  // extern "C"

@@ -63,6 +63,8 @@ const char *sa_version(void);
 
 /* ---- one-shot batch: replaces doFqzEncode@0x42d2d0 per block ---------- */
 uint64_t sa_output_bound(const sa_block *blk);
+/* Batches above 3 Gi bases (env SA_BATCH_BASES lowers the cap) are encoded as
+ * consecutive sub-batches; outputs keep the input order. */
 int sa_encode_blocks(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, sa_out *out);
 
 /* ---- staged API (inputs resident in HBM; used by bench.py) ------------ */

@@ -45,7 +45,7 @@ def _records(names: list[bytes], seq: np.ndarray, qual: np.ndarray) -> bytes:
 
 
 def generate(n_reads: int, read_len: int = 150, paired: bool = False, seed: int = 12345,
-             genome_len: int = 5_000_000, chunk: int = 250_000):
+             genome_len: int = 5_000_000, chunk: int = 250_000, progress=None):
     """Return (r1_bytes, r2_bytes or None) of n_reads records (pairs if paired)."""
     rng = np.random.default_rng(seed)
     genome = rng.integers(0, 4, size=genome_len, dtype=np.uint8)
@@ -73,6 +73,8 @@ def generate(n_reads: int, read_len: int = 150, paired: bool = False, seed: int 
             s2 = _COMP[r2]
             q2 = _QUALS[rng.choice(3, size=(n, read_len), p=[0.90, 0.07, 0.03])]
             out2.append(_records(_headers(rng, s, n, 2), s2, q2))
+        if progress is not None and (s // chunk) % 40 == 39:
+            progress(s + n)
     return b"".join(out1), (b"".join(out2) if paired else None)
 
 

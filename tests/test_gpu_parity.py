@@ -79,6 +79,22 @@ def test_many_blocks_one_batch(enc):
     _check(enc, blocks, fq.Config())
 
 
+def test_encode_blocks_sub_batches(enc, monkeypatch):
+    """sa_encode_blocks (the one-call drop-in) splits a batch over its HBM cap into
+    consecutive sub-batches; a cap of ~2 blocks' bases forces several splits and
+    the outputs stay equal to the oracle, in input order."""
+    a, b = synth.generate(8000, paired=True, seed=23)
+    blocks = fq.blocks_from_fastq(a, b, 300_000)
+    assert len(blocks) >= 8
+    want = _oracle_outs(blocks, fq.Config())
+    assert enc.encode_blocks(blocks, fq.Config()) == want          # one batch
+    monkeypatch.setenv("SA_BATCH_BASES", str(2 * int(blocks[0].seq.size)))
+    assert enc.encode_blocks(blocks, fq.Config()) == want          # ~len/2 sub-batches
+    monkeypatch.setenv("SA_BATCH_BASES", "1")
+    assert enc.encode_blocks(blocks, fq.Config()) == want          # one block per sub-batch
+    assert enc.encode_blocks([], fq.Config()) == []
+
+
 def test_full_size_block(enc):
     """One full 50 MiB block (146,716 x 150 bp reads) -- the bench's unit of work --
     equal to the oracle, and decoding back to the input (CPU decoder, MD5s match)."""
