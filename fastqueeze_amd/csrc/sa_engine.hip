@@ -60,6 +60,7 @@ struct sa_ctx {
     hipEvent_t ev_seq_done = nullptr, ev_long_done = nullptr;
     uint32_t long_lds = 0;
     bool serial_seq = false;
+    uint32_t pf_segs = PF_SEGS;
     std::string err;
     bool timing = false;
     uint32_t coder_restarts = 0;
@@ -255,7 +256,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
     if (ph >= 0) ev_begin(c, ph, st);
     hipLaunchKernelGGL(k_coder_r, dim3(tl.count), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r,
                        c->d_err.as<uint32_t>(), reinterpret_cast<const uint2*>(cv.prs[0]),
-                       reinterpret_cast<const uint2*>(cv.prs[1]));
+                       reinterpret_cast<const uint2*>(cv.prs[1]), c->pf_segs);
     if (ph >= 0) ev_finish(c, ph, st);
 }
 
@@ -381,6 +382,8 @@ sa_ctx* sa_create(int device)
     const char* el = std::getenv("SA_LONG_LDS");
     c->long_lds = el ? (uint32_t)std::atoi(el) : 0u;
     c->serial_seq = std::getenv("SA_SERIAL_SEQ") != nullptr;
+    const char* ep = std::getenv("SA_PF_SEGS");   // pass R prefetch distance (tuning override)
+    c->pf_segs = ep ? (uint32_t)std::min(std::max(std::atoi(ep), 1), 64) : PF_SEGS;
     std::vector<uint32_t> m_long((prop.multiProcessorCount + 31) / 32, 0u), m_seq(m_long.size(), 0u);
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);

@@ -1464,16 +1464,18 @@ __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t 
     return r0;
 }
 
-// The records are also touched PF_SEGS segments ahead by one lane-parallel
-// vector load per segment (the same arrays through pf0 / pf1), so that the
-// scalar loads find them in L2: with many chains in flight the scalar-cache
-// misses to HBM would otherwise outlast the 15 steps a chunk load overlaps.
+// The records are also touched pf_segs segments ahead (default PF_SEGS) by one
+// lane-parallel vector load per segment (the same arrays through pf0 / pf1), so
+// that the scalar loads find them in L2: with many chains in flight the
+// scalar-cache misses to HBM would otherwise outlast the 15 steps a chunk load
+// overlaps.
 constexpr uint32_t PF_SEGS = 4;
 
 __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ tasks, const TaskList tl,
                                                 const PRec* __restrict__ prs0, const PRec* __restrict__ prs1,
                                                 uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err,
-                                                const uint2* __restrict__ pf0, const uint2* __restrict__ pf1)
+                                                const uint2* __restrict__ pf0, const uint2* __restrict__ pf1,
+                                                const uint32_t pf_segs)
 {
     const uint32_t li = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -1494,9 +1496,9 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
         const uint2* PF = (tk.space ? pf1 : pf0) + tk.rec_base + lane;
         uint32_t pf_acc = 0, pf_prev = 0;
         for (; g < last; g++, C += 4) {
-            if (g + PF_SEGS < last) {
+            if (g + pf_segs < last) {
                 pf_acc += pf_prev;   // consumed a segment later: no wait on the load
-                pf_prev = PF[(size_t)(g + PF_SEGS) * SEG_SYMS].x;
+                pf_prev = PF[(size_t)(g + pf_segs) * SEG_SYMS].x;
             }
             kv = lane == (g & 63) ? r : kv;
             if ((g & 63) == 63) {
