@@ -1,33 +1,44 @@
 """bench.py -- MB/s of FASTQ compressed by the MI355X SeqArc block encoder.
 
-Workload (BASELINE.json configs[1]): synthetic 10M x 150 bp single-end reads,
-no reference, default SeqArc parameters (Slevel 3 -> order-10 base model,
-Qlevel 2, 50 MiB blocks, per-block MD5), generated with the SURVEY.md 8(d)
-spec.  A step = one pass of the encoder over all blocks of the shard, inputs
-resident in HBM (staged once), outputs left in HBM.  Multi-GPU: one process per
-GPU, each encodes its own shard of blocks (weak scaling, no data-path
-collective); value = all ranks' FASTQ bytes / max-over-ranks time.
+Workload (BASELINE.json metric "150 bp PE"; configs[2]'s per-GPU shape):
+synthetic 150 bp paired-end reads, no reference, default SeqArc parameters
+(Slevel 3 -> order-10 base model, Qlevel 2, 50 MiB blocks, per-block MD5),
+generated with the SURVEY.md 8(d) spec (tests/synth.py).  Every GPU holds
+`--batches` distinct batches of `--pairs` mate pairs (5 M pairs = 3.57 GB of
+FASTQ = 69 blocks) resident in HBM.  A step = one encode of one batch (all its
+blocks, every stream, MD5, assembly; outputs left in HBM).  `--contexts` encoder
+contexts per GPU run steps concurrently from their own host threads, so one
+batch's throughput-bound front (symbol extraction, sorts, model replay) runs
+while another batch's latency-bound range coder chains finish.
+
+Multi-GPU: one process per GPU.  `--gpus N` without WORLD_SIZE in the
+environment launches the N ranks itself (before any GPU call); under
+torch.distributed.run the ranks come from the environment.  The global list of
+batches is dealt to the ranks with fastqueeze_amd.shard.shard_indices (weak
+scaling: each rank encodes its own batches, no data-path collective); the
+barrier and the max-over-ranks time are the only collectives (gloo, host).
+value = all ranks' FASTQ bytes of the timed steps / max-over-ranks time.
+
+`--dry-run` runs the same launcher, sharding and gather on a tiny workload with
+the CPU restatement as the encoder (no GPU; tests/test_shard.py).
 
 Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-
-import numpy as np  # noqa: E402
-
-import torch  # noqa: E402  (torch first: the library then binds to torch's HIP runtime)
-import torch.distributed as dist  # noqa: E402
-
-import fastqueeze_amd as fq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Dependency-chain bound of pass R: one wave issues at most one
@@ -35,34 +46,175 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # stream of L symbols needs >= L * 40 cycles at 2.4 GHz.
 R_SALU_PER_SYMBOL = 10
 R_NS_PER_SYMBOL = R_SALU_PER_SYMBOL * 4 / 2.4
+# reference per-block stream sizes of a 50 MiB 150 bp PE block
+SURVEY_STREAMS = {"name": 58_700, "seq": 5_261_000, "qual": 1_552_000}
+STREAM_IDS = {1: "count", 4: "len", 5: "name", 7: "qual", 23: "dege_tip", 14: "dege_ch", 24: "dege_maxq",
+              25: "dege_ncnt", 26: "dege_npos", 6: "seq"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU shard")
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--contexts", type=int, default=2, help="encoder contexts (pipeline lanes) per GPU")
+    ap.add_argument("--batches", type=int, default=4, help="distinct resident batches per GPU")
+    ap.add_argument("--pairs", type=int, default=5_000_000, help="mate pairs per batch (reads with --se)")
+    ap.add_argument("--se", action="store_true", help="single-end reads (configs[1] shape) instead of PE")
     ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--paired", action="store_true",
-                    help="150 bp PE (configs[2] shape): --reads/2 mate pairs, r2 the reverse complement of "
-                         "the fragment end; same FASTQ volume per GPU as the SE default")
-    ap.add_argument("--block-size", type=int, default=fq.BLOCK_SIZE)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--slevel", type=int, default=3)
+    ap.add_argument("--qlevel", type=int, default=2)
+    ap.add_argument("--block-size", type=int, default=50 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (each leg)")
+    ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: the CPU share)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="per-launch HBM bytes per kernel from the two rocprofv3 --pmc passes "
-                         "(FETCH_SIZE x2 + WRITE_SIZE; scripts/gpu_r2.sh + scripts/pmc_traffic.py) of this "
-                         "tree's default bench, committed under profiles/")
-    args = ap.parse_args()
+                    help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
+                         "(scripts/pmc_traffic.py), committed under profiles/")
+    a = ap.parse_args(argv)
+    if a.dry_run:
+        a.pairs = min(a.pairs, 3000)
+        a.block_size = min(a.block_size, 300_000)
+        a.steps = min(a.steps, 2)
+        a.warmup = 0
+        a.cpu_seconds = 0.0
+    return a
+
+
+def cpu_share() -> dict:
+    """Host cores this process may use: affinity mask, capped by the cgroup quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota,
+            "usable": min(aff, quota) if quota else aff}
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv: list[str], n: int) -> int:
+    """--gpus N outside torch.distributed.run: one child process per GPU, started
+    before this process touches a GPU; rank 0's stdout is the bench line."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        rc = p.wait() or rc
+    return rc
+
+
+def make_batch(gid: int, args, workers: int):
+    """Global batch `gid`: its FASTQ (seed 1000 + gid), cut and parsed as the
+    reference's reader does.  Returns the parsed blocks."""
+    import synth
+    import fastqueeze_amd as fq
+    paired = not args.se
+    t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers)
+    return fq.blocks_from_fastq(t1, t2, args.block_size)
+
+
+def stream_sizes(block: bytes) -> dict:
+    """Payload bytes of each encap of one encoded block (doFqzEncode@0x42d2d0 layout)."""
+    def vint(i):
+        b0 = block[i]
+        w = 1
+        while w <= 8 and not b0 & (0x80 >> (w - 1)):
+            w += 1
+        v = b0 & ((0x80 >> (w - 1)) - 1)
+        for k in range(1, w):
+            v = (v << 8) | block[i + k]
+        return v, i + w
+    _, i = vint(0)
+    size, i = vint(i)
+    end = i + size
+    out = {}
+    while i < end:
+        sid, i = vint(i)
+        sz, i = vint(i)
+        out[STREAM_IDS.get(sid, str(sid))] = sz
+        i += sz
+    return out
+
+
+class Workers:
+    """C encoder contexts on one GPU, each driven by its own host thread, taking
+    steps (batch encodes) from a shared counter."""
+
+    def __init__(self, encoders, inputs, cfg):
+        self.encs, self.inputs, self.cfg = encoders, inputs, cfg
+        self.phases, self.restarts, self.stats = [], 0, (0, 0)
+
+    def run(self, nsteps: int, record: bool):
+        lock = threading.Lock()
+        nxt = [0]
+        errs = []
+
+        def worker(enc):
+            try:
+                while True:
+                    with lock:
+                        s = nxt[0]
+                        if s >= nsteps:
+                            return
+                        nxt[0] += 1
+                    enc.run_input(self.inputs[s % len(self.inputs)], self.cfg)
+                    if record:
+                        ph = enc.phase_times()
+                        with lock:
+                            self.phases.append(ph)
+                            self.restarts += enc.coder_restarts()
+                            self.stats = max(self.stats, enc.stream_stats())
+            except Exception as e:   # surfaced after join
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(e,)) for e in self.encs]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(argv, args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    # streams of several contexts each get a hardware queue (HIP's default is 4
+    # per process): 4 streams per context plus the runtime's own
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(32, 4 * args.contexts + 4)))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import fastqueeze_amd as fq
+    from fastqueeze_amd.shard import gather_blocks, shard_indices
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -71,111 +223,137 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def device_sync():
-        torch.cuda.synchronize(local)
-
+    share = cpu_share()
+    workers = args.gen_workers or max(1, min(16, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
+                                                                                               world)))))
+    # ---- this rank's batches (global ids dealt round robin) ----
+    gids = shard_indices(world * args.batches, rank, world)
     t0 = time.time()
-    n_gen = args.reads // 2 if args.paired else args.reads
-    text, text2 = __import__("synth").generate(n_gen, read_len=args.read_len, paired=args.paired,
-                                               seed=1000 + rank,
-                                               progress=lambda k: log(f"[rank {rank}] generated {k} records"))
-    t_gen = time.time() - t0
-    t0 = time.time()
-    blocks = fq.blocks_from_fastq(text, text2, args.block_size)
-    t_parse = time.time() - t0
-    in_bytes = sum(b.text_bytes for b in blocks)
-    gen_bytes = len(text) + (len(text2) if text2 is not None else 0)
-    del text, text2
-    tmpl = fq.analyze_ids(blocks[0], not args.paired)
-    cfg = fq.Config(bin_mode=int(tmpl[0]))
-    log(f"[rank {rank}] generated {gen_bytes/1e9:.2f} GB in {t_gen:.1f}s, {len(blocks)} blocks parsed in "
-        f"{t_parse:.1f}s, bin_mode={cfg.bin_mode}")
+    batches = []
+    for g in gids:
+        batches.append(make_batch(g, args, workers))
+        log(f"[rank {rank}] batch {g}: {len(batches[-1])} blocks, "
+            f"{sum(b.text_bytes for b in batches[-1]) / 1e9:.2f} GB ({time.time() - t0:.1f}s)")
+    tmpl = fq.analyze_ids(batches[0][0], args.se)
+    cfg = fq.Config(slevel=args.slevel, qlevel=args.qlevel, bin_mode=int(tmpl[0]))
+    batch_bytes = [sum(b.text_bytes for b in bl) for bl in batches]
 
-    enc = fq.Encoder(local)
-    enc.set_timing(True)
-    enc.stage(blocks)
-    for _ in range(args.warmup):
-        enc.run(cfg)
+    if args.dry_run:
+        import oracle_py
+        local_out = []
+        for g, bl in zip(gids, batches):
+            outs = [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode) for b in bl]
+            local_out.append((g, b"".join(hashlib.sha256(o).digest() for o in outs)))
+        allb = gather_blocks(local_out, world * args.batches) if world > 1 else [o for _, o in local_out]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "batches": len(allb),
+                              "blocks_digest": hashlib.sha256(b"".join(allb)).hexdigest()}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # ---- resident inputs, encoder contexts ----
+    keep = {"verify": batches[0], "cpu": batches[0]}
+    inputs = [fq.Input(bl, local) for bl in batches]
+    del batches
+    encs = [fq.Encoder(local) for _ in range(args.contexts)]
+    for e in encs:
+        e.set_timing(True)
+    W = Workers(encs, inputs, cfg)
+    W.run(max(args.warmup, args.contexts), record=False)
     barrier()
-    device_sync()
+    torch.cuda.synchronize(local)
     ts = time.perf_counter()
-    phases = []
-    for _ in range(args.steps):
-        enc.run(cfg)
-        phases.append(enc.phase_times())
-    device_sync()
+    W.run(args.steps, record=True)
+    torch.cuda.synchronize(local)
     barrier()
     elapsed = time.perf_counter() - ts
+    step_bytes = sum(inputs[s % len(inputs)].text_bytes for s in range(args.steps))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot_in = torch.tensor([float(in_bytes)], dtype=torch.float64)
-        dist.all_reduce(tot_in, op=dist.ReduceOp.SUM)
-        total_in = float(tot_in.item())
+        t = torch.tensor([elapsed, float(step_bytes)], dtype=torch.float64)
+        tm = t.clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, total_bytes = float(tm[0]), float(t[1])
     else:
-        total_in = float(in_bytes)
+        total_bytes = float(step_bytes)
 
-    max_syms, all_syms = enc.stream_stats()
-    outs = enc.fetch()
+    # ---- outputs of batch 0: spot-check against the oracle, stream sizes,
+    #      checksum of the block checksums over all ranks ----
+    encs[0].run_input(inputs[0], cfg)
+    outs = encs[0].fetch()
     out_bytes = sum(len(o) for o in outs)
+    vb = keep["verify"]
     if not args.no_verify and rank == 0:
         import oracle_py
-        for i in sorted({0, len(blocks) - 1}):
-            b = blocks[i]
+        for i in sorted({0, len(vb) - 1}):
+            b = vb[i]
             if outs[i] != oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode):
                 raise SystemExit(f"bench output of block {i} differs from the CPU restatement")
-            if not cfg.bin_mode:   # round trip: decode (CPU) back to the block, MD5s verified
+            if not cfg.bin_mode:
                 nm, nl, sq, sl, ql, ok = oracle_py.decode_block(outs[i], b.nreads, b.names.size, b.seq.size,
                                                                cfg.slevel, cfg.qlevel, cfg.md5)
                 if not (ok and np.array_equal(sq, b.seq) and np.array_equal(ql, b.qual)
                         and np.array_equal(nm, b.names)):
                     raise SystemExit(f"bench output of block {i} does not decode back to its input")
-        log("[rank 0] spot-check: first and last block bit-identical to the oracle and decode back to the input")
+        log("[rank 0] spot-check: first and last block of batch 0 bit-identical to the oracle, decode back")
+    digest = hashlib.sha256(b"".join(hashlib.sha256(o).digest() for o in outs)).digest()
+    if world > 1:
+        digs = gather_blocks([(rank, digest)], world)
+    else:
+        digs = [digest]
+    streams = stream_sizes(outs[0])
 
-    # dominant kernel phase (device time from HIP events on its own stream)
-    ph = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
+    # ---- dominant kernel phase (device time from HIP events on its stream) ----
+    ph = {k: float(np.median([p[k] for p in W.phases])) for k in W.phases[0]}
     kern = {k: v for k, v in ph.items() if k != "total"}
     dom = max(kern, key=kern.get)
-    algo_bytes = in_bytes + out_bytes           # FASTQ in + encoded out
+    in0 = inputs[0].text_bytes
+    algo_bytes = in0 + out_bytes          # FASTQ in + encoded out, per launch (one batch)
     achieved = algo_bytes / (kern[dom] / 1e3) / 1e9
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f).get(dom)
+    max_syms, all_syms = W.stats
+    hbm_per_ctx = [e.device_bytes() for e in encs]
 
     cpu = cpu_mt = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         import oracle_py
+        from concurrent.futures import ThreadPoolExecutor
+        blocks = keep["cpu"]
+        enc1 = lambda b: oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode)  # noqa: E731
         t0 = time.perf_counter()
-        nb, nbytes = 0, 0
+        nb = nbytes = 0
         for b in blocks:
-            oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode)
+            enc1(b)
             nb += 1
             nbytes += b.text_bytes
             if time.perf_counter() - t0 > args.cpu_seconds:
                 break
         ct = time.perf_counter() - t0
         cpu = {"value": round(nbytes / ct / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
-               "sample": f"{nb} of the bench's 50 MiB blocks ({nbytes/1e6:.0f} MB FASTQ) encoded by "
+               "sample": f"{nb} of the bench's 50 MiB PE blocks ({nbytes/1e6:.0f} MB FASTQ) encoded by "
                          f"oracle/fqz_oracle.c (-O2, 1 thread) on this host"}
-        # the same restatement on the host cores this process may use, one block
-        # per thread (the reference's -t N shape: independent blocks per thread;
-        # ctypes releases the GIL during the C call)
-        from concurrent.futures import ThreadPoolExecutor
-        nt = max(1, min(16, len(os.sched_getaffinity(0))))
-        sample = blocks[: min(len(blocks), max(nt, int(nt * (nb / ct) * args.cpu_seconds / 2)))]   # ~half the budget
+        # the same restatement on every host core this process may use, one block
+        # per thread (the reference's -t N shape; ctypes releases the GIL)
+        nt = share["usable"]
+        per_core = nb / ct
+        count = min(len(blocks), max(nt, int(nt * per_core * args.cpu_seconds)))
+        sample = [blocks[i % len(blocks)] for i in range(count)]
         t0 = time.perf_counter()
         with ThreadPoolExecutor(nt) as ex:
-            list(ex.map(lambda b: oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode), sample))
+            list(ex.map(enc1, sample))
         ct2 = time.perf_counter() - t0
         sb = sum(b.text_bytes for b in sample)
         cpu_mt = {"value": round(sb / ct2 / 1e6, 2), "unit": "MB/s", "cores": nt, "kind": "port",
-                  "sample": f"{len(sample)} of the bench's 50 MiB blocks ({sb/1e6:.0f} MB FASTQ) encoded by "
+                  "host": share,
+                  "sample": f"{len(sample)} 50 MiB PE blocks ({sb/1e6:.0f} MB FASTQ) encoded by "
                             f"oracle/fqz_oracle.c on {nt} host threads, one block per thread"}
 
     step_ms = elapsed / args.steps * 1e3
-    value = total_in * args.steps / elapsed / 1e6
+    value = total_bytes / elapsed / 1e6
     res = {
         "metric": "MB/s FASTQ compressed (whole node) + ratio, 150 bp PE, 1/2/4/8 MI355X",
         "value": round(value, 1),
@@ -188,13 +366,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (SURVEY.md 8(d) generator, seed 1000+rank), inputs resident in HBM",
-        "config": {"workload": f"synthetic {args.reads/1e6:g}M x {args.read_len} bp "
-                               f"{'PE (interleaved mate pairs)' if args.paired else 'SE'} per GPU, no-ref, "
-                               f"Slevel 3 (order-10), Qlevel 2, 50 MiB blocks, MD5 on",
-                   "blocks_per_gpu": len(blocks), "fastq_bytes_per_gpu": in_bytes,
-                   "parallelism": f"block-shard x{world}"},
-        "ratio": round(in_bytes / out_bytes, 3),
+        "data": "synthetic (SURVEY.md 8(d) generator, tests/synth.py, seed 1000 + global batch id), "
+                "inputs resident in HBM",
+        "config": {"workload": f"synthetic {args.pairs/1e6:g}M x {args.read_len} bp "
+                               f"{'SE reads' if args.se else 'PE mate pairs (interleaved r1,r2)'} per batch, "
+                               f"{args.batches} distinct batches per GPU, no-ref, Slevel {args.slevel} "
+                               f"(order-{args.slevel + 7}), Qlevel {args.qlevel}, 50 MiB blocks, MD5 on",
+                   "blocks_per_batch": len(keep["verify"]), "fastq_bytes_per_batch": in0,
+                   "contexts_per_gpu": args.contexts, "batches_per_gpu": args.batches,
+                   "parallelism": f"block-shard x{world} (batches dealt by shard_indices)"},
+        "ratio": round(in0 / out_bytes, 3),
+        "streams_block0": streams,
+        "streams_survey_ref": SURVEY_STREAMS,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "traffic_unit": "bytes per launch (rocprofv3 --pmc, profiles/traffic_latest.json)"},
@@ -203,12 +386,18 @@ def main():
                         "achieved_ms": round(ph.get("coder_r", 0.0), 2),
                         "frac": round(max_syms * R_NS_PER_SYMBOL / 1e6 / max(ph.get("coder_r", 1e-9), 1e-9), 3)},
         "phase_ms": {k: round(v, 2) for k, v in ph.items()},
+        "coder_restarts": W.restarts,
+        "hbm_bytes_per_context": hbm_per_ctx,
+        "checksum": hashlib.sha256(b"".join(digs)).hexdigest(),
         "cpu_baseline": cpu,
         "cpu_baseline_threads": cpu_mt,
     }
     if rank == 0:
         print(json.dumps(res), flush=True)
-    enc.close()
+    for e in encs:
+        e.close()
+    for i in inputs:
+        i.close()
     if world > 1:
         dist.destroy_process_group()
 

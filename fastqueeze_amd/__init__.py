@@ -22,7 +22,7 @@ import numpy as np
 from . import build as _build
 
 __all__ = ["SeqArcError", "blocks_from_fastq", "Block", "Config", "Encoder", "cut_se", "cut_pe", "parse_se", "parse_pe", "analyze_ids",
-           "load_library", "BLOCK_SIZE"]
+           "load_library", "BLOCK_SIZE", "Input"]
 
 BLOCK_SIZE = 50 << 20   # SeqArcParam BlockSize(M) = 50 (ctor @0x40776f)
 
@@ -85,7 +85,8 @@ def load_library(path: str | None = None):
         "sa_parse_se": ([P, U64, P, P, P, P, P], I64), "sa_parse_pe": ([P, U64, P, U64, P, P, P, P, P], I64),
         "sa_analyze_ids": ([P, I32, P], I32),
         "sa_code_records": ([P, I32, P, P, P, P, P, U64, P], I32), "sa_coder_restarts": ([P], C.c_uint32),
-        "sa_stream_stats": ([P, P, P], None),
+        "sa_stream_stats": ([P, P, P], None), "sa_device_bytes": ([P], U64),
+        "sa_input_create": ([I32, P, I32], P), "sa_input_destroy": ([P], None), "sa_run_input": ([P, P, P], I32),
         "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
         "sa_decode_block": ([P, U64, P, P, I32, P], I64),
     }
@@ -265,6 +266,9 @@ class Encoder:
             self._err("sa_run")
 
     def fetch(self) -> list[bytes]:
+        if self._staged is None:
+            raise SeqArcError("fetch(): nothing staged (encode_blocks() fetched its own output; stage() or "
+                              "run_input() first)")
         outs, keep = [], []
         for b in self._staged:
             cb = b._c()
@@ -292,8 +296,18 @@ class Encoder:
         c = cfg._c()
         if self._lib.sa_encode_blocks(self._ctx, ins, len(blocks), C.byref(c), arr) != 0:
             self._err("sa_encode_blocks")
-        self._staged = []
+        self._staged = None   # the context's last output is a sub-batch: nothing to fetch()
         return [keep[i][: arr[i].size].tobytes() for i in range(len(outs))]
+
+    def run_input(self, inp: "Input", cfg: Config):
+        """Encode a resident batch (sa_run_input); fetch() then returns its blocks."""
+        c = cfg._c()
+        if self._lib.sa_run_input(self._ctx, inp._h, C.byref(c)) != 0:
+            self._err("sa_run_input")
+        self._staged = inp.blocks
+
+    def device_bytes(self) -> int:
+        return int(self._lib.sa_device_bytes(self._ctx))
 
     def encode(self, blocks: list[Block], cfg: Config) -> list[bytes]:
         self.stage(blocks)
@@ -331,6 +345,31 @@ class Encoder:
         ms = (C.c_float * self.PHASES)()
         n = self._lib.sa_phase_times(self._ctx, names, ms, self.PHASES)
         return {names[i].decode(): float(ms[i]) for i in range(n)}
+
+
+class Input:
+    """A batch of blocks resident in HBM (sa_input_create): uploaded once, encoded
+    by any Encoder of the same device, concurrently from several host threads."""
+
+    def __init__(self, blocks: list[Block], device: int = 0):
+        self._lib = load_library()
+        self.blocks = list(blocks)
+        arr = (_SaBlock * max(1, len(blocks)))(*[b._c() for b in blocks])
+        self._h = self._lib.sa_input_create(device, arr, len(blocks))
+        if not self._h:
+            raise SeqArcError(f"sa_input_create failed on device {device}")
+        self.text_bytes = sum(b.text_bytes for b in blocks)
+
+    def close(self):
+        if self._h:
+            self._lib.sa_input_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def bare_plus(text) -> int:

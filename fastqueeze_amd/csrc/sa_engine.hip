@@ -27,7 +27,7 @@ struct DBuf {
         if (bytes <= cap && p) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
-        size_t want = std::max(bytes, cap + cap / 4);
+        size_t want = std::max(bytes, cap + cap / 16);   // slack for the next, slightly larger batch
         want = std::max<size_t>(want, 256);
         hipError_t e = hipMalloc(&p, want);
         cap = e == hipSuccess ? want : 0;
@@ -52,6 +52,24 @@ enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX,
 
 }  // namespace
 
+// A batch of parsed blocks resident in HBM (names, bases, qualities and the
+// per-read offsets), read-only while it is encoded: any number of contexts of
+// its device may encode it, one after the other or concurrently.
+struct sa_input {
+    int device = 0;
+    std::vector<DevBlock> blocks;   // layout fields only (the symbol spaces are per run)
+    uint32_t nblocks = 0, nreads = 0;
+    uint64_t names_bytes = 0, seq_bytes = 0, text_bytes = 0;
+    DBuf d_names, d_seq, d_qual, d_read_block, d_name_off, d_name_len, d_seq_off, d_seq_len;
+    std::vector<uint32_t> h_read_block, h_name_off, h_seq_off, h_seq_len;
+    std::vector<uint16_t> h_name_len;
+    ~sa_input()
+    {
+        for (DBuf* b : {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off, &d_seq_len})
+            b->release();
+    }
+};
+
 struct sa_ctx {
     int device = 0;
     // main/AUX, MD5, SEQ path (CU-masked), long AUX runs (CU-masked, disjoint)
@@ -68,16 +86,13 @@ struct sa_ctx {
     hipEvent_t ev_beg[PH_N], ev_end[PH_N];
     float ph_ms[PH_N];
 
-    // staged batch
+    // the batch sa_stage uploads (sa_run encodes it); blocks = the working copy
+    // of the batch being encoded (its symbol spaces filled by plan_batch)
+    sa_input own;
     std::vector<DevBlock> blocks;
-    uint32_t nblocks = 0, nreads = 0;
-    uint64_t names_bytes = 0, seq_bytes = 0;
-    DBuf d_names, d_seq, d_qual, d_read_block, d_name_off, d_name_len, d_seq_off, d_seq_len, d_blocks;
-    std::vector<uint32_t> h_read_block, h_name_off, h_seq_off, h_seq_len;
-    std::vector<uint16_t> h_name_len;
 
     // work
-    DBuf d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
+    DBuf d_blocks, d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
     DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_asm_copies, d_task_out_base, d_final, d_final_len;
@@ -91,18 +106,28 @@ struct sa_ctx {
     std::vector<uint64_t> final_base, final_len;
     bool have_output = false;
 
+    std::vector<DBuf*> work_buffers()
+    {
+        return {&d_blocks, &d_counts, &d_totals, &d_name_p, &d_name_s, &d_maxlen, &d_err,
+                 &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
+                 &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
+                 &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
+                 &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base, &d_final,
+                 &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_short_at, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                 &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry,
+                 &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
+                 &d_list_gbase[1], &d_list_run[1]};
+    }
+    uint64_t held_bytes()
+    {
+        uint64_t h = own.d_names.cap + own.d_seq.cap + own.d_qual.cap;
+        for (DBuf* b : work_buffers()) h += b->cap;
+        return h;
+    }
+
     ~sa_ctx()
     {
-        DBuf* all[] = {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off,
-                       &d_seq_len, &d_blocks, &d_counts, &d_totals, &d_name_p, &d_name_s, &d_maxlen, &d_err,
-                       &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
-                       &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
-                       &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
-                       &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base, &d_final,
-                       &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_short_at, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                       &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry,
-                       &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
-                       &d_list_gbase[1], &d_list_run[1]};
+        std::vector<DBuf*> all = work_buffers();
         for (DBuf* b : all) b->release();
         for (int i = 0; i < PH_N; i++) {
             if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
@@ -163,7 +188,7 @@ void ev_finish(sa_ctx* c, int ph, hipStream_t st);
 // d_qual_q, which the QUAL stream then codes (speculative chunks, one carry
 // lane per block, chunk replay; sa_logic.h).  The staged qualities stay
 // untouched: the N/IUPAC side streams use them, and the batch can be re-run.
-int run_rblock(sa_ctx* c, double ratio, BatchView& bv)
+int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
 {
     hipStream_t st = c->st;
     std::vector<RbChunk> ck;
@@ -178,7 +203,7 @@ int run_rblock(sa_ctx* c, double ratio, BatchView& bv)
     }
     ck0.push_back((uint32_t)ck.size());
     const uint32_t nck = (uint32_t)ck.size(), nbk = (uint32_t)c->blocks.size();
-    SA_CHECK(c, c->d_qual_q.ensure(c->seq_bytes + 16));
+    SA_CHECK(c, c->d_qual_q.ensure(seq_bytes + 16));
     bv.qual_q = c->d_qual_q.as<uint8_t>();
     if (!nck) return 0;
     SA_CHECK(c, c->d_rb_chunks.ensure(sizeof(RbChunk) * nck));
@@ -310,20 +335,25 @@ int coder_run(sa_ctx* c, const std::vector<CoderTask>& tasks, const CoderView& c
         SA_CHECK(c, hipMemcpyAsync(out_len.data(), cv.out_len, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
         SA_CHECK(c, hipStreamSynchronize(st));
         std::vector<uint32_t> ids;
-        std::vector<CoderRun> runs;
         for (size_t t = 0; t < tasks.size(); t++) {
             const uint32_t k = first_sq[t];
-            if (k == 0xffffffffu || k + 1 >= tasks[t].nseg) continue;
-            LowMap endst;
-            uint32_t off;
-            SA_CHECK(c, hipMemcpy(&endst, cv.maps + tasks[t].seg_base + k, sizeof endst, hipMemcpyDeviceToHost));
-            SA_CHECK(c, hipMemcpy(&off, cv.off_at + tasks[t].seg_base + k, 4, hipMemcpyDeviceToHost));
-            ids.push_back((uint32_t)t);
-            runs.push_back(CoderRun{endst.B, endst.s, k + 1, off + endst.nbytes, 0u});
-            const uint32_t none = 0xffffffffu;
-            SA_CHECK(c, hipMemcpy(cv.first_sq + t, &none, 4, hipMemcpyHostToDevice));
+            if (k != 0xffffffffu && k + 1 < tasks[t].nseg) ids.push_back((uint32_t)t);
         }
         if (ids.empty()) break;
+        // the exact end state L3 left at each restarted stream's squeezed
+        // segment: all copies queued on st, one wait
+        std::vector<LowMap> endst(ids.size());
+        std::vector<uint32_t> off(ids.size());
+        for (size_t i = 0; i < ids.size(); i++) {
+            const uint64_t sg = tasks[ids[i]].seg_base + first_sq[ids[i]];
+            SA_CHECK(c, hipMemcpyAsync(&endst[i], cv.maps + sg, sizeof(LowMap), hipMemcpyDeviceToHost, st));
+            SA_CHECK(c, hipMemcpyAsync(&off[i], cv.off_at + sg, 4, hipMemcpyDeviceToHost, st));
+        }
+        SA_CHECK(c, hipMemsetAsync(cv.first_sq, 0xff, 4 * tasks.size(), st));
+        SA_CHECK(c, hipStreamSynchronize(st));
+        std::vector<CoderRun> runs;
+        for (size_t i = 0; i < ids.size(); i++)
+            runs.push_back(CoderRun{endst[i].B, endst[i].s, first_sq[ids[i]] + 1, off[i] + endst[i].nbytes, 0u});
         if (round > 1000) {
             c->err = "range coder: too many restarts";
             return -1;
@@ -440,23 +470,38 @@ uint64_t sa_output_bound(const sa_block* b)
            + nn;
 }
 
-int sa_stage(sa_ctx* c, const sa_block* in, int n)
+}  // extern "C"
+
+namespace {
+
+// Uploads a batch of parsed blocks into `in` (its buffers grow as needed) on
+// stream st and waits for the copies.  Returns 0 or -1 with err set.
+int input_upload(sa_input* I, const sa_block* in, int n, hipStream_t st, std::string& err)
 {
-    if (!c) return -1;
-    SA_CHECK(c, hipSetDevice(c->device));
-    c->have_output = false;
-    c->nblocks = (uint32_t)n;
-    c->blocks.assign((size_t)n, DevBlock{});
-    uint64_t nb = 0, sb = 0;
+#define IN_CHECK(expr)                                                                   \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            err = std::string(#expr) + ": " + hipGetErrorString(e_);                     \
+            return -1;                                                                   \
+        }                                                                                \
+    } while (0)
+    if (n < 0 || (n > 0 && !in)) {
+        err = "invalid block list";
+        return -1;
+    }
+    I->nblocks = (uint32_t)n;
+    I->blocks.assign((size_t)n, DevBlock{});
+    uint64_t nb = 0, sb = 0, tb = 0;
     uint32_t nr = 0;
     for (int b = 0; b < n; b++) {
-        DevBlock& d = c->blocks[(size_t)b];
+        DevBlock& d = I->blocks[(size_t)b];
         d.nreads = in[b].nreads;
         d.read0 = nr;
         uint64_t ln = 0, ls = 0;
         for (uint32_t r = 0; r < in[b].nreads; r++) {
             if (in[b].seq_lens[r] < 0) {
-                c->err = "negative read length";
+                err = "negative read length";
                 return -1;
             }
             ln += in[b].name_lens[r];
@@ -464,7 +509,11 @@ int sa_stage(sa_ctx* c, const sa_block* in, int n)
             if (in[b].seq_lens[r] > 0xffff) d.len_long = 1;   // getBlockRead@0x411d2a
         }
         if (ls >= (1ull << 30) || ln >= (1ull << 32)) {
-            c->err = "block too large (a reference block is 50 MiB of FASTQ)";
+            err = "block too large (a reference block is 50 MiB of FASTQ)";
+            return -1;
+        }
+        if ((uint64_t)nr + in[b].nreads >= (1ull << 31)) {
+            err = "too many reads in one batch";
             return -1;
         }
         d.name_base = nb;
@@ -473,68 +522,121 @@ int sa_stage(sa_ctx* c, const sa_block* in, int n)
         d.seq_bytes = ls;
         nb = align_up(nb + ln, 16);
         sb = align_up(sb + ls, 16);
+        tb += ln + 2 * ls;
         nr += in[b].nreads;
     }
-    c->nreads = nr;
-    c->names_bytes = nb;
-    c->seq_bytes = sb;
-    c->h_read_block.resize(nr);
-    c->h_name_off.resize(nr);
-    c->h_name_len.resize(nr);
-    c->h_seq_off.resize(nr);
-    c->h_seq_len.resize(nr);
+    I->nreads = nr;
+    I->names_bytes = nb;
+    I->seq_bytes = sb;
+    I->text_bytes = tb;
+    I->h_read_block.resize(nr);
+    I->h_name_off.resize(nr);
+    I->h_name_len.resize(nr);
+    I->h_seq_off.resize(nr);
+    I->h_seq_len.resize(nr);
     for (int b = 0; b < n; b++) {
-        const DevBlock& d = c->blocks[(size_t)b];
+        const DevBlock& d = I->blocks[(size_t)b];
         uint32_t no = 0, so = 0;
         for (uint32_t r = 0; r < d.nreads; r++) {
             const uint32_t g = d.read0 + r;
-            c->h_read_block[g] = (uint32_t)b;
-            c->h_name_off[g] = no;
-            c->h_name_len[g] = in[b].name_lens[r];
-            c->h_seq_off[g] = so;
-            c->h_seq_len[g] = (uint32_t)in[b].seq_lens[r];
+            I->h_read_block[g] = (uint32_t)b;
+            I->h_name_off[g] = no;
+            I->h_name_len[g] = in[b].name_lens[r];
+            I->h_seq_off[g] = so;
+            I->h_seq_len[g] = (uint32_t)in[b].seq_lens[r];
             no += in[b].name_lens[r];
             so += (uint32_t)in[b].seq_lens[r];
         }
     }
-    SA_CHECK(c, c->d_names.ensure(nb + 16));
-    SA_CHECK(c, c->d_seq.ensure(sb + 16));
-    SA_CHECK(c, c->d_qual.ensure(sb + 16));
+    IN_CHECK(I->d_names.ensure(nb + 16));
+    IN_CHECK(I->d_seq.ensure(sb + 16));
+    IN_CHECK(I->d_qual.ensure(sb + 16));
     const size_t nr4 = (size_t)std::max<uint32_t>(nr, 1) * 4;
-    SA_CHECK(c, c->d_read_block.ensure(nr4));
-    SA_CHECK(c, c->d_name_off.ensure(nr4));
-    SA_CHECK(c, c->d_name_len.ensure(nr4));
-    SA_CHECK(c, c->d_seq_off.ensure(nr4));
-    SA_CHECK(c, c->d_seq_len.ensure(nr4));
+    IN_CHECK(I->d_read_block.ensure(nr4));
+    IN_CHECK(I->d_name_off.ensure(nr4));
+    IN_CHECK(I->d_name_len.ensure(nr4));
+    IN_CHECK(I->d_seq_off.ensure(nr4));
+    IN_CHECK(I->d_seq_len.ensure(nr4));
     for (int b = 0; b < n; b++) {
-        const DevBlock& d = c->blocks[(size_t)b];
+        const DevBlock& d = I->blocks[(size_t)b];
         if (d.name_bytes)
-            SA_CHECK(c, hipMemcpyAsync(c->d_names.as<uint8_t>() + d.name_base, in[b].names, d.name_bytes,
-                                       hipMemcpyHostToDevice, c->st));
+            IN_CHECK(hipMemcpyAsync(I->d_names.as<uint8_t>() + d.name_base, in[b].names, d.name_bytes,
+                                    hipMemcpyHostToDevice, st));
         if (d.seq_bytes) {
-            SA_CHECK(c, hipMemcpyAsync(c->d_seq.as<uint8_t>() + d.seq_base, in[b].seq, d.seq_bytes,
-                                       hipMemcpyHostToDevice, c->st));
-            SA_CHECK(c, hipMemcpyAsync(c->d_qual.as<uint8_t>() + d.seq_base, in[b].qual, d.seq_bytes,
-                                       hipMemcpyHostToDevice, c->st));
+            IN_CHECK(hipMemcpyAsync(I->d_seq.as<uint8_t>() + d.seq_base, in[b].seq, d.seq_bytes,
+                                    hipMemcpyHostToDevice, st));
+            IN_CHECK(hipMemcpyAsync(I->d_qual.as<uint8_t>() + d.seq_base, in[b].qual, d.seq_bytes,
+                                    hipMemcpyHostToDevice, st));
         }
     }
     if (nr) {
-        SA_CHECK(c, hipMemcpyAsync(c->d_read_block.p, c->h_read_block.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_name_off.p, c->h_name_off.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_name_len.p, c->h_name_len.data(), nr * 2ull, hipMemcpyHostToDevice, c->st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_seq_off.p, c->h_seq_off.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_seq_len.p, c->h_seq_len.data(), nr * 4ull, hipMemcpyHostToDevice, c->st));
+        IN_CHECK(hipMemcpyAsync(I->d_read_block.p, I->h_read_block.data(), nr * 4ull, hipMemcpyHostToDevice, st));
+        IN_CHECK(hipMemcpyAsync(I->d_name_off.p, I->h_name_off.data(), nr * 4ull, hipMemcpyHostToDevice, st));
+        IN_CHECK(hipMemcpyAsync(I->d_name_len.p, I->h_name_len.data(), nr * 2ull, hipMemcpyHostToDevice, st));
+        IN_CHECK(hipMemcpyAsync(I->d_seq_off.p, I->h_seq_off.data(), nr * 4ull, hipMemcpyHostToDevice, st));
+        IN_CHECK(hipMemcpyAsync(I->d_seq_len.p, I->h_seq_len.data(), nr * 4ull, hipMemcpyHostToDevice, st));
     }
-    SA_CHECK(c, hipStreamSynchronize(c->st));
+    IN_CHECK(hipStreamSynchronize(st));
+#undef IN_CHECK
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sa_stage(sa_ctx* c, const sa_block* in, int n)
+{
+    if (!c) return -1;
+    SA_CHECK(c, hipSetDevice(c->device));
+    c->have_output = false;
+    return input_upload(&c->own, in, n, c->st, c->err);
+}
+
+sa_input* sa_input_create(int device, const sa_block* in, int n)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    sa_input* I = new sa_input();
+    I->device = device;
+    std::string err;
+    const int rc = input_upload(I, in, n, st, err);
+    (void)hipStreamDestroy(st);
+    if (rc) {
+        std::fprintf(stderr, "seqarc_amd: sa_input_create: %s\n", err.c_str());
+        delete I;
+        return nullptr;
+    }
+    return I;
+}
+
+void sa_input_destroy(sa_input* in)
+{
+    if (!in) return;
+    (void)hipSetDevice(in->device);
+    delete in;
 }
 
 int sa_run(sa_ctx* c, const sa_cfg* cfg)
 {
     if (!c) return -1;
+    return sa_run_input(c, &c->own, cfg);
+}
+
+int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
+{
+    if (!c) return -1;
+    if (!I || !cfg || I->device != c->device) {
+        c->err = "sa_run_input: no input, no config, or an input of another device";
+        return -1;
+    }
     SA_CHECK(c, hipSetDevice(c->device));
     c->have_output = false;
-    const uint32_t nbk = c->nblocks;
+    c->blocks = I->blocks;
+    const uint32_t nbk = I->nblocks;
     if (nbk == 0) {
         c->final_base.clear();
         c->final_len.clear();
@@ -551,7 +653,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     const int seq_bits = (2 * k) & 31;   // NS = 1 << seq_bits (x86 shl masks the count)
     const int aux_bits = cfg->qlevel > 2 ? 21 : 17;
     hipStream_t st = c->st;
-    const uint32_t nr = c->nreads;
+    const uint32_t nr = I->nreads;
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
@@ -567,16 +669,16 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     bv.blocks = c->d_blocks.as<DevBlock>();
     bv.nblocks = nbk;
     bv.nreads_total = nr;
-    bv.read_block = c->d_read_block.as<uint32_t>();
-    bv.names = c->d_names.as<uint8_t>();
-    bv.seq = c->d_seq.as<uint8_t>();
-    bv.qual = c->d_qual.as<uint8_t>();
+    bv.read_block = I->d_read_block.as<uint32_t>();
+    bv.names = I->d_names.as<uint8_t>();
+    bv.seq = I->d_seq.as<uint8_t>();
+    bv.qual = I->d_qual.as<uint8_t>();
     bv.qual_q = bv.qual;
     bv.lossy = lossy ? 1 : 0;
-    bv.name_off = c->d_name_off.as<uint32_t>();
-    bv.name_len = c->d_name_len.as<uint16_t>();
-    bv.seq_off = c->d_seq_off.as<uint32_t>();
-    bv.seq_len = c->d_seq_len.as<uint32_t>();
+    bv.name_off = I->d_name_off.as<uint32_t>();
+    bv.name_len = I->d_name_len.as<uint16_t>();
+    bv.seq_off = I->d_seq_off.as<uint32_t>();
+    bv.seq_len = I->d_seq_len.as<uint32_t>();
     bv.seq_mask = ns - 1;
     bv.qlevel = cfg->qlevel;
     bv.bin_mode = cfg->bin_mode ? 1 : 0;
@@ -589,9 +691,9 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     std::vector<Md5Task> md5t;
     for (uint32_t b = 0; b < nbk; b++) {
         const DevBlock& d = c->blocks[b];
-        md5t.push_back(Md5Task{c->d_names.as<uint8_t>() + d.name_base, d.name_bytes});
-        md5t.push_back(Md5Task{c->d_seq.as<uint8_t>() + d.seq_base, d.seq_bytes});
-        md5t.push_back(Md5Task{c->d_qual.as<uint8_t>() + d.seq_base, d.seq_bytes});
+        md5t.push_back(Md5Task{I->d_names.as<uint8_t>() + d.name_base, d.name_bytes});
+        md5t.push_back(Md5Task{I->d_seq.as<uint8_t>() + d.seq_base, d.seq_bytes});
+        md5t.push_back(Md5Task{I->d_qual.as<uint8_t>() + d.seq_base, d.seq_bytes});
     }
     if (cfg->md5) {
         SA_CHECK(c, c->d_md5tasks.ensure(sizeof(Md5Task) * md5t.size()));
@@ -610,7 +712,7 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
         SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
     }
     ev_begin(c, PH_PREP, st);
-    if (lossy && run_rblock(c, cfg->lossy, bv)) return -1;
+    if (lossy && run_rblock(c, cfg->lossy, I->seq_bytes, bv)) return -1;
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
         hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
@@ -947,35 +1049,58 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
 
 uint32_t sa_coder_restarts(const sa_ctx* c) { return c ? c->coder_restarts : 0; }
 
+uint64_t sa_device_bytes(const sa_ctx* c) { return c ? const_cast<sa_ctx*>(c)->held_bytes() : 0; }
+
 void sa_stream_stats(const sa_ctx* c, uint64_t* max_symbols, uint64_t* total_symbols)
 {
     if (max_symbols) *max_symbols = c ? c->max_stream_syms : 0;
     if (total_symbols) *total_symbols = c ? c->total_stream_syms : 0;
 }
 
+// HBM a block needs while its batch is encoded: per SEQ symbol the
+// double-buffered u32 keys and values plus the 8-byte record (24 B); per AUX
+// symbol the same plus its u16 cum (26 B); per symbol up to 2 payload and 2
+// final bytes; per read the count columns and the read arrays; the input.
+// AUX symbols ~ qualities + name bytes + 8 per read (len, name tokens, dege).
+static uint64_t block_footprint(const sa_block& b)
+{
+    uint64_t bases = 0, nb = 0;
+    for (uint32_t r = 0; r < b.nreads; r++) {
+        bases += (uint64_t)std::max(b.seq_lens[r], 0);
+        nb += b.name_lens[r];
+    }
+    const uint64_t aux = bases + nb + 8ull * b.nreads;
+    return (24 + 4) * bases + (26 + 4) * aux + (nb + 2 * bases + 16) + 64ull * b.nreads;
+}
+
 int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, sa_out* out)
 {
     if (!ctx || !cfg || (n > 0 && (!in || !out))) return -1;
-    // Blocks are independent, so a large batch is encoded as consecutive
-    // sub-batches of at most SA_BATCH_BASES bases: the symbol records and sort
-    // buffers of one sub-batch (~8 B per symbol, x2 for the sort) stay well
-    // inside 288 GB of HBM whatever the caller hands over.  SA_BATCH_BASES in
-    // the environment lowers the cap (tests split a small batch with it).
-    uint64_t cap_bases = 3ull << 30;
+    if (n == 0) return 0;
+    SA_CHECK(ctx, hipSetDevice(ctx->device));
+    // Blocks are independent, so a batch larger than the HBM this context can
+    // use is encoded as consecutive sub-batches (outputs keep the input order).
+    // Budget: 85 % of what is free plus what this context already holds (its
+    // buffers are reused).  SA_BATCH_BASES caps the bases per sub-batch (tests).
+    size_t free_b = 0, total_b = 0;
+    SA_CHECK(ctx, hipMemGetInfo(&free_b, &total_b));
+    const uint64_t budget = (uint64_t)((double)(free_b + ctx->held_bytes()) * 0.85);
+    uint64_t cap_bases = ~0ull;
     if (const char* e = std::getenv("SA_BATCH_BASES")) {
         const unsigned long long v = std::strtoull(e, nullptr, 10);
-        if (v > 0 && v < cap_bases) cap_bases = v;
+        if (v > 0) cap_bases = v;
     }
-    if (n == 0) return 0;
     int b0 = 0;
     while (b0 < n) {
         int b1 = b0;
-        uint64_t bases = 0;
+        uint64_t bases = 0, bytes = 0;
         while (b1 < n) {
             uint64_t ls = 0;
             for (uint32_t r = 0; r < in[b1].nreads; r++) ls += (uint64_t)std::max(in[b1].seq_lens[r], 0);
-            if (b1 > b0 && bases + ls > cap_bases) break;
+            const uint64_t fb = block_footprint(in[b1]);
+            if (b1 > b0 && (bases + ls > cap_bases || bytes + fb > budget)) break;
             bases += ls;
+            bytes += fb;
             b1++;
         }
         if (sa_stage(ctx, in + b0, b1 - b0)) return -1;

@@ -1733,38 +1733,87 @@ __device__ inline void md5_block(uint32_t h[4], const uint32_t M[16])
     h[3] += d;
 }
 
+// One wave per message.  MD5 is one dependent chain per message, so one lane
+// computes; the whole wave streams the message through LDS a 1 KiB chunk (16
+// MD5 blocks, one 16-byte load per lane) ahead of it, so the chain never waits
+// on a load (the compute of a chunk, ~16 x 1000 cycles, covers the next
+// chunk's HBM latency).
+constexpr uint32_t MD5_CHUNK_BLOCKS = 16;
+
 __global__ __launch_bounds__(64) void k_md5(const Md5Task* __restrict__ tasks, uint32_t ntasks,
                                             uint32_t* __restrict__ digests)
 {
+    __shared__ uint4 ring[2][64];
     const uint32_t t = blockIdx.x;
-    if (t >= ntasks || threadIdx.x != 0) return;
+    if (t >= ntasks) return;
+    const uint32_t lane = threadIdx.x;
     const Md5Task tk = tasks[t];
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    const uint4* p = reinterpret_cast<const uint4*>(tk.ptr);
+    // global (not flat) loads: a flat load also counts in lgkmcnt, so the LDS
+    // waits of the compute would wait for the prefetch
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
+    g_u32x4* gp = (g_u32x4*)(tk.ptr);
+    auto p = [&](uint64_t i) __attribute__((always_inline)) {
+        const u32x4 v = gp[i];
+        return make_uint4(v.x, v.y, v.z, v.w);
+    };
     const uint64_t nfull = tk.len / 64;
+    const uint64_t nvec = nfull * 4;   // 16-byte words of the full blocks
+    const uint64_t nck = (nfull + MD5_CHUNK_BLOCKS - 1) / MD5_CHUNK_BLOCKS;
     uint32_t M[16];
-    for (uint64_t blkn = 0; blkn < nfull; blkn++) {
-        const uint4 a = p[4 * blkn + 0], b = p[4 * blkn + 1], c = p[4 * blkn + 2], d = p[4 * blkn + 3];
-        M[0] = a.x; M[1] = a.y; M[2] = a.z; M[3] = a.w;
-        M[4] = b.x; M[5] = b.y; M[6] = b.z; M[7] = b.w;
-        M[8] = c.x; M[9] = c.y; M[10] = c.z; M[11] = c.w;
-        M[12] = d.x; M[13] = d.y; M[14] = d.z; M[15] = d.w;
-        md5_block(h, M);
+    uint4 nxt = lane < nvec ? p(lane) : make_uint4(0u, 0u, 0u, 0u);
+    for (uint64_t c = 0; c < nck; c++) {
+        uint4* slot = ring[c & 1];
+        slot[lane] = nxt;
+        const uint64_t at = (c + 1) * 64 + lane;
+        if (c + 1 < nck) nxt = at < nvec ? p(at) : make_uint4(0u, 0u, 0u, 0u);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        if (lane == 0) {
+            const uint64_t left = nfull - c * MD5_CHUNK_BLOCKS;
+            const uint32_t nb = left < MD5_CHUNK_BLOCKS ? (uint32_t)left : MD5_CHUNK_BLOCKS;
+            uint4 a = slot[0], b = slot[1], cc = slot[2], d = slot[3];
+            for (uint32_t k = 0; k < nb; k++) {
+                // the next block's words are read from LDS before this block's chain
+                const uint32_t kn = k + 1 < nb ? 4 * (k + 1) : 0;
+                const uint4 na = slot[kn], nb_ = slot[kn + 1], nc = slot[kn + 2], nd = slot[kn + 3];
+                M[0] = a.x; M[1] = a.y; M[2] = a.z; M[3] = a.w;
+                M[4] = b.x; M[5] = b.y; M[6] = b.z; M[7] = b.w;
+                M[8] = cc.x; M[9] = cc.y; M[10] = cc.z; M[11] = cc.w;
+                M[12] = d.x; M[13] = d.y; M[14] = d.z; M[15] = d.w;
+                md5_block(h, M);
+                a = na;
+                b = nb_;
+                cc = nc;
+                d = nd;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
     }
-    // tail + padding (bit length of the u32 length, as the RSA MDString)
+    // tail + padding (bit length of the u32 length, as the RSA MDString): the
+    // wave writes the last one or two 64-byte blocks into LDS, two bytes a lane
     const uint32_t rem = (uint32_t)(tk.len - nfull * 64);
     const uint8_t* tail = tk.ptr + nfull * 64;
-    uint8_t buf[128];
-    for (uint32_t k = 0; k < 128; k++) buf[k] = 0;
-    for (uint32_t k = 0; k < rem; k++) buf[k] = tail[k];
-    buf[rem] = 0x80;
     const uint32_t tl = rem < 56 ? 64 : 128;
     const uint64_t bits = (uint64_t)(uint32_t)tk.len << 3;
-    for (int k = 0; k < 8; k++) buf[tl - 8 + k] = (uint8_t)(bits >> (8 * k));
-    for (uint32_t o = 0; o < tl; o += 64) {
-        for (int k = 0; k < 16; k++)
-            M[k] = (uint32_t)buf[o + 4 * k] | ((uint32_t)buf[o + 4 * k + 1] << 8) |
-                   ((uint32_t)buf[o + 4 * k + 2] << 16) | ((uint32_t)buf[o + 4 * k + 3] << 24);
+    uint8_t* tb = reinterpret_cast<uint8_t*>(ring[0]);
+#pragma unroll
+    for (uint32_t j = lane; j < 128; j += 64) {
+        uint8_t v = 0;
+        if (j < rem) v = tail[j];
+        else if (j == rem) v = 0x80;
+        else if (j >= tl - 8 && j < tl) v = (uint8_t)(bits >> (8 * (j - (tl - 8))));
+        tb[j] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane != 0) return;
+    const uint32_t* tw = reinterpret_cast<const uint32_t*>(ring[0]);
+    for (uint32_t o = 0; o < tl / 4; o += 16) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) M[k] = tw[o + k];
         md5_block(h, M);
     }
     for (int k = 0; k < 4; k++) digests[(size_t)t * 4 + k] = h[k];

@@ -75,6 +75,19 @@ int sa_fetch(sa_ctx *ctx, sa_out *out, int n);             /* D2H of the encaps 
  * the stream each phase runs on; returns the number of phases written */
 int sa_phase_times(const sa_ctx *ctx, const char **names, float *ms, int max);
 void sa_set_timing(sa_ctx *ctx, int on);
+/* HBM bytes the context's work buffers hold (they grow to the largest batch) */
+uint64_t sa_device_bytes(const sa_ctx *ctx);
+
+/* ---- resident inputs: a batch uploaded once, encoded by any context ----
+ * The reference keeps a pool of parsed blocks between its reader and its
+ * encode threads (ReadBufPool::getEmptybuf/getFullbuf@0x4341e0/0x4343d0); an
+ * sa_input is such a batch resident in HBM.  Several contexts of one device
+ * (one host thread each) encode their batches concurrently: one batch's
+ * throughput-bound front overlaps another's latency-bound range coder. */
+typedef struct sa_input sa_input;
+sa_input *sa_input_create(int device, const sa_block *in, int n);   /* NULL on error */
+void sa_input_destroy(sa_input *in);
+int sa_run_input(sa_ctx *ctx, const sa_input *in, const sa_cfg *cfg);   /* then sa_fetch */
 
 /* ---- range coder over pre-modelled symbols ---------------------------- */
 /* The carry-less range coder inlined in every EncapFqzComp::encode_* (e.g.

@@ -4,8 +4,15 @@ Test / bench infrastructure.  Genome of 5,000,000 uniform random bases; fragment
 with uniform start and insert 250-449; r1 = forward read, r2 = reverse complement
 of the fragment end; 0.2 % substitutions; qualities from {F, :, ,} with
 p = {0.90, 0.07, 0.03}; 0.05 % N on r1 with quality '#'; Illumina-style headers
-whose mate IDs differ (`1:N:0:` / `2:N:0:`), which keeps the reference out of its
-identical-mate-ID PE livelock (defect i).
+`@A00123:8:H5KJ2DSXX:1:<tile>:<x>:<y> {1|2}:N:0:ACGTACGT`: both mates of a pair
+carry the same tile:x:y (as a sequencer writes them) and differ only in the
+`1:`/`2:` comment, which keeps the reference out of its identical-mate-ID PE
+livelock (defect i).
+
+Chunks of `chunk` records are drawn from their own generator (seed, chunk index),
+so the output does not depend on how many worker processes produce it.
+Qualities are drawn as 16-bit integers (p = k / 65536, within 1e-5 of the spec);
+substitutions and N are placed at a binomial number of uniform positions.
 """
 from __future__ import annotations
 
@@ -14,14 +21,29 @@ import numpy as np
 _COMP = np.frombuffer(b"TGCA", dtype=np.uint8)  # complement of ACGT by code
 _BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
 _QUALS = np.frombuffer(b"F:,", dtype=np.uint8)
+_Q1, _Q2 = 58982, 63570        # 0.90, 0.97 of 65536 -> 'F' / ':' / ','
+_SUB = 131                     # 0.002 of 65536
+_NRATE = 33                    # 0.0005 of 65536
+
+_genome_cache: dict = {}
 
 
-def _headers(rng: np.random.Generator, start: int, n: int, mate: int) -> list[bytes]:
+def _genome(seed: int, genome_len: int) -> np.ndarray:
+    key = (seed, genome_len)
+    g = _genome_cache.get(key)
+    if g is None:
+        g = np.random.default_rng(seed).integers(0, 4, size=genome_len, dtype=np.uint8)
+        _genome_cache.clear()
+        _genome_cache[key] = g
+    return g
+
+
+def _headers(start: int, x: np.ndarray, mate: int) -> list[bytes]:
     # tiles of 4000 reads; y increases within a tile, x random (variable width)
+    n = x.shape[0]
     idx = np.arange(start, start + n)
     tile = 1101 + (idx // 4000) % 78
     y = 1000 + (idx % 4000) * 8
-    x = rng.integers(1000, 32000, size=n)
     return [
         b"@A00123:8:H5KJ2DSXX:1:%d:%d:%d %d:N:0:ACGTACGT" % (t, xx, yy, mate)
         for t, xx, yy in zip(tile.tolist(), x.tolist(), y.tolist())
@@ -31,50 +53,83 @@ def _headers(rng: np.random.Generator, start: int, n: int, mate: int) -> list[by
 def _records(names: list[bytes], seq: np.ndarray, qual: np.ndarray) -> bytes:
     L = seq.shape[1]
     n = seq.shape[0]
-    body = np.empty((n, 2 * L + 4), dtype=np.uint8)
+    body = np.empty((n, 2 * L + 5), dtype=np.uint8)
     body[:, 0] = ord("\n")
     body[:, 1 : L + 1] = seq
     body[:, L + 1] = ord("\n")
     body[:, L + 2] = ord("+")
     body[:, L + 3] = ord("\n")
-    body[:, L + 4 :] = qual
-    tail = b"\n"
+    body[:, L + 4 : 2 * L + 4] = qual
+    body[:, 2 * L + 4] = ord("\n")
     bodies = body.tobytes()
-    w = 2 * L + 4
-    return b"".join(nm + bodies[i * w : (i + 1) * w] + tail for i, nm in enumerate(names))
+    w = 2 * L + 5
+    return b"".join(nm + bodies[i * w : (i + 1) * w] for i, nm in enumerate(names))
+
+
+def _sparse(rng: np.random.Generator, total: int, rate: float) -> np.ndarray:
+    """Flat positions of a Bernoulli(rate) event over `total` cells (a binomial
+    count of uniform positions; a repeated position counts once)."""
+    return rng.integers(0, total, size=int(rng.binomial(total, rate)))
+
+
+def _chunk(args):
+    seed, ci, s, n, read_len, paired, genome_len = args
+    genome = _genome(seed, genome_len)
+    win = np.lib.stride_tricks.sliding_window_view(genome, read_len)
+    rng = np.random.default_rng([seed, ci])
+    start = rng.integers(0, genome_len - max(450, read_len), size=n)
+    ins = rng.integers(250, 450, size=n)
+    x = rng.integers(1000, 32000, size=n)
+    cells = n * read_len
+
+    def quals():
+        u = rng.bit_generator.random_raw((cells + 3) // 4).view(np.uint16)[:cells].reshape(n, read_len)
+        return _QUALS[(u >= _Q1).astype(np.uint8) + (u >= _Q2)]
+
+    def mutate(r):
+        r = np.ascontiguousarray(r).reshape(-1)
+        at = _sparse(rng, cells, _SUB / 65536)
+        r[at] = (r[at] + rng.integers(1, 4, size=at.size, dtype=np.uint8)) & 3
+        return r.reshape(n, read_len)
+
+    s1 = _BASES[mutate(win[start])]
+    q1 = quals()
+    at = _sparse(rng, cells, _NRATE / 65536)
+    s1.reshape(-1)[at] = ord("N")
+    q1.reshape(-1)[at] = ord("#")
+    out1 = _records(_headers(s, x, 1), s1, q1)
+    out2 = None
+    if paired:
+        s2 = _COMP[mutate(win[start + ins - read_len][:, ::-1])]
+        out2 = _records(_headers(s, x, 2), s2, quals())
+    return out1, out2
 
 
 def generate(n_reads: int, read_len: int = 150, paired: bool = False, seed: int = 12345,
-             genome_len: int = 5_000_000, chunk: int = 250_000, progress=None):
-    """Return (r1_bytes, r2_bytes or None) of n_reads records (pairs if paired)."""
-    rng = np.random.default_rng(seed)
-    genome = rng.integers(0, 4, size=genome_len, dtype=np.uint8)
+             genome_len: int = 5_000_000, chunk: int = 250_000, progress=None, workers: int = 1):
+    """Return (r1_bytes, r2_bytes or None) of n_reads records (pairs if paired).
+    workers > 1 draws the chunks in that many spawned processes (same bytes)."""
+    jobs = [(seed, ci, s, min(chunk, n_reads - s), read_len, paired, genome_len)
+            for ci, s in enumerate(range(0, n_reads, chunk))]
     out1: list[bytes] = []
     out2: list[bytes] = []
-    ar = np.arange(read_len)
-    for s in range(0, n_reads, chunk):
-        n = min(chunk, n_reads - s)
-        start = rng.integers(0, genome_len - max(450, read_len), size=n)
-        ins = rng.integers(250, 450, size=n)
-        r1 = genome[start[:, None] + ar[None, :]]
-        sub = rng.random((n, read_len)) < 0.002
-        r1 = np.where(sub, (r1 + rng.integers(1, 4, size=(n, read_len), dtype=np.uint8)) % 4, r1)
-        s1 = _BASES[r1]
-        q1 = _QUALS[rng.choice(3, size=(n, read_len), p=[0.90, 0.07, 0.03])]
-        nmask = rng.random((n, read_len)) < 0.0005
-        s1 = np.where(nmask, np.uint8(ord("N")), s1)
-        q1 = np.where(nmask, np.uint8(ord("#")), q1)
-        out1.append(_records(_headers(rng, s, n, 1), s1, q1))
-        if paired:
-            end = start + ins
-            r2 = genome[(end - read_len)[:, None] + ar[None, :]][:, ::-1]
-            sub2 = rng.random((n, read_len)) < 0.002
-            r2 = np.where(sub2, (r2 + rng.integers(1, 4, size=(n, read_len), dtype=np.uint8)) % 4, r2)
-            s2 = _COMP[r2]
-            q2 = _QUALS[rng.choice(3, size=(n, read_len), p=[0.90, 0.07, 0.03])]
-            out2.append(_records(_headers(rng, s, n, 2), s2, q2))
-        if progress is not None and (s // chunk) % 40 == 39:
-            progress(s + n)
+    if workers > 1 and len(jobs) > 1:
+        import multiprocessing as mp
+        with mp.get_context("spawn").Pool(min(workers, len(jobs))) as pool:
+            for k, (a, b) in enumerate(pool.imap(_chunk, jobs)):
+                out1.append(a)
+                if paired:
+                    out2.append(b)
+                if progress is not None and k % 40 == 39:
+                    progress(jobs[k][2] + jobs[k][3])
+    else:
+        for k, job in enumerate(jobs):
+            a, b = _chunk(job)
+            out1.append(a)
+            if paired:
+                out2.append(b)
+            if progress is not None and k % 40 == 39:
+                progress(job[2] + job[3])
     return b"".join(out1), (b"".join(out2) if paired else None)
 
 

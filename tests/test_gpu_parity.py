@@ -268,3 +268,81 @@ def test_cli_multi_device_gather(tmp_path, test_pair):
     tmpl = fq.analyze_ids(blocks[0], False)
     cfg = fq.Config(bin_mode=int(tmpl[0]))
     assert one == fq.arc_archive(_oracle_outs(blocks, cfg), blocks, "m_1.fq", "m_2.fq", tmpl, cfg)
+
+
+@pytest.fixture(scope="module")
+def pe_full():
+    """Two full 50 MiB 150 bp PE blocks (~73k mate pairs each, Illumina headers:
+    tokenizer path) plus a partial third: configs[2]'s unit of work."""
+    a, b = synth.generate(150_000, paired=True, seed=31)
+    blocks = fq.blocks_from_fastq(a, b)
+    assert len(blocks) == 3 and blocks[0].text_bytes > 50_000_000 and blocks[0].nreads > 140_000
+    tmpl = fq.analyze_ids(blocks[0], False)
+    assert int(tmpl[0]) == 0   # Illumina-style mate IDs: the name tokenizer
+    return blocks
+
+
+def test_full_size_pe_block(enc, pe_full):
+    """One full 50 MiB PE block, alone, equal to the oracle and decoding back."""
+    got = _check(enc, pe_full[:1], fq.Config())
+    b = pe_full[0]
+    names, nl, seq, sl, qual, ok = oracle_py.decode_block(got[0], b.nreads, b.names.size, b.seq.size)
+    assert ok and np.array_equal(names, b.names) and np.array_equal(seq, b.seq) and np.array_equal(qual, b.qual)
+
+
+def test_two_block_pe_batch(enc, pe_full):
+    """A 2-block PE batch (both full size) and the 3-block batch with its short tail."""
+    _check(enc, pe_full[:2], fq.Config())
+    _check(enc, pe_full, fq.Config())
+
+
+@pytest.mark.parametrize("slevel", [5, 6, 8])
+def test_high_order_seq_model(enc, slevel):
+    """Slevel 5/6/8: k = 12/13/15 (2^24..2^30 contexts; 30-bit sort keys at k = 15),
+    the README's "16-order" model as the binary builds it (ctor@0x42f63e)."""
+    a, b = synth.generate(6000, paired=True, seed=40 + slevel)
+    blocks = fq.blocks_from_fastq(a, b, 1_000_000)
+    _check(enc, blocks, fq.Config(slevel=slevel))
+    blocks = fq.blocks_from_fastq(_long_read_fastq(50 + slevel, 400))
+    _check(enc, blocks, fq.Config(slevel=slevel, qlevel=3))
+
+
+def test_full_size_block_slevel8(enc, pe_full):
+    """A full 50 MiB PE block at Slevel 8 (k = 15: 4 GiB of BASE_MODEL tables in
+    the oracle; context runs of ~1 symbol on the GPU)."""
+    _check(enc, pe_full[:1], fq.Config(slevel=8))
+
+
+def test_resident_inputs_concurrent_contexts(pe_full):
+    """sa_input_create / sa_run_input: two resident batches encoded by two contexts
+    from two host threads at once (the bench's pipeline) == the oracle."""
+    import threading
+    a, b = synth.generate(20000, paired=True, seed=77)
+    b1 = fq.blocks_from_fastq(a, b, 2_000_000)
+    b2 = pe_full[2:]
+    cfg = fq.Config()
+    want = {0: _oracle_outs(b1, cfg), 1: _oracle_outs(b2, cfg)}
+    inputs = [fq.Input(b1, 0), fq.Input(b2, 0)]
+    encs = [fq.Encoder(0), fq.Encoder(0)]
+    got, errs = {}, []
+
+    def work(i):
+        try:
+            for rep in range(3):
+                encs[i].run_input(inputs[(i + rep) % 2], cfg)
+                got[(i, rep)] = ((i + rep) % 2, encs[i].fetch())
+        except Exception as e:
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in encs:
+        e.close()
+    for i in inputs:
+        i.close()
+    assert not errs, errs
+    for (i, rep), (which, outs) in got.items():
+        assert outs == want[which], (i, rep)

@@ -1,45 +1,19 @@
-"""Multi-GPU path on the CPU: world_size-2 gloo ranks shard blocks round-robin,
-encode their share and gather them back in order (fastqueeze_amd/shard.py).
-Without a GPU the ranks encode with the CPU restatement (test infrastructure);
-the sharding and the gather are the code bench.py / a multi-GPU host runs."""
+"""Multi-GPU path on the CPU: `bench.py --gpus 2 --dry-run` launches two ranks
+itself (its --gpus launcher), the ranks join a gloo group, deal the global
+batches with fastqueeze_amd.shard.shard_indices, encode their share and gather
+the per-block digests back in global order with shard.gather_blocks -- the code
+the GPU bench runs, with the CPU restatement standing in for the GPU encoder
+(dry run only; the product path has no CPU encoder)."""
+import json
 import os
-import socket
+import subprocess
+import sys
 
 import pytest
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
-import oracle_py
-import synth
+from fastqueeze_amd.shard import shard_indices
 
-from fastqueeze_amd import blocks_from_fastq
-from fastqueeze_amd.shard import encode_shard, gather_blocks, shard_indices
-
-BLOCK = 300_000
-
-
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _oracle_encode(bl):
-    return [oracle_py.encode_block(b, 3, 2, 1, 0) for b in bl]
-
-
-def _rank(rank, world, port, text, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        blocks = blocks_from_fastq(text, None, BLOCK)
-        local = encode_shard(blocks, rank, world, _oracle_encode)
-        assert [i for i, _ in local] == shard_indices(len(blocks), rank, world)
-        out = gather_blocks(local, len(blocks))
-        q.put((rank, [len(b) for b in out], b"".join(out)))
-    finally:
-        dist.destroy_process_group()
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_shard_indices_cover_every_block_once():
@@ -51,21 +25,20 @@ def test_shard_indices_cover_every_block_once():
         shard_indices(4, 2, 2)
 
 
-def test_two_gloo_ranks_gather_blocks_in_order():
-    text, _ = synth.generate(4000, seed=21)
-    blocks = blocks_from_fastq(text, None, BLOCK)
-    assert len(blocks) >= 3
-    want = _oracle_encode(blocks)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, text, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for rank, lens, blob in res:
-        assert lens == [len(w) for w in want], rank
-        assert blob == b"".join(want), rank
+def _bench(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--pairs", "2000", *args],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_launches_two_gloo_ranks_and_gathers_in_order():
+    one = _bench("--gpus", "1", "--batches", "4")
+    two = _bench("--gpus", "2", "--batches", "2")
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert one["batches"] == two["batches"] == 4
+    # the same global batches, encoded on two ranks and gathered in order
+    assert one["blocks_digest"] == two["blocks_digest"]
