@@ -61,8 +61,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--contexts", type=int, default=2, help="encoder contexts (pipeline lanes) per GPU")
+    ap.add_argument("--contexts", type=int, default=3, help="encoder contexts (pipeline lanes) per GPU")
     ap.add_argument("--batches", type=int, default=4, help="distinct resident batches per GPU")
+    ap.add_argument("--no-share", action="store_true", help="contexts with their own front scratch (A/B)")
     ap.add_argument("--pairs", type=int, default=5_000_000, help="mate pairs per batch (reads with --se)")
     ap.add_argument("--se", action="store_true", help="single-end reads (configs[1] shape) instead of PE")
     ap.add_argument("--read-len", type=int, default=150)
@@ -72,6 +73,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (each leg)")
     ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: the CPU share)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--e2e-batches", type=int, default=1,
+                    help="batches written to disk for the end-to-end seqarc_amd -c run (0: skip)")
+    ap.add_argument("--e2e-dir", default=os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
@@ -121,14 +125,51 @@ def launch_ranks(argv: list[str], n: int) -> int:
     return rc
 
 
-def make_batch(gid: int, args, workers: int):
+def make_batch(gid: int, args, workers: int, files=None):
     """Global batch `gid`: its FASTQ (seed 1000 + gid), cut and parsed as the
-    reference's reader does.  Returns the parsed blocks."""
+    reference's reader does.  Returns the parsed blocks; `files` (paths) get the
+    FASTQ text appended (the end-to-end run's input)."""
     import synth
     import fastqueeze_amd as fq
     paired = not args.se
     t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers)
+    if files:
+        for path, t in zip(files, (t1, t2)):
+            if t is not None:
+                with open(path, "ab") as f:
+                    f.write(t)
     return fq.blocks_from_fastq(t1, t2, args.block_size)
+
+
+def end_to_end(args, files, contexts, expect: bytes, nblocks: int, threads: int):
+    """`seqarc_amd -c` (the streaming reader / parser / encoder / writer
+    pipeline) on the FASTQ files on disk: wall time of the whole process, and
+    its own clock (device init to the closed .arc).  The archive's blocks must
+    be the bench's blocks of the same input, byte for byte."""
+    from fastqueeze_amd import build
+    out = os.path.join(os.path.dirname(files[0]), "e2e")
+    batch = max(1, -(-nblocks // (2 * contexts)))   # every context gets >= 2 batches
+    cmd = [build.CLI, "-c", "-f", "-t", str(threads), "-1", files[0]] + (["-2", files[1]] if len(files) > 1 else []) \
+        + ["-o", out, "--contexts", str(contexts), "--batch", str(batch), "--slevel", str(args.slevel),
+           "--qlevel", str(args.qlevel)]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise SystemExit(f"end-to-end run failed: {r.stderr[-2000:]}")
+    in_bytes = sum(os.path.getsize(f) for f in files)
+    with open(out + ".arc", "rb") as f:
+        arc = f.read()
+    same = arc[16:16 + len(expect)] == expect if expect else None
+    clock = None
+    for ln in r.stderr.splitlines():
+        if "MB/s" in ln:
+            clock = float(ln.rsplit(",", 1)[1].split()[0])
+    os.remove(out + ".arc")
+    return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
+            "cli_clock_mb_s": clock, "fastq_bytes": in_bytes, "contexts": contexts, "batch_blocks": batch,
+            "parse_threads": threads, "first_batch_blocks_identical": same,
+            "command": "seqarc_amd -c -1 r1.fq -2 r2.fq (FASTQ on disk, page cache warm)"}
 
 
 def stream_sizes(block: bytes) -> dict:
@@ -161,6 +202,26 @@ class Workers:
     def __init__(self, encoders, inputs, cfg):
         self.encs, self.inputs, self.cfg = encoders, inputs, cfg
         self.phases, self.restarts, self.stats = [], 0, (0, 0)
+
+    def warm_all(self):
+        """Every context encodes every batch once (its buffers reach the size of
+        the largest batch: no allocation, hence no device-wide hipFree, later)."""
+        errs = []
+
+        def worker(enc):
+            try:
+                for inp in self.inputs:
+                    enc.run_input(inp, self.cfg)
+            except Exception as e:
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(e,)) for e in self.encs]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
 
     def run(self, nsteps: int, record: bool):
         lock = threading.Lock()
@@ -230,8 +291,15 @@ def main():
     gids = shard_indices(world * args.batches, rank, world)
     t0 = time.time()
     batches = []
-    for g in gids:
-        batches.append(make_batch(g, args, workers))
+    e2e_files = None
+    if args.e2e_batches > 0 and not args.dry_run:
+        d = os.path.join(args.e2e_dir, f"seqarc_bench_{os.getpid()}")
+        os.makedirs(d, exist_ok=True)
+        e2e_files = [os.path.join(d, "r1.fq")] + ([] if args.se else [os.path.join(d, "r2.fq")])
+        for f in e2e_files:
+            open(f, "wb").close()
+    for k, g in enumerate(gids):
+        batches.append(make_batch(g, args, workers, e2e_files if e2e_files and k < args.e2e_batches else None))
         log(f"[rank {rank}] batch {g}: {len(batches[-1])} blocks, "
             f"{sum(b.text_bytes for b in batches[-1]) / 1e9:.2f} GB ({time.time() - t0:.1f}s)")
     tmpl = fq.analyze_ids(batches[0][0], args.se)
@@ -256,11 +324,14 @@ def main():
     keep = {"verify": batches[0], "cpu": batches[0]}
     inputs = [fq.Input(bl, local) for bl in batches]
     del batches
-    encs = [fq.Encoder(local) for _ in range(args.contexts)]
+    encs = [fq.Encoder(local)]
+    for _ in range(args.contexts - 1):   # one front scratch per GPU, fronts one at a time
+        encs.append(fq.Encoder(local, share_with=None if args.no_share else encs[0]))
     for e in encs:
         e.set_timing(True)
     W = Workers(encs, inputs, cfg)
-    W.run(max(args.warmup, args.contexts), record=False)
+    W.warm_all()
+    W.run(args.warmup, record=False)
     barrier()
     torch.cuda.synchronize(local)
     ts = time.perf_counter()
@@ -317,6 +388,7 @@ def main():
             traffic = json.load(f).get(dom)
     max_syms, all_syms = W.stats
     hbm_per_ctx = [e.device_bytes() for e in encs]
+    hbm_front = sorted({e.front_bytes() for e in encs})
 
     cpu = cpu_mt = None
     if rank == 0 and args.cpu_seconds > 0:
@@ -388,16 +460,34 @@ def main():
         "phase_ms": {k: round(v, 2) for k, v in ph.items()},
         "coder_restarts": W.restarts,
         "hbm_bytes_per_context": hbm_per_ctx,
+        "hbm_bytes_front_scratch": hbm_front,
         "checksum": hashlib.sha256(b"".join(digs)).hexdigest(),
         "cpu_baseline": cpu,
         "cpu_baseline_threads": cpu_mt,
     }
-    if rank == 0:
-        print(json.dumps(res), flush=True)
     for e in encs:
         e.close()
     for i in inputs:
         i.close()
+    if e2e_files:
+        # the whole host path: the CLI reads the FASTQ from disk (HBM of the bench's
+        # contexts released above); per rank, then max over ranks
+        barrier()
+        expect = b"".join(outs) if args.e2e_batches == 1 else None
+        e2e = end_to_end(args, e2e_files, args.contexts, expect, len(keep["verify"]) * args.e2e_batches,
+                         max(1, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
+        for f in e2e_files:
+            os.remove(f)
+        os.rmdir(os.path.dirname(e2e_files[0]))
+        if world > 1:
+            t = torch.tensor([e2e["wall_s"], float(e2e["fastq_bytes"])], dtype=torch.float64)
+            tm = t.clone()
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            e2e["value"] = round(float(t[1]) / float(tm[0]) / 1e6, 1)
+        res["end_to_end"] = e2e
+    if rank == 0:
+        print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

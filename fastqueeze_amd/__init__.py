@@ -85,7 +85,8 @@ def load_library(path: str | None = None):
         "sa_parse_se": ([P, U64, P, P, P, P, P], I64), "sa_parse_pe": ([P, U64, P, U64, P, P, P, P, P], I64),
         "sa_analyze_ids": ([P, I32, P], I32),
         "sa_code_records": ([P, I32, P, P, P, P, P, U64, P], I32), "sa_coder_restarts": ([P], C.c_uint32),
-        "sa_stream_stats": ([P, P, P], None), "sa_device_bytes": ([P], U64),
+        "sa_stream_stats": ([P, P, P], None), "sa_device_bytes": ([P], U64), "sa_front_bytes": ([P], U64),
+        "sa_create_shared": ([I32, P], P),
         "sa_input_create": ([I32, P, I32], P), "sa_input_destroy": ([P], None), "sa_run_input": ([P, P, P], I32),
         "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
         "sa_decode_block": ([P, U64, P, P, I32, P], I64),
@@ -229,9 +230,12 @@ class Encoder:
 
     PHASES = 11
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, share_with: "Encoder | None" = None):
+        """share_with: another Encoder of the same device whose front scratch this
+        one shares (sa_create_shared): their fronts then run one at a time."""
         self._lib = load_library()
-        self._ctx = self._lib.sa_create(device)
+        self._ctx = (self._lib.sa_create_shared(device, share_with._ctx) if share_with is not None
+                     else self._lib.sa_create(device))
         if not self._ctx:
             raise SeqArcError(f"no usable gfx950 device {device} (the HIP path is the only path)")
         self._staged: list[Block] = []
@@ -308,6 +312,9 @@ class Encoder:
 
     def device_bytes(self) -> int:
         return int(self._lib.sa_device_bytes(self._ctx))
+
+    def front_bytes(self) -> int:
+        return int(self._lib.sa_front_bytes(self._ctx))
 
     def encode(self, blocks: list[Block], cfg: Config) -> list[bytes]:
         self.stage(blocks)

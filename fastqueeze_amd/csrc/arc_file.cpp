@@ -124,7 +124,7 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     uint8_t* pbeg = o.p;
     field_bool(o, 1, 1);                        // param+0x3: no reference index
     field_bool(o, 2, in->bare_plus);            // param+0x4: '+' lines carry no ID (getFirstLine@0x431eb0)
-    field_bool(o, 3, 0);                        // param+0x5
+    field_bool(o, 3, in->paired ? 0 : 1);       // param+0x5: single-end (set by -1, cleared by -2: parseOptFromCmd@0x40b460)
     field_bool(o, 4, in->gz1);                  // param+0x6: getFileType@0x40d9f0 of input 1
     field_bool(o, 5, 1);                        // param+0x7 (cleared by -q)
     field_bool(o, 6, 0);                        // param+0x8: usemodel

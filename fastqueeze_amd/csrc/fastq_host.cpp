@@ -110,6 +110,42 @@ int64_t sa_cut_pe(const uint8_t* t1, uint64_t len1, const uint8_t* t2, uint64_t 
     }
 }
 
+// Streaming forms of the two cuts: the next block of a window of the input.
+int64_t sa_cut_next_se(const uint8_t* win, uint64_t avail, int eof, uint64_t bs, const uint8_t* first,
+                       uint64_t flen)
+{
+    if (!win || bs == 0 || !first || flen == 0) return -1;
+    if (avail < bs) return eof ? (int64_t)avail : -1;   // the short read of the file's last buffer
+    const int64_t e = end_pos(win, bs, (int64_t)(bs - flen), first, (size_t)flen);
+    return e <= 0 ? -1 : e + 1;
+}
+
+int sa_cut_next_pe(const uint8_t* w1, uint64_t avail1, int eof1, const uint8_t* w2, uint64_t avail2, int eof2,
+                   uint64_t bs, const uint8_t* first, uint64_t flen, uint64_t* end1, uint64_t* end2)
+{
+    if (!w1 || !w2 || !end1 || !end2 || bs < 2 || !first || flen == 0) return -1;
+    const uint64_t half = (uint64_t)((uint32_t)bs >> 1);
+    if ((avail1 < half && !eof1) || (avail2 < half && !eof2)) return -1;   // the caller reads more first
+    const uint64_t a1 = std::min<uint64_t>(avail1, half), a2 = std::min<uint64_t>(avail2, half);
+    if (a1 < half && a2 < half) {   // both reads short: the last block takes the rest
+        *end1 = avail1;
+        *end2 = avail2;
+        return 0;
+    }
+    std::vector<uint64_t> nl1, nl2;
+    newline_positions(w1, a1, nl1);
+    newline_positions(w2, a2, nl2);
+    const size_t k = std::min(nl1.size(), nl2.size());
+    if (k < 2) return -1;
+    int64_t j = (int64_t)k - 2;
+    const int64_t pos = end_pos(w1, a1, (int64_t)nl1[(size_t)j], first, (size_t)flen);
+    while (j >= 0 && (int64_t)nl1[(size_t)j] != pos) --j;
+    if (j < 0) return -1;   // the reference spins forever here (defect i)
+    *end1 = nl1[(size_t)j] + 1;
+    *end2 = nl2[(size_t)j] + 1;
+    return 0;
+}
+
 int64_t sa_parse_se(const uint8_t* t, uint64_t len, uint8_t* names, uint16_t* nlens, uint8_t* seq,
                     int32_t* slens, uint8_t* qual)
 {

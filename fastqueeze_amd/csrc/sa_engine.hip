@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,37 @@ enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX,
 
 }  // namespace
 
+// The front scratch of a device: buffers only the throughput-bound front of a
+// batch uses (count columns, name prefix/suffix, the SEQ sort's key/value ping
+// pong, one half of the AUX sort's, histograms, run lists of the front), shared
+// by the contexts of one device that are created together (sa_create_shared).
+// Their fronts run one at a time -- they are throughput-bound, two at once only
+// slow each other -- while each context's latency-bound part (long model runs,
+// range-coder chains, MD5) overlaps the next context's front.  `mu` is held
+// while a context enqueues its front; its stream first waits for `ev_free`,
+// recorded after the previous front's last kernel.
+struct FrontShare {
+    int refs = 0;
+    std::mutex mu;
+    hipEvent_t ev_free = nullptr;
+    bool have_ev = false;
+    DBuf d_counts, d_name_p, d_name_s, d_maxlen, d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
+    DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux, d_seq_longs, d_nseq_long, d_short_at;
+    std::vector<DBuf*> buffers()
+    {
+        return {&d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1],
+                &d_auxs_k, &d_auxs_v, &d_hist_seq, &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux,
+                &d_seq_longs, &d_nseq_long, &d_short_at};
+    }
+    uint64_t held_bytes()
+    {
+        uint64_t h = 0;
+        for (DBuf* b : buffers()) h += b->cap;
+        return h;
+    }
+};
+std::mutex g_share_mu;   // FrontShare::refs
+
 // A batch of parsed blocks resident in HBM (names, bases, qualities and the
 // per-read offsets), read-only while it is encoded: any number of contexts of
 // its device may encode it, one after the other or concurrently.
@@ -79,11 +111,18 @@ struct sa_ctx {
     uint32_t long_lds = 0;
     bool serial_seq = false;
     uint32_t pf_segs = PF_SEGS;
+    uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
+    // pass-R placement (k_coder_rv): four chains per workgroup, one per SIMD, and
+    // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
+    // SA_CODER_LDS)
+    uint32_t coder_waves = 4;
+    uint32_t coder_lds = 82 * 1024;
+    uint32_t coder_vgpr = 1;   // pass R fed through VGPRs (k_coder_rv); SA_CODER_VGPR=0: the scalar-load pass
     std::string err;
     bool timing = false;
     uint32_t coder_restarts = 0;
     uint64_t max_stream_syms = 0, total_stream_syms = 0;
-    hipEvent_t ev_beg[PH_N], ev_end[PH_N];
+    hipEvent_t ev_beg[PH_N] = {}, ev_end[PH_N] = {};
     float ph_ms[PH_N];
 
     // the batch sa_stage uploads (sa_run encodes it); blocks = the working copy
@@ -92,15 +131,15 @@ struct sa_ctx {
     std::vector<DevBlock> blocks;
 
     // work
-    DBuf d_blocks, d_counts, d_totals, d_name_p, d_name_s, d_maxlen, d_err;
-    DBuf d_seq_k[2], d_seq_v[2], d_aux_k[2], d_aux_v[2], d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;
-    DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux;
+    FrontShare* fs = nullptr;   // front scratch, possibly shared with other contexts of the device
+    DBuf d_blocks, d_totals, d_err;
+    DBuf d_auxp_k, d_auxp_v, d_prs_seq, d_prs_aux, d_cum_seq, d_cum_aux;   // d_auxp: the sorted AUX keys/values
+    DBuf d_task_ends;
     DBuf d_tasks, d_out_len, d_payload, d_md5tasks, d_digests, d_asm, d_asm_copies, d_task_out_base, d_final, d_final_len;
-    DBuf d_longs, d_huge_sorted, d_nlong, d_seq_longs, d_nseq_long, d_short_at;
+    DBuf d_longs, d_huge_sorted, d_nlong;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
     DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry;   // -l (rblock)
-    int seq_sorted_buf = 0, aux_sorted_buf = 0;
 
     // last run
     std::vector<uint64_t> final_base, final_len;
@@ -108,25 +147,30 @@ struct sa_ctx {
 
     std::vector<DBuf*> work_buffers()
     {
-        return {&d_blocks, &d_counts, &d_totals, &d_name_p, &d_name_s, &d_maxlen, &d_err,
-                 &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_aux_k[0], &d_aux_k[1],
-                 &d_aux_v[0], &d_aux_v[1], &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux, &d_hist_seq,
-                 &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_tasks, &d_out_len,
-                 &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base, &d_final,
-                 &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_short_at, &d_seq_longs, &d_nseq_long, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                 &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry,
-                 &d_first_sq, &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1],
-                 &d_list_gbase[1], &d_list_run[1]};
+        return {&d_blocks, &d_totals, &d_err, &d_auxp_k, &d_auxp_v, &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux,
+                &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
+                &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_first_sq,
+                &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1]};
     }
     uint64_t held_bytes()
     {
         uint64_t h = own.d_names.cap + own.d_seq.cap + own.d_qual.cap;
         for (DBuf* b : work_buffers()) h += b->cap;
-        return h;
+        return h;   // (the front scratch: front_bytes)
     }
 
     ~sa_ctx()
     {
+        if (fs) {
+            std::lock_guard<std::mutex> g(g_share_mu);
+            if (--fs->refs == 0) {
+                for (DBuf* b : fs->buffers()) b->release();
+                if (fs->ev_free) (void)hipEventDestroy(fs->ev_free);
+                delete fs;
+            }
+            fs = nullptr;
+        }
         std::vector<DBuf*> all = work_buffers();
         for (DBuf* b : all) b->release();
         for (int i = 0; i < PH_N; i++) {
@@ -155,7 +199,7 @@ namespace {
 
 // sorts keys by bits [lo, hi) in 8-bit digits (bits below lo ride along)
 int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
-             DBuf* keys, DBuf* vals, int lo, int hi, int& result_buf)
+             DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf)
 {
     result_buf = 0;
     if (plan.total == 0 || hi <= lo) return 0;
@@ -169,11 +213,11 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     int cur = 0;
     for (int shift = lo; shift < hi; shift += 8) {
         hipLaunchKernelGGL(k_sort_hist, dim3((sv.ntiles + HIST_TILES - 1) / HIST_TILES), dim3(SORT_THREADS), 0, st, sv,
-                           keys[cur].as<uint32_t>(), (uint32_t)shift);
+                           keys[cur]->as<uint32_t>(), (uint32_t)shift);
         hipLaunchKernelGGL(k_sort_scan, dim3(sv.nsegs), dim3(1024), 0, st, sv);
         hipLaunchKernelGGL(k_sort_scatter, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,
-                           keys[cur].as<uint32_t>(), vals[cur].as<uint32_t>(), keys[cur ^ 1].as<uint32_t>(),
-                           vals[cur ^ 1].as<uint32_t>(), (uint32_t)shift);
+                           keys[cur]->as<uint32_t>(), vals[cur]->as<uint32_t>(), keys[cur ^ 1]->as<uint32_t>(),
+                           vals[cur ^ 1]->as<uint32_t>(), (uint32_t)shift);
         cur ^= 1;
     }
     SA_CHECK(c, hipGetLastError());
@@ -224,17 +268,6 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     return 0;
 }
 
-// Range coder driver (DESIGN.md "Coder").  A group = a contiguous range of
-// tasks coded on one stream: pass R, L1, L2, L3.  After all groups of a round
-// finish, the streams whose exact coding squeezed before their last segment
-// restart after that segment from the state L3 computed (on the first group's
-// stream), until none does.
-struct CoderGroup {
-    hipStream_t st;
-    uint32_t t0, t1;
-    int ph_r, ph_l;   // phase slots for the first round (-1: untimed)
-};
-
 int coder_buffers(sa_ctx* c, size_t ntasks, uint64_t total_segs, CoderView& cv)
 {
     const uint64_t nsegs = std::max<uint64_t>(total_segs, 1);
@@ -279,57 +312,92 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
 {
     if (!tl.count) return;
     if (ph >= 0) ev_begin(c, ph, st);
-    hipLaunchKernelGGL(k_coder_r, dim3(tl.count), dim3(64), 0, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r,
-                       c->d_err.as<uint32_t>(), reinterpret_cast<const uint2*>(cv.prs[0]),
-                       reinterpret_cast<const uint2*>(cv.prs[1]), c->pf_segs);
+    if (c->coder_vgpr) {
+        hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves),
+                           dim3(64 * c->coder_waves), c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r,
+                           c->d_err.as<uint32_t>(), c->chain_prio);
+        if (ph >= 0) ev_finish(c, ph, st);
+        return;
+    }
+    hipLaunchKernelGGL(k_coder_r, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
+                       c->coder_lds, st,
+                       cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
+                       reinterpret_cast<const uint2*>(cv.prs[0]), reinterpret_cast<const uint2*>(cv.prs[1]), c->pf_segs,
+                       c->chain_prio);
     if (ph >= 0) ev_finish(c, ph, st);
 }
 
-void coder_launch_l(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv, int ph)
+void coder_launch_l12(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv)
 {
     if (!tl.count) return;
     const uint32_t lgrid = (uint32_t)((tl.total_segs + 255) / 256);
-    if (ph >= 0) ev_begin(c, ph, st);
     hipLaunchKernelGGL(k_coder_l1, dim3(lgrid), dim3(256), 0, st, cv, tl);
     hipLaunchKernelGGL(k_coder_l2, dim3(tl.count), dim3(L2_THREADS), 0, st, cv, tl);
-    hipLaunchKernelGGL(k_coder_l3, dim3(lgrid), dim3(256), 0, st, cv, tl);
-    if (ph >= 0) ev_finish(c, ph, st);
 }
 
-// Runs pass R of every group concurrently (each group's stream must already be
-// ordered after that group's records), then -- once every pass R is done, so
-// that the parallel L passes never share the GPU with a latency-bound chain --
-// the L passes of every group; then the restarts.  On return every stream of
-// every group is coded and all group streams are idle.
-int coder_run(sa_ctx* c, const std::vector<CoderTask>& tasks, const CoderView& cv, const CoderGroup* groups,
-              int ngroups, hipEvent_t before_l = nullptr)
+void coder_launch_l3(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv)
 {
+    if (!tl.count) return;
+    const uint32_t lgrid = (uint32_t)((tl.total_segs + 255) / 256);
+    hipLaunchKernelGGL(k_coder_l3, dim3(lgrid), dim3(256), 0, st, cv, tl);
+}
+
+// Range coder driver (DESIGN.md "Coder"): pass R of every listed chain (on st,
+// longest first), then -- once `before_l` (the long model runs) is done -- L1
+// and L2.  With `exact`, the payload arena is then sized from the streams'
+// real byte counts (k_task_ends; a stream's out_cap gets 1/64 + 4 KiB of slack
+// for squeeze restarts) instead of the 2-bytes-per-symbol bound the plan
+// carries: tasks' out_base / out_cap, d_tasks and the payload are set here.
+// Then L3, and the streams whose exact coding squeezed before their last
+// segment restart after that segment from the state L3 computed, until none
+// does.  out_len: every stream's bytes.  Returns 0, -1 on error, 2 when a
+// stream outgrew its slack (the caller re-runs with exact = false).
+int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream_t st, int ph_r, int ph_l,
+              hipEvent_t before_l, bool exact, std::vector<uint32_t>& out_len, uint64_t& payload_bytes)
+{
+    out_len.assign(tasks.size(), 0);
     if (tasks.empty()) return 0;
     c->coder_restarts = 0;
-    std::vector<uint64_t> gb[2];
-    TaskList tl[2];
-    for (int g = 0; g < ngroups; g++) {
+    std::vector<uint64_t> gb;
+    TaskList tl;
+    {
         std::vector<uint32_t> ids;
-        std::vector<CoderRun> runs;
-        for (uint32_t t = groups[g].t0; t < groups[g].t1; t++) ids.push_back(t);
-        // longest streams first: workgroups are dealt round-robin over the XCDs and
-        // their CUs, so the long chains get CUs of their own
+        for (uint32_t t = 0; t < (uint32_t)tasks.size(); t++) ids.push_back(t);
+        // longest streams first: a pass-R workgroup's chains are of similar length
         std::stable_sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t b) { return tasks[a].n > tasks[b].n; });
-        runs.assign(ids.size(), CoderRun{0ull, 0xffffffffu, 0u, 0u, 0u});
-        if (coder_list(c, groups[g].st, g, tasks, ids, runs, gb[g], tl[g])) return -1;
-        coder_launch_r(c, groups[g].st, tl[g], cv, c->timing ? groups[g].ph_r : -1);
-        SA_CHECK(c, hipEventRecord(c->ev_r[g], groups[g].st));
+        std::vector<CoderRun> runs(ids.size(), CoderRun{0ull, 0xffffffffu, 0u, 0u, 0u});
+        if (coder_list(c, st, 0, tasks, ids, runs, gb, tl)) return -1;
     }
-    for (int g = 0; g < ngroups; g++) {
-        for (int h = 0; h < ngroups; h++)
-            if (h != g) SA_CHECK(c, hipStreamWaitEvent(groups[g].st, c->ev_r[h], 0));
-        if (before_l) SA_CHECK(c, hipStreamWaitEvent(groups[g].st, before_l, 0));
-        coder_launch_l(c, groups[g].st, tl[g], cv, c->timing ? groups[g].ph_l : -1);
-        SA_CHECK(c, hipGetLastError());
+    coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1);
+    if (before_l) SA_CHECK(c, hipStreamWaitEvent(st, before_l, 0));
+    if (c->timing && ph_l >= 0) ev_begin(c, ph_l, st);
+    coder_launch_l12(c, st, tl, cv);
+    SA_CHECK(c, hipGetLastError());
+    if (exact) {
+        SA_CHECK(c, c->d_task_ends.ensure(4 * tasks.size()));
+        hipLaunchKernelGGL(k_task_ends, dim3((tl.count + 255) / 256), dim3(256), 0, st, cv, tl,
+                           c->d_task_ends.as<uint32_t>());
+        std::vector<uint32_t> ends(tasks.size());
+        SA_CHECK(c, hipMemcpyAsync(ends.data(), c->d_task_ends.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipStreamSynchronize(st));
+        uint64_t payload = 0, slack = 4096;
+        if (const char* e = std::getenv("SA_PAYLOAD_SLACK")) slack = std::strtoull(e, nullptr, 10);   // (tests)
+        for (size_t t = 0; t < tasks.size(); t++) {
+            const uint64_t cap = (uint64_t)ends[t] + ends[t] / 64 + slack;
+            tasks[t].out_cap = (uint32_t)std::min<uint64_t>(cap, tasks[t].out_cap);
+            tasks[t].out_base = payload;
+            payload = align_up(payload + tasks[t].out_cap, 16);
+        }
+        payload_bytes = payload;
+        SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
+        cv.out = c->d_payload.as<uint8_t>();
+        SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice,
+                                   st));
     }
-    for (int g = 0; g < ngroups; g++) SA_CHECK(c, hipStreamSynchronize(groups[g].st));
-    hipStream_t st = groups[0].st;
-    std::vector<uint32_t> first_sq(tasks.size()), out_len(tasks.size());
+    coder_launch_l3(c, st, tl, cv);
+    if (c->timing && ph_l >= 0) ev_finish(c, ph_l, st);
+    SA_CHECK(c, hipGetLastError());
+    std::vector<uint32_t> first_sq(tasks.size());
     for (int round = 0;; round++) {
         SA_CHECK(c, hipMemcpyAsync(first_sq.data(), cv.first_sq, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
         SA_CHECK(c, hipMemcpyAsync(out_len.data(), cv.out_len, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
@@ -359,13 +427,15 @@ int coder_run(sa_ctx* c, const std::vector<CoderTask>& tasks, const CoderView& c
             return -1;
         }
         c->coder_restarts += (uint32_t)ids.size();
-        if (coder_list(c, st, 0, tasks, ids, runs, gb[0], tl[0])) return -1;
-        coder_launch_r(c, st, tl[0], cv, -1);
-        coder_launch_l(c, st, tl[0], cv, -1);
+        if (coder_list(c, st, 0, tasks, ids, runs, gb, tl)) return -1;
+        coder_launch_r(c, st, tl, cv, -1);
+        coder_launch_l12(c, st, tl, cv);
+        coder_launch_l3(c, st, tl, cv);
         SA_CHECK(c, hipGetLastError());
     }
     for (size_t t = 0; t < tasks.size(); t++)
         if (out_len[t] > tasks[t].out_cap) {
+            if (exact) return 2;
             c->err = "range coder output overflowed its buffer";
             return -1;
         }
@@ -400,6 +470,22 @@ sa_ctx* sa_create(int device)
     }
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     sa_ctx* c = new sa_ctx();
+    // pass-R placement knobs (k_coder_r): waves per workgroup, unused LDS per workgroup
+    if (const char* e = std::getenv("SA_CODER_WAVES")) {
+        const int w = std::atoi(e);
+        c->coder_waves = (w == 1 || w == 2) ? (uint32_t)w : 4u;
+    }
+    if (const char* e = std::getenv("SA_CODER_VGPR")) c->coder_vgpr = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SA_CODER_LDS")) c->coder_lds = (uint32_t)std::min(std::max(std::atoi(e), 0), 160 * 1024);
+    if (c->coder_lds > 64 * 1024 &&
+        (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_r), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess ||
+         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess)) {
+        std::fprintf(stderr, "seqarc_amd: cannot reserve %u B of LDS for pass R\n", c->coder_lds);
+        delete c;
+        return nullptr;
+    }
     c->device = device;
     for (int i = 0; i < PH_N; i++) c->ev_beg[i] = c->ev_end[i] = nullptr;
     // st carries the critical path (AUX symbols -> QUAL coder chain).  While the
@@ -414,6 +500,7 @@ sa_ctx* sa_create(int device)
     c->serial_seq = std::getenv("SA_SERIAL_SEQ") != nullptr;
     const char* ep = std::getenv("SA_PF_SEGS");   // pass R prefetch distance (tuning override)
     c->pf_segs = ep ? (uint32_t)std::min(std::max(std::atoi(ep), 1), 64) : PF_SEGS;
+    if (const char* cp = std::getenv("SA_CHAIN_PRIO")) c->chain_prio = std::atoi(cp) != 0;
     std::vector<uint32_t> m_long((prop.multiProcessorCount + 31) / 32, 0u), m_seq(m_long.size(), 0u);
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
@@ -438,8 +525,31 @@ sa_ctx* sa_create(int device)
             return nullptr;
         }
     }
+    c->fs = new FrontShare();
+    c->fs->refs = 1;
+    if (hipEventCreateWithFlags(&c->fs->ev_free, hipEventDisableTiming) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
     return c;
 }
+
+sa_ctx* sa_create_shared(int device, sa_ctx* peer)
+{
+    if (!peer || peer->device != device) return nullptr;
+    sa_ctx* c = sa_create(device);
+    if (!c) return nullptr;
+    std::lock_guard<std::mutex> g(g_share_mu);
+    FrontShare* own = c->fs;
+    c->fs = peer->fs;
+    c->fs->refs++;
+    for (DBuf* b : own->buffers()) b->release();
+    if (own->ev_free) (void)hipEventDestroy(own->ev_free);
+    delete own;
+    return c;
+}
+
+uint64_t sa_front_bytes(const sa_ctx* c) { return c && c->fs ? c->fs->held_bytes() : 0; }
 
 void sa_destroy(sa_ctx* ctx)
 {
@@ -626,7 +736,14 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
     return sa_run_input(c, &c->own, cfg);
 }
 
-int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
+}  // extern "C"
+
+namespace {
+
+// One encode of a resident batch; exact: the payload arena sized from the
+// streams' real byte counts after L2 (else the 2-bytes-per-symbol bound).
+// Returns 0, -1, or 2 when a stream outgrew its exact cap.
+int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
 {
     if (!c) return -1;
     if (!I || !cfg || I->device != c->device) {
@@ -654,14 +771,17 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     const int aux_bits = cfg->qlevel > 2 ? 21 : 17;
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
+    FrontShare* F = c->fs;
+    // the front (up to the short model runs) holds the device's front scratch
+    std::unique_lock<std::mutex> front_lock(F->mu);
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, c->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
+    SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
     SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
-    SA_CHECK(c, c->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, c->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, c->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, F->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, F->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, F->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
     SA_CHECK(c, c->d_err.ensure(16));
     SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 16, st));
 
@@ -704,24 +824,25 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
                                    c->st2));
         ev_begin(c, PH_MD5, c->st2);
         hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(64), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
-                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>());
+                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>(), c->chain_prio);
         ev_finish(c, PH_MD5, c->st2);
         SA_CHECK(c, hipGetLastError());
         SA_CHECK(c, hipEventRecord(c->ev_md5_done, c->st2));
     } else {
         SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
     }
+    if (F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));   // the previous front is done with it
     ev_begin(c, PH_PREP, st);
     if (lossy && run_rblock(c, cfg->lossy, I->seq_bytes, bv)) return -1;
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
-        hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                           c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
+        hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
+                           F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(), d_err);
         hipLaunchKernelGGL(k_prep_sq, dim3((nr + EMIT_WAVES - 1) / EMIT_WAVES), dim3(64 * EMIT_WAVES), 0, st, bv,
-                           c->d_counts.as<uint32_t>(), d_err);
+                           F->d_counts.as<uint32_t>(), d_err);
     }
-    hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
-                       c->d_totals.as<uint32_t>(), c->d_maxlen.as<uint16_t>());
+    hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, F->d_counts.as<uint32_t>(),
+                       c->d_totals.as<uint32_t>(), F->d_maxlen.as<uint16_t>());
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_PREP, st);
     std::vector<uint32_t> tot((size_t)nbk * NCOL);
@@ -744,28 +865,34 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     }
     const SortPlan& ps = bp.seq;
     const SortPlan& pa = bp.aux;
-    const std::vector<CoderTask>& tasks = bp.tasks;
+    std::vector<CoderTask> tasks = bp.tasks;
     c->max_stream_syms = c->total_stream_syms = 0;
     for (const CoderTask& tk : tasks) {
         c->max_stream_syms = std::max<uint64_t>(c->max_stream_syms, tk.n);
         c->total_stream_syms += tk.n;
     }
-    const std::vector<uint64_t>& task_out_base = bp.task_out_base;
-    const std::vector<AsmBlock>& asmb = bp.asmb;
-    const uint64_t payload = bp.payload_bytes, final_bytes = bp.final_bytes;
-    c->final_base.assign(nbk, 0);
-    for (uint32_t b = 0; b < nbk; b++) c->final_base[b] = asmb[b].out_base;
+    std::vector<AsmBlock> asmb = bp.asmb;
 
     // ---- device buffers ----
     // slack: the replay loops read up to 2 chunks past a run's end, pass R one
     // 16-record chunk past a stream's last full segment
     const uint64_t stot = ps.total + KEY_SLACK, atot = pa.total + KEY_SLACK;
     for (int i = 0; i < 2; i++) {
-        SA_CHECK(c, c->d_seq_k[i].ensure(stot * 4));
-        SA_CHECK(c, c->d_seq_v[i].ensure(stot * 4));
-        SA_CHECK(c, c->d_aux_k[i].ensure(atot * 4));
-        SA_CHECK(c, c->d_aux_v[i].ensure(atot * 4));
+        SA_CHECK(c, F->d_seq_k[i].ensure(stot * 4));
+        SA_CHECK(c, F->d_seq_v[i].ensure(stot * 4));
     }
+    SA_CHECK(c, F->d_auxs_k.ensure(atot * 4));
+    SA_CHECK(c, F->d_auxs_v.ensure(atot * 4));
+    SA_CHECK(c, c->d_auxp_k.ensure(atot * 4));
+    SA_CHECK(c, c->d_auxp_v.ensure(atot * 4));
+    // AUX sort ping-pong: the sorted keys/values must land in this context's
+    // buffers (the long model runs read them after the front scratch is released)
+    const int aux_passes = (aux_bits + 7) / 8;
+    DBuf* akb[2] = {aux_passes % 2 ? &F->d_auxs_k : &c->d_auxp_k, aux_passes % 2 ? &c->d_auxp_k : &F->d_auxs_k};
+    DBuf* avb[2] = {aux_passes % 2 ? &F->d_auxs_v : &c->d_auxp_v, aux_passes % 2 ? &c->d_auxp_v : &F->d_auxs_v};
+    DBuf* skb[2] = {&F->d_seq_k[0], &F->d_seq_k[1]};
+    DBuf* svb[2] = {&F->d_seq_v[0], &F->d_seq_v[1]};
+    int seq_sorted_buf = 0, aux_sorted_buf = 0;
     SA_CHECK(c, c->d_prs_seq.ensure(stot * sizeof(PRec)));
     SA_CHECK(c, c->d_prs_aux.ensure(atot * sizeof(PRec)));
     SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
@@ -773,38 +900,36 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
     SA_CHECK(c, c->d_huge_sorted.ensure((pa.total / HUGE_RUN + 1) * sizeof(LongRun)));
     const uint64_t max_seq_long = ps.total / (SEQ_HALVE_J + 1) + 1;
-    SA_CHECK(c, c->d_seq_longs.ensure(max_seq_long * 8));
-    SA_CHECK(c, c->d_nseq_long.ensure(4));
+    SA_CHECK(c, F->d_seq_longs.ensure(max_seq_long * 8));
+    SA_CHECK(c, F->d_nseq_long.ensure(4));
     SA_CHECK(c, c->d_nlong.ensure(16));   // RunLists counters: short, huge, long, queue
     // at most one run per (block, model) and per symbol
     const uint64_t max_short = std::max<uint64_t>(std::min<uint64_t>(pa.total, (uint64_t)nbk << aux_bits), 1);
-    SA_CHECK(c, c->d_short_at.ensure(max_short * 8));
-    SA_CHECK(c, c->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
-    SA_CHECK(c, c->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
-    SA_CHECK(c, c->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
-    SA_CHECK(c, c->d_segs_aux.ensure(sizeof(SortSeg) * nbk));
-    SA_CHECK(c, c->d_tile_seq.ensure(std::max<size_t>(ps.tile_seg.size(), 1) * 4));
-    SA_CHECK(c, c->d_tile_aux.ensure(std::max<size_t>(pa.tile_seg.size(), 1) * 4));
+    SA_CHECK(c, F->d_short_at.ensure(max_short * 8));
+    SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
+    SA_CHECK(c, F->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
+    SA_CHECK(c, F->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
+    SA_CHECK(c, F->d_segs_aux.ensure(sizeof(SortSeg) * nbk));
+    SA_CHECK(c, F->d_tile_seq.ensure(std::max<size_t>(ps.tile_seg.size(), 1) * 4));
+    SA_CHECK(c, F->d_tile_aux.ensure(std::max<size_t>(pa.tile_seg.size(), 1) * 4));
     SA_CHECK(c, c->d_tasks.ensure(sizeof(CoderTask) * tasks.size()));
     SA_CHECK(c, c->d_out_len.ensure(4 * tasks.size()));
-    SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
+    uint64_t payload = bp.payload_bytes;
+    if (!exact) SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
     SA_CHECK(c, c->d_asm.ensure(sizeof(AsmBlock) * nbk));
     SA_CHECK(c, c->d_asm_copies.ensure(4ull * ASM_COPY_WORDS * nbk));
-    SA_CHECK(c, c->d_task_out_base.ensure(8 * task_out_base.size()));
-    SA_CHECK(c, c->d_final.ensure(std::max<uint64_t>(final_bytes, 16)));
+    SA_CHECK(c, c->d_task_out_base.ensure(8 * tasks.size()));
     SA_CHECK(c, c->d_final_len.ensure(8 * nbk));
 
     SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_segs_seq.p, ps.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_segs_aux.p, pa.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(F->d_segs_seq.p, ps.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(F->d_segs_aux.p, pa.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
     if (!ps.tile_seg.empty())
-        SA_CHECK(c, hipMemcpyAsync(c->d_tile_seq.p, ps.tile_seg.data(), ps.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
+        SA_CHECK(c, hipMemcpyAsync(F->d_tile_seq.p, ps.tile_seg.data(), ps.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
     if (!pa.tile_seg.empty())
-        SA_CHECK(c, hipMemcpyAsync(c->d_tile_aux.p, pa.tile_seg.data(), pa.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
+        SA_CHECK(c, hipMemcpyAsync(F->d_tile_aux.p, pa.tile_seg.data(), pa.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
     SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_asm.p, asmb.data(), sizeof(AsmBlock) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_task_out_base.p, task_out_base.data(), 8 * task_out_base.size(),
-                               hipMemcpyHostToDevice, st));
+
 
     CoderView cv{};
     cv.tasks = c->d_tasks.as<CoderTask>();
@@ -819,29 +944,29 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     // ---- emit (main stream) ----
     ev_begin(c, PH_EMIT, st);
     {
-        const SortView pv_s{c->d_segs_seq.as<SortSeg>(), nullptr, nullptr, ps.total, 0u, nbk};
-        const SortView pv_a{c->d_segs_aux.as<SortSeg>(), nullptr, nullptr, pa.total, 0u, nbk};
+        const SortView pv_s{F->d_segs_seq.as<SortSeg>(), nullptr, nullptr, ps.total, 0u, nbk};
+        const SortView pv_a{F->d_segs_aux.as<SortSeg>(), nullptr, nullptr, pa.total, 0u, nbk};
         const uint32_t pgrid = (uint32_t)(((uint64_t)(nbk + 1) * SORT_TILE + 255) / 256);
-        hipLaunchKernelGGL(k_pad_keys, dim3(pgrid), dim3(256), 0, st, pv_s, c->d_seq_k[0].as<uint32_t>(),
-                           c->d_seq_k[1].as<uint32_t>());
-        hipLaunchKernelGGL(k_pad_keys, dim3(pgrid), dim3(256), 0, st, pv_a, c->d_aux_k[0].as<uint32_t>(),
-                           c->d_aux_k[1].as<uint32_t>());
+        hipLaunchKernelGGL(k_pad_keys, dim3(pgrid), dim3(256), 0, st, pv_s, F->d_seq_k[0].as<uint32_t>(),
+                           F->d_seq_k[1].as<uint32_t>());
+        hipLaunchKernelGGL(k_pad_keys, dim3(pgrid), dim3(256), 0, st, pv_a, akb[0]->as<uint32_t>(),
+                           akb[1]->as<uint32_t>());
     }
     SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
     if (nr) {
-        hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                           c->d_totals.as<uint32_t>(), c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(),
-                           c->d_maxlen.as<uint16_t>(), c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(),
-                           c->d_aux_k[0].as<uint32_t>(), c->d_aux_v[0].as<uint32_t>(), d_err);
+        hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
+                           c->d_totals.as<uint32_t>(), F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(),
+                           F->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
+                           akb[0]->as<uint32_t>(), avb[0]->as<uint32_t>(), d_err);
         hipLaunchKernelGGL(k_emit_sq, dim3((nr + EMIT_WAVES - 1) / EMIT_WAVES), dim3(64 * EMIT_WAVES), 0, st, bv,
-                           c->d_counts.as<uint32_t>(), c->d_seq_k[0].as<uint32_t>(), c->d_seq_v[0].as<uint32_t>(),
-                           c->d_aux_k[0].as<uint32_t>(), c->d_aux_v[0].as<uint32_t>());
+                           F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
+                           akb[0]->as<uint32_t>(), avb[0]->as<uint32_t>());
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);
-    SortView svs{c->d_segs_seq.as<SortSeg>(), c->d_tile_seq.as<uint32_t>(), c->d_hist_seq.as<uint32_t>(),
+    SortView svs{F->d_segs_seq.as<SortSeg>(), F->d_tile_seq.as<uint32_t>(), F->d_hist_seq.as<uint32_t>(),
                  ps.total, (uint32_t)ps.tile_seg.size(), nbk};
-    SortView sva{c->d_segs_aux.as<SortSeg>(), c->d_tile_aux.as<uint32_t>(), c->d_hist_aux.as<uint32_t>(),
+    SortView sva{F->d_segs_aux.as<SortSeg>(), F->d_tile_aux.as<uint32_t>(), F->d_hist_aux.as<uint32_t>(),
                  pa.total, (uint32_t)pa.tile_seg.size(), nbk};
     const SymSink sink_seq{c->d_prs_seq.as<PRec>(), nullptr};   // packed
     const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>()};
@@ -853,33 +978,37 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     //      records the long runs have not written yet (k_coder_r) ----
     SA_CHECK(c, hipMemsetAsync(c->d_prs_aux.p, 0, atot * sizeof(PRec), st));
     ev_begin(c, PH_SORT_SEQ, st);
-    if (run_sort(c, st, ps, c->d_segs_seq, c->d_tile_seq, c->d_hist_seq, c->d_seq_k, c->d_seq_v, 0,
-                 ns > 1 ? seq_bits : 0, c->seq_sorted_buf))
+    if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, 0, ns > 1 ? seq_bits : 0,
+                 seq_sorted_buf))
         return -1;
     ev_finish(c, PH_SORT_SEQ, st);
     ev_begin(c, PH_REPLAY_SEQ, st);
     if (ps.total) {
-        SA_CHECK(c, hipMemsetAsync(c->d_nseq_long.p, 0, 4, st));
+        SA_CHECK(c, hipMemsetAsync(F->d_nseq_long.p, 0, 4, st));
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,
-                           c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(), c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(),
-                           sink_seq, c->d_seq_longs.as<uint64_t>(), c->d_nseq_long.as<uint32_t>());
+                           F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
+                           sink_seq, F->d_seq_longs.as<uint64_t>(), F->d_nseq_long.as<uint32_t>());
         hipLaunchKernelGGL(k_replay_seq_long, dim3((uint32_t)std::min<uint64_t>(max_seq_long, 2048)), dim3(128), 0,
-                           st, svs, c->d_seq_k[c->seq_sorted_buf].as<uint32_t>(),
-                           c->d_seq_v[c->seq_sorted_buf].as<uint32_t>(), sink_seq, c->d_seq_longs.as<uint64_t>(),
-                           c->d_nseq_long.as<uint32_t>(), d_err);
+                           st, svs, F->d_seq_k[seq_sorted_buf].as<uint32_t>(),
+                           F->d_seq_v[seq_sorted_buf].as<uint32_t>(), sink_seq, F->d_seq_longs.as<uint64_t>(),
+                           F->d_nseq_long.as<uint32_t>(), d_err);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_SORT_AUX, st);
-    if (run_sort(c, st, pa, c->d_segs_aux, c->d_tile_aux, c->d_hist_aux, c->d_aux_k, c->d_aux_v, AUX_SYM_BITS,
-                 AUX_SYM_BITS + aux_bits, c->aux_sorted_buf))
+    if (run_sort(c, st, pa, F->d_segs_aux, F->d_tile_aux, F->d_hist_aux, akb, avb, AUX_SYM_BITS,
+                 AUX_SYM_BITS + aux_bits, aux_sorted_buf))
         return -1;
     ev_finish(c, PH_SORT_AUX, st);
     ev_begin(c, PH_REPLAY_AUX, st);
-    const uint32_t* ak = c->d_aux_k[c->aux_sorted_buf].as<uint32_t>();
-    const uint32_t* av = c->d_aux_v[c->aux_sorted_buf].as<uint32_t>();
+    if (pa.total && akb[aux_sorted_buf] != &c->d_auxp_k) {
+        c->err = "internal: sorted AUX keys not in the context's buffer";
+        return -1;
+    }
+    const uint32_t* ak = akb[aux_sorted_buf]->as<uint32_t>();
+    const uint32_t* av = avb[aux_sorted_buf]->as<uint32_t>();
     uint32_t* ctr = c->d_nlong.as<uint32_t>();
-    const RunLists rl{c->d_short_at.as<uint64_t>(), ctr, c->d_longs.as<LongRun>(), ctr + 1, ctr + 2, max_long, ctr + 3,
+    const RunLists rl{F->d_short_at.as<uint64_t>(), ctr, c->d_longs.as<LongRun>(), ctr + 1, ctr + 2, max_long, ctr + 3,
                       c->d_huge_sorted.as<LongRun>()};
     SA_CHECK(c, hipMemsetAsync(ctr, 0, 16, st));
     if (pa.total) {
@@ -891,11 +1020,15 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     }
     SA_CHECK(c, hipGetLastError());
     SA_CHECK(c, hipEventRecord(c->ev_fork_seq, st));
+    // the front scratch is free once the kernels enqueued so far on st are done
+    SA_CHECK(c, hipEventRecord(F->ev_free, st));
+    F->have_ev = true;
+    front_lock.unlock();
     hipStream_t st3 = c->st3, st4 = c->st4;
     SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
     if (pa.total)
         hipLaunchKernelGGL(k_replay_aux_long, dim3(LONG_GRID), dim3(128), c->long_lds, st4, rl, ak, av, sink_aux,
-                           d_err);
+                           d_err, c->chain_prio);
     SA_CHECK(c, hipGetLastError());
     SA_CHECK(c, hipEventRecord(c->ev_long_done, st4));
     ev_finish(c, PH_REPLAY_AUX, st4);
@@ -904,8 +1037,28 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     //      (concurrent latency-bound launches land on shared SIMDs); the L passes
     //      after the long runs are done ----
     SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
-    const CoderGroup group{st3, 0u, (uint32_t)tasks.size(), PH_CODER_R, PH_CODER_L};
-    if (coder_run(c, tasks, cv, &group, 1, c->ev_long_done)) return -1;
+    std::vector<uint32_t> out_len;
+    {
+        const int rc = coder_run(c, tasks, cv, st3, PH_CODER_R, PH_CODER_L, c->ev_long_done, exact, out_len, payload);
+        if (rc) return rc;
+    }
+    // the final arena from the streams' real sizes: per block its encaps
+    // (<= 32 header bytes each), count / MD5s, and the ID-bin first ID
+    uint64_t final_bytes = 0;
+    std::vector<uint64_t> task_out_base(tasks.size());
+    for (size_t t = 0; t < tasks.size(); t++) task_out_base[t] = tasks[t].out_base;
+    c->final_base.assign(nbk, 0);
+    for (uint32_t b = 0; b < nbk; b++) {
+        uint64_t blk = 64 + 2 + 0x10000;
+        for (int s = 0; s < NSTREAM; s++) blk += out_len[asmb[b].task[s]] + 32;
+        asmb[b].out_base = final_bytes;
+        c->final_base[b] = final_bytes;
+        final_bytes = align_up(final_bytes + blk, 16);
+    }
+    SA_CHECK(c, c->d_final.ensure(std::max<uint64_t>(final_bytes, 16)));
+    SA_CHECK(c, hipMemcpyAsync(c->d_asm.p, asmb.data(), sizeof(AsmBlock) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(c->d_task_out_base.p, task_out_base.data(), 8 * tasks.size(), hipMemcpyHostToDevice,
+                               st));
 
     // ---- assembly (after MD5) ----
     if (cfg->md5) SA_CHECK(c, hipStreamWaitEvent(st, c->ev_md5_done, 0));
@@ -938,6 +1091,18 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
     }
     c->have_output = true;
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
+{
+    if (!c) return -1;
+    int rc = run_input(c, I, cfg, true);
+    if (rc == 2) rc = run_input(c, I, cfg, false);   // a stream outgrew its exact payload cap (rare)
+    return rc ? -1 : 0;
 }
 
 int sa_phase_times(const sa_ctx* c, const char** names, float* ms, int max)
@@ -1027,8 +1192,8 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
     c->have_output = false;
     if (coder_buffers(c, tasks.size(), segs, cv)) return -1;
     SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * std::max<size_t>(tasks.size(), 1), st));
-    const CoderGroup group{st, 0u, (uint32_t)tasks.size(), -1, -1};
-    if (coder_run(c, tasks, cv, &group, 1)) return -1;
+    std::vector<uint32_t> out_len;
+    if (coder_run(c, tasks, cv, st, -1, -1, nullptr, false, out_len, payload)) return -1;
     std::vector<uint32_t> ol(tasks.size());
     if (!tasks.empty())
         SA_CHECK(c, hipMemcpyAsync(ol.data(), c->d_out_len.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));

@@ -11,6 +11,8 @@
 //   k_assemble    per block: encaps in doFqzEncode@0x42d2d0 order
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "sa_common.h"
 #include "sa_device.h"
 #include "sa_logic.h"
@@ -82,6 +84,18 @@ __device__ inline void wg256_excl_scan(uint32_t v, uint32_t& excl, uint32_t* sh 
     uint32_t wpre = 0;
     for (uint32_t k = 0; k < w; k++) wpre += sh[k];
     excl = wpre + inc - v;
+}
+
+// s_setprio 3 when `prio` (a kernel argument, so uniform): the branch is scalar
+// code of its own, outside the compiler's control flow
+__device__ __forceinline__ void set_chain_prio(uint32_t prio)
+{
+    asm volatile(
+        "s_cmp_eq_u32 %0, 0\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "s_setprio 3\n"
+        "1:" ::"s"(prio)
+        : "scc");
 }
 
 // ---------------------------------------------------------------------------
@@ -1284,8 +1298,9 @@ constexpr uint32_t LONG_GRID = 2048;
 
 __global__ __launch_bounds__(128) void k_replay_aux_long(const RunLists rl, const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, const SymSink rec_all,
-                                                         uint32_t* __restrict__ err)
+                                                         uint32_t* __restrict__ err, uint32_t prio)
 {
+    set_chain_prio(prio);
     __shared__ RunModel md;
     __shared__ RunRing rg;
     __shared__ uint32_t job;
@@ -1448,7 +1463,7 @@ __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t 
 // records are in, read through L2 (the scalar cache may hold the zeros).
 __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t tmask, uint32_t& bad)
 {
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
     for (uint32_t spin = 0; spin < (1u << 22); spin++) {
         const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(P + lane), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
@@ -1471,14 +1486,23 @@ __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t 
 // overlaps.
 constexpr uint32_t PF_SEGS = 4;
 
-__global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ tasks, const TaskList tl,
-                                                const PRec* __restrict__ prs0, const PRec* __restrict__ prs1,
-                                                uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err,
-                                                const uint2* __restrict__ pf0, const uint2* __restrict__ pf1,
-                                                const uint32_t pf_segs)
+// Pass R, one launch per batch: one chain per wave, chains listed longest
+// first, workgroups of `coder_waves` (1, 2 or 4) waves.  Chain placement is what
+// the hardware dispatcher makes of it; two knobs steer it: waves per workgroup
+// (the waves of a workgroup share a CU, one per SIMD) and unused dynamic LDS per
+// workgroup (`coder_lds`, limiting pass-R workgroups per CU).  Measured
+// (DESIGN.md section 4.4): one chain per CU beats four per CU (22.7 vs 26.9 ns
+// per symbol); two chains on one SIMD run at half speed each.
+constexpr uint32_t CODER_MAX_WAVES = 4;
+
+__device__ __forceinline__ void coder_r_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
+                                              const TaskList& tl, const PRec* __restrict__ prs0,
+                                              const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
+                                              uint32_t* __restrict__ err, const uint2* __restrict__ pf0,
+                                              const uint2* __restrict__ pf1, const uint32_t pf_segs,
+                                              const uint32_t prio)
 {
-    const uint32_t li = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t t = tl.ids[li];
     const CoderTask tk = tasks[t];
     const CoderRun run = tl.run[li];
@@ -1489,6 +1513,11 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
     uint32_t r = run.r0;
     uint32_t g = first;
     uint32_t kv = 0;
+    // a latency-bound chain beside throughput kernels of other batches: issue
+    // priority over their waves on a shared SIMD (arbitration is priority, then
+    // age).  (After the prologue: at the kernel's top the scheduler moves the
+    // task loads behind it and fails to keep the chunk registers scalar.)
+    set_chain_prio(prio);
     if (g < last) {
         const PChunk* C = reinterpret_cast<const PChunk*>(P + (size_t)g * SEG_SYMS);
         PChunk A = C[0], B;
@@ -1535,7 +1564,218 @@ __global__ __launch_bounds__(64) void k_coder_r(const CoderTask* __restrict__ ta
     const uint32_t s = (g & ~63u) + lane;
     if (s >= first && s <= g) ck[s] = kv;
 }
+
+__global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_r(
+    const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
+    const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err,
+    const uint2* __restrict__ pf0, const uint2* __restrict__ pf1, const uint32_t pf_segs, const uint32_t prio)
+{
+    const uint32_t wpg = blockDim.x >> 6;
+    const uint32_t li = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (li >= tl.count) return;
+    coder_r_chain(li, tasks, tl, prs0, prs1, ck_r, err, pf0, pf1, pf_segs, prio);
+}
 #undef SA_CHUNK_STEPS
+
+// Pass R with the records fed through VGPRs: one lane-parallel global load per
+// 64-record segment, CODER_LA segments ahead of the chain (vector loads return
+// in order, so the compiler's counted vmcnt waits keep all of them in flight),
+// and per symbol two v_readlane into the SGPRs of the same 10-instruction SALU
+// step.  Unlike the scalar path (SMEM loads return out of order, so only one
+// 16-record chunk can be in flight, and the L2 prefetch it relies on is evicted
+// under the other batches' traffic), the lookahead here covers HBM latency
+// under load, and the scalar cache is not involved.  (Microbenchmark r3d:
+// 27 ns per symbol flat from 1 to 128 chains.)
+constexpr uint32_t CODER_LA = 6;
+
+// Eight steps of the chain per asm block.  Each step reads the record of the
+// step after it out of its lane first (readlane -> SGPR; used one step later,
+// so the SALU never waits on it); two register pairs alternate, so there are
+// no copies.  (One block per step made the compiler put an s_nop between the
+// blocks: a ninth of the issue slots.)
+#define SA_RV_STEP8                                                                              \
+        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l0]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l1]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l2]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l3]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l4]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l5]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l6]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l7]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        ""
+
+template <int J>
+__device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& mb, uint32_t& tb,
+                                         uint32_t cm, uint32_t ctf, uint32_t tmask)
+{
+    uint32_t t, f, q, p;
+    asm volatile(SA_RV_STEP8
+                 : [r] "+s"(r), [ma] "+s"(ma), [ta] "+s"(ta), [mb] "+s"(mb), [tb] "+s"(tb), [t] "=&s"(t),
+                   [f] "=&s"(f), [q] "=&s"(q), [p] "=&s"(p)
+                 : [tmask] "s"(tmask), [cm] "v"(cm), [ctf] "v"(ctf), [l0] "i"((J + 1) & 63), [l1] "i"((J + 2) & 63),
+                   [l2] "i"((J + 3) & 63), [l3] "i"((J + 4) & 63), [l4] "i"((J + 5) & 63), [l5] "i"((J + 6) & 63),
+                   [l6] "i"((J + 7) & 63), [l7] "i"((J + 8) & 63)
+                 : "scc");
+}
+#undef SA_RV_STEP8
+
+// the 64 steps of one segment (records in lanes 0..63 of cm / ctf)
+template <int... P>
+__device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t ctf, uint32_t tmask,
+                                           std::integer_sequence<int, P...>)
+{
+    uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(ctf, 0), mb = 0, tb = 0;
+    (rv_step8<8 * P>(r, ma, ta, mb, tb, cm, ctf, tmask), ...);
+}
+
+__device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
+                                               const TaskList& tl, const PRec* __restrict__ prs0,
+                                               const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
+                                               uint32_t* __restrict__ err, const uint32_t prio)
+{
+    typedef const __attribute__((address_space(1))) uint64_t g_u64;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t t = tl.ids[li];
+    const CoderTask tk = tasks[t];
+    const CoderRun run = tl.run[li];
+    const PRec* P = (tk.space ? prs1 : prs0) + tk.rec_base;
+    g_u64* G = (g_u64*)(P) + lane;
+    const uint32_t tmask = tk.space ? 0xffffu : 0xffu;   // wide AUX / packed SEQ records
+    uint32_t* ck = ck_r + tk.seg_base;
+    const uint32_t first = run.start_seg, last = tk.nseg - 1;
+    uint32_t r = run.r0;
+    uint32_t g = first;
+    uint32_t kv = 0;
+    set_chain_prio(prio);
+    if (g < last) {
+        uint32_t bad = 0;
+        // segment loads at or past the last segment read the last one (the
+        // record arrays hold >= 64 records of slack past every stream's end)
+        uint64_t buf[CODER_LA];
+#pragma unroll
+        for (uint32_t k = 0; k < CODER_LA; k++) buf[k] = G[(size_t)min(g + k, last) * SEG_SYMS];
+        for (; g < last;) {
+#pragma unroll
+            for (uint32_t k = 0; k < CODER_LA; k++) {
+                if (g >= last) break;
+                const uint64_t cur = buf[k];
+                buf[k] = G[(size_t)min(g + CODER_LA, last) * SEG_SYMS];
+                kv = lane == (g & 63) ? r : kv;
+                if ((g & 63) == 63) {
+                    const uint32_t s = g - 63 + lane;
+                    if (s >= first) ck[s] = kv;
+                }
+                const uint32_t r_seg = r;
+                const uint32_t cm = (uint32_t)cur, ctf = (uint32_t)(cur >> 32);
+                rv_segment(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
+                if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
+                g++;
+            }
+        }
+        if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
+    }
+    kv = lane == (g & 63) ? r : kv;
+    const uint32_t s = (g & ~63u) + lane;
+    if (s >= first && s <= g) ck[s] = kv;
+}
+
+__global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
+    const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
+    const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio)
+{
+    const uint32_t wpg = blockDim.x >> 6;
+    const uint32_t li = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (li >= tl.count) return;
+    coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+}
 
 // Locate list entry and segment of global coder-lane gi (gbase ascending).
 __device__ inline uint32_t list_find(const TaskList& tl, uint64_t gi)
@@ -1621,6 +1861,18 @@ __global__ __launch_bounds__(L2_THREADS) void k_coder_l2(const CoderView cv, con
         }
         __syncthreads();
     }
+}
+
+// Bytes of every listed stream up to its last segment's flush (L1 maps + L2
+// offsets): the host sizes the payload arena from them before L3 writes it.
+__global__ __launch_bounds__(256) void k_task_ends(const CoderView cv, const TaskList tl, uint32_t* __restrict__ ends)
+{
+    const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= tl.count) return;
+    const uint32_t t = tl.ids[li];
+    const CoderTask& tk = cv.tasks[t];
+    const uint64_t sg = tk.seg_base + tk.nseg - 1;
+    ends[t] = cv.off_at[sg] + cv.maps[sg].nbytes;
 }
 
 // L3: one lane per segment: the exact coder from (range, low) at its offset.
@@ -1741,8 +1993,9 @@ __device__ inline void md5_block(uint32_t h[4], const uint32_t M[16])
 constexpr uint32_t MD5_CHUNK_BLOCKS = 16;
 
 __global__ __launch_bounds__(64) void k_md5(const Md5Task* __restrict__ tasks, uint32_t ntasks,
-                                            uint32_t* __restrict__ digests)
+                                            uint32_t* __restrict__ digests, uint32_t prio)
 {
+    set_chain_prio(prio);
     __shared__ uint4 ring[2][64];
     const uint32_t t = blockIdx.x;
     if (t >= ntasks) return;

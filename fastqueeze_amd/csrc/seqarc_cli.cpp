@@ -1,33 +1,46 @@
-// seqarc_amd -- the SeqArc -c command line over libseqarc_amd (host C++).
+// seqarc_amd -- the SeqArc command line over libseqarc_amd (host C++).
 //
-//   seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]
-//              [--slevel K] [--qlevel Q] [--device D] [--devices N] [--batch BLOCKS]
-//   seqarc_amd -d [-t N] ARCHIVE.arc PREFIX
+//   seqarc_amd -c [options] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)     -> OUT.arc
+//   seqarc_amd -d [options] ARCHIVE.arc [PREFIX] [-o PREFIX]
 //
-// --devices N: batches of blocks are dealt to N gfx950 devices (one host
-// thread and sa_ctx each; blocks are independent, so there is no device-to-
-// device exchange) and gathered back in input order (--share-device: N
-// contexts on one device, for testing the scatter/gather on one GPU).
+//   -t N       host threads that parse (-c) or decode (-d) blocks
+//   -l R       R-Block lossy qualities (rblock@0x426c10)      -n  no per-block MD5
+//   -f         overwrite existing outputs ("%s has exist!" otherwise, .rodata +0x877)
+//   -p         outputs in the directory of the input (README.md "-p")
+//   -P 1|2|3   decode to stdout: SE or PE1 reads / PE2 reads / each pair in order
+//              (DecodePipeOutJob@0x42f930)
+//   --slevel K --qlevel Q   the reference's developer options (./seqarc.config)
+//   --devices N   GPUs (default 1), --contexts K   encoder contexts per GPU
+//   --batch B     blocks per encode, --block-size MiB (default 50)
+//   --share-device   all contexts on one GPU (tests of the multi-GPU gather)
 //
-// Mirrors the reference's encode path (SeqArc-1.6 main@0x41fd40 ->
-// SeqArcContext::doReadAndEncode@0x41a4e0): the reader cuts 50 MiB blocks
-// (SeqArcRead::doReadJob@0x432a80 / doReadPEJob@0x432d10), the first block
-// decides the ID template (IDProcess::analysisIDBinType@0x4310a0), every block
-// is encoded (here on one gfx950 device, a batch of blocks per launch) and the
-// blocks are written after a 16-byte header in input order, followed by the
-// trailer (SeqArcFile::writeFileInfo@0x4171b0).  Output: PREFIX.arc.
-// -t is accepted for command-line compatibility (the GPU encodes a batch of
-// blocks concurrently); Slevel / Qlevel are the reference's developer options
-// (./seqarc.config), given here as --slevel / --qlevel.
+// Compression mirrors SeqArc-1.6 main@0x41fd40 -> SeqArcContext::doReadAndEncode
+// @0x41a4e0 as a stream: one reader thread cuts 50 MiB blocks as the input
+// arrives (doReadJob@0x432a80 / doReadPEJob@0x432d10, plain or gzip), -t parser
+// threads turn them into the SoA blocks (getBlockRead[PE]), the first block
+// decides the ID template (IDProcess::analysisIDBinType@0x4310a0), encoder
+// threads -- K contexts per GPU sharing one front scratch, batches dealt round
+// robin -- encode batches of blocks, and this thread writes them in input order
+// (the reference's -t 1 order) after a 16-byte header, then the trailer
+// (SeqArcFile::writeFileInfo@0x4171b0).  The blocks in flight are bounded
+// (ReadBufPool@0x4341e0 plays that role in the reference).
+#include <errno.h>
+#include <fcntl.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -37,38 +50,84 @@
 
 namespace {
 
-bool slurp(const char* path, std::vector<uint8_t>& out, bool& gz)
+int usage()
 {
-    FILE* f = fopen(path, "rb");
-    if (!f) return false;
-    unsigned char m[2] = {0, 0};
-    gz = fread(m, 1, 2, f) == 2 && m[0] == 0x1f && m[1] == 0x8b;   // getFileType@0x40d9f0
-    fclose(f);
-    gzFile g = gzopen(path, "rb");
-    if (!g) return false;
-    gzbuffer(g, 1 << 18);
-    out.clear();
-    std::vector<uint8_t> buf(1 << 22);
-    for (;;) {
-        const int n = gzread(g, buf.data(), (unsigned)buf.size());
-        if (n < 0) { gzclose(g); return false; }
-        if (n == 0) break;
-        out.insert(out.end(), buf.begin(), buf.begin() + n);
+    fprintf(stderr,
+            "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
+            "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
+            "                  [--block-size MiB] [--device D] [--share-device]\n"
+            "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] ARCHIVE.arc [PREFIX] [-o PREFIX]\n");
+    return 2;
+}
+
+std::string dir_of(const std::string& p)
+{
+    const size_t s = p.rfind('/');
+    return s == std::string::npos ? std::string() : p.substr(0, s + 1);
+}
+
+
+// isFileExist@0x40cc50 + getFileSize@0x40cc10: an existing non-empty output
+// stops the run unless -f (SeqArcParam::parseOptFromMem@0x407210)
+bool may_write(const std::string& path, bool force)
+{
+    struct stat sb;
+    if (!force && stat(path.c_str(), &sb) == 0 && sb.st_size > 0) {
+        fprintf(stderr, "seqarc_amd: %s has exist!\n", path.c_str());
+        return false;
     }
-    gzclose(g);
     return true;
 }
 
-// getFirstLine@0x431eb0: the '+' line of the first record is bare ("+\n")
-int bare_plus(const std::vector<uint8_t>& t)
-{
-    size_t nl[3] = {0, 0, 0};
-    int k = 0;
-    for (size_t i = 0; i < t.size() && k < 3; i++)
-        if (t[i] == '\n') nl[k++] = i + 1;
-    if (k < 3) return 1;
-    return nl[2] - nl[1] > 2 ? 0 : 1;
-}
+// ---- input ---------------------------------------------------------------
+// getFileType@0x40d9f0 (gzip magic); plain files are read with read(2), gzip
+// through zlib's gzread.
+struct Input {
+    int fd = -1;
+    gzFile gz = nullptr;
+    bool is_gz = false, eof = false;
+    bool open(const char* path)
+    {
+        fd = ::open(path, O_RDONLY);
+        if (fd < 0) return false;
+        unsigned char m[2] = {0, 0};
+        is_gz = ::pread(fd, m, 2, 0) == 2 && m[0] == 0x1f && m[1] == 0x8b;
+        if (is_gz) {
+            gz = gzdopen(fd, "rb");
+            if (!gz) return false;
+            gzbuffer(gz, 1 << 20);
+            fd = -1;
+        }
+        return true;
+    }
+    // appends up to n bytes to b; false on a read error
+    bool fill(std::vector<uint8_t>& b, size_t n)
+    {
+        size_t have = b.size();
+        b.resize(have + n);
+        size_t got = 0;
+        while (got < n && !eof) {
+            long r;
+            if (is_gz) {
+                const unsigned want = (unsigned)std::min<size_t>(n - got, 1u << 30);
+                r = gzread(gz, b.data() + have + got, want);
+            } else {
+                r = (long)::read(fd, b.data() + have + got, n - got);
+                if (r < 0 && errno == EINTR) continue;
+            }
+            if (r < 0) { b.resize(have + got); return false; }
+            if (r == 0) eof = true;
+            got += (size_t)r;
+        }
+        b.resize(have + got);
+        return true;
+    }
+    ~Input()
+    {
+        if (gz) gzclose(gz);
+        if (fd >= 0) ::close(fd);
+    }
+};
 
 struct Parsed {
     std::vector<uint8_t> names, seq, qual;
@@ -79,16 +138,331 @@ struct Parsed {
     sa_block view() const { return sa_block{names.data(), nl.data(), seq.data(), sl.data(), qual.data(), nreads}; }
 };
 
-int usage()
+struct Job {                     // one block between the reader and the writer
+    std::vector<uint8_t> t1, t2;  // its FASTQ text (freed once parsed)
+    Parsed p;
+    std::vector<uint8_t> out;     // the encoded block
+    int state = 0;                // 0 read, 1 parsed, 2 encoded
+};
+
+// getFirstLine@0x431eb0: the '+' line of the first record carries no ID
+int bare_plus(const std::vector<uint8_t>& t)
 {
-    fprintf(stderr,
-            "usage: seqarc_amd -c -1 A.fq[.gz] [-2 B.fq[.gz]] -o PREFIX [-l R] [-n] [-t N]\n"
-            "                  [--slevel K] [--qlevel Q] [--device D] [--devices N] [--batch BLOCKS]\n"
-            "                  [--block-size MiB]\n"
-            "       seqarc_amd -d [-t N] [--slevel K] [--qlevel Q] ARCHIVE.arc PREFIX\n");
-    return 2;
+    size_t nl[3] = {0, 0, 0};
+    int k = 0;
+    for (size_t i = 0; i < t.size() && k < 3; i++)
+        if (t[i] == '\n') nl[k++] = i + 1;
+    if (k < 3) return 1;
+    return nl[2] - nl[1] > 2 ? 0 : 1;
 }
 
+bool parse_job(Job& j, bool pe)
+{
+    const uint64_t cap = j.t1.size() + j.t2.size() + 16;
+    Parsed& p = j.p;
+    p.names.resize(cap);
+    p.seq.resize(cap);
+    p.qual.resize(cap);
+    p.nl.resize(cap / 4 + 8);
+    p.sl.resize(cap / 4 + 8);
+    const int64_t n = pe ? sa_parse_pe(j.t1.data(), j.t1.size(), j.t2.data(), j.t2.size(), p.names.data(), p.nl.data(),
+                                       p.seq.data(), p.sl.data(), p.qual.data())
+                         : sa_parse_se(j.t1.data(), j.t1.size(), p.names.data(), p.nl.data(), p.seq.data(),
+                                       p.sl.data(), p.qual.data());
+    if (n < 0) return false;
+    p.nreads = (uint32_t)n;
+    p.text1 = j.t1.size();
+    p.text2 = j.t2.size();
+    uint64_t nb = 0, sb = 0;
+    for (uint32_t r = 0; r < p.nreads; r++) {
+        nb += p.nl[r];
+        sb += (uint64_t)p.sl[r];
+    }
+    p.names.resize(nb);
+    p.seq.resize(sb);
+    p.qual.resize(sb);
+    p.nl.resize(p.nreads);
+    p.sl.resize(p.nreads);
+    std::vector<uint8_t>().swap(j.t1);
+    std::vector<uint8_t>().swap(j.t2);
+    return true;
+}
+
+struct Options {
+    const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr;
+    bool compress = false, decompress = false, force = false, in_dir = false, share_device = false;
+    int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50;
+    sa_cfg cfg{3, 2, 1, 0, 0.0};
+};
+
+// ---- compression: the streaming pipeline ------------------------------------
+int compress(const Options& o)
+{
+    const auto t_start = std::chrono::steady_clock::now();
+    const bool pe = o.f2 && *o.f2;
+    Input in1, in2;
+    struct stat sb;
+    for (const char* f : {o.f1, pe ? o.f2 : nullptr}) {
+        if (f && (stat(f, &sb) != 0 || sb.st_size == 0)) {   // doCheckSetEncodeOpt@0x407fa0
+            fprintf(stderr, "Error:The Src file %s may be not exist or empty!\n", f);
+            return 1;
+        }
+    }
+    if (!in1.open(o.f1) || (pe && !in2.open(o.f2))) {
+        fprintf(stderr, "seqarc_amd: cannot open the input\n");
+        return 1;
+    }
+    std::string outp = o.out;
+    if (o.in_dir && outp.find('/') == std::string::npos) outp = dir_of(o.f1) + outp;
+    const std::string path = outp + ".arc";
+    if (!may_write(path, o.force)) return 1;
+
+    const uint64_t bs = (uint64_t)o.block_mib << 20;   // BlockSize(M), default 50 (param+0x1b78)
+    const int nparse = o.threads > 0 ? o.threads
+                                     : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // contexts: K per device; every device's contexts share one front scratch
+    std::vector<sa_ctx*> ctxs;
+    for (int d = 0; d < o.devices; d++) {
+        sa_ctx* first = nullptr;
+        for (int k = 0; k < o.contexts; k++) {
+            const int dev = o.device + (o.share_device ? 0 : d);
+            sa_ctx* c = first ? sa_create_shared(dev, first) : sa_create(dev);
+            if (!c) break;
+            if (!first) first = c;
+            ctxs.push_back(c);
+        }
+        if (!first) break;
+    }
+    if (ctxs.empty()) {
+        fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", o.device);
+        return 1;
+    }
+    const int64_t B = std::max(1, o.batch);
+    const size_t max_inflight = (size_t)B * (ctxs.size() + 2);   // blocks read but not yet written
+
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<int64_t, std::unique_ptr<Job>> jobs;
+    std::deque<int64_t> to_parse;
+    int64_t nread = 0, nblocks = -1, written = 0, next_batch = 0;
+    bool failed = false, tmpl_ready = false;
+    std::string err;
+    uint8_t tmpl[512] = {0};
+    sa_cfg cfg = o.cfg;
+    int plus_bare = 1;
+    uint64_t total_in = 0;
+    auto fail = [&](const std::string& m) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!failed) err = m;
+        failed = true;
+        cv.notify_all();
+    };
+
+    // reader: cuts blocks as the input arrives
+    std::thread reader([&]() {
+        std::vector<uint8_t> b1, b2, first;
+        const uint64_t want = pe ? (uint64_t)((uint32_t)bs >> 1) : bs;
+        for (int64_t i = 0;; i++) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return failed || (size_t)(nread - written) < max_inflight; });
+                if (failed) return;
+            }
+            b1.reserve(want);
+            if (pe) b2.reserve(want);
+            if (b1.size() < want && !in1.eof && !in1.fill(b1, want - b1.size())) return fail("read error on input 1");
+            if (pe && b2.size() < want && !in2.eof && !in2.fill(b2, want - b2.size()))
+                return fail("read error on input 2");
+            if (b1.empty() && (!pe || b2.empty())) {   // the input ended on a block boundary
+                std::lock_guard<std::mutex> g(mu);
+                nblocks = i;
+                cv.notify_all();
+                return;
+            }
+            if (i == 0) {
+                const void* nl = memchr(b1.data(), '\n', b1.size());
+                first.assign(b1.begin(), nl ? b1.begin() + ((const uint8_t*)nl - b1.data()) + 1 : b1.end());
+                plus_bare = bare_plus(pe ? b2 : b1);
+            }
+            uint64_t e1 = 0, e2 = 0;
+            if (pe) {
+                if (sa_cut_next_pe(b1.data(), b1.size(), in1.eof, b2.data(), b2.size(), in2.eof, bs, first.data(),
+                                   first.size(), &e1, &e2) != 0)
+                    return fail("PE block cut failed (mates out of step)");
+            } else {
+                const int64_t e = sa_cut_next_se(b1.data(), b1.size(), in1.eof, bs, first.data(), first.size());
+                if (e < 0) return fail("block cut failed");
+                e1 = (uint64_t)e;
+            }
+            std::unique_ptr<Job> j(new Job());
+            j->t1.assign(b1.begin() + (ptrdiff_t)e1, b1.end());   // the carry, swapped in below
+            j->t1.swap(b1);
+            j->t1.resize(e1);
+            if (pe) {
+                j->t2.assign(b2.begin() + (ptrdiff_t)e2, b2.end());
+                j->t2.swap(b2);
+                j->t2.resize(e2);
+            }
+            const bool last = b1.empty() && b2.empty() && in1.eof && (!pe || in2.eof);
+            {
+                std::lock_guard<std::mutex> g(mu);
+                total_in += e1 + e2;
+                jobs[i] = std::move(j);
+                to_parse.push_back(i);
+                nread = i + 1;
+                if (last) nblocks = nread;
+            }
+            cv.notify_all();
+            if (last) return;
+        }
+    });
+
+    // parsers
+    std::vector<std::thread> parsers;
+    for (int t = 0; t < nparse; t++)
+        parsers.emplace_back([&]() {
+            for (;;) {
+                int64_t i;
+                Job* j;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return failed || !to_parse.empty() || nblocks >= 0; });
+                    if (failed || (to_parse.empty() && nblocks >= 0)) return;
+                    i = to_parse.front();
+                    to_parse.pop_front();
+                    j = jobs[i].get();
+                }
+                if (!parse_job(*j, pe)) return fail("parse failed");
+                if (i == 0) {   // the ID template of the first block
+                    const sa_block fb = j->p.view();
+                    if (sa_analyze_ids(&fb, pe ? 0 : 1, tmpl) != 0) return fail("ID analysis failed");
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    j->state = 1;
+                    if (i == 0) {
+                        cfg.bin_mode = tmpl[0];
+                        tmpl_ready = true;
+                    }
+                }
+                cv.notify_all();
+            }
+        });
+
+    // encoders: one host thread per context, batches of B blocks in order
+    auto batch_ready = [&](int64_t k) {   // under mu
+        if (!tmpl_ready) return false;
+        const int64_t b0 = k * B;
+        const int64_t b1 = nblocks >= 0 ? std::min(nblocks, b0 + B) : b0 + B;
+        if (nblocks < 0 && nread < b1) return false;
+        for (int64_t i = b0; i < b1; i++)
+            if (jobs.count(i) == 0 || jobs[i]->state < 1) return false;
+        return true;
+    };
+    std::vector<std::thread> encoders;
+    for (sa_ctx* ctx : ctxs)
+        encoders.emplace_back([&, ctx]() {
+            for (;;) {
+                int64_t k, b0, b1;
+                std::vector<Job*> js;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    if (failed) return;
+                    k = next_batch++;
+                    cv.wait(lk, [&] { return failed || (nblocks >= 0 && k * B >= nblocks) || batch_ready(k); });
+                    if (failed || (nblocks >= 0 && k * B >= nblocks)) return;
+                    b0 = k * B;
+                    b1 = nblocks >= 0 ? std::min(nblocks, b0 + B) : b0 + B;
+                    for (int64_t i = b0; i < b1; i++) js.push_back(jobs[i].get());
+                }
+                std::vector<sa_block> in(js.size());
+                std::vector<sa_out> outs(js.size());
+                for (size_t i = 0; i < js.size(); i++) {
+                    in[i] = js[i]->p.view();
+                    js[i]->out.resize(sa_output_bound(&in[i]));
+                    outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                }
+                const sa_cfg c = cfg;
+                if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
+                    return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    for (size_t i = 0; i < js.size(); i++) {
+                        js[i]->out.resize(outs[i].size);
+                        js[i]->state = 2;
+                    }
+                }
+                cv.notify_all();
+            }
+        });
+
+    // writer (this thread): blocks in input order
+    FILE* fo = fopen(path.c_str(), "wb");
+    int rc = 0;
+    std::vector<sa_arc_block> info;
+    uint64_t total = 0;
+    uint8_t hdr[16] = {0};
+    if (!fo) {
+        fail("cannot write " + path);
+    } else {
+        fwrite(hdr, 1, 16, fo);   // patched at the end (createOutFile@0x417480 / writeFileInfo@0x4171b0)
+    }
+    for (int64_t i = 0;; i++) {
+        std::unique_ptr<Job> j;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] {
+                return failed || (nblocks >= 0 && i >= nblocks) || (jobs.count(i) && jobs[i]->state == 2);
+            });
+            if (failed || (nblocks >= 0 && i >= nblocks)) break;
+            j = std::move(jobs[i]);
+            jobs.erase(i);
+        }
+        uint32_t lng = 0;
+        for (uint32_t r = 0; r < j->p.nreads; r++) lng |= j->p.sl[r] > 0xffff;
+        if (fwrite(j->out.data(), 1, j->out.size(), fo) != j->out.size()) {   // writeData@0x40e070: exit(1)
+            fail("write error on " + path);
+            break;
+        }
+        info.push_back(sa_arc_block{(uint32_t)j->out.size(), lng, j->p.text1, j->p.text2});
+        total += j->out.size();
+        {
+            std::lock_guard<std::mutex> g(mu);
+            written = i + 1;
+        }
+        cv.notify_all();
+    }
+    reader.join();
+    for (auto& t : parsers) t.join();
+    for (auto& t : encoders) t.join();
+    for (sa_ctx* c : ctxs) sa_destroy(c);
+    if (failed) {
+        fprintf(stderr, "seqarc_amd: %s\n", err.c_str());
+        if (fo) fclose(fo);
+        return 1;
+    }
+    sa_arc_info ai{o.f1, pe ? o.f2 : nullptr, pe ? 1 : 0, in1.is_gz ? 1 : 0, plus_bare, cfg.md5,
+                   cfg.lossy > 0.0 ? 1 : 0, tmpl};
+    std::vector<uint8_t> tr(4096 + 40 * info.size());
+    const int64_t tl = sa_arc_trailer(&ai, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
+    if (tl < 0) {
+        fprintf(stderr, "seqarc_amd: trailer failed\n");
+        rc = 1;
+    } else {
+        fwrite(tr.data(), 1, (size_t)tl, fo);
+        sa_arc_header(total, hdr);
+        fseek(fo, 0, SEEK_SET);
+        fwrite(hdr, 1, 16, fo);
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        fprintf(stderr, "seqarc_amd: %zu block(s), %llu -> %llu bytes (%.2fx), %.3f s, %.1f MB/s\n", info.size(),
+                (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
+                (double)total_in / (double)(16 + total + tl), secs, (double)total_in / secs / 1e6);
+    }
+    if (fclose(fo) != 0) rc = 1;
+    return rc;
+}
+
+// ---- decompression --------------------------------------------------------
 uint64_t be(const uint8_t* p, int n)
 {
     uint64_t v = 0;
@@ -108,16 +482,47 @@ uint64_t vint(const uint8_t* p, const uint8_t* end, int& w)
     return v;
 }
 
+// One decoded block, written as FASTQ records.  mate: -1 all reads in order,
+// 0 / 1 only the r1 / r2 reads of a PE block (DecodePipeOutJob::recoverData*,
+// mode 1 / 2); bare: '+' lines without the ID.
+void write_reads(FILE* f, FILE* f2, const std::vector<uint8_t>& names, const std::vector<uint16_t>& nl,
+                 const std::vector<uint8_t>& seq, const std::vector<int32_t>& sl, const std::vector<uint8_t>& qual,
+                 uint32_t n, bool paired, int mate, bool bare)
+{
+    const uint8_t *nm = names.data(), *sq = seq.data(), *ql = qual.data();
+    for (uint32_t r = 0; r < n; r++) {
+        const size_t L = (size_t)sl[r], N = nl[r];
+        const bool keep = mate < 0 || (int)(r & 1) == mate;
+        FILE* o = (paired && mate < 0 && f2 && (r & 1)) ? f2 : f;
+        if (keep) {
+            fputc('@', o);
+            fwrite(nm, 1, N, o);
+            fputc('\n', o);
+            fwrite(sq, 1, L, o);
+            fputs("\n+", o);
+            if (!bare) fwrite(nm, 1, N, o);
+            fputc('\n', o);
+            fwrite(ql, 1, L, o);
+            fputc('\n', o);
+        }
+        nm += N;
+        sq += L;
+        ql += L;
+    }
+}
+
 // SeqArc -d: SeqArcFile::readFileInfo@0x419660 (header, trailer params, block
-// table), one block per host thread (ISeqArcDecodeThread::doJob@0x435580),
-// FASTQ written in block order as PREFIX_1.fastq / PREFIX_2.fastq (PE,
-// .rodata +0x7b2) or PREFIX.fastq (SE).
-int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads)
+// table), -t blocks decoded at once (ISeqArcDecodeThread::doJob@0x435580),
+// written in block order.  Output names (SeqArcParam::getDecodeFile@0x405f70,
+// appendname@0x405f10): PREFIX_1.fastq / PREFIX_2.fastq (PE) or PREFIX.fastq
+// (SE); without a prefix the stored input names (3 more bytes cut when input 1
+// was gzip, as the binary does).  -P writes to stdout instead.
+int decompress(const Options& o)
 {
     std::vector<uint8_t> a;
     {
-        FILE* f = fopen(path, "rb");
-        if (!f) { fprintf(stderr, "seqarc_amd: cannot read %s\n", path); return 1; }
+        FILE* f = fopen(o.arc, "rb");
+        if (!f) { fprintf(stderr, "Error:The file %s may be not exist!\n", o.arc); return 1; }
         fseek(f, 0, SEEK_END);
         a.resize((size_t)ftell(f));
         fseek(f, 0, SEEK_SET);
@@ -125,7 +530,7 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
         fclose(f);
     }
     if (a.size() < 16 || memcmp(a.data(), ".arc", 4) || a[7] != 0x82) {
-        fprintf(stderr, "seqarc_amd: %s is not a SeqArc 1.6 archive\n", path);
+        fprintf(stderr, "seqarc_amd: %s is not a SeqArc 1.6 archive\n", o.arc);
         return 1;
     }
     const uint64_t region = be(a.data() + 8, 8) & ((1ull << 56) - 1);
@@ -134,15 +539,16 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
     int w;
     if (vint(t, end, w) != 3 || !w) return 1;
     t += w + 4;
-    // params encap (ID 1, 2-byte size): fields 1-18
+    // params encap (ID 1, 2-byte size): fields 1-18 (writeParam@0x416450)
     if (vint(t, end, w) != 1 || !w) return 1;
     t += w;
     const uint64_t psz = be(t, 2) & 0x3fff;
     t += 2;
     const uint8_t* pend = t + psz;
     uint8_t tmpl[512] = {0};
-    int bare = 1, paired = 0, lossy = 0, md5 = 1;
+    int bare = 1, paired = 0, lossy = 0, md5 = 1, gz1 = 0;
     uint32_t nblocks = 0;
+    std::string name1, name2;
     while (t < pend) {
         const uint64_t id = vint(t, pend, w);
         if (!w) return 1;
@@ -152,8 +558,10 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
         t += sw;
         if (t + ln > pend) return 1;
         if (id == 2) bare = t[0];
+        else if (id == 4) gz1 = t[0];
         else if (id == 11 && ln >= 4) nblocks = (uint32_t)(t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24);
-        else if (id == 14 && ln) paired = 1;
+        else if (id == 13) name1.assign((const char*)t, ln);
+        else if (id == 14 && ln) { paired = 1; name2.assign((const char*)t, ln); }
         else if (id == 15 && ln == 512) memcpy(tmpl, t, 512);
         else if (id == 16) lossy = t[0];
         else if (id == 17) md5 = t[0];
@@ -178,13 +586,37 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
         blks[b] = Blk{off, s2 >> 1, text, s2 & 1u};
         if (off + blks[b].size > 16 + region) return 1;
     }
+    sa_cfg cfg = o.cfg;
     cfg.md5 = md5;
     cfg.lossy = lossy ? 1.0 : 0.0;
     cfg.bin_mode = tmpl[0];
-    const std::string p1 = std::string(prefix) + (paired ? "_1.fastq" : ".fastq"), p2 = std::string(prefix) + "_2.fastq";
-    FILE* o1 = fopen(p1.c_str(), "wb");
-    FILE* o2 = paired ? fopen(p2.c_str(), "wb") : nullptr;
-    if (!o1 || (paired && !o2)) { fprintf(stderr, "seqarc_amd: cannot write %s\n", p1.c_str()); return 1; }
+
+    // outputs
+    FILE *o1 = nullptr, *o2 = nullptr;
+    int mate = -1;
+    if (o.pipe) {   // DecodePipeOutJob ctor@0x42fd00: SE -> all reads; PE: 1 -> r1, 2 -> r2, 3 -> pairs in order
+        if (o.pipe < 1 || o.pipe > 3) return usage();
+        o1 = stdout;
+        mate = !paired ? -1 : o.pipe == 1 ? 0 : o.pipe == 2 ? 1 : -1;
+    } else {
+        const std::string dir = o.in_dir ? dir_of(o.arc) : std::string();
+        auto name = [&](int i) {   // getDecodeFile(i)
+            if (o.out && *o.out) {
+                std::string p = o.out;
+                if (o.in_dir && p.find('/') == std::string::npos) p = dir + p;
+                return p + (i == 0 ? ".fastq" : i == 1 ? "_1.fastq" : "_2.fastq");
+            }
+            std::string s = i <= 1 ? name1 : name2;
+            if (gz1 && s.size() >= 3) s = s.substr(0, s.size() - 3);
+            if (s == "@empty*" || s.empty()) s = std::string("decode") + (i == 0 ? ".fastq" : i == 1 ? "_1.fastq" : "_2.fastq");
+            return dir + s;
+        };
+        const std::string p1 = name(paired ? 1 : 0), p2 = paired ? name(2) : std::string();
+        if (!may_write(p1, o.force) || (paired && !may_write(p2, o.force))) return 1;
+        o1 = fopen(p1.c_str(), "wb");
+        o2 = paired ? fopen(p2.c_str(), "wb") : nullptr;
+        if (!o1 || (paired && !o2)) { fprintf(stderr, "seqarc_amd: cannot write %s\n", p1.c_str()); return 1; }
+    }
     struct Dec {
         std::vector<uint8_t> names, seq, qual;
         std::vector<uint16_t> nl;
@@ -193,7 +625,7 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
         int64_t rc = -1;
     };
     int rc = 0, bad_md5 = 0;
-    const uint32_t nt = (uint32_t)std::max(1, threads);
+    const uint32_t nt = (uint32_t)std::max(1, o.threads > 0 ? o.threads : 1);
     for (uint32_t b0 = 0; b0 < nblocks && !rc; b0 += nt) {
         const uint32_t n = std::min(nt, nblocks - b0);
         std::vector<Dec> ds(n);
@@ -214,21 +646,11 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
             Dec& d = ds[i];
             if (d.rc < 0) { fprintf(stderr, "seqarc_amd: block %u does not decode\n", b0 + i); rc = 1; break; }
             bad_md5 |= !d.d.md5_ok;
-            const uint8_t *nm = d.names.data(), *sq = d.seq.data(), *ql = d.qual.data();
-            for (uint32_t r = 0; r < d.d.nreads; r++) {
-                FILE* f = paired && (r & 1) ? o2 : o1;
-                const size_t L = (size_t)d.sl[r], N = d.nl[r];
-                fputc('@', f); fwrite(nm, 1, N, f); fputc('\n', f);
-                fwrite(sq, 1, L, f);
-                fputs("\n+", f);
-                if (!bare) fwrite(nm, 1, N, f);
-                fputc('\n', f);
-                fwrite(ql, 1, L, f); fputc('\n', f);
-                nm += N; sq += L; ql += L;
-            }
+            write_reads(o1, o2, d.names, d.nl, d.seq, d.sl, d.qual, d.d.nreads, paired, mate, bare);
         }
     }
-    fclose(o1);
+    if (o1 && o1 != stdout) fclose(o1);
+    else if (o1) fflush(o1);
     if (o2) fclose(o2);
     if (bad_md5) {   // blockMd5Verify@0x414e00: "Name/Seq/Qual md5 unequal"
         fprintf(stderr, "seqarc_amd: Name/Seq/Qual md5 unequal\n");
@@ -241,206 +663,58 @@ int decode_archive(const char* path, const char* prefix, sa_cfg cfg, int threads
 
 int main(int argc, char** argv)
 {
-    const char *f1 = nullptr, *f2 = nullptr, *outp = nullptr;
-    bool compress = false, decompress = false;
-    const char* arc = nullptr;
-    int threads = 1;
-    sa_cfg cfg{3, 2, 1, 0, 0.0};
-    int device = 0, batch = 16, devices = 1, block_mib = 50;
-    bool share_device = false;
+    Options o;
+    std::vector<const char*> pos;
     for (int i = 1; i < argc; i++) {
         const char* a = argv[i];
         auto val = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : nullptr; };
-        if (!strcmp(a, "-c")) compress = true;
-        else if (!strcmp(a, "-1")) f1 = val();
-        else if (!strcmp(a, "-2")) f2 = val();
-        else if (!strcmp(a, "-o")) outp = val();
-        else if (!strcmp(a, "-n")) cfg.md5 = 0;
-        else if (!strcmp(a, "-l")) { const char* v = val(); if (!v) return usage(); cfg.lossy = atof(v); }
-        else if (!strcmp(a, "-t")) { const char* v = val(); if (!v) return usage(); threads = atoi(v) > 0 ? atoi(v) : 1; }
-        else if (!strcmp(a, "--slevel")) { const char* v = val(); if (!v) return usage(); cfg.slevel = atoi(v); }
-        else if (!strcmp(a, "--qlevel")) { const char* v = val(); if (!v) return usage(); cfg.qlevel = atoi(v); }
-        else if (!strcmp(a, "--device")) { const char* v = val(); if (!v) return usage(); device = atoi(v); }
-        else if (!strcmp(a, "--devices")) { const char* v = val(); if (!v) return usage(); devices = atoi(v) > 0 ? atoi(v) : 1; }
-        else if (!strcmp(a, "--share-device")) share_device = true;
-        else if (!strcmp(a, "--block-size")) { const char* v = val(); if (!v) return usage(); block_mib = atoi(v) > 0 ? atoi(v) : 50; }
-        else if (!strcmp(a, "--batch")) { const char* v = val(); if (!v) return usage(); batch = atoi(v) > 0 ? atoi(v) : 1; }
-        else if (!strcmp(a, "-d")) decompress = true;
-        else if (a[0] != '-' && decompress && !arc) arc = a;
-        else if (a[0] != '-' && decompress && !outp) outp = a;
+        auto ival = [&](int& dst, int lo) -> bool {
+            const char* v = val();
+            if (!v) return false;
+            dst = std::max(lo, atoi(v));
+            return true;
+        };
+        if (!strcmp(a, "-c")) o.compress = true;
+        else if (!strcmp(a, "-d")) o.decompress = true;
+        else if (!strcmp(a, "-1")) { if (!(o.f1 = val())) return usage(); }
+        else if (!strcmp(a, "-2")) { if (!(o.f2 = val())) return usage(); }
+        else if (!strcmp(a, "-o")) { if (!(o.out = val())) return usage(); }
+        else if (!strcmp(a, "-n")) o.cfg.md5 = 0;
+        else if (!strcmp(a, "-f")) o.force = true;
+        else if (!strcmp(a, "-p")) o.in_dir = true;
+        else if (!strcmp(a, "-l")) { const char* v = val(); if (!v) return usage(); o.cfg.lossy = atof(v); }
+        else if (!strcmp(a, "-P")) { if (!ival(o.pipe, 0)) return usage(); }
+        else if (!strcmp(a, "-t")) { if (!ival(o.threads, 1)) return usage(); }
+        else if (!strcmp(a, "--slevel")) { if (!ival(o.cfg.slevel, 0)) return usage(); }
+        else if (!strcmp(a, "--qlevel")) { if (!ival(o.cfg.qlevel, 0)) return usage(); }
+        else if (!strcmp(a, "--device")) { if (!ival(o.device, 0)) return usage(); }
+        else if (!strcmp(a, "--devices")) { if (!ival(o.devices, 1)) return usage(); }
+        else if (!strcmp(a, "--contexts")) { if (!ival(o.contexts, 1)) return usage(); }
+        else if (!strcmp(a, "--batch")) { if (!ival(o.batch, 1)) return usage(); }
+        else if (!strcmp(a, "--block-size")) { if (!ival(o.block_mib, 1)) return usage(); }
+        else if (!strcmp(a, "--share-device")) o.share_device = true;
+        else if (a[0] != '-') pos.push_back(a);
         else return usage();
     }
-    if (decompress) {
-        if (!arc || !outp) return usage();
-        return decode_archive(arc, outp, cfg, threads);
+    if (o.compress == o.decompress) return usage();
+    if (o.decompress) {
+        // SeqArc -d [ref.fa] ARCHIVE [PREFIX]: a reference index is not part of this build
+        if (pos.empty() || pos.size() > 2) return usage();
+        o.arc = pos[0];
+        if (pos.size() == 2 && !o.out) o.out = pos[1];
+        return decompress(o);
     }
-    if (!compress || !f1 || !outp) return usage();
-    const bool pe = f2 && *f2;
-
-    std::vector<uint8_t> t1, t2;
-    bool gz1 = false, gz2 = false;
-    if (!slurp(f1, t1, gz1) || (pe && !slurp(f2, t2, gz2))) {
-        fprintf(stderr, "seqarc_amd: cannot read input\n");
-        return 1;
-    }
-    const uint64_t bs = (uint64_t)block_mib << 20;   // BlockSize(M), default 50 (param+0x1b78)
-    const uint64_t maxb = (t1.size() + t2.size()) / 1024 + 16;
-    std::vector<uint64_t> e1(maxb), e2(maxb);
-    const int64_t nb = pe ? sa_cut_pe(t1.data(), t1.size(), t2.data(), t2.size(), bs, e1.data(), e2.data(), maxb)
-                          : sa_cut_se(t1.data(), t1.size(), bs, e1.data(), maxb);
-    if (nb < 0) {
-        fprintf(stderr, "seqarc_amd: block cut failed\n");
-        return 1;
-    }
-    auto parse = [&](int64_t b, Parsed& p) -> bool {
-        const uint64_t s1 = b ? e1[b - 1] : 0, s2 = (pe && b) ? e2[b - 1] : 0;
-        const uint64_t l1 = e1[b] - s1, l2 = pe ? e2[b] - s2 : 0;
-        const uint64_t cap = l1 + l2 + 16;
-        p.names.resize(cap); p.seq.resize(cap); p.qual.resize(cap);
-        p.nl.resize(cap / 4 + 8); p.sl.resize(cap / 4 + 8);
-        const int64_t n = pe ? sa_parse_pe(t1.data() + s1, l1, t2.data() + s2, l2, p.names.data(), p.nl.data(),
-                                           p.seq.data(), p.sl.data(), p.qual.data())
-                             : sa_parse_se(t1.data() + s1, l1, p.names.data(), p.nl.data(), p.seq.data(), p.sl.data(),
-                                           p.qual.data());
-        if (n < 0) return false;
-        p.nreads = (uint32_t)n;
-        p.text1 = l1;
-        p.text2 = l2;
-        return true;
-    };
-
-    uint8_t tmpl[512] = {0};
-    if (nb > 0) {
-        Parsed first;
-        if (!parse(0, first)) { fprintf(stderr, "seqarc_amd: parse failed\n"); return 1; }
-        const sa_block fb = first.view();
-        if (sa_analyze_ids(&fb, pe ? 0 : 1, tmpl) != 0) {
-            fprintf(stderr, "seqarc_amd: ID analysis failed\n");
-            return 1;
+    // SeqArc -c [ref.fa] -1 A [-2 B] OUT
+    for (const char* p : pos) {
+        const std::string s(p);
+        const std::string ext = s.size() > 3 ? s.substr(s.rfind('.') == std::string::npos ? s.size() : s.rfind('.')) : "";
+        if (ext == ".fa" || ext == ".fasta" || ext == ".fna") {
+            fprintf(stderr, "seqarc_amd: reference-index compression (%s) is not part of this build\n", p);
+            return 2;
         }
+        if (o.out) return usage();
+        o.out = p;
     }
-    cfg.bin_mode = tmpl[0];
-
-    // one encoder context (and host thread) per device: batches of blocks are
-    // dealt to the devices in order, encoded independently (blocks share no
-    // model state), and gathered back in input order by this thread
-    std::vector<sa_ctx*> ctxs;
-    for (int d = 0; d < devices; d++) {
-        sa_ctx* c = sa_create(device + (share_device ? 0 : d));
-        if (!c) {
-            if (ctxs.empty()) { fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", device); return 1; }
-            break;   // fewer devices than asked for: use those present
-        }
-        ctxs.push_back(c);
-    }
-    const std::string path = std::string(outp) + ".arc";
-    FILE* fo = fopen(path.c_str(), "wb");
-    if (!fo) {
-        fprintf(stderr, "seqarc_amd: cannot write %s\n", path.c_str());
-        for (sa_ctx* c : ctxs) sa_destroy(c);
-        return 1;
-    }
-    uint8_t hdr[16] = {0};
-    fwrite(hdr, 1, 16, fo);   // patched at the end (createOutFile@0x417480 / writeFileInfo@0x4171b0)
-    std::vector<sa_arc_block> info;
-    uint64_t total = 0;
-    int rc = 0;
-    struct Batch {
-        std::vector<Parsed> ps;
-        std::vector<std::vector<uint8_t>> bufs;
-        std::vector<sa_out> outs;
-        int status = 0;   // 0 pending, 1 done, -1 failed
-        std::string err;
-    };
-    const int64_t nbatch = (nb + batch - 1) / batch;
-    std::vector<Batch> bt((size_t)nbatch);
-    std::mutex mu;
-    std::condition_variable cv;
-    std::atomic<int64_t> next{0};
-    std::atomic<bool> stop{false};
-    const size_t max_ahead = 2 * ctxs.size();   // batches held in memory beyond the writer
-    int64_t written = 0;
-    auto worker = [&](sa_ctx* ctx) {
-        for (;;) {
-            int64_t k;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop || next.load() < written + (int64_t)max_ahead || next.load() >= nbatch; });
-                if (stop || next.load() >= nbatch) return;
-                k = next++;
-            }
-            Batch& B = bt[(size_t)k];
-            const int64_t b0 = k * batch, n = std::min<int64_t>(batch, nb - b0);
-            B.ps.resize((size_t)n);
-            B.bufs.resize((size_t)n);
-            B.outs.resize((size_t)n);
-            std::vector<sa_block> in((size_t)n);
-            int st = 1;
-            for (int64_t i = 0; i < n; i++) {
-                if (!parse(b0 + i, B.ps[(size_t)i])) { st = -1; B.err = "parse failed"; break; }
-                in[(size_t)i] = B.ps[(size_t)i].view();
-                B.bufs[(size_t)i].resize(sa_output_bound(&in[(size_t)i]));
-                B.outs[(size_t)i] = sa_out{B.bufs[(size_t)i].data(), B.bufs[(size_t)i].size(), 0};
-            }
-            if (st > 0 && sa_encode_blocks(ctx, in.data(), (int)n, &cfg, B.outs.data()) != 0) {
-                st = -1;
-                B.err = std::string("encode failed: ") + sa_last_error(ctx);
-            }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                B.status = st;
-            }
-            cv.notify_all();
-        }
-    };
-    std::vector<std::thread> th;
-    for (sa_ctx* c : ctxs) th.emplace_back(worker, c);
-    for (int64_t k = 0; k < nbatch && !rc; k++) {
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return bt[(size_t)k].status != 0; });
-        }
-        Batch& B = bt[(size_t)k];
-        if (B.status < 0) { fprintf(stderr, "seqarc_amd: %s\n", B.err.c_str()); rc = 1; break; }
-        for (size_t i = 0; i < B.ps.size(); i++) {
-            const Parsed& p = B.ps[i];
-            uint32_t lng = 0;
-            for (uint32_t r = 0; r < p.nreads; r++) lng |= p.sl[r] > 0xffff;
-            fwrite(B.outs[i].data, 1, B.outs[i].size, fo);
-            info.push_back(sa_arc_block{(uint32_t)B.outs[i].size, lng, p.text1, p.text2});
-            total += B.outs[i].size;
-        }
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            B = Batch{};
-            B.status = 1;
-            written = k + 1;
-        }
-        cv.notify_all();
-    }
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        stop = true;
-    }
-    cv.notify_all();
-    for (auto& x : th) x.join();
-    for (sa_ctx* c : ctxs) sa_destroy(c);
-    if (!rc) {
-        sa_arc_info ai{f1, pe ? f2 : nullptr, pe ? 1 : 0, gz1 ? 1 : 0, bare_plus(pe ? t2 : t1), cfg.md5,
-                       cfg.lossy > 0.0 ? 1 : 0, tmpl};
-        std::vector<uint8_t> tr(4096 + 40 * info.size());
-        const int64_t tl = sa_arc_trailer(&ai, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
-        if (tl < 0) { fprintf(stderr, "seqarc_amd: trailer failed\n"); rc = 1; }
-        else {
-            fwrite(tr.data(), 1, (size_t)tl, fo);
-            sa_arc_header(total, hdr);
-            fseek(fo, 0, SEEK_SET);
-            fwrite(hdr, 1, 16, fo);
-            fprintf(stderr, "seqarc_amd: %lld block(s), %llu -> %llu bytes (%.2fx)\n", (long long)nb,
-                    (unsigned long long)(t1.size() + t2.size()), (unsigned long long)(16 + total + tl),
-                    (double)(t1.size() + t2.size()) / (double)(16 + total + tl));
-        }
-    }
-    fclose(fo);
-    return rc;
+    if (!o.f1 || !o.out) return usage();
+    return compress(o);
 }

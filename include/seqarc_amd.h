@@ -57,6 +57,11 @@ typedef struct {
 
 /* ---- lifecycle ------------------------------------------------------- */
 sa_ctx *sa_create(int device);               /* NULL if no usable gfx950 device */
+/* A context of the same device sharing `peer`'s front scratch: the contexts'
+ * throughput-bound fronts (symbol extraction, sorts, short model runs) run one
+ * at a time on it while each one's latency-bound range coder chains overlap the
+ * next front (the pipeline of encoder lanes on one GPU). */
+sa_ctx *sa_create_shared(int device, sa_ctx *peer);
 void sa_destroy(sa_ctx *ctx);
 const char *sa_last_error(const sa_ctx *ctx);
 const char *sa_version(void);
@@ -77,6 +82,8 @@ int sa_phase_times(const sa_ctx *ctx, const char **names, float *ms, int max);
 void sa_set_timing(sa_ctx *ctx, int on);
 /* HBM bytes the context's work buffers hold (they grow to the largest batch) */
 uint64_t sa_device_bytes(const sa_ctx *ctx);
+/* HBM bytes of the (possibly shared) front scratch */
+uint64_t sa_front_bytes(const sa_ctx *ctx);
 
 /* ---- resident inputs: a batch uploaded once, encoded by any context ----
  * The reference keeps a pool of parsed blocks between its reader and its
@@ -111,6 +118,16 @@ int64_t sa_cut_se(const uint8_t *text, uint64_t len, uint64_t block_size,
                   uint64_t *ends, uint64_t max_blocks);
 int64_t sa_cut_pe(const uint8_t *t1, uint64_t len1, const uint8_t *t2, uint64_t len2,
                   uint64_t block_size, uint64_t *ends1, uint64_t *ends2, uint64_t max_blocks);
+/* Streaming forms (the reader thread's view, doReadJob / doReadPEJob): the end of
+ * the next block in a window of the input that starts at a block boundary.
+ * first/flen: the input's first line, '\n' included (getFirstLine@0x431eb0);
+ * eof: the window holds the rest of that input.  SE: returns the block's
+ * bytes, or -1 when the window is too short (read more) or no cut exists.  PE:
+ * 0 and the block's bytes of each file in end1/end2, or -1 likewise. */
+int64_t sa_cut_next_se(const uint8_t *win, uint64_t avail, int eof, uint64_t block_size,
+                       const uint8_t *first, uint64_t flen);
+int sa_cut_next_pe(const uint8_t *w1, uint64_t avail1, int eof1, const uint8_t *w2, uint64_t avail2, int eof2,
+                   uint64_t block_size, const uint8_t *first, uint64_t flen, uint64_t *end1, uint64_t *end2);
 /* Block parse: getBlockRead@0x411b60 (SE) / getBlockReadPE@0x412920 (PE).
  * Output arrays sized >= text bytes (names/seq/qual) and text/4+1 (lens). */
 int64_t sa_parse_se(const uint8_t *text, uint64_t len, uint8_t *names, uint16_t *name_lens,

@@ -86,13 +86,14 @@ def test_trailer_fields_pe_and_se():
     assert sorted(f) == list(range(1, 19)) and f[14] == b"ERR2755197_test_2.fq"
     assert f[13] == b"ERR2755197_test_1.fq" and f[15] == tmpl.tobytes()
     assert f[1] == b"\x01" and f[17] == b"\x01" and f[16] == b"\x00"
+    assert f[3] == b"\x00"                        # param+0x5: set by -1, cleared by -2 (parseOptFromCmd@0x40b460)
     assert struct.unpack("<H", f[9])[0] == 6 and struct.unpack("<I", f[11])[0] == 1
     size2, l1, l2, pad, off, o1, o2 = struct.unpack("<IIIIQQQ", table)
     assert size2 >> 1 == len(enc[0]) and size2 & 1 == 0 and off == 16
     assert (l1, l2) == (os.path.getsize(T1), os.path.getsize(T2)) and (pad, o1, o2) == (0, 0, 0)
     se, enc, _, _ = _archive([T1])
     f, table = _fields(se[16 + sum(map(len, enc)):])
-    assert 14 not in f and len(table) == 32
+    assert 14 not in f and len(table) == 32 and f[3] == b"\x01"   # single-end
     size2, fi, l1, pad, off, o1 = struct.unpack("<IIIIQQ", table)
     assert size2 >> 1 == len(enc[0]) and fi == 1 and l1 == os.path.getsize(T1) and off == 16
 

@@ -1,0 +1,156 @@
+"""The seqarc_amd command line without a GPU: the decode side (-d, -P, -f, -p,
+output naming of SeqArcParam::getDecodeFile@0x405f70) on archives built from
+the CPU restatement's blocks, and the streaming block cut the -c reader uses
+(sa_cut_next_se / sa_cut_next_pe) against the whole-buffer cut."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py
+import synth
+from conftest import GOLDEN
+
+import fastqueeze_amd as fq
+from fastqueeze_amd import build
+
+EXE = build.CLI
+
+
+def _write_archive(tmp_path, texts, names, arc="t.arc", block_size=fq.BLOCK_SIZE, gz1=False):
+    blocks = fq.blocks_from_fastq(texts[0], texts[1] if len(texts) > 1 else None, block_size)
+    tmpl = fq.analyze_ids(blocks[0], len(texts) == 1)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    enc = [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode) for b in blocks]
+    data = fq.arc_archive(enc, blocks, names[0], names[1] if len(names) > 1 else None, tmpl, cfg, gz1=gz1,
+                          plus_bare=fq.bare_plus(texts[-1]))
+    path = tmp_path / arc
+    path.write_bytes(data)
+    return str(path), len(blocks)
+
+
+def _run(args, cwd):
+    return subprocess.run([EXE] + args, capture_output=True, cwd=cwd, timeout=300)
+
+
+def _records(text):
+    lines = text.split(b"\n")
+    return [b"\n".join(lines[i:i + 4]) + b"\n" for i in range(0, len(lines) - 1, 4)]
+
+
+@pytest.fixture(scope="module")
+def pair():
+    a, b = synth.generate(3000, paired=True, seed=61)
+    return a, b
+
+
+def test_pipe_out_se_pe1_pe2_interleaved(tmp_path, pair):
+    """-P 1 / 2 / 3 (DecodePipeOutJob::recoverData*@0x42f930): SE reads, PE1,
+    PE2 and each pair in order, on stdout, over a multi-block archive."""
+    a, b = pair
+    arc, nb = _write_archive(tmp_path, (a, b), ["p_1.fq", "p_2.fq"], block_size=200_000)
+    assert nb > 3
+    assert _run(["-d", "-P", "1", arc], tmp_path).stdout == a
+    assert _run(["-d", "-P", "2", arc], tmp_path).stdout == b
+    inter = b"".join(x + y for x, y in zip(_records(a), _records(b)))
+    assert _run(["-d", "-t", "4", "-P", "3", arc], tmp_path).stdout == inter
+    se, _ = _write_archive(tmp_path, (a,), ["s.fq"], arc="s.arc", block_size=150_000)
+    assert _run(["-d", "-P", "1", se], tmp_path).stdout == a
+    with open(os.path.join(GOLDEN, "ERR2755197_test_1.fq"), "rb") as f:
+        t1 = f.read()
+    ref, _ = _write_archive(tmp_path, (t1,), ["ERR2755197_test_1.fq"], arc="r.arc")
+    assert _run(["-d", "-P", "1", ref], tmp_path).stdout == t1   # ID-bin names, bare '+'
+
+
+def test_decode_names_force_and_dir(tmp_path, pair):
+    """Outputs: PREFIX_1/_2.fastq (PE) or PREFIX.fastq (SE) (appendname@0x405f10);
+    without a prefix the stored input names (3 more bytes cut after a gzip
+    input 1, as the binary does); an existing output stops the run ("has
+    exist!") unless -f; -p writes next to the archive."""
+    a, b = pair
+    sub = tmp_path / "arcdir"
+    sub.mkdir()
+    arc, _ = _write_archive(sub, (a, b), ["m_1.fq", "m_2.fq"])
+    r = _run(["-d", arc, "back"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "back_1.fastq").read_bytes() == a and (tmp_path / "back_2.fastq").read_bytes() == b
+    r = _run(["-d", arc, "-o", "back"], tmp_path)
+    assert r.returncode == 1 and b"has exist!" in r.stderr
+    r = _run(["-d", "-f", arc, "-o", "back"], tmp_path)
+    assert r.returncode == 0
+    r = _run(["-d", arc], tmp_path)   # the stored names
+    assert r.returncode == 0 and (tmp_path / "m_1.fq").read_bytes() == a and (tmp_path / "m_2.fq").read_bytes() == b
+    r = _run(["-d", "-p", arc, "x"], tmp_path)
+    assert r.returncode == 0 and (sub / "x_1.fastq").read_bytes() == a
+    se, _ = _write_archive(tmp_path, (a,), ["reads.fq.gz"], arc="se.arc", gz1=True)
+    r = _run(["-d", se, "s"], tmp_path)
+    assert r.returncode == 0 and (tmp_path / "s.fastq").read_bytes() == a
+    r = _run(["-d", se], tmp_path)   # "reads.fq" stored, 3 more bytes cut for the gzip input
+    assert r.returncode == 0 and (tmp_path / "reads").read_bytes() == a
+
+
+def test_compress_usage_errors(tmp_path):
+    """-c argument checks that need no GPU: missing / empty input, a reference
+    index (not part of this build)."""
+    r = _run(["-c", "-1", str(tmp_path / "missing.fq"), "-o", "x"], tmp_path)
+    assert r.returncode == 1 and b"may be not exist or empty" in r.stderr
+    (tmp_path / "e.fq").write_bytes(b"")
+    r = _run(["-c", "-1", str(tmp_path / "e.fq"), "x"], tmp_path)
+    assert r.returncode == 1
+    r = _run(["-c", "ref.fa", "-1", str(tmp_path / "e.fq"), "x"], tmp_path)
+    assert r.returncode == 2
+
+
+def _stream_cut(t1, t2, bs, step):
+    """The -c reader's loop over windows that grow `step` bytes at a time."""
+    lib = fq.load_library()
+    lib.sa_cut_next_se.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_uint64, C.c_void_p, C.c_uint64]
+    lib.sa_cut_next_se.restype = C.c_int64
+    lib.sa_cut_next_pe.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_uint64,
+                                   C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    lib.sa_cut_next_pe.restype = C.c_int
+    a = np.frombuffer(t1, np.uint8)
+    b = np.frombuffer(t2, np.uint8) if t2 is not None else None
+    first = a[: int(np.flatnonzero(a == 10)[0]) + 1].copy()
+    o1 = o2 = 0
+    h1 = h2 = 0   # bytes "read" so far
+    out = []
+    while o1 < a.size or (b is not None and o2 < b.size):
+        h1 = min(a.size, max(h1, o1 + step))
+        w1 = a[o1:h1]
+        eof1 = int(h1 == a.size)
+        if b is None:
+            e = lib.sa_cut_next_se(w1.ctypes.data, w1.size, eof1, bs, first.ctypes.data, first.size)
+            if e < 0:
+                assert not eof1
+                h1 += step
+                continue
+            out.append((o1, o1 + e))
+            o1 += e
+        else:
+            h2 = min(b.size, max(h2, o2 + step))
+            w2 = b[o2:h2]
+            eof2 = int(h2 == b.size)
+            e1, e2 = C.c_uint64(0), C.c_uint64(0)
+            if lib.sa_cut_next_pe(w1.ctypes.data, w1.size, eof1, w2.ctypes.data, w2.size, eof2, bs,
+                                  first.ctypes.data, first.size, C.byref(e1), C.byref(e2)) != 0:
+                assert not (eof1 and eof2)
+                h1 += step
+                h2 += step
+                continue
+            out.append(((o1, o1 + e1.value), (o2, o2 + e2.value)))
+            o1 += e1.value
+            o2 += e2.value
+    return out
+
+
+@pytest.mark.parametrize("step", [70_000, 1 << 20])
+def test_streaming_cut_equals_whole_buffer_cut(pair, step):
+    a, b = pair
+    bs = 300_000
+    assert _stream_cut(a, None, bs, step) == [tuple(x) for x in fq.cut_se(a, bs)]
+    _, short = synth.generate(3000, paired=True, seed=62, read_len=90)   # mates of unequal length
+    assert _stream_cut(a, short, bs, step) == [tuple(map(tuple, x)) for x in fq.cut_pe(a, short, bs)]
+    assert _stream_cut(a, b, bs, step) == [tuple(map(tuple, x)) for x in fq.cut_pe(a, b, bs)]

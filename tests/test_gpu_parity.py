@@ -109,6 +109,16 @@ def test_full_size_block(enc):
     assert np.array_equal(seq, b.seq) and np.array_equal(sl, b.seq_lens) and np.array_equal(qual, b.qual)
 
 
+def test_exact_payload_fallback(enc, monkeypatch):
+    """The payload arena is sized from the streams' real byte counts after L2
+    with slack for squeeze restarts; with no slack the tiny streams outgrow it
+    (their 8 flush bytes) and the batch is re-encoded with the 2-byte-per-symbol
+    caps -- same bytes."""
+    blocks = fq.blocks_from_fastq(synth.edge_cases())
+    monkeypatch.setenv("SA_PAYLOAD_SLACK", "0")
+    _check(enc, blocks, fq.Config())
+
+
 def test_deterministic_rerun(enc):
     a, b = synth.generate(2000, paired=True, seed=4)
     blocks = fq.blocks_from_fastq(a, b)
@@ -257,12 +267,16 @@ def test_cli_multi_device_gather(tmp_path, test_pair):
     for p, t in zip(paths, test_pair):
         open(p, "wb").write(t)
     base = [exe, "-c", "-1", paths[0], "-2", paths[1], "--block-size", "1", "--batch", "1"]
-    r1 = subprocess.run(base + ["-o", str(tmp_path / "one")], capture_output=True, text=True, timeout=120)
+    r1 = subprocess.run(base + ["--contexts", "1", "-o", str(tmp_path / "one")], capture_output=True, text=True,
+                        timeout=120)
     r3 = subprocess.run(base + ["--devices", "3", "--share-device", "-o", str(tmp_path / "three")],
                         capture_output=True, text=True, timeout=120)
-    assert r1.returncode == 0 and r3.returncode == 0, (r1.stderr, r3.stderr)
+    # the streaming pipeline with several contexts sharing a front, 2-block batches, 2 parser threads
+    r4 = subprocess.run(base[:-1] + ["2", "--contexts", "3", "-t", "2", "-o", str(tmp_path / "four")],
+                        capture_output=True, text=True, timeout=120)
+    assert r1.returncode == 0 and r3.returncode == 0 and r4.returncode == 0, (r1.stderr, r3.stderr, r4.stderr)
     one = open(tmp_path / "one.arc", "rb").read()
-    assert one == open(tmp_path / "three.arc", "rb").read()
+    assert one == open(tmp_path / "three.arc", "rb").read() == open(tmp_path / "four.arc", "rb").read()
     blocks = fq.blocks_from_fastq(*test_pair, 1 << 20)
     assert len(blocks) > 3
     tmpl = fq.analyze_ids(blocks[0], False)
@@ -315,7 +329,8 @@ def test_full_size_block_slevel8(enc, pe_full):
 
 def test_resident_inputs_concurrent_contexts(pe_full):
     """sa_input_create / sa_run_input: two resident batches encoded by two contexts
-    from two host threads at once (the bench's pipeline) == the oracle."""
+    sharing one front scratch (sa_create_shared) from two host threads at once
+    (the bench's pipeline) == the oracle."""
     import threading
     a, b = synth.generate(20000, paired=True, seed=77)
     b1 = fq.blocks_from_fastq(a, b, 2_000_000)
@@ -323,7 +338,8 @@ def test_resident_inputs_concurrent_contexts(pe_full):
     cfg = fq.Config()
     want = {0: _oracle_outs(b1, cfg), 1: _oracle_outs(b2, cfg)}
     inputs = [fq.Input(b1, 0), fq.Input(b2, 0)]
-    encs = [fq.Encoder(0), fq.Encoder(0)]
+    e0 = fq.Encoder(0)
+    encs = [e0, fq.Encoder(0, share_with=e0)]   # one front scratch, fronts one at a time
     got, errs = {}, []
 
     def work(i):
