@@ -73,14 +73,16 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (each leg)")
     ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: the CPU share)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--e2e-batches", type=int, default=1,
-                    help="batches written to disk for the end-to-end seqarc_amd -c run (0: skip)")
-    ap.add_argument("--e2e-dir", default=os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--e2e-batches", type=int, default=-1,
+                    help="batches written as FASTQ files for the end-to-end seqarc_amd -c run (-1: all, 0: skip)")
+    ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
                          "(scripts/pmc_traffic.py), committed under profiles/")
     a = ap.parse_args(argv)
+    if a.e2e_batches < 0:
+        a.e2e_batches = a.batches
     if a.dry_run:
         a.pairs = min(a.pairs, 3000)
         a.block_size = min(a.block_size, 300_000)
@@ -149,7 +151,7 @@ def end_to_end(args, files, contexts, expect: bytes, nblocks: int, threads: int)
     from fastqueeze_amd import build
     out = os.path.join(os.path.dirname(files[0]), "e2e")
     batch = max(1, -(-nblocks // (2 * contexts)))   # every context gets >= 2 batches
-    cmd = [build.CLI, "-c", "-f", "-t", str(threads), "-1", files[0]] + (["-2", files[1]] if len(files) > 1 else []) \
+    cmd = [build.CLI, "-c", "-f", "-v", "-t", str(threads), "-1", files[0]] + (["-2", files[1]] if len(files) > 1 else []) \
         + ["-o", out, "--contexts", str(contexts), "--batch", str(batch), "--slevel", str(args.slevel),
            "--qlevel", str(args.qlevel)]
     t0 = time.perf_counter()
@@ -160,15 +162,17 @@ def end_to_end(args, files, contexts, expect: bytes, nblocks: int, threads: int)
     in_bytes = sum(os.path.getsize(f) for f in files)
     with open(out + ".arc", "rb") as f:
         arc = f.read()
-    same = arc[16:16 + len(expect)] == expect if expect else None
-    clock = None
+    same = arc[16:16 + len(expect)] == expect   # (the batch's last, short block merges with the next batch's text)
+    clock, stages = None, None
     for ln in r.stderr.splitlines():
         if "MB/s" in ln:
             clock = float(ln.rsplit(",", 1)[1].split()[0])
+        if "contexts ready" in ln:
+            stages = ln.split(": ", 1)[1]
     os.remove(out + ".arc")
     return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
-            "cli_clock_mb_s": clock, "fastq_bytes": in_bytes, "contexts": contexts, "batch_blocks": batch,
-            "parse_threads": threads, "first_batch_blocks_identical": same,
+            "cli_clock_mb_s": clock, "cli_stages": stages, "fastq_bytes": in_bytes, "contexts": contexts, "batch_blocks": batch,
+            "parse_threads": threads, "leading_blocks_identical_to_bench": same,
             "command": "seqarc_amd -c -1 r1.fq -2 r2.fq (FASTQ on disk, page cache warm)"}
 
 
@@ -296,6 +300,9 @@ def main():
         d = os.path.join(args.e2e_dir, f"seqarc_bench_{os.getpid()}")
         os.makedirs(d, exist_ok=True)
         e2e_files = [os.path.join(d, "r1.fq")] + ([] if args.se else [os.path.join(d, "r2.fq")])
+        import atexit
+        import shutil
+        atexit.register(shutil.rmtree, d, True)   # /dev/shm is memory: never leave the files behind
         for f in e2e_files:
             open(f, "wb").close()
     for k, g in enumerate(gids):
@@ -473,12 +480,12 @@ def main():
         # the whole host path: the CLI reads the FASTQ from disk (HBM of the bench's
         # contexts released above); per rank, then max over ranks
         barrier()
-        expect = b"".join(outs) if args.e2e_batches == 1 else None
-        e2e = end_to_end(args, e2e_files, args.contexts, expect, len(keep["verify"]) * args.e2e_batches,
-                         max(1, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
-        for f in e2e_files:
-            os.remove(f)
-        os.rmdir(os.path.dirname(e2e_files[0]))
+        expect = b"".join(outs if args.e2e_batches == 1 else outs[:-1])
+        try:
+            e2e = end_to_end(args, e2e_files, args.contexts, expect, len(keep["verify"]) * args.e2e_batches,
+                             max(1, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
+        finally:
+            shutil.rmtree(os.path.dirname(e2e_files[0]), True)
         if world > 1:
             t = torch.tensor([e2e["wall_s"], float(e2e["fastq_bytes"])], dtype=torch.float64)
             tm = t.clone()

@@ -572,12 +572,14 @@ uint64_t sa_output_bound(const sa_block* b)
         nb += (uint64_t)(b->seq_lens[r] > 0 ? b->seq_lens[r] : 0);
         nn += b->name_lens[r];
     }
-    // every stream's coder output is bounded by 2 bytes per symbol + flush
-    return 4096 + 2 * (nb + 3ull * b->nreads)          /* seq, len  */
-           + 2 * (nn + 3ull * b->nreads)                /* names     */
-           + 2 * (nb + b->nreads)                       /* qual      */
-           + 2 * (b->nreads + 2 * nb) + 68ull * 2 * nb  /* dege      */
-           + nn;
+    // coded symbols per stream: len <= 5 per read, names <= 3 per read + the
+    // name bytes, quals <= bases + 1 per read, tip / max-qual 1 per read, N/IUPAC
+    // chars <= bases, exception counts <= 33 per read (kModel), gaps <= bases
+    // (1 + bits(g) symbols per g + 1 bases), bases; each symbol narrows the
+    // range by < 2^16 (<= 2 bytes); + per stream flush and header, the MD5s and
+    // the ID-bin first ID
+    const uint64_t syms = 3 * nb + nn + 45ull * b->nreads;
+    return 2 * syms + 9 * 96 + 4096 + 0x10000;
 }
 
 }  // extern "C"

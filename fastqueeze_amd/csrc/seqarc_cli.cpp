@@ -79,6 +79,38 @@ bool may_write(const std::string& path, bool force)
     return true;
 }
 
+// An uninitialised growable array (std::vector would zero-fill the tens of MB
+// of every block's buffers, which costs more than parsing them).
+template <class T>
+struct Buf {
+    std::unique_ptr<T[]> d;
+    size_t n = 0, cap = 0;
+    void reserve(size_t c)
+    {
+        if (c <= cap) return;
+        std::unique_ptr<T[]> nd(new T[c]);
+        if (n) memcpy(nd.get(), d.get(), n * sizeof(T));
+        d = std::move(nd);
+        cap = c;
+    }
+    void resize(size_t c)
+    {
+        reserve(c);
+        n = c;
+    }
+    void release()
+    {
+        d.reset();
+        n = cap = 0;
+    }
+    T& operator[](size_t i) { return d[i]; }
+    const T& operator[](size_t i) const { return d[i]; }
+    T* data() { return d.get(); }
+    const T* data() const { return d.get(); }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+};
+
 // ---- input ---------------------------------------------------------------
 // getFileType@0x40d9f0 (gzip magic); plain files are read with read(2), gzip
 // through zlib's gzread.
@@ -101,7 +133,7 @@ struct Input {
         return true;
     }
     // appends up to n bytes to b; false on a read error
-    bool fill(std::vector<uint8_t>& b, size_t n)
+    bool fill(Buf<uint8_t>& b, size_t n)
     {
         size_t have = b.size();
         b.resize(have + n);
@@ -130,23 +162,23 @@ struct Input {
 };
 
 struct Parsed {
-    std::vector<uint8_t> names, seq, qual;
-    std::vector<uint16_t> nl;
-    std::vector<int32_t> sl;
+    Buf<uint8_t> names, seq, qual;
+    Buf<uint16_t> nl;
+    Buf<int32_t> sl;
     uint32_t nreads = 0;
     uint64_t text1 = 0, text2 = 0;
     sa_block view() const { return sa_block{names.data(), nl.data(), seq.data(), sl.data(), qual.data(), nreads}; }
 };
 
 struct Job {                     // one block between the reader and the writer
-    std::vector<uint8_t> t1, t2;  // its FASTQ text (freed once parsed)
+    Buf<uint8_t> t1, t2;          // its FASTQ text (freed once parsed)
     Parsed p;
-    std::vector<uint8_t> out;     // the encoded block
+    Buf<uint8_t> out;             // the encoded block
     int state = 0;                // 0 read, 1 parsed, 2 encoded
 };
 
 // getFirstLine@0x431eb0: the '+' line of the first record carries no ID
-int bare_plus(const std::vector<uint8_t>& t)
+int bare_plus(const Buf<uint8_t>& t)
 {
     size_t nl[3] = {0, 0, 0};
     int k = 0;
@@ -178,19 +210,19 @@ bool parse_job(Job& j, bool pe)
         nb += p.nl[r];
         sb += (uint64_t)p.sl[r];
     }
-    p.names.resize(nb);
-    p.seq.resize(sb);
-    p.qual.resize(sb);
-    p.nl.resize(p.nreads);
-    p.sl.resize(p.nreads);
-    std::vector<uint8_t>().swap(j.t1);
-    std::vector<uint8_t>().swap(j.t2);
+    p.names.n = nb;
+    p.seq.n = sb;
+    p.qual.n = sb;
+    p.nl.n = p.nreads;
+    p.sl.n = p.nreads;
+    j.t1.release();
+    j.t2.release();
     return true;
 }
 
 struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr;
-    bool compress = false, decompress = false, force = false, in_dir = false, share_device = false;
+    bool compress = false, decompress = false, force = false, in_dir = false, share_device = false, verbose = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
 };
@@ -243,6 +275,10 @@ int compress(const Options& o)
     std::mutex mu;
     std::condition_variable cv;
     std::map<int64_t, std::unique_ptr<Job>> jobs;
+    // -v: when the stages first / last did something (seconds from the start)
+    auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
+    const double t_ctx = now_s();
+    std::atomic<double> t_read_done{0}, t_first_enc{1e30}, t_last_enc{0}, enc_busy{0}, parse_busy{0};
     std::deque<int64_t> to_parse;
     int64_t nread = 0, nblocks = -1, written = 0, next_batch = 0;
     bool failed = false, tmpl_ready = false;
@@ -260,7 +296,8 @@ int compress(const Options& o)
 
     // reader: cuts blocks as the input arrives
     std::thread reader([&]() {
-        std::vector<uint8_t> b1, b2, first;
+        Buf<uint8_t> b1, b2;
+        std::vector<uint8_t> first;
         const uint64_t want = pe ? (uint64_t)((uint32_t)bs >> 1) : bs;
         for (int64_t i = 0;; i++) {
             {
@@ -281,7 +318,8 @@ int compress(const Options& o)
             }
             if (i == 0) {
                 const void* nl = memchr(b1.data(), '\n', b1.size());
-                first.assign(b1.begin(), nl ? b1.begin() + ((const uint8_t*)nl - b1.data()) + 1 : b1.end());
+                const uint8_t* f0 = b1.data();
+                first.assign(f0, nl ? (const uint8_t*)nl + 1 : f0 + b1.size());
                 plus_bare = bare_plus(pe ? b2 : b1);
             }
             uint64_t e1 = 0, e2 = 0;
@@ -295,15 +333,19 @@ int compress(const Options& o)
                 e1 = (uint64_t)e;
             }
             std::unique_ptr<Job> j(new Job());
-            j->t1.assign(b1.begin() + (ptrdiff_t)e1, b1.end());   // the carry, swapped in below
-            j->t1.swap(b1);
-            j->t1.resize(e1);
-            if (pe) {
-                j->t2.assign(b2.begin() + (ptrdiff_t)e2, b2.end());
-                j->t2.swap(b2);
-                j->t2.resize(e2);
-            }
+            auto hand_over = [&](Buf<uint8_t>& b, Buf<uint8_t>& to, uint64_t e) {
+                Buf<uint8_t> carry;   // the bytes after the cut start the next window
+                carry.reserve(want);
+                memcpy(carry.data(), b.data() + e, b.size() - e);
+                carry.n = b.size() - e;
+                b.n = e;
+                to = std::move(b);
+                b = std::move(carry);
+            };
+            hand_over(b1, j->t1, e1);
+            if (pe) hand_over(b2, j->t2, e2);
             const bool last = b1.empty() && b2.empty() && in1.eof && (!pe || in2.eof);
+            if (last) t_read_done = now_s();
             {
                 std::lock_guard<std::mutex> g(mu);
                 total_in += e1 + e2;
@@ -332,7 +374,12 @@ int compress(const Options& o)
                     to_parse.pop_front();
                     j = jobs[i].get();
                 }
+                const double tp = now_s();
                 if (!parse_job(*j, pe)) return fail("parse failed");
+                {
+                    double cur = parse_busy.load();
+                    while (!parse_busy.compare_exchange_weak(cur, cur + now_s() - tp)) {}
+                }
                 if (i == 0) {   // the ID template of the first block
                     const sa_block fb = j->p.view();
                     if (sa_analyze_ids(&fb, pe ? 0 : 1, tmpl) != 0) return fail("ID analysis failed");
@@ -379,16 +426,28 @@ int compress(const Options& o)
                 std::vector<sa_out> outs(js.size());
                 for (size_t i = 0; i < js.size(); i++) {
                     in[i] = js[i]->p.view();
-                    js[i]->out.resize(sa_output_bound(&in[i]));
+                    js[i]->out.resize(sa_output_bound(&in[i]));   // (uninitialised: only the real bytes are touched)
                     outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
                 }
                 const sa_cfg c = cfg;
+                const double te = now_s();
+                {
+                    double cur = t_first_enc.load();
+                    while (te < cur && !t_first_enc.compare_exchange_weak(cur, te)) {}
+                }
                 if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
                     return fail(std::string("encode failed: ") + sa_last_error(ctx));
                 {
+                    const double tf = now_s();
+                    double cur = enc_busy.load();
+                    while (!enc_busy.compare_exchange_weak(cur, cur + tf - te)) {}
+                    cur = t_last_enc.load();
+                    while (tf > cur && !t_last_enc.compare_exchange_weak(cur, tf)) {}
+                }
+                {
                     std::lock_guard<std::mutex> g(mu);
                     for (size_t i = 0; i < js.size(); i++) {
-                        js[i]->out.resize(outs[i].size);
+                        js[i]->out.n = outs[i].size;
                         js[i]->state = 2;
                     }
                 }
@@ -454,6 +513,12 @@ int compress(const Options& o)
         fseek(fo, 0, SEEK_SET);
         fwrite(hdr, 1, 16, fo);
         const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        if (o.verbose)
+            fprintf(stderr,
+                    "seqarc_amd: contexts ready %.3f s, input read %.3f s, first encode %.3f s, last encode "
+                    "done %.3f s; encode busy %.3f s over %zu contexts, parse busy %.3f s over %d threads\n",
+                    t_ctx, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
+                    parse_busy.load(), nparse);
         fprintf(stderr, "seqarc_amd: %zu block(s), %llu -> %llu bytes (%.2fx), %.3f s, %.1f MB/s\n", info.size(),
                 (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
                 (double)total_in / (double)(16 + total + tl), secs, (double)total_in / secs / 1e6);
@@ -693,6 +758,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--batch")) { if (!ival(o.batch, 1)) return usage(); }
         else if (!strcmp(a, "--block-size")) { if (!ival(o.block_mib, 1)) return usage(); }
         else if (!strcmp(a, "--share-device")) o.share_device = true;
+        else if (!strcmp(a, "-v")) o.verbose = true;
         else if (a[0] != '-') pos.push_back(a);
         else return usage();
     }
