@@ -76,6 +76,7 @@ def parse_args(argv=None):
     ap.add_argument("--e2e-batches", type=int, default=-1,
                     help="batches written as FASTQ files for the end-to-end seqarc_amd -c run (-1: all, 0: skip)")
     ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--e2e-log", default=None, help="write the CLI's stderr (-v stage lines, SA_TRACE) here")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
@@ -159,6 +160,9 @@ def end_to_end(args, files, contexts, expect: bytes, nblocks: int, threads: int)
     wall = time.perf_counter() - t0
     if r.returncode != 0:
         raise SystemExit(f"end-to-end run failed: {r.stderr[-2000:]}")
+    if args.e2e_log:
+        with open(args.e2e_log, "w") as f:
+            f.write(r.stderr)
     in_bytes = sum(os.path.getsize(f) for f in files)
     with open(out + ".arc", "rb") as f:
         arc = f.read()

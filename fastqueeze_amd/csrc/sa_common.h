@@ -282,11 +282,12 @@ SA_HD bool name_mid(const uint8_t* name, int len, int p, int s, Last last, Emit 
 }
 
 // ---- range coder records ----------------------------------------------------
-// Pass-R record of one coded symbol: reciprocal m = ceil(2^32 / tot) and
-// tot | freq << 16.  q0 = mulhi(range, m) is q or q + 1 and q0 * tot never
-// wraps (DESIGN.md "Coder"), so one borrow corrects it.
-struct alignas(8) PRec {
-    uint32_t m;
+// Coder record of one coded symbol: tf = tot | freq << 16 (AUX; cum in its own
+// array) or tot | cum << 8 | freq << 16 (SEQ, tot <= 253).  The readers derive
+// the reciprocal m = ceil(2^32 / tot) themselves (recip32z, off the range
+// chain): q0 = mulhi(range, m) is q or q + 1 and q0 * tot never wraps
+// (DESIGN.md "Coder"), so one borrow corrects it.  4 bytes per symbol.
+struct PRec {
     uint32_t tf;
 };
 

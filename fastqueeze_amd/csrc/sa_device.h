@@ -69,11 +69,9 @@ struct RbRun {
 // A sort segment = one block's symbol space.
 struct SortSeg {
     uint64_t base;       // element offset (multiple of SORT_TILE)
-    uint64_t hist_base;  // offset of the segment's 256 x ntiles digit counts
     uint32_t count;      // real symbols (the rest of the last tile is padding)
     uint32_t tile0;      // global index of the segment's first tile
     uint32_t ntiles;
-    uint32_t pad_;
 };
 
 struct SortView {

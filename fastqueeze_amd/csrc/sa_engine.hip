@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -20,18 +22,29 @@ using namespace sa;
 
 namespace {
 
+std::atomic<uint32_t> g_grows{0};   // buffer re-allocations (each hipFree synchronises the device)
+std::atomic<uint64_t> g_alloc_ns{0};  // host time in hipMalloc / hipFree (SA_TRACE)
+
 struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
     hipError_t ensure(size_t bytes)
     {
         if (bytes <= cap && p) return hipSuccess;
-        if (p) (void)hipFree(p);
+        const auto t0 = std::chrono::steady_clock::now();
+        if (p) {
+            (void)hipFree(p);
+            g_grows++;
+        }
         p = nullptr;
-        size_t want = std::max(bytes, cap + cap / 16);   // slack for the next, slightly larger batch
+        // slack for the next, slightly larger batch: a re-allocation's hipFree
+        // synchronises the whole device, stalling every other context on it
+        size_t want = std::max(bytes + bytes / 16, cap + cap / 16);
         want = std::max<size_t>(want, 256);
         hipError_t e = hipMalloc(&p, want);
         cap = e == hipSuccess ? want : 0;
+        g_alloc_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now() - t0).count();
         return e;
     }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
@@ -110,16 +123,16 @@ struct sa_ctx {
     hipEvent_t ev_seq_done = nullptr, ev_long_done = nullptr;
     uint32_t long_lds = 0;
     bool serial_seq = false;
-    uint32_t pf_segs = PF_SEGS;
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     // pass-R placement (k_coder_rv): four chains per workgroup, one per SIMD, and
     // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
     // SA_CODER_LDS)
     uint32_t coder_waves = 4;
     uint32_t coder_lds = 82 * 1024;
-    uint32_t coder_vgpr = 1;   // pass R fed through VGPRs (k_coder_rv); SA_CODER_VGPR=0: the scalar-load pass
     std::string err;
     bool timing = false;
+    bool trace = std::getenv("SA_TRACE") != nullptr;
+    uint32_t n_cu = 256;
     uint32_t coder_restarts = 0;
     uint64_t max_stream_syms = 0, total_stream_syms = 0;
     hipEvent_t ev_beg[PH_N] = {}, ev_end[PH_N] = {};
@@ -197,7 +210,51 @@ struct sa_ctx {
 
 namespace {
 
-// sorts keys by bits [lo, hi) in 8-bit digits (bits below lo ride along)
+// grid of a wave-per-read, grid-stride kernel (EMIT_WAVES waves per workgroup):
+// 8 workgroups per CU, fewer for a small batch
+uint32_t wave_grid(const sa_ctx* c, uint32_t nreads)
+{
+    return std::max<uint32_t>(1, std::min<uint32_t>((nreads + EMIT_WAVES - 1) / EMIT_WAVES, 8 * c->n_cu));
+}
+
+// Digit widths of a sort over bits [lo, hi): the fewest passes of at most
+// SORT_MAX_DB bits, widths as even as possible and at least SORT_MIN_DB (a
+// digit may reach above hi: those key bits are 0, or 1 in the pad keys, which
+// sort last anyway).
+std::vector<int> sort_digits(int lo, int hi)
+{
+    std::vector<int> w;
+    if (hi <= lo) return w;
+    const int bits = hi - lo, passes = (bits + SORT_MAX_DB - 1) / SORT_MAX_DB;
+    for (int p = 0, done = 0; p < passes; p++) {
+        const int d = (bits - done + (passes - p) - 1) / (passes - p);
+        w.push_back(std::max(d, SORT_MIN_DB));
+        done += d;
+    }
+    return w;
+}
+
+// histogram words per tile of a sort over bits [lo, hi)
+uint64_t sort_hist_per_tile(int lo, int hi)
+{
+    int m = SORT_MIN_DB;
+    for (int d : sort_digits(lo, hi)) m = std::max(m, d);
+    return 1ull << m;
+}
+
+template <int DB>
+void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+               uint32_t* vout, uint32_t shift)
+{
+    hipLaunchKernelGGL(k_sort_hist<DB>, dim3((sv.ntiles + HIST_TILES - 1) / HIST_TILES), dim3(SORT_THREADS), 0, st,
+                       sv, kin, shift);
+    hipLaunchKernelGGL(k_sort_scan<DB>, dim3(sv.nsegs), dim3(1024), 0, st, sv);
+    hipLaunchKernelGGL(k_sort_scatter<DB>, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout, vout,
+                       shift);
+}
+
+// sorts keys by bits [lo, hi) (bits below lo ride along); the result is in
+// keys[result_buf] / vals[result_buf]
 int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
              DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf)
 {
@@ -210,14 +267,15 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     sv.total = plan.total;
     sv.ntiles = (uint32_t)plan.tile_seg.size();
     sv.nsegs = (uint32_t)plan.segs.size();
-    int cur = 0;
-    for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL(k_sort_hist, dim3((sv.ntiles + HIST_TILES - 1) / HIST_TILES), dim3(SORT_THREADS), 0, st, sv,
-                           keys[cur]->as<uint32_t>(), (uint32_t)shift);
-        hipLaunchKernelGGL(k_sort_scan, dim3(sv.nsegs), dim3(1024), 0, st, sv);
-        hipLaunchKernelGGL(k_sort_scatter, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv,
-                           keys[cur]->as<uint32_t>(), vals[cur]->as<uint32_t>(), keys[cur ^ 1]->as<uint32_t>(),
-                           vals[cur ^ 1]->as<uint32_t>(), (uint32_t)shift);
+    int cur = 0, shift = lo;
+    for (const int db : sort_digits(lo, hi)) {
+        const uint32_t* kin = keys[cur]->as<uint32_t>();
+        const uint32_t* vin = vals[cur]->as<uint32_t>();
+        uint32_t* kout = keys[cur ^ 1]->as<uint32_t>();
+        uint32_t* vout = vals[cur ^ 1]->as<uint32_t>();
+        if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
+        else sort_pass<9>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
+        shift += db;
         cur ^= 1;
     }
     SA_CHECK(c, hipGetLastError());
@@ -312,17 +370,8 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
 {
     if (!tl.count) return;
     if (ph >= 0) ev_begin(c, ph, st);
-    if (c->coder_vgpr) {
-        hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves),
-                           dim3(64 * c->coder_waves), c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r,
-                           c->d_err.as<uint32_t>(), c->chain_prio);
-        if (ph >= 0) ev_finish(c, ph, st);
-        return;
-    }
-    hipLaunchKernelGGL(k_coder_r, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
-                       c->coder_lds, st,
-                       cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
-                       reinterpret_cast<const uint2*>(cv.prs[0]), reinterpret_cast<const uint2*>(cv.prs[1]), c->pf_segs,
+    hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
+                       c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio);
     if (ph >= 0) ev_finish(c, ph, st);
 }
@@ -470,23 +519,22 @@ sa_ctx* sa_create(int device)
     }
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     sa_ctx* c = new sa_ctx();
-    // pass-R placement knobs (k_coder_r): waves per workgroup, unused LDS per workgroup
+    // pass-R placement knobs (k_coder_rv): waves per workgroup, unused LDS per workgroup
     if (const char* e = std::getenv("SA_CODER_WAVES")) {
         const int w = std::atoi(e);
         c->coder_waves = (w == 1 || w == 2) ? (uint32_t)w : 4u;
     }
-    if (const char* e = std::getenv("SA_CODER_VGPR")) c->coder_vgpr = std::atoi(e) != 0;
     if (const char* e = std::getenv("SA_CODER_LDS")) c->coder_lds = (uint32_t)std::min(std::max(std::atoi(e), 0), 160 * 1024);
     if (c->coder_lds > 64 * 1024 &&
-        (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_r), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)c->coder_lds) != hipSuccess ||
-         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)c->coder_lds) != hipSuccess)) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)c->coder_lds) != hipSuccess) {
         std::fprintf(stderr, "seqarc_amd: cannot reserve %u B of LDS for pass R\n", c->coder_lds);
         delete c;
         return nullptr;
     }
     c->device = device;
+    c->timing = c->trace;
+    c->n_cu = (uint32_t)prop.multiProcessorCount;
     for (int i = 0; i < PH_N; i++) c->ev_beg[i] = c->ev_end[i] = nullptr;
     // st carries the critical path (AUX symbols -> QUAL coder chain).  While the
     // long AUX model runs replay (latency-bound, st4: every 4th CU), the SEQ path
@@ -498,8 +546,6 @@ sa_ctx* sa_create(int device)
     const char* el = std::getenv("SA_LONG_LDS");
     c->long_lds = el ? (uint32_t)std::atoi(el) : 0u;
     c->serial_seq = std::getenv("SA_SERIAL_SEQ") != nullptr;
-    const char* ep = std::getenv("SA_PF_SEGS");   // pass R prefetch distance (tuning override)
-    c->pf_segs = ep ? (uint32_t)std::min(std::max(std::atoi(ep), 1), 64) : PF_SEGS;
     if (const char* cp = std::getenv("SA_CHAIN_PRIO")) c->chain_prio = std::atoi(cp) != 0;
     std::vector<uint32_t> m_long((prop.multiProcessorCount + 31) / 32, 0u), m_seq(m_long.size(), 0u);
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
@@ -840,7 +886,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     if (nr) {
         hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
                            F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(), d_err);
-        hipLaunchKernelGGL(k_prep_sq, dim3((nr + EMIT_WAVES - 1) / EMIT_WAVES), dim3(64 * EMIT_WAVES), 0, st, bv,
+        hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                            F->d_counts.as<uint32_t>(), d_err);
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, F->d_counts.as<uint32_t>(),
@@ -889,7 +935,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     SA_CHECK(c, c->d_auxp_v.ensure(atot * 4));
     // AUX sort ping-pong: the sorted keys/values must land in this context's
     // buffers (the long model runs read them after the front scratch is released)
-    const int aux_passes = (aux_bits + 7) / 8;
+    const int aux_passes = (int)sort_digits(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits).size();
     DBuf* akb[2] = {aux_passes % 2 ? &F->d_auxs_k : &c->d_auxp_k, aux_passes % 2 ? &c->d_auxp_k : &F->d_auxs_k};
     DBuf* avb[2] = {aux_passes % 2 ? &F->d_auxs_v : &c->d_auxp_v, aux_passes % 2 ? &c->d_auxp_v : &F->d_auxs_v};
     DBuf* skb[2] = {&F->d_seq_k[0], &F->d_seq_k[1]};
@@ -908,8 +954,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     // at most one run per (block, model) and per symbol
     const uint64_t max_short = std::max<uint64_t>(std::min<uint64_t>(pa.total, (uint64_t)nbk << aux_bits), 1);
     SA_CHECK(c, F->d_short_at.ensure(max_short * 8));
-    SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.hist, 1) * 4));
-    SA_CHECK(c, F->d_hist_aux.ensure(std::max<uint64_t>(pa.hist, 1) * 4));
+    SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.tile_seg.size(), 1) * 4 *
+                                     sort_hist_per_tile(0, ns > 1 ? seq_bits : 0)));
+    SA_CHECK(c, F->d_hist_aux.ensure(std::max<uint64_t>(pa.tile_seg.size(), 1) * 4 *
+                                     sort_hist_per_tile(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits)));
     SA_CHECK(c, F->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
     SA_CHECK(c, F->d_segs_aux.ensure(sizeof(SortSeg) * nbk));
     SA_CHECK(c, F->d_tile_seq.ensure(std::max<size_t>(ps.tile_seg.size(), 1) * 4));
@@ -960,7 +1008,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
                            c->d_totals.as<uint32_t>(), F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(),
                            F->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                            akb[0]->as<uint32_t>(), avb[0]->as<uint32_t>(), d_err);
-        hipLaunchKernelGGL(k_emit_sq, dim3((nr + EMIT_WAVES - 1) / EMIT_WAVES), dim3(64 * EMIT_WAVES), 0, st, bv,
+        hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                            F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                            akb[0]->as<uint32_t>(), avb[0]->as<uint32_t>());
     }
@@ -1164,7 +1212,7 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
         segs += tk.nseg;
         payload = align_up(payload + cap, 16);
     }
-    std::vector<PRec> prs(nsym + 128, PRec{0, 0});
+    std::vector<PRec> prs(nsym + 128, PRec{0});
     std::vector<uint16_t> cm(nsym + 128, 0);
     for (uint64_t i = 0; i < nsym; i++) {
         const uint32_t t = tot[i], f = freq[i], cu = cum[i];
@@ -1172,7 +1220,7 @@ int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_
             c->err = "sa_code_records: invalid (cum, freq, tot)";   // the reference abort()s
             return -1;
         }
-        prs[i] = PRec{recip32(t), t | (f << 16)};
+        prs[i] = PRec{t | (f << 16)};
         cm[i] = (uint16_t)cu;
     }
     hipStream_t st = c->st;
@@ -1225,8 +1273,8 @@ void sa_stream_stats(const sa_ctx* c, uint64_t* max_symbols, uint64_t* total_sym
 }
 
 // HBM a block needs while its batch is encoded: per SEQ symbol the
-// double-buffered u32 keys and values plus the 8-byte record (24 B); per AUX
-// symbol the same plus its u16 cum (26 B); per symbol up to 2 payload and 2
+// double-buffered u32 keys and values plus the 4-byte record (20 B); per AUX
+// symbol the same plus its u16 cum (22 B); per symbol up to 2 payload and 2
 // final bytes; per read the count columns and the read arrays; the input.
 // AUX symbols ~ qualities + name bytes + 8 per read (len, name tokens, dege).
 static uint64_t block_footprint(const sa_block& b)
@@ -1237,7 +1285,7 @@ static uint64_t block_footprint(const sa_block& b)
         nb += b.name_lens[r];
     }
     const uint64_t aux = bases + nb + 8ull * b.nreads;
-    return (24 + 4) * bases + (26 + 4) * aux + (nb + 2 * bases + 16) + 64ull * b.nreads;
+    return (20 + 4) * bases + (22 + 4) * aux + (nb + 2 * bases + 16) + 64ull * b.nreads;
 }
 
 int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, sa_out* out)
@@ -1270,9 +1318,27 @@ int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, 
             bytes += fb;
             b1++;
         }
+        const auto t0 = std::chrono::steady_clock::now();
         if (sa_stage(ctx, in + b0, b1 - b0)) return -1;
+        const auto t1 = std::chrono::steady_clock::now();
         if (sa_run(ctx, cfg)) return -1;
+        const auto t2 = std::chrono::steady_clock::now();
         if (sa_fetch(ctx, out + b0, b1 - b0)) return -1;
+        if (ctx->trace) {   // SA_TRACE: per sub-batch host-side stage timings
+            const auto t3 = std::chrono::steady_clock::now();
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::string ph;
+            for (int i = 0; i < PH_N; i++) {
+                char pb[48];
+                std::snprintf(pb, sizeof pb, " %s %.0f", kPhaseNames[i], ctx->ph_ms[i]);
+                ph += pb;
+            }
+            std::fprintf(stderr,
+                         "seqarc_amd[%p]: %d blocks: stage %.1f ms, run %.1f ms, fetch %.1f ms, grows %u, "
+                         "alloc %.1f ms (all contexts); phases ms:%s\n",
+                         (void*)ctx, b1 - b0, ms(t0, t1), ms(t1, t2), ms(t2, t3), g_grows.load(),
+                         g_alloc_ns.load() / 1e6, ph.c_str());
+        }
         b0 = b1;
     }
     return 0;

@@ -124,6 +124,8 @@ __device__ __forceinline__ void stage_read(const uint8_t* s, const uint8_t* q, u
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t pre = len < EMIT_STAGE ? len : EMIT_STAGE;
     uint32_t sb[EMIT_STAGE / 64], qb[EMIT_STAGE / 64];
+    __builtin_amdgcn_wave_barrier();   // after the previous read's reads of the stage
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (uint32_t k = 0; k < EMIT_STAGE / 64; k++) {
         const uint32_t i = 64 * k + lane;
@@ -152,22 +154,19 @@ __device__ inline int wave_max_i32(int v)
 // seq_stat + qual_nonhash + the quality range check of one read (sa_common.h),
 // 64 positions per step; the gap statistics of reads with an N/IUPAC base run
 // on one lane over the staged bytes.
-__global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv, uint32_t* __restrict__ counts,
-                                                              uint32_t* __restrict__ err)
+__device__ __forceinline__ void prep_sq_read(const BatchView& bv, const uint32_t r, const uint32_t lane,
+                                             uint8_t (&stg)[2][EMIT_STAGE], uint32_t* __restrict__ counts,
+                                             uint32_t* __restrict__ err)
 {
-    __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t r = blockIdx.x * EMIT_WAVES + w;
-    if (r >= bv.nreads_total) return;   // wave-uniform
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
     const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
     const uint8_t* q = bv.qual + blk.seq_base + bv.seq_off[r];
     const uint32_t len = bv.seq_len[r];
     const uint8_t* qv = bv.qual_q + blk.seq_base + bv.seq_off[r];   // QUAL stream (rblock output with -l)
-    stage_read(s, q, len, stage[w]);
-    auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][0][i] : s[i]; };
-    auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][1][i] : q[i]; };
+    stage_read(s, q, len, stg);
+    auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[0][i] : s[i]; };
+    auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[1][i] : q[i]; };
     uint32_t valid = 0, nch = 0, n = 0;
     int maxq = 0;
     bool nonascii = false;
@@ -212,6 +211,17 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv,
         const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, n, st, qbad);
         if (e) atomicOr(err, e);
     }
+}
+
+// a wave per read, grid-stride (a launch of one tiny workgroup per 4 reads is
+// bound by workgroup dispatch)
+__global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv, uint32_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ err)
+{
+    __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
+        prep_sq_read(bv, r, lane, stage[w], counts, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -343,26 +353,21 @@ __device__ inline uint32_t shfl_up0(uint32_t v, uint32_t d)   // lane - d's valu
 // previous codes.  QUAL (encode_qual@0x422180): the context after symbol i
 // depends on symbols i-1, i-2 and the running sum delta of the drops, an
 // inclusive scan.
-__global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv, const uint32_t* __restrict__ counts,
-                                                              uint32_t* __restrict__ seq_key,
-                                                              uint32_t* __restrict__ seq_val,
-                                                              uint32_t* __restrict__ aux_key,
-                                                              uint32_t* __restrict__ aux_val)
+__device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t r, const uint32_t lane,
+                                             uint32_t (&comp)[64], uint8_t (&stg)[2][EMIT_STAGE],
+                                             const uint32_t* __restrict__ counts, uint32_t* __restrict__ seq_key,
+                                             uint32_t* __restrict__ seq_val, uint32_t* __restrict__ aux_key,
+                                             uint32_t* __restrict__ aux_val)
 {
-    __shared__ uint32_t comp[EMIT_WAVES][64];
-    __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t r = blockIdx.x * EMIT_WAVES + w;
-    if (r >= bv.nreads_total) return;   // wave-uniform
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
     const uint8_t* s = bv.seq + blk.seq_base + bv.seq_off[r];
     const uint8_t* q = bv.qual_q + blk.seq_base + bv.seq_off[r];   // QUAL stream only (rblock output with -l)
     const uint32_t len = bv.seq_len[r];
     const uint32_t* off = counts + (size_t)r * NCOL;
-    stage_read(s, q, len, stage[w]);
-    auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][0][i] : s[i]; };
-    auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stage[w][1][i] : q[i]; };
+    stage_read(s, q, len, stg);
+    auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[0][i] : s[i]; };
+    auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[1][i] : q[i]; };
     {
         uint32_t* K = seq_key + blk.seq_sym_base;
         uint32_t* V = seq_val + blk.seq_sym_base;
@@ -377,10 +382,10 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
             const uint32_t in_step = len - i0 < 64 ? len - i0 : 64;
             uint32_t c = cd;
             if (vm != (in_step == 64 ? ~0ull : (1ull << in_step) - 1ull)) {   // compact the ACGT codes
-                if (cd <= 3) comp[w][lanes_below(vm)] = cd;
+                if (cd <= 3) comp[lanes_below(vm)] = cd;
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
-                c = lane < nv ? comp[w][lane] : 0u;
+                c = lane < nv ? comp[lane] : 0u;
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
             }
@@ -445,6 +450,19 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
     }
 }
 
+__global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv, const uint32_t* __restrict__ counts,
+                                                              uint32_t* __restrict__ seq_key,
+                                                              uint32_t* __restrict__ seq_val,
+                                                              uint32_t* __restrict__ aux_key,
+                                                              uint32_t* __restrict__ aux_val)
+{
+    __shared__ uint32_t comp[EMIT_WAVES][64];
+    __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
+        emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val);
+}
+
 // SORT_PAD into the key slots no symbol is written to: each segment's tail up to
 // its last tile (ping buffer), and the slack slots past the space (both buffers;
 // the replays read past a run's end).
@@ -466,37 +484,43 @@ __global__ __launch_bounds__(256) void k_pad_keys(const SortView sv, uint32_t* _
 }
 
 // ---------------------------------------------------------------------------
-// Segmented stable LSD radix sort (8-bit digits).
+// Segmented stable LSD radix sort, DB-bit digits (DB = 8 or 9; the host
+// picks the widths of a sort's passes, sort_digits()).
 // A segment is one block's symbol space, padded with key 0xffffffff to a whole
 // number of tiles.  Tile = 256 threads x 16 keys; each wave owns 1024
-// consecutive keys processed in 16 rounds of 64, ranked with an 8-ballot
+// consecutive keys processed in 16 rounds of 64, ranked with a DB-ballot
 // match (the wavefront "multi-split"), so the scatter is stable.  The scatter
 // stages the tile in digit order in LDS and writes each digit's run with
-// consecutive threads.
+// consecutive threads.  Digit counts are tile-major: row t (global tile index)
+// holds tile t's 2^DB counts.
 // ---------------------------------------------------------------------------
 constexpr uint32_t HIST_TILES = 2;
+// (10-bit digits measured slower than 8: a 4096-key tile scatters ~4 keys per
+// digit run, too short for coalesced writes)
+constexpr int SORT_MIN_DB = 8, SORT_MAX_DB = 9;
 
+template <int DB>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, const uint32_t* __restrict__ keys,
                                                             uint32_t shift)
 {
+    constexpr uint32_t ND = 1u << DB, PER = ND / SORT_THREADS;
     // HIST_TILES consecutive tiles per workgroup (amortises the per-workgroup
     // prologue; each tile's counts still go to its own row)
-    __shared__ uint32_t h[HIST_TILES][256];
+    __shared__ uint32_t h[HIST_TILES][ND];
     uint32_t k[HIST_TILES][SORT_ITEMS];
     const SortSeg* sgp[HIST_TILES];
-    uint32_t ltv[HIST_TILES];
 #pragma unroll
     for (int j = 0; j < HIST_TILES; j++) {
         const uint32_t t = blockIdx.x * HIST_TILES + j;
-        h[j][threadIdx.x] = 0;
+#pragma unroll
+        for (uint32_t p = 0; p < PER; p++) h[j][threadIdx.x + p * SORT_THREADS] = 0;
         sgp[j] = t < sv.ntiles ? &sv.segs[sv.tile_seg[t]] : nullptr;
     }
 #pragma unroll
     for (int j = 0; j < HIST_TILES; j++) {
         if (!sgp[j]) continue;
         const uint32_t t = blockIdx.x * HIST_TILES + j;
-        ltv[j] = t - sgp[j]->tile0;
-        const uint32_t* K = keys + sgp[j]->base + (size_t)ltv[j] * SORT_TILE;
+        const uint32_t* K = keys + sgp[j]->base + (size_t)(t - sgp[j]->tile0) * SORT_TILE;
 #pragma unroll
         for (int i = 0; i < SORT_ITEMS; i++) k[j][i] = K[threadIdx.x + i * SORT_THREADS];
     }
@@ -505,93 +529,121 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, c
     for (int j = 0; j < HIST_TILES; j++) {
         if (!sgp[j]) continue;
 #pragma unroll
-        for (int i = 0; i < SORT_ITEMS; i++) atomicAdd(&h[j][(k[j][i] >> shift) & 255], 1u);
+        for (int i = 0; i < SORT_ITEMS; i++) atomicAdd(&h[j][(k[j][i] >> shift) & (ND - 1)], 1u);
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < HIST_TILES; j++)   // tile-major: one coalesced row per tile
-        if (sgp[j]) sv.hist[sgp[j]->hist_base + (size_t)ltv[j] * 256 + threadIdx.x] = h[j][threadIdx.x];
+    for (int j = 0; j < HIST_TILES; j++)   // one coalesced row per tile
+        if (sgp[j]) {
+            const uint32_t t = blockIdx.x * HIST_TILES + j;
+#pragma unroll
+            for (uint32_t p = 0; p < PER; p++)
+                sv.hist[(size_t)t * ND + threadIdx.x + p * SORT_THREADS] = h[j][threadIdx.x + p * SORT_THREADS];
+        }
 }
 
-// The segment's digit counts are tile-major (row t = tile t's 256 counts); the
-// output is, in place, each (tile, digit)'s start in the sorted segment:
-// base[d] + the counts of d in earlier tiles.  Four thread groups take a
-// quarter of the tiles each; a thread walks one digit column, reading rows
-// coalesced across the 256 digits.
+// The segment's digit counts -> in place, each (tile, digit)'s start in the
+// sorted segment: base[d] + the counts of d in earlier tiles.  G groups of
+// threads take 1/G of the tiles each; a thread walks DPT digit columns, reading
+// rows coalesced across the digits.
+template <int DB>
 __global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
 {
-    __shared__ uint32_t part[4][256];
-    __shared__ uint32_t dsum[4];
+    constexpr uint32_t ND = 1u << DB;
+    constexpr uint32_t TG = ND < 1024 ? ND : 1024;   // threads per group
+    constexpr uint32_t G = 1024 / TG, DPT = ND / TG;
+    constexpr uint32_t C = ND >= 1024 ? ND / 1024 : 1;   // digits per thread in the digit scan
+    __shared__ uint32_t part[G][ND];
+    __shared__ uint32_t sh[16];
     const SortSeg& sg = sv.segs[blockIdx.x];
-    uint32_t* H = sv.hist + sg.hist_base;
-    const uint32_t d = threadIdx.x & 255, g = threadIdx.x >> 8;
-    const uint32_t nt = sg.ntiles, q = (nt + 3) / 4;
+    uint32_t* H = sv.hist + (size_t)sg.tile0 * ND;
+    const uint32_t dl = threadIdx.x % TG, g = threadIdx.x / TG;
+    const uint32_t nt = sg.ntiles, q = (nt + G - 1) / G;
     const uint32_t t0 = g * q < nt ? g * q : nt, t1 = t0 + q < nt ? t0 + q : nt;
-    uint32_t sum = 0;
-    uint32_t t = t0;
-    for (; t + 8 <= t1; t += 8) {
-        uint32_t v[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = H[(size_t)(t + j) * 256 + d];
+    for (uint32_t j = 0; j < DPT; j++) {
+        const uint32_t d = dl + j * TG;
+        uint32_t sum = 0;
+        uint32_t t = t0;
+        for (; t + 8 <= t1; t += 8) {
+            uint32_t v[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) sum += v[j];
-    }
-    for (; t < t1; t++) sum += H[(size_t)t * 256 + d];
-    part[g][d] = sum;
-    __syncthreads();
-    // digit bases: exclusive scan of the digit totals by waves 0-3 (group 0);
-    // every thread reaches both barriers
-    uint32_t tot = 0, inc = 0;
-    if (g == 0) {
-        tot = part[0][d] + part[1][d] + part[2][d] + part[3][d];
-        inc = wave_incl_scan_dpp(tot);
-        if (lane_id() == 63) dsum[threadIdx.x >> 6] = inc;
-    }
-    __syncthreads();
-    if (g == 0) {
-        uint32_t acc = inc - tot;
-        for (uint32_t k = 0; k < (threadIdx.x >> 6); k++) acc += dsum[k];
+            for (int i = 0; i < 8; i++) v[i] = H[(size_t)(t + i) * ND + d];
 #pragma unroll
-        for (int gg = 0; gg < 4; gg++) {
-            const uint32_t p = part[gg][d];
-            part[gg][d] = acc;
-            acc += p;
+            for (int i = 0; i < 8; i++) sum += v[i];
         }
+        for (; t < t1; t++) sum += H[(size_t)t * ND + d];
+        part[g][d] = sum;
     }
     __syncthreads();
-    uint32_t run = part[g][d];
-    t = t0;
-    for (; t + 8 <= t1; t += 8) {
-        uint32_t v[8];
+    // digit bases: exclusive scan of the digit totals in digit order (thread i
+    // owns digits [i C, i C + C)); then each group's start per digit
+    uint32_t tot[C], s = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = H[(size_t)(t + j) * 256 + d];
+    for (uint32_t c = 0; c < C; c++) {
+        const uint32_t d = threadIdx.x * C + c;
+        tot[c] = 0;
+        if (d < ND)
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            H[(size_t)(t + j) * 256 + d] = run;
-            run += v[j];
-        }
+            for (uint32_t gg = 0; gg < G; gg++) tot[c] += part[gg][d];
+        s += tot[c];
     }
-    for (; t < t1; t++) {
-        const uint32_t v = H[(size_t)t * 256 + d];
-        H[(size_t)t * 256 + d] = run;
-        run += v;
+    uint32_t ex;
+    wg1024_excl_scan(s, ex, sh);
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++) {
+        const uint32_t d = threadIdx.x * C + c;
+        if (d < ND) {
+            uint32_t acc = ex;
+#pragma unroll
+            for (uint32_t gg = 0; gg < G; gg++) {
+                const uint32_t p = part[gg][d];
+                part[gg][d] = acc;
+                acc += p;
+            }
+        }
+        ex += tot[c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < DPT; j++) {
+        const uint32_t d = dl + j * TG;
+        uint32_t run = part[g][d];
+        uint32_t t = t0;
+        for (; t + 8 <= t1; t += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) v[i] = H[(size_t)(t + i) * ND + d];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                H[(size_t)(t + i) * ND + d] = run;
+                run += v[i];
+            }
+        }
+        for (; t < t1; t++) {
+            const uint32_t v = H[(size_t)t * ND + d];
+            H[(size_t)t * ND + d] = run;
+            run += v;
+        }
     }
 }
 
+template <int DB>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv,
                                                                const uint32_t* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin,
                                                                uint32_t* __restrict__ kout,
                                                                uint32_t* __restrict__ vout, uint32_t shift)
 {
-    __shared__ uint32_t wc[SORT_THREADS / 64][256];
-    __shared__ uint32_t lstart[256], gstart[256], dsum[SORT_THREADS / 64];
+    constexpr uint32_t ND = 1u << DB, NW = SORT_THREADS / 64, C = ND / SORT_THREADS;
+    __shared__ uint32_t wc[NW][ND];   // per wave and digit: count, then the wave's slot base in the tile
+    __shared__ uint32_t gstart[ND], dsum[NW];
     __shared__ uint32_t sk[SORT_TILE], svl[SORT_TILE];
     const uint32_t t = blockIdx.x;
     const SortSeg& sg = sv.segs[sv.tile_seg[t]];
     const uint32_t lt = t - sg.tile0;
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    for (uint32_t i = threadIdx.x; i < (SORT_THREADS / 64) * 256; i += SORT_THREADS) (&wc[0][0])[i] = 0;
+    for (uint32_t i = threadIdx.x; i < NW * ND; i += SORT_THREADS) (&wc[0][0])[i] = 0;
     __syncthreads();
     const size_t wbase = sg.base + (size_t)lt * SORT_TILE + (size_t)w * (64 * SORT_ITEMS);
     uint32_t k[SORT_ITEMS], v[SORT_ITEMS], rk[SORT_ITEMS];
@@ -603,10 +655,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t d = (k[r] >> shift) & 255;
+        const uint32_t d = (k[r] >> shift) & (ND - 1);
         uint64_t peers = ~0ull;
 #pragma unroll
-        for (int bit = 0; bit < 8; bit++) {
+        for (int bit = 0; bit < DB; bit++) {
             const uint64_t bal = __ballot((d >> bit) & 1);
             peers &= ((d >> bit) & 1) ? bal : ~bal;
         }
@@ -616,29 +668,42 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     }
     __syncthreads();
     {
-        // per digit: the tile's count, each wave's start within the tile's run of
-        // that digit, the run's start in the tile (scan over digits) and in the
-        // output (the scanned histogram)
-        const uint32_t d = threadIdx.x;   // SORT_THREADS == 256 digits
-        uint32_t acc = 0;
+        // per digit (thread i owns digits [i C, i C + C)): each wave's start
+        // within the tile's run of that digit, the run's start in the tile (scan
+        // over digits), folded into wc; and the run's start in the output (the
+        // scanned counts) minus its start in the tile
+        uint32_t cnt[C], s = 0;
 #pragma unroll
-        for (int ww = 0; ww < SORT_THREADS / 64; ww++) {
-            const uint32_t tcount = wc[ww][d];
-            wc[ww][d] = acc;
-            acc += tcount;
+        for (uint32_t c = 0; c < C; c++) {
+            const uint32_t d = threadIdx.x * C + c;
+            uint32_t acc = 0;
+#pragma unroll
+            for (uint32_t ww = 0; ww < NW; ww++) {
+                const uint32_t tcount = wc[ww][d];
+                wc[ww][d] = acc;
+                acc += tcount;
+            }
+            cnt[c] = acc;
+            s += acc;
         }
         uint32_t ex;
-        wg256_excl_scan(acc, ex, dsum);
-        lstart[d] = ex;
-        gstart[d] = sv.hist[sg.hist_base + (size_t)lt * 256 + d] - ex;
+        wg256_excl_scan(s, ex, dsum);
+#pragma unroll
+        for (uint32_t c = 0; c < C; c++) {
+            const uint32_t d = threadIdx.x * C + c;
+#pragma unroll
+            for (uint32_t ww = 0; ww < NW; ww++) wc[ww][d] += ex;
+            gstart[d] = sv.hist[(size_t)t * ND + d] - ex;
+            ex += cnt[c];
+        }
     }
     __syncthreads();
     // stage the tile in digit order in LDS, then write it out: consecutive
     // threads write consecutive slots of one digit's run (coalesced)
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t d = (k[r] >> shift) & 255;
-        const uint32_t at = lstart[d] + wc[w][d] + rk[r];
+        const uint32_t d = (k[r] >> shift) & (ND - 1);
+        const uint32_t at = wc[w][d] + rk[r];
         sk[at] = k[r];
         svl[at] = v[r];
     }
@@ -647,7 +712,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     for (int r = 0; r < SORT_ITEMS; r++) {
         const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
         const uint32_t kk = sk[i];
-        const size_t dst = sg.base + gstart[(kk >> shift) & 255] + i;
+        const size_t dst = sg.base + gstart[(kk >> shift) & (ND - 1)] + i;
         kout[dst] = kk;
         vout[dst] = svl[i];
     }
@@ -1209,7 +1274,7 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
             const uint32_t f = f0 + 8u * same;
             const uint32_t t = tot + 8u * lane;
             if (cum < 0 || (uint32_t)cum + f > t || f == 0) bad = true;
-            rec.prs[pos] = PRec{recip32(t), t | (f << 16)};
+            rec.prs[pos] = PRec{t | (f << 16)};
             rec.cum[pos] = (uint16_t)cum;
         }
         PROF_T(4);
@@ -1423,16 +1488,11 @@ __global__ __launch_bounds__(128) void k_replay_seq_long(const SortView sv, cons
 // ---------------------------------------------------------------------------
 // Range coder, decomposed (sa_logic.h "decomposed range coder").
 //
-// k_coder_r: pass R, one wave per stream.  The range chain runs on the scalar
-// unit: 16 records (32 dwords) per s_load chunk, double-buffered so the next
-// chunk's s_load is in flight while the current one is coded; the chain step is
-// hand-scheduled (10 SALU instructions).  One range checkpoint per segment is
+// k_coder_rv: pass R, one wave per stream.  The range chain runs on the scalar
+// unit (a hand-scheduled 10-instruction SALU step per symbol); the records are
+// fed to it through VGPRs (below).  One range checkpoint per segment is
 // collected in a VGPR (lane = segment mod 64) and stored 64 at a time.
 // ---------------------------------------------------------------------------
-struct PChunk {
-    uint32_t w[32];   // 16 PRec
-};
-
 __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t tf, uint32_t tmask)
 {
     uint32_t t, f, q, p;
@@ -1452,22 +1512,19 @@ __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t 
         : "scc");
 }
 
-#define SA_CHUNK_STEPS(X, j0)                                                         \
-    _Pragma("unroll") for (int j = (j0); j < 16; j++) rc_range_salu(r, X.w[2 * j], X.w[2 * j + 1], tmask)
-
 // Pass R may start before the model replays have written every record (the
 // long runs are replayed concurrently): the record arrays are zeroed first, a
-// written record has m >= 1, and an unwritten one (m = 0) sends the range to 0,
-// where it stays -- a range chain never reaches 0 otherwise (q >= 1, f >= 1).
-// So a segment that ends with r == 0 is re-coded from its start once its
-// records are in, read through L2 (the scalar cache may hold the zeros).
+// written record has tot >= 1, and an unwritten one (tot = 0, m = 0) sends the
+// range to 0, where it stays -- a range chain never reaches 0 otherwise
+// (q >= 1, f >= 1).  So a segment that ends with r == 0 is re-coded from its
+// start once its records are in, read through L2.
 __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t tmask, uint32_t& bad)
 {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t spin = 0; spin < (1u << 22); spin++) {
-        const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(P + lane), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t m = (uint32_t)v, tf = (uint32_t)(v >> 32);
+        const uint32_t tf = __hip_atomic_load(reinterpret_cast<const uint32_t*>(P + lane), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t m = recip32z(tf & tmask);
         uint32_t r = r0;
 #pragma unroll 8
         for (int k = 0; k < 64; k++)
@@ -1479,113 +1536,22 @@ __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t 
     return r0;
 }
 
-// The records are also touched pf_segs segments ahead (default PF_SEGS) by one
-// lane-parallel vector load per segment (the same arrays through pf0 / pf1), so
-// that the scalar loads find them in L2: with many chains in flight the
-// scalar-cache misses to HBM would otherwise outlast the 15 steps a chunk load
-// overlaps.
-constexpr uint32_t PF_SEGS = 4;
-
-// Pass R, one launch per batch: one chain per wave, chains listed longest
-// first, workgroups of `coder_waves` (1, 2 or 4) waves.  Chain placement is what
-// the hardware dispatcher makes of it; two knobs steer it: waves per workgroup
-// (the waves of a workgroup share a CU, one per SIMD) and unused dynamic LDS per
-// workgroup (`coder_lds`, limiting pass-R workgroups per CU).  Measured
-// (DESIGN.md section 4.4): one chain per CU beats four per CU (22.7 vs 26.9 ns
-// per symbol); two chains on one SIMD run at half speed each.
+// Chains are listed longest first, in workgroups of `coder_waves` (1, 2 or 4)
+// waves.  Chain placement is what the hardware dispatcher makes of it; two
+// knobs steer it: waves per workgroup (the waves of a workgroup share a CU, one
+// per SIMD) and unused dynamic LDS per workgroup (`coder_lds`, limiting pass-R
+// workgroups per CU).  Two chains on one SIMD run at half speed each (DESIGN.md
+// section 4.4).
 constexpr uint32_t CODER_MAX_WAVES = 4;
 
-__device__ __forceinline__ void coder_r_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
-                                              const TaskList& tl, const PRec* __restrict__ prs0,
-                                              const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
-                                              uint32_t* __restrict__ err, const uint2* __restrict__ pf0,
-                                              const uint2* __restrict__ pf1, const uint32_t pf_segs,
-                                              const uint32_t prio)
-{
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t t = tl.ids[li];
-    const CoderTask tk = tasks[t];
-    const CoderRun run = tl.run[li];
-    const PRec* P = (tk.space ? prs1 : prs0) + tk.rec_base;
-    const uint32_t tmask = tk.space ? 0xffffu : 0xffu;   // wide AUX / packed SEQ records
-    uint32_t* ck = ck_r + tk.seg_base;
-    const uint32_t first = run.start_seg, last = tk.nseg - 1;
-    uint32_t r = run.r0;
-    uint32_t g = first;
-    uint32_t kv = 0;
-    // a latency-bound chain beside throughput kernels of other batches: issue
-    // priority over their waves on a shared SIMD (arbitration is priority, then
-    // age).  (After the prologue: at the kernel's top the scheduler moves the
-    // task loads behind it and fails to keep the chunk registers scalar.)
-    set_chain_prio(prio);
-    if (g < last) {
-        const PChunk* C = reinterpret_cast<const PChunk*>(P + (size_t)g * SEG_SYMS);
-        PChunk A = C[0], B;
-        uint32_t bad = 0;
-        const uint2* PF = (tk.space ? pf1 : pf0) + tk.rec_base + lane;
-        uint32_t pf_acc = 0, pf_prev = 0;
-        for (; g < last; g++, C += 4) {
-            if (g + pf_segs < last) {
-                pf_acc += pf_prev;   // consumed a segment later: no wait on the load
-                pf_prev = PF[(size_t)(g + pf_segs) * SEG_SYMS].x;
-            }
-            kv = lane == (g & 63) ? r : kv;
-            if ((g & 63) == 63) {
-                const uint32_t s = g - 63 + lane;
-                if (s >= first) ck[s] = kv;
-            }
-            const uint32_t r_seg = r;
-            rc_range_salu(r, A.w[0], A.w[1], tmask);
-            __builtin_amdgcn_sched_barrier(0);
-            B = C[1];
-            __builtin_amdgcn_sched_barrier(0);
-            SA_CHUNK_STEPS(A, 1);
-            rc_range_salu(r, B.w[0], B.w[1], tmask);
-            __builtin_amdgcn_sched_barrier(0);
-            A = C[2];
-            __builtin_amdgcn_sched_barrier(0);
-            SA_CHUNK_STEPS(B, 1);
-            rc_range_salu(r, A.w[0], A.w[1], tmask);
-            __builtin_amdgcn_sched_barrier(0);
-            B = C[3];
-            __builtin_amdgcn_sched_barrier(0);
-            SA_CHUNK_STEPS(A, 1);
-            rc_range_salu(r, B.w[0], B.w[1], tmask);
-            __builtin_amdgcn_sched_barrier(0);
-            A = C[4];   // the next segment (the record arrays carry >= 64 records of slack)
-            __builtin_amdgcn_sched_barrier(0);
-            SA_CHUNK_STEPS(B, 1);
-            if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
-        }
-        if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
-        if (pf_acc + pf_prev == 0x9e3779b9u && tl.count == 0) ck[0] = 0;   // keeps the touch loads (never true)
-    }
-    kv = lane == (g & 63) ? r : kv;
-    const uint32_t s = (g & ~63u) + lane;
-    if (s >= first && s <= g) ck[s] = kv;
-}
-
-__global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_r(
-    const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
-    const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err,
-    const uint2* __restrict__ pf0, const uint2* __restrict__ pf1, const uint32_t pf_segs, const uint32_t prio)
-{
-    const uint32_t wpg = blockDim.x >> 6;
-    const uint32_t li = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (li >= tl.count) return;
-    coder_r_chain(li, tasks, tl, prs0, prs1, ck_r, err, pf0, pf1, pf_segs, prio);
-}
-#undef SA_CHUNK_STEPS
-
-// Pass R with the records fed through VGPRs: one lane-parallel global load per
-// 64-record segment, CODER_LA segments ahead of the chain (vector loads return
-// in order, so the compiler's counted vmcnt waits keep all of them in flight),
-// and per symbol two v_readlane into the SGPRs of the same 10-instruction SALU
-// step.  Unlike the scalar path (SMEM loads return out of order, so only one
-// 16-record chunk can be in flight, and the L2 prefetch it relies on is evicted
-// under the other batches' traffic), the lookahead here covers HBM latency
-// under load, and the scalar cache is not involved.  (Microbenchmark r3d:
-// 27 ns per symbol flat from 1 to 128 chains.)
+// Records through VGPRs: one lane-parallel global load per 64-record segment,
+// CODER_LA segments ahead of the chain (vector loads return in order, so the
+// compiler's counted vmcnt waits keep all of them in flight); each lane derives
+// its record's reciprocal, and per symbol two v_readlane move m and tf into the
+// SGPRs of the SALU step.  (A scalar-load variant -- s_load chunks of 16
+// records -- can keep only one chunk in flight, since SMEM returns out of order,
+// and needed an L2 touch-prefetch that other batches' traffic evicts; DESIGN.md
+// section 4.4.)
 constexpr uint32_t CODER_LA = 6;
 
 // Eight steps of the chain per asm block.  Each step reads the record of the
@@ -1721,13 +1687,13 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                                                const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
                                                uint32_t* __restrict__ err, const uint32_t prio)
 {
-    typedef const __attribute__((address_space(1))) uint64_t g_u64;
+    typedef const __attribute__((address_space(1))) uint32_t g_u32;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t t = tl.ids[li];
     const CoderTask tk = tasks[t];
     const CoderRun run = tl.run[li];
     const PRec* P = (tk.space ? prs1 : prs0) + tk.rec_base;
-    g_u64* G = (g_u64*)(P) + lane;
+    g_u32* G = (g_u32*)(P) + lane;
     const uint32_t tmask = tk.space ? 0xffffu : 0xffu;   // wide AUX / packed SEQ records
     uint32_t* ck = ck_r + tk.seg_base;
     const uint32_t first = run.start_seg, last = tk.nseg - 1;
@@ -1739,14 +1705,14 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
         uint32_t bad = 0;
         // segment loads at or past the last segment read the last one (the
         // record arrays hold >= 64 records of slack past every stream's end)
-        uint64_t buf[CODER_LA];
+        uint32_t buf[CODER_LA];
 #pragma unroll
         for (uint32_t k = 0; k < CODER_LA; k++) buf[k] = G[(size_t)min(g + k, last) * SEG_SYMS];
         for (; g < last;) {
 #pragma unroll
             for (uint32_t k = 0; k < CODER_LA; k++) {
                 if (g >= last) break;
-                const uint64_t cur = buf[k];
+                const uint32_t ctf = buf[k];
                 buf[k] = G[(size_t)min(g + CODER_LA, last) * SEG_SYMS];
                 kv = lane == (g & 63) ? r : kv;
                 if ((g & 63) == 63) {
@@ -1754,7 +1720,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                     if (s >= first) ck[s] = kv;
                 }
                 const uint32_t r_seg = r;
-                const uint32_t cm = (uint32_t)cur, ctf = (uint32_t)(cur >> 32);
+                const uint32_t cm = recip32z(ctf & tmask);
                 rv_segment(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
                 if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
                 g++;

@@ -403,6 +403,8 @@ SA_HD uint32_t replay_simple_run(const uint32_t* keys, const uint32_t* vals, siz
 
 // ceil(2^32 / t) for 2 <= t < 2^32 (t = 2^32 = a t + b: b > 0 -> a + 1; b = 0 -> a)
 SA_HD uint32_t recip32(uint32_t t) { return 0xffffffffu / t + 1u; }
+// ... and 0 for t = 0 (a record not written yet: sends the range to 0)
+SA_HD uint32_t recip32z(uint32_t t) { return t ? recip32(t) : 0u; }
 
 // Two record formats.  Wide (AUX, SIMPLE_MODEL totals up to 0xffe0):
 // tf = t | f << 16, cum in its own array.  Packed (SEQ, BASE_MODEL: t <= 253):
@@ -411,9 +413,9 @@ SA_HD uint32_t recip32(uint32_t t) { return 0xffffffffu / t + 1u; }
 SA_HD void sink_put(const SymSink& o, uint32_t pos, uint32_t cum, uint32_t f, uint32_t t)
 {
     if (!o.cum) {
-        o.prs[pos] = PRec{recip32(t), t | (cum << 8) | (f << 16)};
+        o.prs[pos] = PRec{t | (cum << 8) | (f << 16)};
     } else {
-        o.prs[pos] = PRec{recip32(t), t | (f << 16)};
+        o.prs[pos] = PRec{t | (f << 16)};
         o.cum[pos] = (uint16_t)cum;
     }
 }
@@ -431,11 +433,12 @@ SA_HD uint32_t clz32(uint32_t v)
 
 SA_HD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
-// one symbol of the range chain; returns q, updates r, sets n (bytes shifted)
-SA_HD uint32_t range_step(uint32_t& r, const PRec p, uint32_t tmask, uint32_t& n)
+// one symbol of the range chain (m = recip32z(t)); returns q, updates r, sets
+// n (bytes shifted)
+SA_HD uint32_t range_step(uint32_t& r, const PRec p, uint32_t m, uint32_t tmask, uint32_t& n)
 {
     const uint32_t t = p.tf & tmask, f = p.tf >> 16;
-    uint32_t q = mulhi32(r, p.m);
+    uint32_t q = mulhi32(r, m);
     q -= (r < q * t) ? 1u : 0u;
     const uint32_t rr = q * f;
     const uint32_t sh = clz32(rr) & 24u;
@@ -463,12 +466,15 @@ SA_HD LowMap lowmap_compose(const LowMap& a, const LowMap& b)
 // chunk re-reads record n - 1 instead of reading past the segment.
 constexpr uint32_t RC_CHUNK = 16;
 
+// The reciprocals of a chunk are computed after its loads, independently of
+// the chain.
 template <bool PACKED, class Fn>
 SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
 {
+    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
     for (uint32_t b = 0; b < n; b += RC_CHUNK) {
         PRec p[RC_CHUNK];
-        uint32_t c[RC_CHUNK];
+        uint32_t c[RC_CHUNK], m[RC_CHUNK];
 #pragma unroll
         for (uint32_t k = 0; k < RC_CHUNK; k++) {
             const uint32_t i = b + k < n ? b + k : n - 1;
@@ -477,8 +483,10 @@ SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
             else c[k] = cum[i];
         }
 #pragma unroll
+        for (uint32_t k = 0; k < RC_CHUNK; k++) m[k] = recip32z(p[k].tf & tmask);
+#pragma unroll
         for (uint32_t k = 0; k < RC_CHUNK; k++)
-            if (b + k < n) fn(p[k], c[k]);
+            if (b + k < n) fn(p[k], m[k], c[k]);
     }
 }
 
@@ -489,9 +497,9 @@ SA_HD LowMap seg_lowmap_t(const PRec* P, const uint16_t* cum, uint32_t r, uint32
     uint64_t low = 0;
     uint32_t sbits = 0;
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t c) {
+    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
         uint32_t nb;
-        const uint32_t q = range_step(r, pr, tmask, nb);
+        const uint32_t q = range_step(r, pr, pm, tmask, nb);
         low = shl64(low + (uint64_t)c * q, 8 * nb);
         sbits += 8 * nb;
         m.nbytes += nb;
@@ -521,9 +529,9 @@ SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t
     SegEnd e{0, 0, 0, 0};
     uint32_t op = 0;
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t c) {
+    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
         const uint32_t t = pr.tf & tmask, f = pr.tf >> 16;
-        uint32_t q = mulhi32(r, pr.m);
+        uint32_t q = mulhi32(r, pm);
         q -= (r < q * t) ? 1u : 0u;
         low += (uint64_t)c * q;
         r = q * f;

@@ -15,13 +15,13 @@ inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 struct SortPlan {
     std::vector<SortSeg> segs;
     std::vector<uint32_t> tile_seg;
-    uint64_t total = 0, hist = 0;
+    uint64_t total = 0;
 };
 
 inline SortPlan plan_sort(const std::vector<uint64_t>& counts)
 {
     SortPlan p;
-    uint64_t base = 0, hist = 0;
+    uint64_t base = 0;
     uint32_t tile = 0;
     for (size_t s = 0; s < counts.size(); s++) {
         SortSeg g{};
@@ -29,15 +29,12 @@ inline SortPlan plan_sort(const std::vector<uint64_t>& counts)
         g.count = (uint32_t)counts[s];
         g.ntiles = (uint32_t)((counts[s] + SORT_TILE - 1) / SORT_TILE);
         g.tile0 = tile;
-        g.hist_base = hist;
         for (uint32_t t = 0; t < g.ntiles; t++) p.tile_seg.push_back((uint32_t)s);
         tile += g.ntiles;
         base += (uint64_t)g.ntiles * SORT_TILE;
-        hist += (uint64_t)g.ntiles * 256;
         p.segs.push_back(g);
     }
     p.total = base;
-    p.hist = hist;
     return p;
 }
 

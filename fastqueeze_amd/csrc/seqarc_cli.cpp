@@ -39,6 +39,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -307,9 +308,15 @@ int compress(const Options& o)
             }
             b1.reserve(want);
             if (pe) b2.reserve(want);
-            if (b1.size() < want && !in1.eof && !in1.fill(b1, want - b1.size())) return fail("read error on input 1");
-            if (pe && b2.size() < want && !in2.eof && !in2.fill(b2, want - b2.size()))
-                return fail("read error on input 2");
+            {   // the two mate files are read concurrently
+                std::future<bool> r2;
+                if (pe && b2.size() < want && !in2.eof)
+                    r2 = std::async(std::launch::async, [&]() { return in2.fill(b2, want - b2.size()); });
+                const bool ok1 = b1.size() >= want || in1.eof || in1.fill(b1, want - b1.size());
+                const bool ok2 = !r2.valid() || r2.get();
+                if (!ok1) return fail("read error on input 1");
+                if (!ok2) return fail("read error on input 2");
+            }
             if (b1.empty() && (!pe || b2.empty())) {   // the input ended on a block boundary
                 std::lock_guard<std::mutex> g(mu);
                 nblocks = i;

@@ -54,7 +54,7 @@ static uint32_t code_decomposed(const PRec* P, const uint16_t* C, uint32_t n, ui
             if (g + 1 < nseg)
                 for (uint32_t i = 0; i < SEG_SYMS; i++) {
                     uint32_t nb;
-                    range_step(r, P[g * SEG_SYMS + i], rec_tmask(C), nb);
+                    range_step(r, P[g * SEG_SYMS + i], recip32z(P[g * SEG_SYMS + i].tf & rec_tmask(C)), rec_tmask(C), nb);
                 }
         }
         for (uint32_t g = start; g < nseg; g++)
@@ -105,7 +105,7 @@ static int coder_selftest()
             else if (kind == 1) { t = 2 + rnd() % 0xffdf; f = 1 + rnd() % t; if (f > t) f = t; c = rnd() % (t - f + 1); }
             else if (kind == 2) { t = 0xffe0; f = (rnd() & 1) ? 0xffd0 : 1; c = f == 1 ? 0xffdf : 0; }
             else { t = 12 + rnd() % 240; f = 1 + rnd() % (t - 1); c = rnd() % (t - f + 1); }
-            P[i] = PRec{recip32(t), t | (f << 16)};
+            P[i] = PRec{t | (f << 16)};
             C[i] = (uint16_t)c;
         }
         const uint32_t cap = 2 * n + 64;
