@@ -124,6 +124,7 @@ struct sa_ctx {
     uint32_t long_lds = 0;
     bool serial_seq = false;
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
+    uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
     // pass-R placement (k_coder_rv): four chains per workgroup, one per SIMD, and
     // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
     // SA_CODER_LDS)
@@ -132,6 +133,20 @@ struct sa_ctx {
     std::string err;
     bool timing = false;
     bool trace = std::getenv("SA_TRACE") != nullptr;
+    // pinned host mailbox for the run's small copies (plans, task lists, count
+    // and length read-backs): a pageable copy goes through the runtime's
+    // staging path, which the other contexts' bulk copies hold up; bump
+    // allocation, reset at the start of a run (no copy of the previous run is
+    // in flight then); D2H copies land in it and reach their destination at the
+    // next sync_d2h
+    uint8_t* mail = nullptr;
+    size_t mail_cap = 0, mail_used = 0, mail_high = 0;
+    struct Pending {
+        void* dst;
+        const void* src;
+        size_t n;
+    };
+    std::vector<Pending> pending;
     uint32_t n_cu = 256;
     uint32_t coder_restarts = 0;
     uint64_t max_stream_syms = 0, total_stream_syms = 0;
@@ -192,6 +207,7 @@ struct sa_ctx {
         }
         for (hipEvent_t e : {ev_fork, ev_fork_seq, ev_md5_done, ev_r[0], ev_r[1], ev_seq_done, ev_long_done})
             if (e) (void)hipEventDestroy(e);
+        if (mail) (void)hipHostFree(mail);
         if (st) (void)hipStreamDestroy(st);
         if (st2) (void)hipStreamDestroy(st2);
         if (st3) (void)hipStreamDestroy(st3);
@@ -209,6 +225,64 @@ struct sa_ctx {
     } while (0)
 
 namespace {
+
+// ---- the pinned mailbox (sa_ctx::mail) ----
+// Starts a run's use of the mailbox: grows it (to the previous runs' high-water
+// mark) while nothing of this context is in flight.
+int mail_reset(sa_ctx* c)
+{
+    c->pending.clear();
+    c->mail_used = 0;
+    const size_t want = std::max<size_t>(c->mail_high + c->mail_high / 8, 1u << 20);
+    if (want > c->mail_cap) {
+        if (c->mail) (void)hipHostFree(c->mail);
+        c->mail = nullptr;
+        c->mail_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->mail), want, hipHostMallocDefault) != hipSuccess) {
+            c->mail = nullptr;
+            return 0;   // (copies fall back to pageable memory)
+        }
+        c->mail_cap = want;
+    }
+    return 0;
+}
+
+uint8_t* mail_take(sa_ctx* c, size_t n)
+{
+    const size_t at = align_up(c->mail_used, 64);
+    c->mail_high = std::max(c->mail_high, at + n);
+    if (!c->mail || at + n > c->mail_cap) return nullptr;
+    c->mail_used = at + n;
+    return c->mail + at;
+}
+
+// host -> device through the mailbox (the source may be reused at once)
+hipError_t h2d(sa_ctx* c, void* dst, const void* src, size_t n, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    uint8_t* m = mail_take(c, n);
+    if (!m) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+    std::memcpy(m, src, n);
+    return hipMemcpyAsync(dst, m, n, hipMemcpyHostToDevice, st);
+}
+
+// device -> host through the mailbox: `dst` holds the bytes after sync_d2h
+hipError_t d2h(sa_ctx* c, void* dst, const void* src, size_t n, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    uint8_t* m = mail_take(c, n);
+    if (!m) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st);
+    c->pending.push_back(sa_ctx::Pending{dst, m, n});
+    return hipMemcpyAsync(m, src, n, hipMemcpyDeviceToHost, st);
+}
+
+hipError_t sync_d2h(sa_ctx* c, hipStream_t st)
+{
+    const hipError_t e = hipStreamSynchronize(st);
+    for (const sa_ctx::Pending& p : c->pending) std::memcpy(p.dst, p.src, p.n);
+    c->pending.clear();
+    return e;
+}
 
 // grid of a wave-per-read, grid-stride kernel (EMIT_WAVES waves per workgroup):
 // 8 workgroups per CU, fewer for a small batch
@@ -313,8 +387,8 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     SA_CHECK(c, c->d_rb_opens.ensure(4ull * RB_WORDS * nck));
     SA_CHECK(c, c->d_rb_spec.ensure(sizeof(RbRun) * nck));
     SA_CHECK(c, c->d_rb_entry.ensure(sizeof(RbRun) * nck));
-    SA_CHECK(c, hipMemcpyAsync(c->d_rb_chunks.p, ck.data(), sizeof(RbChunk) * nck, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_rb_ck0.p, ck0.data(), 4ull * (nbk + 1), hipMemcpyHostToDevice, st));
+    SA_CHECK(c, h2d(c, c->d_rb_chunks.p, ck.data(), sizeof(RbChunk) * nck, st));
+    SA_CHECK(c, h2d(c, c->d_rb_ck0.p, ck0.data(), 4ull * (nbk + 1), st));
     const RbChunk* dck = c->d_rb_chunks.as<RbChunk>();
     hipLaunchKernelGGL(k_rb_spec, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, dck, nck, ratio,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>());
@@ -356,10 +430,9 @@ int coder_list(sa_ctx* c, hipStream_t st, int slot, const std::vector<CoderTask>
     gbase.assign(cnt + 1, 0);
     for (size_t i = 0; i < cnt; i++) gbase[i + 1] = gbase[i] + (tasks[ids[i]].nseg - runs[i].start_seg);
     if (cnt) {
-        SA_CHECK(c, hipMemcpyAsync(c->d_list_ids[slot].p, ids.data(), 4 * cnt, hipMemcpyHostToDevice, st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_list_gbase[slot].p, gbase.data(), 8 * (cnt + 1), hipMemcpyHostToDevice, st));
-        SA_CHECK(c, hipMemcpyAsync(c->d_list_run[slot].p, runs.data(), sizeof(CoderRun) * cnt, hipMemcpyHostToDevice,
-                                   st));
+        SA_CHECK(c, h2d(c, c->d_list_ids[slot].p, ids.data(), 4 * cnt, st));
+        SA_CHECK(c, h2d(c, c->d_list_gbase[slot].p, gbase.data(), 8 * (cnt + 1), st));
+        SA_CHECK(c, h2d(c, c->d_list_run[slot].p, runs.data(), sizeof(CoderRun) * cnt, st));
     }
     tl = TaskList{c->d_list_ids[slot].as<uint32_t>(), c->d_list_gbase[slot].as<uint64_t>(),
                   c->d_list_run[slot].as<CoderRun>(), (uint32_t)cnt, 0u, gbase[cnt]};
@@ -427,8 +500,8 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         hipLaunchKernelGGL(k_task_ends, dim3((tl.count + 255) / 256), dim3(256), 0, st, cv, tl,
                            c->d_task_ends.as<uint32_t>());
         std::vector<uint32_t> ends(tasks.size());
-        SA_CHECK(c, hipMemcpyAsync(ends.data(), c->d_task_ends.p, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
-        SA_CHECK(c, hipStreamSynchronize(st));
+        SA_CHECK(c, d2h(c, ends.data(), c->d_task_ends.p, 4 * tasks.size(), st));
+        SA_CHECK(c, sync_d2h(c, st));
         uint64_t payload = 0, slack = 4096;
         if (const char* e = std::getenv("SA_PAYLOAD_SLACK")) slack = std::strtoull(e, nullptr, 10);   // (tests)
         for (size_t t = 0; t < tasks.size(); t++) {
@@ -440,17 +513,16 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         payload_bytes = payload;
         SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
         cv.out = c->d_payload.as<uint8_t>();
-        SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice,
-                                   st));
+        SA_CHECK(c, h2d(c, c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), st));
     }
     coder_launch_l3(c, st, tl, cv);
     if (c->timing && ph_l >= 0) ev_finish(c, ph_l, st);
     SA_CHECK(c, hipGetLastError());
     std::vector<uint32_t> first_sq(tasks.size());
     for (int round = 0;; round++) {
-        SA_CHECK(c, hipMemcpyAsync(first_sq.data(), cv.first_sq, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
-        SA_CHECK(c, hipMemcpyAsync(out_len.data(), cv.out_len, 4 * tasks.size(), hipMemcpyDeviceToHost, st));
-        SA_CHECK(c, hipStreamSynchronize(st));
+        SA_CHECK(c, d2h(c, first_sq.data(), cv.first_sq, 4 * tasks.size(), st));
+        SA_CHECK(c, d2h(c, out_len.data(), cv.out_len, 4 * tasks.size(), st));
+        SA_CHECK(c, sync_d2h(c, st));
         std::vector<uint32_t> ids;
         for (size_t t = 0; t < tasks.size(); t++) {
             const uint32_t k = first_sq[t];
@@ -463,11 +535,11 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         std::vector<uint32_t> off(ids.size());
         for (size_t i = 0; i < ids.size(); i++) {
             const uint64_t sg = tasks[ids[i]].seg_base + first_sq[ids[i]];
-            SA_CHECK(c, hipMemcpyAsync(&endst[i], cv.maps + sg, sizeof(LowMap), hipMemcpyDeviceToHost, st));
-            SA_CHECK(c, hipMemcpyAsync(&off[i], cv.off_at + sg, 4, hipMemcpyDeviceToHost, st));
+            SA_CHECK(c, d2h(c, &endst[i], cv.maps + sg, sizeof(LowMap), st));
+            SA_CHECK(c, d2h(c, &off[i], cv.off_at + sg, 4, st));
         }
         SA_CHECK(c, hipMemsetAsync(cv.first_sq, 0xff, 4 * tasks.size(), st));
-        SA_CHECK(c, hipStreamSynchronize(st));
+        SA_CHECK(c, sync_d2h(c, st));
         std::vector<CoderRun> runs;
         for (size_t i = 0; i < ids.size(); i++)
             runs.push_back(CoderRun{endst[i].B, endst[i].s, first_sq[ids[i]] + 1, off[i] + endst[i].nbytes, 0u});
@@ -547,6 +619,8 @@ sa_ctx* sa_create(int device)
     c->long_lds = el ? (uint32_t)std::atoi(el) : 0u;
     c->serial_seq = std::getenv("SA_SERIAL_SEQ") != nullptr;
     if (const char* cp = std::getenv("SA_CHAIN_PRIO")) c->chain_prio = std::atoi(cp) != 0;
+    c->md5_prio = c->chain_prio;
+    if (const char* cp = std::getenv("SA_MD5_PRIO")) c->md5_prio = std::atoi(cp) != 0;
     std::vector<uint32_t> m_long((prop.multiProcessorCount + 31) / 32, 0u), m_seq(m_long.size(), 0u);
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
@@ -800,6 +874,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     }
     SA_CHECK(c, hipSetDevice(c->device));
     c->have_output = false;
+    if (mail_reset(c)) return -1;
     c->blocks = I->blocks;
     const uint32_t nbk = I->nblocks;
     if (nbk == 0) {
@@ -824,7 +899,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     std::unique_lock<std::mutex> front_lock(F->mu);
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
-    SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
     SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
     SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
     SA_CHECK(c, F->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
@@ -868,11 +943,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
         SA_CHECK(c, hipEventRecord(c->ev_fork, st));
         SA_CHECK(c, hipStreamWaitEvent(c->st2, c->ev_fork, 0));
-        SA_CHECK(c, hipMemcpyAsync(c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), hipMemcpyHostToDevice,
-                                   c->st2));
+        SA_CHECK(c, h2d(c, c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), c->st2));
         ev_begin(c, PH_MD5, c->st2);
         hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(64), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
-                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>(), c->chain_prio);
+                           (uint32_t)md5t.size(), c->d_digests.as<uint32_t>(), c->md5_prio);
         ev_finish(c, PH_MD5, c->st2);
         SA_CHECK(c, hipGetLastError());
         SA_CHECK(c, hipEventRecord(c->ev_md5_done, c->st2));
@@ -882,7 +956,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     if (F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));   // the previous front is done with it
     ev_begin(c, PH_PREP, st);
     if (lossy && run_rblock(c, cfg->lossy, I->seq_bytes, bv)) return -1;
-    const uint32_t rgrid = (nr + 255) / 256;
+    // thread-per-read kernels, grid-stride: 8 workgroups of 256 per CU
+    const uint32_t rgrid = std::max<uint32_t>(1, std::min<uint32_t>((nr + 255) / 256, 8 * c->n_cu));
     if (nr) {
         hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
                            F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(), d_err);
@@ -895,9 +970,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     ev_finish(c, PH_PREP, st);
     std::vector<uint32_t> tot((size_t)nbk * NCOL);
     uint32_t herr[4];
-    SA_CHECK(c, hipMemcpyAsync(tot.data(), c->d_totals.p, tot.size() * 4, hipMemcpyDeviceToHost, st));
-    SA_CHECK(c, hipMemcpyAsync(herr, c->d_err.p, 16, hipMemcpyDeviceToHost, st));
-    SA_CHECK(c, hipStreamSynchronize(st));
+    SA_CHECK(c, d2h(c, tot.data(), c->d_totals.p, tot.size() * 4, st));
+    SA_CHECK(c, d2h(c, herr, c->d_err.p, 16, st));
+    SA_CHECK(c, sync_d2h(c, st));
     if (herr[0]) {
         char buf[128];
         std::snprintf(buf, sizeof buf, "input rejected (error bits 0x%x)", herr[0]);
@@ -971,14 +1046,14 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     SA_CHECK(c, c->d_task_out_base.ensure(8 * tasks.size()));
     SA_CHECK(c, c->d_final_len.ensure(8 * nbk));
 
-    SA_CHECK(c, hipMemcpyAsync(c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(F->d_segs_seq.p, ps.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(F->d_segs_aux.p, pa.segs.data(), sizeof(SortSeg) * nbk, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
+    SA_CHECK(c, h2d(c, F->d_segs_seq.p, ps.segs.data(), sizeof(SortSeg) * nbk, st));
+    SA_CHECK(c, h2d(c, F->d_segs_aux.p, pa.segs.data(), sizeof(SortSeg) * nbk, st));
     if (!ps.tile_seg.empty())
-        SA_CHECK(c, hipMemcpyAsync(F->d_tile_seq.p, ps.tile_seg.data(), ps.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
+        SA_CHECK(c, h2d(c, F->d_tile_seq.p, ps.tile_seg.data(), ps.tile_seg.size() * 4, st));
     if (!pa.tile_seg.empty())
-        SA_CHECK(c, hipMemcpyAsync(F->d_tile_aux.p, pa.tile_seg.data(), pa.tile_seg.size() * 4, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), hipMemcpyHostToDevice, st));
+        SA_CHECK(c, h2d(c, F->d_tile_aux.p, pa.tile_seg.data(), pa.tile_seg.size() * 4, st));
+    SA_CHECK(c, h2d(c, c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), st));
 
 
     CoderView cv{};
@@ -1106,9 +1181,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         final_bytes = align_up(final_bytes + blk, 16);
     }
     SA_CHECK(c, c->d_final.ensure(std::max<uint64_t>(final_bytes, 16)));
-    SA_CHECK(c, hipMemcpyAsync(c->d_asm.p, asmb.data(), sizeof(AsmBlock) * nbk, hipMemcpyHostToDevice, st));
-    SA_CHECK(c, hipMemcpyAsync(c->d_task_out_base.p, task_out_base.data(), 8 * tasks.size(), hipMemcpyHostToDevice,
-                               st));
+    SA_CHECK(c, h2d(c, c->d_asm.p, asmb.data(), sizeof(AsmBlock) * nbk, st));
+    SA_CHECK(c, h2d(c, c->d_task_out_base.p, task_out_base.data(), 8 * tasks.size(), st));
 
     // ---- assembly (after MD5) ----
     if (cfg->md5) SA_CHECK(c, hipStreamWaitEvent(st, c->ev_md5_done, 0));
@@ -1123,9 +1197,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     ev_finish(c, PH_TOTAL, st);
 
     c->final_len.assign(nbk, 0);
-    SA_CHECK(c, hipMemcpyAsync(c->final_len.data(), c->d_final_len.p, 8ull * nbk, hipMemcpyDeviceToHost, st));
-    SA_CHECK(c, hipMemcpyAsync(herr, c->d_err.p, 16, hipMemcpyDeviceToHost, st));
-    SA_CHECK(c, hipStreamSynchronize(st));
+    SA_CHECK(c, d2h(c, c->final_len.data(), c->d_final_len.p, 8ull * nbk, st));
+    SA_CHECK(c, d2h(c, herr, c->d_err.p, 16, st));
+    SA_CHECK(c, sync_d2h(c, st));
     if (herr[0]) {
         char buf[128];
         std::snprintf(buf, sizeof buf, "device error bits 0x%x", herr[0]);
@@ -1151,7 +1225,10 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
 {
     if (!c) return -1;
     int rc = run_input(c, I, cfg, true);
-    if (rc == 2) rc = run_input(c, I, cfg, false);   // a stream outgrew its exact payload cap (rare)
+    if (rc == 2) {   // a stream outgrew its exact payload cap (rare): drain, re-run with the bound
+        for (hipStream_t s : {c->st, c->st2, c->st3, c->st4}) SA_CHECK(c, hipStreamSynchronize(s));
+        rc = run_input(c, I, cfg, false);
+    }
     return rc ? -1 : 0;
 }
 

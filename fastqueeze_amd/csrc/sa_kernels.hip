@@ -99,16 +99,17 @@ __device__ __forceinline__ void set_chain_prio(uint32_t prio)
 }
 
 // ---------------------------------------------------------------------------
-// k_prep: one thread per read (name prefix / suffix, length and tip columns);
+// k_prep: one thread per read, grid-stride (name prefix / suffix, length and
+// tip columns);
 // k_prep_sq: one wave per read (SEQ, QUAL and N-IUPAC columns, input checks).
 // ---------------------------------------------------------------------------
 __global__ void k_prep(const BatchView bv, uint32_t* __restrict__ counts,
                        int16_t* __restrict__ name_p, int16_t* __restrict__ name_s,
                        uint32_t* __restrict__ err)
 {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= bv.nreads_total) return;
-    const uint32_t e = prep_read(bv, r, counts, name_p, name_s, false);
+    uint32_t e = 0;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < bv.nreads_total; r += gridDim.x * blockDim.x)
+        e |= prep_read(bv, r, counts, name_p, name_s, false);
     if (e) atomicOr(err, e);
 }
 
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(1024) void k_scan_reads(const BatchView bv, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// k_emit: one thread per read; the length, name and degenerate-base symbols
+// k_emit: one thread per read (grid-stride); the length, name and degenerate-base symbols
 // (the serial per-read tokenizers).  k_emit_sq: one wave per read; the SEQ and
 // QUAL symbols, 64 positions per step, written coalesced.
 // ---------------------------------------------------------------------------
@@ -332,10 +333,9 @@ __global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts, 
                        uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
                        uint32_t* __restrict__ err)
 {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= bv.nreads_total) return;
-    const uint32_t e = emit_read(bv, r, counts, totals, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key,
-                                 aux_val, false);
+    uint32_t e = 0;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < bv.nreads_total; r += gridDim.x * blockDim.x)
+        e |= emit_read(bv, r, counts, totals, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key, aux_val, false);
     if (e) atomicOr(err, e);
 }
 
