@@ -59,9 +59,10 @@ def log(*a):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=32,
+                    help="timed batch encodes (the pipeline drain, ~1 batch latency, is amortised over them)")
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--contexts", type=int, default=3, help="encoder contexts (pipeline lanes) per GPU")
+    ap.add_argument("--contexts", type=int, default=5, help="encoder contexts (pipeline lanes) per GPU")
     ap.add_argument("--batches", type=int, default=4, help="distinct resident batches per GPU")
     ap.add_argument("--no-share", action="store_true", help="contexts with their own front scratch (A/B)")
     ap.add_argument("--pairs", type=int, default=5_000_000, help="mate pairs per batch (reads with --se)")

@@ -90,6 +90,11 @@ def load_library(path: str | None = None):
         "sa_input_create": ([I32, P, I32], P), "sa_input_destroy": ([P], None), "sa_run_input": ([P, P, P], I32),
         "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
         "sa_decode_block": ([P, U64, P, P, I32, P], I64),
+        "sa_host_register": ([P, U64], I32), "sa_host_unregister": ([P], I32),
+        "sa_hash_build": ([P, P, U64, C.c_uint32, C.c_uint32, C.c_uint32], P),
+        "sa_hash_file_bytes": ([P], U64), "sa_hash_serialize": ([P, P, P, U64], I32),
+        "sa_hash_genome_length": ([P], C.c_uint32), "sa_hash_destroy": ([P], None),
+        "sa_hash_align": ([P, P, P, P, P, I64, C.c_int32, C.c_int32, P, P, P, P, P, P], I32),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -434,3 +439,60 @@ def decode_block(data: bytes, text_bytes: int, cfg: Config | None = None, templa
     ln, ls = int(nl[:n].astype(np.int64).sum()), int(sl[:n].astype(np.int64).sum())
     return Block(names[:ln].copy(), nl[:n].copy(), seq[:ls].copy(), sl[:n].copy(), qual[:ls].copy(), text_bytes), \
         bool(d.md5_ok)
+
+
+class HashIndex:
+    """The HASH reference index of a FASTA (`SeqArc -i ref.fa`,
+    buildRefIndex@0x410190), built and kept on an Encoder's device
+    (sa_hash_build), and the gapless seed alignment of reads against it
+    (sa_hash_align, getHashAlignInfo@0x4113c0)."""
+
+    K, STEP, MAXCOUNT, MAXMIS, GOOD = 14, 2, 1 << 16, 7, 1   # SeqArcParam ctor @0x407490
+
+    def __init__(self, enc: "Encoder", fasta: bytes, k: int = K, step: int = STEP, maxcount: int = MAXCOUNT):
+        self._enc, self._lib = enc, enc._lib
+        self._h = self._lib.sa_hash_build(enc._ctx, fasta, len(fasta), k, step, maxcount)
+        if not self._h:
+            enc._err("sa_hash_build")
+
+    def close(self):
+        if self._h:
+            self._lib.sa_hash_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def genome_length(self) -> int:
+        return int(self._lib.sa_hash_genome_length(self._h))
+
+    def file_bytes(self) -> bytes:
+        """The `<ref.fa>.hash` file (HashRefIndex32::writeIndexFile@0x41ed00)."""
+        n = int(self._lib.sa_hash_file_bytes(self._h))
+        out = np.empty(n, dtype=np.uint8)
+        if self._lib.sa_hash_serialize(self._enc._ctx, self._h, _ptr(out), n) != 0:
+            self._enc._err("sa_hash_serialize")
+        return out.tobytes()
+
+    def align(self, reads: list[bytes], maxmis: int = MAXMIS, good: int = GOOD, ai_nmis: int = 0):
+        """The reads in order, one align_info state carried across them
+        (ai_nmis: before the first read; 0 = a zero-filled AlignParam).  Per
+        read: ret (mismatches or -1), rev, pos (1-based), mispos and mistype
+        ([n, maxmis + 1], -1 past the read's mismatches)."""
+        n = len(reads)
+        seq = np.frombuffer(b"".join(reads) or b"\0", dtype=np.uint8)
+        lens = np.array([len(r) for r in reads] or [0], dtype=np.int32)
+        off = np.zeros(max(n, 1), dtype=np.uint64)
+        if n > 1:
+            off[1:n] = np.cumsum(lens[:n - 1])
+        ret = np.zeros(max(n, 1), dtype=np.int32)
+        rev = np.zeros(max(n, 1), dtype=np.uint8)
+        pos = np.zeros(max(n, 1), dtype=np.uint64)
+        mp = np.zeros((max(n, 1), maxmis + 1), dtype=np.int32)
+        mt = np.zeros((max(n, 1), maxmis + 1), dtype=np.int32)
+        st = np.array([ai_nmis], dtype=np.int32)
+        if self._lib.sa_hash_align(self._enc._ctx, self._h, _ptr(seq), _ptr(off), _ptr(lens), n, maxmis, good,
+                                   _ptr(st), _ptr(ret), _ptr(rev), _ptr(pos), _ptr(mp), _ptr(mt)) != 0:
+            self._enc._err("sa_hash_align")
+        return ret[:n], rev[:n], pos[:n], mp[:n], mt[:n]

@@ -1,0 +1,779 @@
+// sa_hash.hip -- the HASH reference-index path on gfx950 (SURVEY.md section
+// 8(f) 3, configs[3]): the index build of `SeqArc -i ref.fa`
+// (HashAlignment::buildRefIndex@0x410190 over HashRefIndex32) and the gapless
+// seed alignment of every read (getHashAlignInfo@0x4113c0, which
+// doSEAlign@0x4117b0 and, per mate, doPEAlign@0x4117d0 call).
+// Included at the end of sa_engine.hip (it sorts with run_sort).
+//
+// Index build (one FASTA, < 5 GiB: the 32-bit index):
+//   host   the base stream (the characters the reference's line loop reads);
+//   k_hash_pack   16 bases a word, codes & 3 (N reads as A), last word left-aligned;
+//   k_hash_count  per 1-based position p: the K-mer ending at p is a seed if
+//                 none of its K characters is N/n and p % step == 0; a global
+//                 atomic count per K-mer (4^K counters);
+//   k_hash_cap    counts at the cap (2^16) -> 0 (repeats are dropped), then an
+//                 exclusive scan of the counts (k_scan_*);
+//   k_hash_emit   the seeds of kept K-mers as (K-mer, 1-based start) pairs in
+//                 position order (per-chunk counts, scan, write);
+//   run_sort      stable LSD radix sort of the pairs by K-mer: the values are
+//                 the position table, each K-mer's list ascending, exactly the
+//                 order of the reference's second pass.
+// Alignment: one lane per read, the restated control flow over the index in
+// HBM (random index reads, latency-bound: many reads in flight).
+// ---------------------------------------------------------------------------
+
+namespace sa {
+
+constexpr uint32_t HASH_CHUNK = 64;   // positions per thread in count / emit
+
+__device__ __forceinline__ uint32_t hash_code(uint8_t c) { return base_code(c); }   // @0x449fc0 (ASCII)
+
+__global__ __launch_bounds__(256) void k_hash_pack(const uint8_t* __restrict__ b, uint64_t n,
+                                                   uint32_t* __restrict__ seq, uint64_t nwords)
+{
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t i = w * 16 + j;
+        v = (v << 2) | (i < n ? hash_code(b[i]) & 3u : 0u);
+    }
+    seq[w] = v;
+}
+
+// The seed ending at 1-based position p (the K characters p-K .. p-1 of the
+// stream): valid when none is N/n ((c & 0xdf) == 'N', buildRefIndex's test)
+// and p % step == 0.  A thread walks HASH_CHUNK positions with a rolling
+// K-mer and the distance to the last N.
+struct SeedWalk {
+    uint64_t p;        // 1-based position of the next character
+    uint32_t kmer;
+    uint32_t since_n;  // characters since the last N (saturating)
+};
+
+__device__ __forceinline__ SeedWalk seed_walk_start(const uint8_t* b, uint64_t p0, uint32_t K, uint64_t mask)
+{
+    SeedWalk s{p0, 0u, 0u};
+    const uint64_t from = p0 > K ? p0 - K : 1;   // 1-based
+    for (uint64_t q = from; q < p0; q++) {
+        const uint8_t c = b[q - 1];
+        s.kmer = (uint32_t)((((uint64_t)s.kmer << 2) | (hash_code(c) & 3u)) & mask);
+        s.since_n = (c & 0xdf) == 'N' ? 0u : s.since_n + 1u;
+    }
+    return s;
+}
+
+// advances over character p; true if a seed ends there
+__device__ __forceinline__ bool seed_walk_step(SeedWalk& s, const uint8_t* b, uint32_t K, uint64_t mask, uint32_t step)
+{
+    const uint8_t c = b[s.p - 1];
+    s.kmer = (uint32_t)((((uint64_t)s.kmer << 2) | (hash_code(c) & 3u)) & mask);
+    s.since_n = (c & 0xdf) == 'N' ? 0u : (s.since_n < K ? s.since_n + 1u : K);
+    const bool seed = s.since_n >= K && s.p % step == 0;
+    s.p++;
+    return seed;
+}
+
+__global__ __launch_bounds__(256) void k_hash_count(const uint8_t* __restrict__ b, uint64_t n, uint32_t K,
+                                                    uint64_t mask, uint32_t step, uint32_t* __restrict__ num)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p0 = t * HASH_CHUNK + 1;
+    if (p0 > n) return;
+    SeedWalk s = seed_walk_start(b, p0, K, mask);
+    const uint64_t p1 = p0 + HASH_CHUNK <= n + 1 ? p0 + HASH_CHUNK : n + 1;
+    while (s.p < p1)
+        if (seed_walk_step(s, b, K, mask, step)) atomicAdd(&num[s.kmer], 1u);
+}
+
+// setSeedind@0x41e820: a K-mer counted maxcount times or more is dropped
+__global__ __launch_bounds__(256) void k_hash_cap(uint32_t* __restrict__ num, uint64_t nk, uint32_t maxcount)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nk && num[i] >= maxcount) num[i] = 0;
+}
+
+// ---- exclusive scan of u32 (3 kernels: 4096-element tiles, tile sums, add) ----
+constexpr uint32_t SCAN_TILE = 4096;   // 256 threads x 16
+
+__global__ __launch_bounds__(256) void k_scan_tiles(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                    uint64_t n, uint32_t* __restrict__ sums)
+{
+    __shared__ uint32_t sh[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * 16;
+    uint32_t v[16], s = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        v[j] = base + j < n ? in[base + j] : 0u;
+        s += v[j];
+    }
+    uint32_t ex;
+    wg256_excl_scan(s, ex, sh);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (base + j < n) out[base + j] = ex;
+        ex += v[j];
+    }
+    if (threadIdx.x == 255) sums[blockIdx.x] = ex;   // the tile's total
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, uint64_t n,
+                                                  const uint32_t* __restrict__ sums)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] += sums[i / SCAN_TILE];
+}
+
+// k_hash_emit: pass 0 counts each thread's kept seeds; pass 1 writes them at
+// the thread's scanned offset (position order)
+__global__ __launch_bounds__(256) void k_hash_emit(const uint8_t* __restrict__ b, uint64_t n, uint32_t K,
+                                                   uint64_t mask, uint32_t step, const uint32_t* __restrict__ num,
+                                                   uint32_t* __restrict__ cnt, const uint32_t* __restrict__ at,
+                                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, int pass)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p0 = t * HASH_CHUNK + 1;
+    if (p0 > n) return;
+    SeedWalk s = seed_walk_start(b, p0, K, mask);
+    const uint64_t p1 = p0 + HASH_CHUNK <= n + 1 ? p0 + HASH_CHUNK : n + 1;
+    uint32_t k = pass ? at[t] : 0u;
+    while (s.p < p1) {
+        const uint64_t p = s.p;
+        if (seed_walk_step(s, b, K, mask, step) && num[s.kmer]) {
+            if (pass) {
+                keys[k] = s.kmer;
+                vals[k] = (uint32_t)(p - (K - 1));   // setSeedpos@0x41e5f0: 1-based start
+            }
+            k++;
+        }
+    }
+    if (!pass) cnt[t] = k;
+}
+
+// ---------------------------------------------------------------------------
+// Alignment (getHashAlignInfo@0x4113c0 and callees; oracle/hash_oracle.c is
+// the CPU restatement, every step below mirrors it).
+// ---------------------------------------------------------------------------
+struct HashView {
+    const uint32_t* seq;
+    const uint32_t* num;
+    const uint32_t* ind;
+    const uint32_t* pos;
+    uint32_t K;
+    uint64_t glen;
+};
+
+struct HashArgs {
+    int32_t maxmis, good;
+};
+
+struct HashRead {   // one read (forward or reverse complement) being aligned
+    const uint8_t* r;    // forward bases
+    int len;
+    bool rc;             // the sequence is the reverse complement of r
+    uint32_t* packed;    // its packed words (scratch)
+};
+
+__device__ __forceinline__ uint8_t comp_base(uint8_t c)   // rev@0x40d9a0
+{
+    switch (c) {
+    case 'A': case 'a': return 'T';
+    case 'C': case 'c': return 'G';
+    case 'G': case 'g': return 'C';
+    case 'T': case 't': return 'A';
+    default: return c;
+    }
+}
+
+__device__ __forceinline__ uint8_t read_at(const HashRead& h, int i)
+{
+    return h.rc ? comp_base(h.r[h.len - 1 - i]) : h.r[i];
+}
+
+__device__ __forceinline__ uint64_t mask2(uint32_t k) { return k >= 32 ? ~0ull : (1ull << (2 * k)) - 1; }
+
+// getHashSeeds@0x4107f0 (packed words; seeds are read back from them); the
+// number of N/IUPAC bases
+__device__ int hash_pack_read(const HashRead& h)
+{
+    int nn = 0;
+    const int nw = ((h.len - 1) >> 4) + 1;
+    for (int w = 0; w < nw; w++) {
+        uint32_t v = 0;
+        for (int j = 0; j < 16; j++) {
+            const int i = w * 16 + j;
+            uint32_t c = 0;
+            if (i < h.len) {
+                c = hash_code(read_at(h, i));
+                nn += c >= 4;
+            }
+            v = (v << 2) | (c & 3u);
+        }
+        h.packed[w] = v;
+    }
+    return nn;
+}
+
+// the K-mer ending at read offset i + K - 1 (seed i), from the packed words
+__device__ __forceinline__ uint32_t seed_at(const HashRead& h, int i, uint32_t K)
+{
+    const int e = i + (int)K - 1;             // last base
+    const int w = e >> 4, sh = 2 * (15 - (e & 15));
+    uint64_t v = (uint64_t)h.packed[w] >> sh;
+    if (w > 0) v |= (uint64_t)h.packed[w - 1] << (32 - sh);
+    return (uint32_t)(v & mask2(K));
+}
+
+__device__ __forceinline__ bool find_seed_d(const HashView& ix, const HashRead& h, int from, int to, uint32_t maxcnt,
+                                            bool stop_first, int& out)   // findHashSeeds@0x4108d0
+{
+    uint32_t best = 100000;
+    for (int i = from; i <= to; i += 2) {
+        const uint32_t c = ix.num[seed_at(h, i, ix.K)];
+        if (c && c < maxcnt && c < best) {
+            best = c;
+            out = i;
+            if (stop_first) return true;
+        }
+    }
+    return best != 100000;
+}
+
+__device__ __forceinline__ uint32_t mis2_d(uint32_t x)   // g_mismatch_count@0x65a7c0
+{
+    const uint32_t y = (x | (x >> 1)) & 0x55555555u;
+    return (uint32_t)__popc(y);
+}
+
+// mismatch type @0x44a0c0, [ref * 4 + read], 2 bits an entry
+__device__ __forceinline__ uint32_t mistype_d(uint32_t rc, uint32_t rb) { return (0xc6b18d87u >> (2 * (rb * 4 + rc))) & 3u; }
+
+// align_info (AlignParam+0x8): nmis is also the state carried from the
+// previous read (oracle/hash_oracle.c, ho_align_read): `fresh` once this
+// read's first candidate was verified; `consulted` when a search step read the
+// carried state before that.
+struct HashAlign {
+    int nmis;
+    uint8_t rev;
+    uint64_t pos;
+    bool fresh, consulted;
+};
+
+// gaplessHashAlignPositions@0x410990
+__device__ int align_at_d(uint64_t pos, const HashRead& h, const HashView& ix, const HashArgs& a, HashAlign& ai,
+                          int* mp, int* mt, int& best)
+{
+    const uint64_t p0 = pos - 1;
+    const uint32_t off = (uint32_t)(p0 & 15);
+    const int lw = (h.len - 1) >> 4, nfull = h.len >> 4;
+    int mis = 0;
+    ai.fresh = true;
+    if (a.maxmis >= 0) {
+        uint64_t w = p0 >> 4;
+        for (int j = 0;; j++, w++) {
+            uint32_t ref = ix.seq[w];
+            if (off) {
+                const uint32_t nxt = ix.seq[w + 1];
+                ref = (uint32_t)(((nxt >> (32 - 2 * off)) & mask2(off)) | (((uint64_t)ref << (2 * off)) & ~mask2(off)));
+            }
+            uint64_t x = ref ^ h.packed[j];
+            if (j >= nfull) x &= ~mask2(16 - (h.len & 15));
+            mis += (int)mis2_d((uint32_t)x);
+            if (mis > a.maxmis || j + 1 > lw) break;
+        }
+    }
+    int limit;
+    if (best > mis) limit = best;
+    else if (a.maxmis >= mis) limit = a.maxmis + 1;
+    else {
+        ai.nmis = -1;
+        return 0;
+    }
+    int n = 0;
+    if (p0 >= ix.glen) n = a.maxmis + 1;
+    else {
+        uint64_t q = p0;
+        for (int i = 0;; i++) {
+            const uint32_t rb = (ix.seq[q >> 4] >> (30 - 2 * (q & 15))) & 3u;
+            const uint32_t rc = hash_code(read_at(h, i));
+            if (rb != rc) {
+                if (n == a.maxmis) {
+                    n++;
+                    break;
+                }
+                mp[n] = i;
+                mt[n] = rc > 3 ? 3 : (int)mistype_d(rc, rb);
+                n++;
+            }
+            if (i == h.len - 1) break;
+            q++;
+            if (q >= ix.glen) {
+                n = a.maxmis + 1;
+                break;
+            }
+        }
+    }
+    if (limit <= n) {
+        ai.nmis = -1;
+        return 0;
+    }
+    ai.pos = pos;
+    ai.rev = h.rc ? 1 : 0;
+    ai.nmis = n;
+    if (n < best) best = n;
+    return 1;
+}
+
+// gaplessSEHashAlign@0x410d80 (mode 0)
+__device__ void try_seed_d(int so, const HashRead& h, const HashView& ix, const HashArgs& a, uint32_t kmer,
+                           HashAlign& ai, int* mp, int* mt, uint32_t& cnt, int& best, int thr)
+{
+    const uint32_t n = ix.num[kmer], base = ix.ind[kmer];
+    for (uint32_t j = 0; j < n; j++) {
+        const uint64_t p = ix.pos[base + j];
+        if (p <= (uint64_t)(int64_t)so) continue;
+        if (p >= (uint64_t)(int64_t)so + ix.glen - (uint64_t)(int64_t)h.len) continue;
+        cnt++;
+        align_at_d(p - (uint64_t)(int64_t)so, h, ix, a, ai, mp, mt, best);
+        if (thr >= best) return;
+        if (ai.nmis >= 0 && ai.nmis <= a.maxmis) return;
+        if (cnt > 300) return;
+    }
+}
+
+__device__ __forceinline__ bool hash_done(HashAlign& ai, const HashArgs& a, uint32_t cnt, int best, int thr)
+{
+    if (!ai.fresh) ai.consulted = true;
+    return thr >= best || cnt > 300 || (ai.nmis >= 0 && ai.nmis <= a.maxmis);
+}
+
+// hashAligner@0x410f50
+__device__ void aligner_d(const HashRead& h, const HashView& ix, const HashArgs& a, int* sidx, HashAlign& ai, int* mp,
+                          int* mt, uint32_t& cnt, int& best, int thr)
+{
+    for (int par = 0; par < 2; par++) {
+        if (find_seed_d(ix, h, par, h.len - (int)ix.K, 100000u, false, sidx[par]))
+            try_seed_d(sidx[par], h, ix, a, seed_at(h, sidx[par], ix.K), ai, mp, mt, cnt, best, thr);
+        if (hash_done(ai, a, cnt, best, thr)) return;
+    }
+}
+
+// hashAlignerShortPart@0x411070
+__device__ void aligner_parts_d(const HashRead& h, const HashView& ix, const HashArgs& a, int* sidx, HashAlign& ai,
+                                int* mp, int* mt, uint32_t& cnt, int& best, int thr)
+{
+    const int len = h.len, K = (int)ix.K;
+    const int np = len > 75 ? 4 : len >= 45 ? 3 : 2;
+    const int ovl = len > np * K ? len / np - K : 0;
+    bool found = false;
+    int b = 0;
+    for (int p = 0; p < np; p++) {
+        const int e = (len + b) / np, s = b / np;
+        b += len;
+        for (int par = 0; par < 2; par++) {
+            found = find_seed_d(ix, h, s + par, e - K, 620u, false, sidx[par + 2]);
+            if (found && sidx[par + 2] != sidx[par]) {
+                try_seed_d(sidx[par + 2], h, ix, a, seed_at(h, sidx[par + 2], ix.K), ai, mp, mt, cnt, best, thr);
+                if (hash_done(ai, a, cnt, best, thr)) return;
+            }
+        }
+    }
+    if (found) return;
+    b = 0;
+    for (int p = 0; p < np; p++) {
+        const int e8 = (len + b) / np - 8, s = b / np + ovl;
+        b += len;
+        for (int par = 0; par < 2; par++) {
+            const int to = e8 < len - K ? e8 : len - K;
+            if (find_seed_d(ix, h, s + par, to, 620u, true, sidx[par + 2]) && sidx[par + 2] != sidx[par]) {
+                try_seed_d(sidx[par + 2], h, ix, a, seed_at(h, sidx[par + 2], ix.K), ai, mp, mt, cnt, best, thr);
+                if (hash_done(ai, a, cnt, best, thr)) return;
+            }
+        }
+    }
+}
+
+// getHashAlignInfo@0x4113c0, one lane per read, with the carried align_info
+// state taken as `stale` (0: not aligned, 1: aligned).  Outputs per read: ret
+// (mismatches, -1 unaligned), strand, 1-based position, maxmis + 1 slots of
+// mismatch offsets / types (-1 past the read's mismatches) and whether the
+// carried state was consulted (the host then re-runs those reads with the
+// other state and picks per read in order, sa_hash_align).  `sel`: the reads
+// to do (NULL: all n), outputs at the read's index.
+__global__ __launch_bounds__(256) void k_hash_align(const HashView ix, const HashArgs a, const uint8_t* __restrict__ seq,
+                                                    const uint64_t* __restrict__ off, const int32_t* __restrict__ lens,
+                                                    const uint64_t* __restrict__ woff, uint32_t* __restrict__ scratch,
+                                                    const uint32_t* __restrict__ sel, uint64_t n, int stale,
+                                                    int32_t* __restrict__ ret, uint8_t* __restrict__ rev,
+                                                    uint64_t* __restrict__ pos, int32_t* __restrict__ mispos,
+                                                    int32_t* __restrict__ mistype, uint8_t* __restrict__ consulted)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t i = sel ? sel[t] : t;
+    const int len = lens[i];
+    const int stride = a.maxmis + 1;
+    int* mp = mispos + i * stride;
+    int* mt = mistype + i * stride;
+    HashRead fw{seq + off[i], len, false, scratch + 2 * woff[i]};
+    HashRead rc{seq + off[i], len, true, scratch + 2 * woff[i] + ((len - 1) >> 4) + 1};
+    HashAlign ai{stale ? 0 : -1, 0, 0, false, false};
+    int sidx[4] = {-1, -1, -1, -1};
+    int best = -1, r = -1;
+    uint32_t cnt = 0;
+    const int thr = a.good < a.maxmis ? a.good : a.maxmis;
+    if (len > 0 && hash_pack_read(fw) <= a.maxmis) {
+        best = a.maxmis + 1;
+        aligner_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+        if (!(a.maxmis >= best) && cnt <= 299) {
+            hash_pack_read(rc);
+            aligner_d(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+            if (!(a.maxmis >= best) && cnt <= 299) {
+                aligner_parts_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+                if (!(a.maxmis >= best) && cnt <= 299) aligner_parts_d(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+            }
+        }
+        if (best <= a.maxmis) r = best;
+    }
+    ret[i] = r;
+    rev[i] = r >= 0 ? ai.rev : 0;
+    pos[i] = r >= 0 ? ai.pos : 0;
+    if (consulted) consulted[i] = ai.consulted ? 1 : 0;
+    for (int k = 0; k < stride; k++)
+        if (r < 0 || k >= ai.nmis) {
+            mp[k] = -1;
+            mt[k] = -1;
+        }
+}
+
+}  // namespace sa
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct sa_hash_index {
+    int device = 0;
+    uint32_t K = 0, step = 0, maxcount = 0, total = 0, nwords = 0, npos = 0;
+    uint64_t nkmers = 0;
+    DBuf seq, num, ind, pos;
+    ~sa_hash_index()
+    {
+        for (DBuf* b : {&seq, &num, &ind, &pos}) b->release();
+    }
+};
+
+namespace {
+
+// a device buffer released when it goes out of scope (DBuf is released by its owner)
+struct DTmp : DBuf {
+    ~DTmp() { release(); }
+};
+
+// exclusive scan of n u32 on the device (tiles of SCAN_TILE, recursing on the
+// tile totals); *total (optional) gets the sum
+int scan_u32(sa_ctx* c, hipStream_t st, const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* total)
+{
+    if (n == 0) {
+        if (total) *total = 0;
+        return 0;
+    }
+    const uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    DTmp sums, sums_x;
+    SA_CHECK(c, sums.ensure(tiles * 4));
+    hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)tiles), dim3(256), 0, st, in, out, n, sums.as<uint32_t>());
+    SA_CHECK(c, hipGetLastError());
+    if (tiles > 1) {
+        SA_CHECK(c, sums_x.ensure(tiles * 4));
+        if (scan_u32(c, st, sums.as<uint32_t>(), sums_x.as<uint32_t>(), tiles, nullptr)) return -1;
+        hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, out, n,
+                           sums_x.as<uint32_t>());
+        SA_CHECK(c, hipGetLastError());
+    }
+    if (total) {
+        uint32_t last_in = 0, last_out = 0;
+        SA_CHECK(c, hipMemcpyAsync(&last_in, in + n - 1, 4, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(&last_out, out + n - 1, 4, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipStreamSynchronize(st));
+        *total = last_in + last_out;
+    }
+    SA_CHECK(c, hipStreamSynchronize(st));   // (sums are freed on return)
+    return 0;
+}
+
+// The characters buildRefIndex@0x410190 reads: every line that does not start
+// with '>', up to strlen(line) - 1 (getdelim keeps the '\n').  Lines before the
+// first header are rejected (the reference counts them in one pass only).
+bool fasta_bases(const char* fa, uint64_t n, std::vector<uint8_t>& out, std::string& err)
+{
+    out.clear();
+    out.reserve(n);
+    bool header = false;
+    for (uint64_t at = 0; at < n;) {
+        const char* p = fa + at;
+        const char* e = static_cast<const char*>(std::memchr(p, '\n', n - at));
+        const uint64_t len = e ? (uint64_t)(e - p) + 1 : n - at;
+        at += len;
+        if (p[0] == '>') {
+            header = true;
+            continue;
+        }
+        const char* z = static_cast<const char*>(std::memchr(p, 0, len));
+        const uint64_t sl = z ? (uint64_t)(z - p) : len;
+        if (sl <= 1) continue;
+        if (!header) {
+            err = "FASTA: sequence before the first '>' header";
+            return false;
+        }
+        out.insert(out.end(), p, p + sl - 1);
+    }
+    if (!header) {
+        err = "FASTA: no '>' header";
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+sa_hash_index* sa_hash_build(sa_ctx* c, const char* fasta, uint64_t bytes, uint32_t K, uint32_t step,
+                             uint32_t maxcount)
+{
+    if (!c || !fasta) return nullptr;
+    if (K < 1 || K > 16 || step < 1 || maxcount < 1) {
+        c->err = "sa_hash_build: K must be 1..16, step and maxcount >= 1";
+        return nullptr;
+    }
+    if ((bytes >> 30) > 4) {
+        c->err = "sa_hash_build: FASTA of 5 GiB or more (HashRefIndex64) is not supported";
+        return nullptr;
+    }
+    std::vector<uint8_t> b;
+    if (!fasta_bases(fasta, bytes, b, c->err)) return nullptr;
+    std::unique_ptr<sa_hash_index> ix(new sa_hash_index());
+    auto fail = [&](int rc) -> sa_hash_index* { return rc ? nullptr : ix.release(); };
+    auto body = [&]() -> int {
+        SA_CHECK(c, hipSetDevice(c->device));
+        hipStream_t st = c->st;
+        const uint64_t n = b.size(), mask = K >= 16 ? 0xffffffffull : (1ull << (2 * K)) - 1;
+        ix->device = c->device;
+        ix->K = K;
+        ix->step = step;
+        ix->maxcount = maxcount;
+        ix->nkmers = mask + 1;
+        ix->total = (uint32_t)n;
+        ix->nwords = n ? (uint32_t)((n - 1) / 16 + 1) : 1u;   // setEndSeqint@0x41e5a0: last word + 1
+        DTmp d_b, cnt, at;
+        SA_CHECK(c, d_b.ensure(n + 16));
+        if (n) SA_CHECK(c, hipMemcpyAsync(d_b.p, b.data(), n, hipMemcpyHostToDevice, st));
+        SA_CHECK(c, ix->seq.ensure(4ull * ix->nwords));
+        hipLaunchKernelGGL(k_hash_pack, dim3((uint32_t)((ix->nwords + 255) / 256)), dim3(256), 0, st, d_b.as<uint8_t>(),
+                           n, ix->seq.as<uint32_t>(), (uint64_t)ix->nwords);
+        SA_CHECK(c, ix->num.ensure(4 * ix->nkmers));
+        SA_CHECK(c, ix->ind.ensure(4 * ix->nkmers));
+        SA_CHECK(c, hipMemsetAsync(ix->num.p, 0, 4 * ix->nkmers, st));
+        const uint64_t nthr = (n + HASH_CHUNK - 1) / HASH_CHUNK;
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, (nthr + 255) / 256);
+        if (n) {
+            hipLaunchKernelGGL(k_hash_count, dim3(grid), dim3(256), 0, st, d_b.as<uint8_t>(), n, K, mask, step,
+                               ix->num.as<uint32_t>());
+            hipLaunchKernelGGL(k_hash_cap, dim3((uint32_t)((ix->nkmers + 255) / 256)), dim3(256), 0, st,
+                               ix->num.as<uint32_t>(), ix->nkmers, maxcount);
+        }
+        SA_CHECK(c, hipGetLastError());
+        uint32_t npos = 0;
+        if (scan_u32(c, st, ix->num.as<uint32_t>(), ix->ind.as<uint32_t>(), ix->nkmers, &npos)) return -1;
+        ix->npos = npos;
+        // the kept seeds as (K-mer, start) in position order, then sorted by K-mer
+        const SortPlan plan = plan_sort({(uint64_t)npos});
+        const uint64_t tot = plan.total + KEY_SLACK;
+        DTmp keys[2], vals[2], segs, tiles, hist;
+        for (int i = 0; i < 2; i++) {
+            SA_CHECK(c, keys[i].ensure(4 * tot));
+            SA_CHECK(c, vals[i].ensure(4 * tot));
+            SA_CHECK(c, hipMemsetAsync(keys[i].p, 0xff, 4 * tot, st));   // SORT_PAD in the tail tiles
+        }
+        if (npos && n) {
+            SA_CHECK(c, cnt.ensure(4 * nthr));
+            SA_CHECK(c, at.ensure(4 * nthr));
+            hipLaunchKernelGGL(k_hash_emit, dim3(grid), dim3(256), 0, st, d_b.as<uint8_t>(), n, K, mask, step,
+                               ix->num.as<uint32_t>(), cnt.as<uint32_t>(), at.as<uint32_t>(), keys[0].as<uint32_t>(),
+                               vals[0].as<uint32_t>(), 0);
+            if (scan_u32(c, st, cnt.as<uint32_t>(), at.as<uint32_t>(), nthr, nullptr)) return -1;
+            hipLaunchKernelGGL(k_hash_emit, dim3(grid), dim3(256), 0, st, d_b.as<uint8_t>(), n, K, mask, step,
+                               ix->num.as<uint32_t>(), cnt.as<uint32_t>(), at.as<uint32_t>(), keys[0].as<uint32_t>(),
+                               vals[0].as<uint32_t>(), 1);
+            SA_CHECK(c, hipGetLastError());
+            SA_CHECK(c, segs.ensure(sizeof(SortSeg) * plan.segs.size()));
+            SA_CHECK(c, tiles.ensure(4 * std::max<size_t>(plan.tile_seg.size(), 1)));
+            SA_CHECK(c, hist.ensure(4 * std::max<size_t>(plan.tile_seg.size(), 1) * sort_hist_per_tile(0, 2 * (int)K)));
+            SA_CHECK(c, hipMemcpyAsync(segs.p, plan.segs.data(), sizeof(SortSeg) * plan.segs.size(),
+                                       hipMemcpyHostToDevice, st));
+            SA_CHECK(c, hipMemcpyAsync(tiles.p, plan.tile_seg.data(), 4 * plan.tile_seg.size(), hipMemcpyHostToDevice,
+                                       st));
+            DBuf* kb[2] = {&keys[0], &keys[1]};
+            DBuf* vb[2] = {&vals[0], &vals[1]};
+            int res = 0;
+            if (run_sort(c, st, plan, segs, tiles, hist, kb, vb, 0, 2 * (int)K, res)) return -1;
+            std::swap(static_cast<DBuf&>(ix->pos), static_cast<DBuf&>(vals[res]));   // the position table
+        } else {
+            SA_CHECK(c, ix->pos.ensure(4));
+        }
+        SA_CHECK(c, hipStreamSynchronize(st));
+        return 0;
+    };
+    return fail(body());
+}
+
+uint64_t sa_hash_file_bytes(const sa_hash_index* ix)
+{
+    return ix ? 16 + 4ull * (ix->nwords + 2 * ix->nkmers + ix->npos) : 0;
+}
+
+uint32_t sa_hash_genome_length(const sa_hash_index* ix) { return ix ? ix->total : 0; }
+
+// HashRefIndex32::writeIndexFile@0x41ed00: K, bases, words, positions (u32),
+// seq[words], num[4^K], ind[4^K], pos[positions]
+int sa_hash_serialize(sa_ctx* c, const sa_hash_index* ix, uint8_t* out, uint64_t cap)
+{
+    if (!c || !ix || !out) return -1;
+    if (cap < sa_hash_file_bytes(ix)) {
+        c->err = "sa_hash_serialize: output buffer too small";
+        return -1;
+    }
+    SA_CHECK(c, hipSetDevice(ix->device));
+    const uint32_t hdr[4] = {ix->K, ix->total, ix->nwords, ix->npos};
+    std::memcpy(out, hdr, 16);
+    uint8_t* o = out + 16;
+    SA_CHECK(c, hipMemcpy(o, ix->seq.p, 4ull * ix->nwords, hipMemcpyDeviceToHost));
+    o += 4ull * ix->nwords;
+    SA_CHECK(c, hipMemcpy(o, ix->num.p, 4 * ix->nkmers, hipMemcpyDeviceToHost));
+    o += 4 * ix->nkmers;
+    SA_CHECK(c, hipMemcpy(o, ix->ind.p, 4 * ix->nkmers, hipMemcpyDeviceToHost));
+    o += 4 * ix->nkmers;
+    if (ix->npos) SA_CHECK(c, hipMemcpy(o, ix->pos.p, 4ull * ix->npos, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+void sa_hash_destroy(sa_hash_index* ix)
+{
+    if (!ix) return;
+    (void)hipSetDevice(ix->device);
+    delete ix;
+}
+
+int sa_hash_align(sa_ctx* c, const sa_hash_index* ix, const char* seq, const uint64_t* off, const int32_t* lens,
+                  int64_t n, int32_t maxmis, int32_t good, int32_t* ai_nmis, int32_t* ret, uint8_t* rev,
+                  uint64_t* pos, int32_t* mispos, int32_t* mistype)
+{
+    if (!c || !ix || n < 0 || !ai_nmis ||
+        (n && (!seq || !off || !lens || !ret || !rev || !pos || !mispos || !mistype)))
+        return -1;
+    if (maxmis < 0 || maxmis > 63) {
+        c->err = "sa_hash_align: maxmis must be 0..63";
+        return -1;
+    }
+    if (n == 0) return 0;
+    SA_CHECK(c, hipSetDevice(c->device));
+    if (ix->device != c->device) {
+        c->err = "sa_hash_align: index and context on different devices";
+        return -1;
+    }
+    hipStream_t st = c->st;
+    uint64_t bytes = 0, words = 0;
+    std::vector<uint64_t> woff((size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+        if (lens[i] < 0) {
+            c->err = "sa_hash_align: negative read length";
+            return -1;
+        }
+        bytes = std::max<uint64_t>(bytes, off[i] + (uint64_t)lens[i]);
+        woff[(size_t)i] = words;
+        words += lens[i] > 0 ? (uint64_t)((lens[i] - 1) >> 4) + 1 : 0;
+    }
+    const uint64_t N = (uint64_t)n, stride = (uint64_t)maxmis + 1;
+    DTmp d_seq, d_off, d_len, d_woff, d_scr, d_sel, d_ret[2], d_rev[2], d_pos[2], d_mp[2], d_mt[2], d_con;
+    SA_CHECK(c, d_seq.ensure(bytes + 16));
+    SA_CHECK(c, d_off.ensure(8 * N));
+    SA_CHECK(c, d_len.ensure(4 * N));
+    SA_CHECK(c, d_woff.ensure(8 * N));
+    SA_CHECK(c, d_scr.ensure(8 * words + 16));
+    SA_CHECK(c, d_con.ensure(N));
+    for (int v = 0; v < 2; v++) {
+        SA_CHECK(c, d_ret[v].ensure(4 * N));
+        SA_CHECK(c, d_rev[v].ensure(N));
+        SA_CHECK(c, d_pos[v].ensure(8 * N));
+        SA_CHECK(c, d_mp[v].ensure(4 * stride * N));
+        SA_CHECK(c, d_mt[v].ensure(4 * stride * N));
+    }
+    SA_CHECK(c, hipMemcpyAsync(d_seq.p, seq, bytes, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(d_off.p, off, 8 * N, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(d_len.p, lens, 4 * N, hipMemcpyHostToDevice, st));
+    SA_CHECK(c, hipMemcpyAsync(d_woff.p, woff.data(), 8 * N, hipMemcpyHostToDevice, st));
+    const HashView v{ix->seq.as<uint32_t>(), ix->num.as<uint32_t>(), ix->ind.as<uint32_t>(), ix->pos.as<uint32_t>(),
+                     ix->K, (uint64_t)ix->total};
+    const HashArgs a{maxmis, good};
+    // every read with the carried state "not aligned"; then the reads that
+    // consulted it again with "aligned"; then the choice, read by read, in order
+    hipLaunchKernelGGL(k_hash_align, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, st, v, a, d_seq.as<uint8_t>(),
+                       d_off.as<uint64_t>(), d_len.as<int32_t>(), d_woff.as<uint64_t>(), d_scr.as<uint32_t>(),
+                       nullptr, N, 0, d_ret[0].as<int32_t>(), d_rev[0].as<uint8_t>(), d_pos[0].as<uint64_t>(),
+                       d_mp[0].as<int32_t>(), d_mt[0].as<int32_t>(), d_con.as<uint8_t>());
+    SA_CHECK(c, hipGetLastError());
+    std::vector<uint8_t> con(N);
+    SA_CHECK(c, hipMemcpyAsync(con.data(), d_con.p, N, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipStreamSynchronize(st));
+    std::vector<uint32_t> sel;
+    for (uint64_t i = 0; i < N; i++)
+        if (con[i]) sel.push_back((uint32_t)i);
+    if (!sel.empty()) {
+        SA_CHECK(c, d_sel.ensure(4 * sel.size()));
+        SA_CHECK(c, hipMemcpyAsync(d_sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_hash_align, dim3((uint32_t)((sel.size() + 255) / 256)), dim3(256), 0, st, v, a,
+                           d_seq.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<int32_t>(), d_woff.as<uint64_t>(),
+                           d_scr.as<uint32_t>(), d_sel.as<uint32_t>(), (uint64_t)sel.size(), 1,
+                           d_ret[1].as<int32_t>(), d_rev[1].as<uint8_t>(), d_pos[1].as<uint64_t>(),
+                           d_mp[1].as<int32_t>(), d_mt[1].as<int32_t>(), nullptr);
+        SA_CHECK(c, hipGetLastError());
+    }
+    SA_CHECK(c, hipMemcpyAsync(ret, d_ret[0].p, 4 * N, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipMemcpyAsync(rev, d_rev[0].p, N, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipMemcpyAsync(pos, d_pos[0].p, 8 * N, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipMemcpyAsync(mispos, d_mp[0].p, 4 * stride * N, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipMemcpyAsync(mistype, d_mt[0].p, 4 * stride * N, hipMemcpyDeviceToHost, st));
+    SA_CHECK(c, hipStreamSynchronize(st));
+    std::vector<int32_t> r1, m1, t1;
+    std::vector<uint8_t> v1;
+    std::vector<uint64_t> p1;
+    if (!sel.empty()) {
+        r1.resize(N);
+        v1.resize(N);
+        p1.resize(N);
+        m1.resize(stride * N);
+        t1.resize(stride * N);
+        SA_CHECK(c, hipMemcpyAsync(r1.data(), d_ret[1].p, 4 * N, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(v1.data(), d_rev[1].p, N, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(p1.data(), d_pos[1].p, 8 * N, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(m1.data(), d_mp[1].p, 4 * stride * N, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipMemcpyAsync(t1.data(), d_mt[1].p, 4 * stride * N, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipStreamSynchronize(st));
+    }
+    bool aligned = *ai_nmis >= 0 && *ai_nmis <= maxmis;
+    for (uint64_t i = 0; i < N; i++) {
+        if (aligned && con[i]) {   // the "aligned" variant of this read
+            ret[i] = r1[i];
+            rev[i] = v1[i];
+            pos[i] = p1[i];
+            std::memcpy(mispos + i * stride, &m1[i * stride], 4 * stride);
+            std::memcpy(mistype + i * stride, &t1[i * stride], 4 * stride);
+        }
+        aligned = ret[i] >= 0;
+    }
+    *ai_nmis = ret[N - 1];   // getHashAlignInfo leaves nmis = the count, or -1
+    return 0;
+}
+
+}  // extern "C"

@@ -163,6 +163,9 @@ struct Input {
 };
 
 struct Parsed {
+    // (not page-locked: hipHostRegister from the parser threads serialised in
+    // the driver -- 129 s of parser time for 14 GB, r2p; pageable staging from
+    // five contexts reaches ~19 GB/s, scripts/probe_h2d.py)
     Buf<uint8_t> names, seq, qual;
     Buf<uint16_t> nl;
     Buf<int32_t> sl;
@@ -171,9 +174,30 @@ struct Parsed {
     sa_block view() const { return sa_block{names.data(), nl.data(), seq.data(), sl.data(), qual.data(), nreads}; }
 };
 
+// Parsed blocks are recycled: a later block reuses their buffers instead of
+// faulting in fresh pages (~150 MB per block).
+struct ParsedPool {
+    std::mutex mu;
+    std::vector<std::unique_ptr<Parsed>> free;
+    std::unique_ptr<Parsed> get()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (free.empty()) return std::unique_ptr<Parsed>(new Parsed());
+        std::unique_ptr<Parsed> p = std::move(free.back());
+        free.pop_back();
+        return p;
+    }
+    void put(std::unique_ptr<Parsed> p)
+    {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        free.push_back(std::move(p));
+    }
+};
+
 struct Job {                     // one block between the reader and the writer
     Buf<uint8_t> t1, t2;          // its FASTQ text (freed once parsed)
-    Parsed p;
+    std::unique_ptr<Parsed> p;
     Buf<uint8_t> out;             // the encoded block
     int state = 0;                // 0 read, 1 parsed, 2 encoded
 };
@@ -189,10 +213,11 @@ int bare_plus(const Buf<uint8_t>& t)
     return nl[2] - nl[1] > 2 ? 0 : 1;
 }
 
-bool parse_job(Job& j, bool pe)
+bool parse_job(Job& j, bool pe, ParsedPool& pool)
 {
     const uint64_t cap = j.t1.size() + j.t2.size() + 16;
-    Parsed& p = j.p;
+    j.p = pool.get();
+    Parsed& p = *j.p;
     p.names.resize(cap);
     p.seq.resize(cap);
     p.qual.resize(cap);
@@ -275,6 +300,7 @@ int compress(const Options& o)
 
     std::mutex mu;
     std::condition_variable cv;
+    ParsedPool pool;   // (declared before the jobs: outlives them)
     std::map<int64_t, std::unique_ptr<Job>> jobs;
     // -v: when the stages first / last did something (seconds from the start)
     auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
@@ -382,13 +408,13 @@ int compress(const Options& o)
                     j = jobs[i].get();
                 }
                 const double tp = now_s();
-                if (!parse_job(*j, pe)) return fail("parse failed");
+                if (!parse_job(*j, pe, pool)) return fail("parse failed");
                 {
                     double cur = parse_busy.load();
                     while (!parse_busy.compare_exchange_weak(cur, cur + now_s() - tp)) {}
                 }
                 if (i == 0) {   // the ID template of the first block
-                    const sa_block fb = j->p.view();
+                    const sa_block fb = j->p->view();
                     if (sa_analyze_ids(&fb, pe ? 0 : 1, tmpl) != 0) return fail("ID analysis failed");
                 }
                 {
@@ -432,7 +458,7 @@ int compress(const Options& o)
                 std::vector<sa_block> in(js.size());
                 std::vector<sa_out> outs(js.size());
                 for (size_t i = 0; i < js.size(); i++) {
-                    in[i] = js[i]->p.view();
+                    in[i] = js[i]->p->view();
                     js[i]->out.resize(sa_output_bound(&in[i]));   // (uninitialised: only the real bytes are touched)
                     outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
                 }
@@ -485,13 +511,14 @@ int compress(const Options& o)
             jobs.erase(i);
         }
         uint32_t lng = 0;
-        for (uint32_t r = 0; r < j->p.nreads; r++) lng |= j->p.sl[r] > 0xffff;
+        for (uint32_t r = 0; r < j->p->nreads; r++) lng |= j->p->sl[r] > 0xffff;
         if (fwrite(j->out.data(), 1, j->out.size(), fo) != j->out.size()) {   // writeData@0x40e070: exit(1)
             fail("write error on " + path);
             break;
         }
-        info.push_back(sa_arc_block{(uint32_t)j->out.size(), lng, j->p.text1, j->p.text2});
+        info.push_back(sa_arc_block{(uint32_t)j->out.size(), lng, j->p->text1, j->p->text2});
         total += j->out.size();
+        pool.put(std::move(j->p));
         {
             std::lock_guard<std::mutex> g(mu);
             written = i + 1;

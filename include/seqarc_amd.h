@@ -68,6 +68,12 @@ const char *sa_version(void);
 
 /* ---- one-shot batch: replaces doFqzEncode@0x42d2d0 per block ---------- */
 uint64_t sa_output_bound(const sa_block *blk);
+/* page-locks host memory the caller hands to the encoder (block SoA buffers)
+ * so that staging is a DMA instead of a pageable copy through the runtime's
+ * bounce buffer (4.9 vs 56 GB/s H2D on MI355X); unregister before freeing it.
+ * 0 on success.  (The reader/parser buffers of seqarc_amd -c.) */
+int sa_host_register(void *p, uint64_t bytes);
+int sa_host_unregister(void *p);
 /* Batches above 3 Gi bases (env SA_BATCH_BASES lowers the cap) are encoded as
  * consecutive sub-batches; outputs keep the input order. */
 int sa_encode_blocks(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, sa_out *out);
@@ -189,6 +195,32 @@ int sa_arc_header(uint64_t block_bytes, uint8_t out[16]);
 /* Trailer bytes written to out (written at offset 16 + block_bytes), or -1. */
 int64_t sa_arc_trailer(const sa_arc_info *info, const sa_arc_block *blocks, uint32_t nblocks,
                        uint8_t *out, uint64_t cap);
+
+/* ---- HASH reference index and gapless seed alignment ----
+ * The index `SeqArc -i ref.fa` builds (HashAlignment::buildRefIndex@0x410190
+ * with HashRefIndex32: FASTA < 5 GiB), built on ctx's device and kept there;
+ * K / step / maxcount = param+0x1b64 / +0x1b70 / 2^(+0x1b6c) (14, 2, 65536).
+ * NULL on error (sa_last_error(ctx)). */
+typedef struct sa_hash_index sa_hash_index;
+sa_hash_index *sa_hash_build(sa_ctx *ctx, const char *fasta, uint64_t bytes, uint32_t K, uint32_t step,
+                             uint32_t maxcount);
+/* the "<ref.fa>.hash" file (HashRefIndex32::writeIndexFile@0x41ed00): K, bases,
+ * words, positions (u32), packed bases, per-K-mer counts, starts, positions */
+uint64_t sa_hash_file_bytes(const sa_hash_index *ix);
+int sa_hash_serialize(sa_ctx *ctx, const sa_hash_index *ix, uint8_t *out, uint64_t cap);
+uint32_t sa_hash_genome_length(const sa_hash_index *ix);
+void sa_hash_destroy(sa_hash_index *ix);
+/* getHashAlignInfo@0x4113c0 for n reads in order (HashAlignment::doSEAlign@
+ * 0x4117b0; doPEAlign@0x4117d0 aligns each mate the same way): per read the
+ * mismatch count or -1 (unaligned), strand (1: reverse complement), 1-based
+ * reference position, and maxmis + 1 slots of mismatch offsets and types (-1
+ * past the read's mismatches).  maxmis = param+0x1b60 (7), good = +0x1b74 (1).
+ * *ai_nmis is the align_info state the reference carries from read to read
+ * (AlignParam+0xc, never reset by doAlign@0x411910): in, before the first
+ * read; out, after the last. */
+int sa_hash_align(sa_ctx *ctx, const sa_hash_index *ix, const char *seq, const uint64_t *off, const int32_t *lens,
+                  int64_t n, int32_t maxmis, int32_t good, int32_t *ai_nmis, int32_t *ret, uint8_t *rev,
+                  uint64_t *pos, int32_t *mispos, int32_t *mistype);
 
 #ifdef __cplusplus
 }

@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-PHASE = {"k_coder_r": "coder_r", "k_replay_aux_long": "replay_aux", "k_md5": "md5", "k_emit_sq": "emit",
+PHASE = {"k_coder_rv": "coder_r", "k_coder_r": "coder_r", "k_replay_aux_long": "replay_aux", "k_md5": "md5", "k_emit_sq": "emit",
          "k_replay_seq": "replay_seq", "k_assemble": "assemble", "k_prep": "prep+scan"}
 
 
@@ -17,7 +17,7 @@ def per_launch(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        k = r["Kernel_Name"].split("(")[0].replace("sa::", "")
+        k = r["Kernel_Name"].split("(")[0].replace("sa::", "").replace("void ", "")
         tot[k] += float(r["Counter_Value"])
         n[k].add(r["Dispatch_Id"])
     return {k: tot[k] / len(n[k]) for k in tot}

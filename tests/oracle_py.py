@@ -34,7 +34,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(ORACLE_DIR, f) for f in ("fqz_oracle.c", "fqz_decode.c", "fqz_oracle.h", "orc_cli.c")]
+        srcs = [os.path.join(ORACLE_DIR, f)
+                for f in ("fqz_oracle.c", "fqz_decode.c", "hash_oracle.c", "fqz_oracle.h", "orc_cli.c")]
         if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
             build()
         l = C.CDLL(LIB)
@@ -51,6 +52,14 @@ def lib():
         l.orc_decode_block.restype = C.c_int64
         l.orc_rblock.argtypes = [P, C.c_size_t, C.c_double]
         l.orc_rblock.restype = None
+        l.ho_build.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        l.ho_build.restype = C.c_int64
+        l.ho_serialize.argtypes = [P, C.c_uint64]
+        l.ho_serialize.restype = C.c_int
+        l.ho_genome_length.argtypes = []
+        l.ho_genome_length.restype = C.c_uint32
+        l.ho_align_reads.argtypes = [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P]
+        l.ho_align_reads.restype = C.c_int
         _lib = l
     return _lib
 
@@ -154,3 +163,45 @@ def squeeze_streams(seed: int = 7, count: int = 12):
             c = (rng.random(n) * (t - f + 1)).astype(np.uint32)
         out.append((c.astype(np.uint16), f.astype(np.uint16), t.astype(np.uint16)))
     return out
+
+
+# ---- HASH reference index + gapless seed alignment (oracle/hash_oracle.c) ----
+HASH_K, HASH_STEP, HASH_MAXCOUNT, HASH_MAXMIS, HASH_GOOD = 14, 2, 1 << 16, 7, 1   # SeqArcParam ctor @0x407490
+
+
+def hash_index(fasta: bytes, k: int = HASH_K, step: int = HASH_STEP, maxcount: int = HASH_MAXCOUNT) -> bytes:
+    """The `.hash` file buildRefIndex@0x410190 writes for this FASTA (the
+    oracle keeps the index for hash_align)."""
+    l = lib()
+    n = l.ho_build(fasta, len(fasta), k, step, maxcount)
+    if n < 0:
+        raise ValueError("hash index build failed")
+    out = np.empty(n, dtype=np.uint8)
+    if l.ho_serialize(_p(out), n):
+        raise ValueError("hash index serialize failed")
+    return out.tobytes()
+
+
+def hash_align(reads: list[bytes], maxmis: int = HASH_MAXMIS, good: int = HASH_GOOD, ai_nmis: int = 0):
+    """getHashAlignInfo@0x4113c0 for the reads in order against the last
+    hash_index, one align_info carried across them (ai_nmis: its state before
+    the first read; 0 = a zero-filled AlignParam).  Arrays ret (mismatches or
+    -1), rev, pos (1-based), mispos / mistype ([n, maxmis+1], -1 past the
+    read's mismatches)."""
+    l = lib()
+    n = len(reads)
+    seq = np.frombuffer(b"".join(reads) or b"\0", dtype=np.uint8)
+    lens = np.array([len(r) for r in reads] or [0], dtype=np.int32)
+    off = np.zeros(max(n, 1), dtype=np.uint64)
+    if n > 1:
+        off[1:n] = np.cumsum(lens[:n - 1])
+    ret = np.zeros(max(n, 1), dtype=np.int32)
+    rev = np.zeros(max(n, 1), dtype=np.uint8)
+    pos = np.zeros(max(n, 1), dtype=np.uint64)
+    mp = np.zeros((max(n, 1), maxmis + 1), dtype=np.int32)
+    mt = np.zeros((max(n, 1), maxmis + 1), dtype=np.int32)
+    st = np.array([ai_nmis], dtype=np.int32)
+    if l.ho_align_reads(_p(seq), _p(off), _p(lens), n, maxmis, good, _p(st), _p(ret), _p(rev), _p(pos), _p(mp),
+                        _p(mt)):
+        raise ValueError("hash align failed")
+    return ret[:n], rev[:n], pos[:n], mp[:n], mt[:n]
