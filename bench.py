@@ -68,6 +68,9 @@ def parse_args(argv=None):
     ap.add_argument("--pairs", type=int, default=5_000_000, help="mate pairs per batch (reads with --se)")
     ap.add_argument("--se", action="store_true", help="single-end reads (configs[1] shape) instead of PE")
     ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--x-span", type=int, default=8,
+                    help="header x coordinates drawn from this many values (8: ~60 kB name stream per block, "
+                         "SURVEY 8's 58.7 kB; 0: uniform over 31000, ~195 kB)")
     ap.add_argument("--slevel", type=int, default=3)
     ap.add_argument("--qlevel", type=int, default=2)
     ap.add_argument("--block-size", type=int, default=50 << 20)
@@ -76,6 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--e2e-batches", type=int, default=-1,
                     help="batches written as FASTQ files for the end-to-end seqarc_amd -c run (-1: all, 0: skip)")
+    ap.add_argument("--e2e-repeat", type=int, default=0,
+                    help="the end-to-end files hold the e2e batches this many times over (a longer stream, so "
+                         "pipeline fill and drain weigh less; 0: 3 at one rank, 1 with more ranks)")
     ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--e2e-log", default=None, help="write the CLI's stderr (-v stage lines, SA_TRACE) here")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
@@ -136,7 +142,8 @@ def make_batch(gid: int, args, workers: int, files=None):
     import synth
     import fastqueeze_amd as fq
     paired = not args.se
-    t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers)
+    t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers,
+                            x_span=args.x_span)
     if files:
         for path, t in zip(files, (t1, t2)):
             if t is not None:
@@ -145,14 +152,13 @@ def make_batch(gid: int, args, workers: int, files=None):
     return fq.blocks_from_fastq(t1, t2, args.block_size)
 
 
-def end_to_end(args, files, contexts, expect: bytes, nblocks: int, threads: int):
+def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int):
     """`seqarc_amd -c` (the streaming reader / parser / encoder / writer
     pipeline) on the FASTQ files on disk: wall time of the whole process, and
     its own clock (device init to the closed .arc).  The archive's blocks must
     be the bench's blocks of the same input, byte for byte."""
     from fastqueeze_amd import build
     out = os.path.join(os.path.dirname(files[0]), "e2e")
-    batch = max(1, -(-nblocks // (2 * contexts)))   # every context gets >= 2 batches
     cmd = [build.CLI, "-c", "-f", "-v", "-t", str(threads), "-1", files[0]] + (["-2", files[1]] if len(files) > 1 else []) \
         + ["-o", out, "--contexts", str(contexts), "--batch", str(batch), "--slevel", str(args.slevel),
            "--qlevel", str(args.qlevel)]
@@ -486,8 +492,21 @@ def main():
         # contexts released above); per rank, then max over ranks
         barrier()
         expect = b"".join(outs if args.e2e_batches == 1 else outs[:-1])
+        rep = args.e2e_repeat or (3 if world == 1 else 1)
+        for f in e2e_files:   # the same FASTQ again, appended (rep - 1) times
+            size0 = os.path.getsize(f)
+            with open(f, "ab") as dst:
+                for _ in range(rep - 1):
+                    with open(f, "rb") as src:
+                        left = size0
+                        while left > 0:
+                            chunk = src.read(min(left, 256 << 20))
+                            dst.write(chunk)
+                            left -= len(chunk)
         try:
-            e2e = end_to_end(args, e2e_files, args.contexts, expect, len(keep["verify"]) * args.e2e_batches,
+            # batches of the bench's size (69 blocks): pass R of a batch takes as long for 28 blocks as
+            # for 69, so smaller batches lose the coder's parallelism
+            e2e = end_to_end(args, e2e_files, args.contexts, expect, len(keep["verify"]),
                              max(1, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
         finally:
             shutil.rmtree(os.path.dirname(e2e_files[0]), True)

@@ -2,9 +2,12 @@
 // FASTQ block cutting and parsing and the ID template analysis, mirroring the
 // reference's reader thread and pre-processing so the GPU receives exactly the
 // blocks SeqArc-1.6 would encode.
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -50,6 +53,56 @@ void newline_positions(const uint8_t* t, uint64_t len, std::vector<uint64_t>& ou
         if (!nl) break;
         out.push_back((uint64_t)((const uint8_t*)nl - t));
         p = (const uint8_t*)nl + 1;
+    }
+}
+
+// Newlines in t[0, len): 64 bytes per step, compare + movemask + popcount.
+uint64_t count_nl(const uint8_t* t, uint64_t len)
+{
+    uint64_t n = 0, i = 0;
+    const __m128i nl = _mm_set1_epi8('\n');
+    for (; i + 64 <= len; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(t + i));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(t + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i*)(t + i + 32));
+        const __m128i d = _mm_loadu_si128((const __m128i*)(t + i + 48));
+        const uint64_t m = (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(a, nl)) |
+                           (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(b, nl)) << 16 |
+                           (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(c, nl)) << 32 |
+                           (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(d, nl)) << 48;
+        n += (uint64_t)__builtin_popcountll(m);
+    }
+    for (; i < len; i++) n += t[i] == '\n';
+    return n;
+}
+
+// count_nl over `parts` concurrent slices
+uint64_t count_nl_par(const uint8_t* t, uint64_t len, int parts)
+{
+    if (parts <= 1 || len < (4u << 20)) return count_nl(t, len);
+    const uint64_t sl = (len + (uint64_t)parts - 1) / (uint64_t)parts;
+    std::vector<std::future<uint64_t>> fs;
+    for (int i = 1; i < parts; i++) {
+        const uint64_t a = std::min(len, (uint64_t)i * sl), b = std::min(len, a + sl);
+        fs.push_back(std::async(std::launch::async, [t, a, b]() { return count_nl(t + a, b - a); }));
+    }
+    uint64_t n = count_nl(t, std::min(len, sl));
+    for (auto& f : fs) n += f.get();
+    return n;
+}
+
+// Position of the newline `back` places before the last one in t[0, len)
+// (back = 0: the last newline), or -1.
+int64_t nl_from_end(const uint8_t* t, uint64_t len, uint64_t back)
+{
+    uint64_t e = len;
+    for (;;) {
+        const void* p = memrchr(t, '\n', (size_t)e);
+        if (!p) return -1;
+        const uint64_t at = (uint64_t)((const uint8_t*)p - t);
+        if (back == 0) return (int64_t)at;
+        --back;
+        e = at;
     }
 }
 
@@ -132,17 +185,33 @@ int sa_cut_next_pe(const uint8_t* w1, uint64_t avail1, int eof1, const uint8_t* 
         *end2 = avail2;
         return 0;
     }
-    std::vector<uint64_t> nl1, nl2;
-    newline_positions(w1, a1, nl1);
-    newline_positions(w2, a2, nl2);
-    const size_t k = std::min(nl1.size(), nl2.size());
+    // The same cut as sa_cut_pe (cultPEbuf@0x432180 over the newline arrays of
+    // both windows) without materialising the arrays: the newline counts of
+    // both windows (counted concurrently), then short walks back from their ends.
+    std::future<uint64_t> f2 = std::async(std::launch::async, [&]() { return count_nl_par(w2, a2, 3); });
+    const uint64_t k1 = count_nl_par(w1, a1, 3);
+    const uint64_t k2 = f2.get();
+    const uint64_t k = std::min(k1, k2);
     if (k < 2) return -1;
     int64_t j = (int64_t)k - 2;
-    const int64_t pos = end_pos(w1, a1, (int64_t)nl1[(size_t)j], first, (size_t)flen);
-    while (j >= 0 && (int64_t)nl1[(size_t)j] != pos) --j;
-    if (j < 0) return -1;   // the reference spins forever here (defect i)
-    *end1 = nl1[(size_t)j] + 1;
-    *end2 = nl2[(size_t)j] + 1;
+    const int64_t pj = nl_from_end(w1, a1, k1 - 1 - (uint64_t)j);
+    if (pj < 0) return -1;
+    const int64_t pos = end_pos(w1, a1, pj, first, (size_t)flen);
+    // index of the newline at pos: walk back from newline j
+    int64_t at = pj;
+    while (j >= 0 && at != pos) {
+        if (at < pos) return -1;   // pos is not a newline (the reference spins forever, SURVEY 5 i)
+        --j;
+        if (j < 0) break;
+        const void* p = memrchr(w1, '\n', (size_t)at);
+        if (!p) return -1;
+        at = (int64_t)((const uint8_t*)p - w1);
+    }
+    if (j < 0) return -1;
+    const int64_t q = nl_from_end(w2, a2, k2 - 1 - (uint64_t)j);
+    if (q < 0) return -1;
+    *end1 = (uint64_t)pos + 1;
+    *end2 = (uint64_t)q + 1;
     return 0;
 }
 

@@ -958,7 +958,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         SA_CHECK(c, hipStreamWaitEvent(c->st2, c->ev_fork, 0));
         SA_CHECK(c, h2d(c, c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), c->st2));
         ev_begin(c, PH_MD5, c->st2);
-        hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(64), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
+        hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(128), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
                            (uint32_t)md5t.size(), c->d_digests.as<uint32_t>(), c->md5_prio);
         ev_finish(c, PH_MD5, c->st2);
         SA_CHECK(c, hipGetLastError());

@@ -1871,153 +1871,147 @@ __global__ __launch_bounds__(256) void k_coder_l3(const CoderView cv, const Task
 // ---------------------------------------------------------------------------
 __device__ inline uint32_t rotl(uint32_t x, int c) { return __builtin_amdgcn_alignbit(x, x, 32 - c); }
 
-#define MD5_STEP(F, a, b, c, d, x, k, s) \
-    a = b + rotl(a + F(b, c, d) + x + k, s)
-#define MD5_F(b, c, d) (((c ^ d) & b) ^ d)
-#define MD5_G(b, c, d) (((b ^ c) & d) ^ c)
-#define MD5_H(b, c, d) (b ^ c ^ d)
-#define MD5_I(b, c, d) (c ^ (b | ~d))
+// One MD5 step.  mk = M[g] + K[i], prepared off the chain by the loader wave,
+// so the chain is F (one v_bitop3), v_add3, v_alignbit, v_add.
+#define MD5_STEP(F, a, b, c, d, mk, s) \
+    a = b + rotl(a + F(b, c, d) + mk, s)
+// the round functions as one v_bitop3 each (truth table over b = 0xf0,
+// c = 0xcc, d = 0xaa): F = b ? c : d, G = d ? b : c, H = b ^ c ^ d, I = c ^ (b | ~d)
+#define MD5_F(b, c, d) __builtin_amdgcn_bitop3_b32(b, c, d, 0xca)
+#define MD5_G(b, c, d) __builtin_amdgcn_bitop3_b32(b, c, d, 0xe4)
+#define MD5_H(b, c, d) __builtin_amdgcn_bitop3_b32(b, c, d, 0x96)
+#define MD5_I(b, c, d) __builtin_amdgcn_bitop3_b32(b, c, d, 0x39)
 
-__device__ inline void md5_block(uint32_t h[4], const uint32_t M[16])
+__device__ const uint32_t kMd5K[64] = {
+    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+    0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+    0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+    0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+    0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+    0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+
+// message word of step i (RFC 1321 3.4)
+__device__ inline uint32_t md5_word_of_step(uint32_t i)
+{
+    return i < 16 ? i : i < 32 ? (5 * i + 1) & 15 : i < 48 ? (3 * i + 5) & 15 : (7 * i) & 15;
+}
+
+// One 64-byte block from its 64 prepared words (read from LDS as 16 x 16 bytes).
+__device__ inline void md5_block_q(uint32_t h[4], const uint4 (&q)[16])
 {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-    MD5_STEP(MD5_F, a, b, c, d, M[0], 0xd76aa478, 7);
-    MD5_STEP(MD5_F, d, a, b, c, M[1], 0xe8c7b756, 12);
-    MD5_STEP(MD5_F, c, d, a, b, M[2], 0x242070db, 17);
-    MD5_STEP(MD5_F, b, c, d, a, M[3], 0xc1bdceee, 22);
-    MD5_STEP(MD5_F, a, b, c, d, M[4], 0xf57c0faf, 7);
-    MD5_STEP(MD5_F, d, a, b, c, M[5], 0x4787c62a, 12);
-    MD5_STEP(MD5_F, c, d, a, b, M[6], 0xa8304613, 17);
-    MD5_STEP(MD5_F, b, c, d, a, M[7], 0xfd469501, 22);
-    MD5_STEP(MD5_F, a, b, c, d, M[8], 0x698098d8, 7);
-    MD5_STEP(MD5_F, d, a, b, c, M[9], 0x8b44f7af, 12);
-    MD5_STEP(MD5_F, c, d, a, b, M[10], 0xffff5bb1, 17);
-    MD5_STEP(MD5_F, b, c, d, a, M[11], 0x895cd7be, 22);
-    MD5_STEP(MD5_F, a, b, c, d, M[12], 0x6b901122, 7);
-    MD5_STEP(MD5_F, d, a, b, c, M[13], 0xfd987193, 12);
-    MD5_STEP(MD5_F, c, d, a, b, M[14], 0xa679438e, 17);
-    MD5_STEP(MD5_F, b, c, d, a, M[15], 0x49b40821, 22);
-    MD5_STEP(MD5_G, a, b, c, d, M[1], 0xf61e2562, 5);
-    MD5_STEP(MD5_G, d, a, b, c, M[6], 0xc040b340, 9);
-    MD5_STEP(MD5_G, c, d, a, b, M[11], 0x265e5a51, 14);
-    MD5_STEP(MD5_G, b, c, d, a, M[0], 0xe9b6c7aa, 20);
-    MD5_STEP(MD5_G, a, b, c, d, M[5], 0xd62f105d, 5);
-    MD5_STEP(MD5_G, d, a, b, c, M[10], 0x02441453, 9);
-    MD5_STEP(MD5_G, c, d, a, b, M[15], 0xd8a1e681, 14);
-    MD5_STEP(MD5_G, b, c, d, a, M[4], 0xe7d3fbc8, 20);
-    MD5_STEP(MD5_G, a, b, c, d, M[9], 0x21e1cde6, 5);
-    MD5_STEP(MD5_G, d, a, b, c, M[14], 0xc33707d6, 9);
-    MD5_STEP(MD5_G, c, d, a, b, M[3], 0xf4d50d87, 14);
-    MD5_STEP(MD5_G, b, c, d, a, M[8], 0x455a14ed, 20);
-    MD5_STEP(MD5_G, a, b, c, d, M[13], 0xa9e3e905, 5);
-    MD5_STEP(MD5_G, d, a, b, c, M[2], 0xfcefa3f8, 9);
-    MD5_STEP(MD5_G, c, d, a, b, M[7], 0x676f02d9, 14);
-    MD5_STEP(MD5_G, b, c, d, a, M[12], 0x8d2a4c8a, 20);
-    MD5_STEP(MD5_H, a, b, c, d, M[5], 0xfffa3942, 4);
-    MD5_STEP(MD5_H, d, a, b, c, M[8], 0x8771f681, 11);
-    MD5_STEP(MD5_H, c, d, a, b, M[11], 0x6d9d6122, 16);
-    MD5_STEP(MD5_H, b, c, d, a, M[14], 0xfde5380c, 23);
-    MD5_STEP(MD5_H, a, b, c, d, M[1], 0xa4beea44, 4);
-    MD5_STEP(MD5_H, d, a, b, c, M[4], 0x4bdecfa9, 11);
-    MD5_STEP(MD5_H, c, d, a, b, M[7], 0xf6bb4b60, 16);
-    MD5_STEP(MD5_H, b, c, d, a, M[10], 0xbebfbc70, 23);
-    MD5_STEP(MD5_H, a, b, c, d, M[13], 0x289b7ec6, 4);
-    MD5_STEP(MD5_H, d, a, b, c, M[0], 0xeaa127fa, 11);
-    MD5_STEP(MD5_H, c, d, a, b, M[3], 0xd4ef3085, 16);
-    MD5_STEP(MD5_H, b, c, d, a, M[6], 0x04881d05, 23);
-    MD5_STEP(MD5_H, a, b, c, d, M[9], 0xd9d4d039, 4);
-    MD5_STEP(MD5_H, d, a, b, c, M[12], 0xe6db99e5, 11);
-    MD5_STEP(MD5_H, c, d, a, b, M[15], 0x1fa27cf8, 16);
-    MD5_STEP(MD5_H, b, c, d, a, M[2], 0xc4ac5665, 23);
-    MD5_STEP(MD5_I, a, b, c, d, M[0], 0xf4292244, 6);
-    MD5_STEP(MD5_I, d, a, b, c, M[7], 0x432aff97, 10);
-    MD5_STEP(MD5_I, c, d, a, b, M[14], 0xab9423a7, 15);
-    MD5_STEP(MD5_I, b, c, d, a, M[5], 0xfc93a039, 21);
-    MD5_STEP(MD5_I, a, b, c, d, M[12], 0x655b59c3, 6);
-    MD5_STEP(MD5_I, d, a, b, c, M[3], 0x8f0ccc92, 10);
-    MD5_STEP(MD5_I, c, d, a, b, M[10], 0xffeff47d, 15);
-    MD5_STEP(MD5_I, b, c, d, a, M[1], 0x85845dd1, 21);
-    MD5_STEP(MD5_I, a, b, c, d, M[8], 0x6fa87e4f, 6);
-    MD5_STEP(MD5_I, d, a, b, c, M[15], 0xfe2ce6e0, 10);
-    MD5_STEP(MD5_I, c, d, a, b, M[6], 0xa3014314, 15);
-    MD5_STEP(MD5_I, b, c, d, a, M[13], 0x4e0811a1, 21);
-    MD5_STEP(MD5_I, a, b, c, d, M[4], 0xf7537e82, 6);
-    MD5_STEP(MD5_I, d, a, b, c, M[11], 0xbd3af235, 10);
-    MD5_STEP(MD5_I, c, d, a, b, M[2], 0x2ad7d2bb, 15);
-    MD5_STEP(MD5_I, b, c, d, a, M[9], 0xeb86d391, 21);
+#define R4(F, i, s0, s1, s2, s3)                 \
+    MD5_STEP(F, a, b, c, d, q[i].x, s0);         \
+    MD5_STEP(F, d, a, b, c, q[i].y, s1);         \
+    MD5_STEP(F, c, d, a, b, q[i].z, s2);         \
+    MD5_STEP(F, b, c, d, a, q[i].w, s3)
+    R4(MD5_F, 0, 7, 12, 17, 22);
+    R4(MD5_F, 1, 7, 12, 17, 22);
+    R4(MD5_F, 2, 7, 12, 17, 22);
+    R4(MD5_F, 3, 7, 12, 17, 22);
+    R4(MD5_G, 4, 5, 9, 14, 20);
+    R4(MD5_G, 5, 5, 9, 14, 20);
+    R4(MD5_G, 6, 5, 9, 14, 20);
+    R4(MD5_G, 7, 5, 9, 14, 20);
+    R4(MD5_H, 8, 4, 11, 16, 23);
+    R4(MD5_H, 9, 4, 11, 16, 23);
+    R4(MD5_H, 10, 4, 11, 16, 23);
+    R4(MD5_H, 11, 4, 11, 16, 23);
+    R4(MD5_I, 12, 6, 10, 15, 21);
+    R4(MD5_I, 13, 6, 10, 15, 21);
+    R4(MD5_I, 14, 6, 10, 15, 21);
+    R4(MD5_I, 15, 6, 10, 15, 21);
+#undef R4
     h[0] += a;
     h[1] += b;
     h[2] += c;
     h[3] += d;
 }
 
-// One wave per message.  MD5 is one dependent chain per message, so one lane
-// computes; the whole wave streams the message through LDS a 1 KiB chunk (16
-// MD5 blocks, one 16-byte load per lane) ahead of it, so the chain never waits
-// on a load (the compute of a chunk, ~16 x 1000 cycles, covers the next
-// chunk's HBM latency).
+__device__ inline void md5_block_mk(uint32_t h[4], const uint4* __restrict__ w4)
+{
+    uint4 q[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) q[i] = w4[i];
+    md5_block_q(h, q);
+}
+
+// One workgroup of two waves per message.  MD5 is one dependent chain per
+// message: wave 0 runs it (every lane the same chain, so no lane masking), and
+// wave 1 streams the message a chunk of 16 blocks ahead: lane i loads the
+// message word of step i of each block and adds K[i], so the chain reads its
+// 64 step words with 16 LDS reads per block and does no other work -- four
+// dependent VALU ops per step (round 1 spent six issue slots per step: the
+// word moves to an SGPR and the add of K rode the chain wave).
 constexpr uint32_t MD5_CHUNK_BLOCKS = 16;
 
-__global__ __launch_bounds__(64) void k_md5(const Md5Task* __restrict__ tasks, uint32_t ntasks,
-                                            uint32_t* __restrict__ digests, uint32_t prio)
+__global__ __launch_bounds__(128) void k_md5(const Md5Task* __restrict__ tasks, uint32_t ntasks,
+                                             uint32_t* __restrict__ digests, uint32_t prio)
 {
-    set_chain_prio(prio);
-    __shared__ uint4 ring[2][64];
+    __shared__ uint4 mk[2][MD5_CHUNK_BLOCKS][16];   // prepared words: [slot][block][step / 4]
+    __shared__ uint32_t tb32[32];                   // the last one or two blocks (tail + padding)
     const uint32_t t = blockIdx.x;
     if (t >= ntasks) return;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave == 0) set_chain_prio(prio);
     const Md5Task tk = tasks[t];
-    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    // global (not flat) loads: a flat load also counts in lgkmcnt, so the LDS
-    // waits of the compute would wait for the prefetch
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
-    g_u32x4* gp = (g_u32x4*)(tk.ptr);
-    auto p = [&](uint64_t i) __attribute__((always_inline)) {
-        const u32x4 v = gp[i];
-        return make_uint4(v.x, v.y, v.z, v.w);
-    };
+    const uint32_t g = md5_word_of_step(lane);
+    const uint32_t kk = kMd5K[lane];
+    typedef const __attribute__((address_space(1))) uint32_t g_u32;
+    g_u32* w = (g_u32*)(tk.ptr);
     const uint64_t nfull = tk.len / 64;
-    const uint64_t nvec = nfull * 4;   // 16-byte words of the full blocks
     const uint64_t nck = (nfull + MD5_CHUNK_BLOCKS - 1) / MD5_CHUNK_BLOCKS;
-    uint32_t M[16];
-    uint4 nxt = lane < nvec ? p(lane) : make_uint4(0u, 0u, 0u, 0u);
+    auto produce = [&](uint64_t c) __attribute__((always_inline)) {
+        uint32_t* slot = reinterpret_cast<uint32_t*>(mk[c & 1]);
+        const uint64_t b0 = c * MD5_CHUNK_BLOCKS;
+        uint32_t v[MD5_CHUNK_BLOCKS];   // (past the last full block: its words again, unused)
+#pragma unroll
+        for (uint32_t k = 0; k < MD5_CHUNK_BLOCKS; k++) v[k] = w[min(b0 + k, nfull - 1) * 16 + g];
+#pragma unroll
+        for (uint32_t k = 0; k < MD5_CHUNK_BLOCKS; k++) slot[k * 64 + lane] = v[k] + kk;
+    };
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (wave == 1 && nck) produce(0);
+    __syncthreads();
     for (uint64_t c = 0; c < nck; c++) {
-        uint4* slot = ring[c & 1];
-        slot[lane] = nxt;
-        const uint64_t at = (c + 1) * 64 + lane;
-        if (c + 1 < nck) nxt = at < nvec ? p(at) : make_uint4(0u, 0u, 0u, 0u);
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        if (lane == 0) {
+        if (wave == 1) {
+            if (c + 1 < nck) produce(c + 1);
+        } else {
             const uint64_t left = nfull - c * MD5_CHUNK_BLOCKS;
             const uint32_t nb = left < MD5_CHUNK_BLOCKS ? (uint32_t)left : MD5_CHUNK_BLOCKS;
-            uint4 a = slot[0], b = slot[1], cc = slot[2], d = slot[3];
-            for (uint32_t k = 0; k < nb; k++) {
-                // the next block's words are read from LDS before this block's chain
-                const uint32_t kn = k + 1 < nb ? 4 * (k + 1) : 0;
-                const uint4 na = slot[kn], nb_ = slot[kn + 1], nc = slot[kn + 2], nd = slot[kn + 3];
-                M[0] = a.x; M[1] = a.y; M[2] = a.z; M[3] = a.w;
-                M[4] = b.x; M[5] = b.y; M[6] = b.z; M[7] = b.w;
-                M[8] = cc.x; M[9] = cc.y; M[10] = cc.z; M[11] = cc.w;
-                M[12] = d.x; M[13] = d.y; M[14] = d.z; M[15] = d.w;
-                md5_block(h, M);
-                a = na;
-                b = nb_;
-                cc = nc;
-                d = nd;
+            // the next block's words are read while this block's chain runs (two
+            // register sets; the scheduler barriers keep the reads ahead)
+            const uint4(*blk)[16] = mk[c & 1];
+            uint4 qa[16], qb[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) qa[i] = blk[0][i];
+            for (uint32_t k = 0; k < nb; k += 2) {
+                const uint32_t k1 = min(k + 1, nb - 1), k2 = min(k + 2, nb - 1);
+#pragma unroll
+                for (int i = 0; i < 16; i++) qb[i] = blk[k1][i];
+                __builtin_amdgcn_sched_barrier(0);
+                md5_block_q(h, qa);
+                __builtin_amdgcn_sched_barrier(0);
+                if (k + 1 >= nb) break;
+#pragma unroll
+                for (int i = 0; i < 16; i++) qa[i] = blk[k2][i];
+                __builtin_amdgcn_sched_barrier(0);
+                md5_block_q(h, qb);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
+        __syncthreads();
     }
+    if (wave == 1) return;
     // tail + padding (bit length of the u32 length, as the RSA MDString): the
     // wave writes the last one or two 64-byte blocks into LDS, two bytes a lane
     const uint32_t rem = (uint32_t)(tk.len - nfull * 64);
     const uint8_t* tail = tk.ptr + nfull * 64;
     const uint32_t tl = rem < 56 ? 64 : 128;
     const uint64_t bits = (uint64_t)(uint32_t)tk.len << 3;
-    uint8_t* tb = reinterpret_cast<uint8_t*>(ring[0]);
+    uint8_t* tb = reinterpret_cast<uint8_t*>(tb32);
 #pragma unroll
     for (uint32_t j = lane; j < 128; j += 64) {
         uint8_t v = 0;
@@ -2028,14 +2022,15 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Task* __restrict__ tasks, u
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    if (lane != 0) return;
-    const uint32_t* tw = reinterpret_cast<const uint32_t*>(ring[0]);
-    for (uint32_t o = 0; o < tl / 4; o += 16) {
-#pragma unroll
-        for (int k = 0; k < 16; k++) M[k] = tw[o + k];
-        md5_block(h, M);
+    uint32_t* slot = reinterpret_cast<uint32_t*>(mk[0]);
+    for (uint32_t o = 0; o < tl / 64; o++) {
+        slot[o * 64 + lane] = tb32[o * 16 + g] + kk;
     }
-    for (int k = 0; k < 4; k++) digests[(size_t)t * 4 + k] = h[k];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    for (uint32_t o = 0; o < tl / 64; o++) md5_block_mk(h, mk[0][o]);
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) digests[(size_t)t * 4 + k] = h[k];
 }
 
 // ---------------------------------------------------------------------------

@@ -13,6 +13,7 @@
 //   --devices N   GPUs (default 1), --contexts K   encoder contexts per GPU
 //   --batch B     blocks per encode, --block-size MiB (default 50)
 //   --share-device   all contexts on one GPU (tests of the multi-GPU gather)
+//   --host-only      read, cut and parse only (no device; measures the host pipeline)
 //
 // Compression mirrors SeqArc-1.6 main@0x41fd40 -> SeqArcContext::doReadAndEncode
 // @0x41a4e0 as a stream: one reader thread cuts 50 MiB blocks as the input
@@ -118,7 +119,8 @@ struct Buf {
 struct Input {
     int fd = -1;
     gzFile gz = nullptr;
-    bool is_gz = false, eof = false;
+    bool is_gz = false, eof = false, seekable = true;
+    uint64_t off = 0;   // file offset of the next byte (plain files)
     bool open(const char* path)
     {
         fd = ::open(path, O_RDONLY);
@@ -133,11 +135,54 @@ struct Input {
         }
         return true;
     }
+    // A plain file is read in slices by several threads at once (pread): one
+    // thread copies ~4 GB/s out of the page cache, below the device's rate.
+    long pread_all(uint8_t* dst, size_t n, uint64_t at)
+    {
+        size_t got = 0;
+        while (got < n) {
+            const ssize_t r = ::pread(fd, dst + got, n - got, (off_t)(at + got));
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0) return -1;
+            if (r == 0) break;
+            got += (size_t)r;
+        }
+        return (long)got;
+    }
     // appends up to n bytes to b; false on a read error
     bool fill(Buf<uint8_t>& b, size_t n)
     {
         size_t have = b.size();
         b.resize(have + n);
+        const size_t kSlice = 8u << 20;
+        if (!is_gz && seekable && !eof && n >= 2 * kSlice) {
+            const size_t ns = std::min<size_t>(8, n / kSlice), part = (n + ns - 1) / ns;
+            std::vector<std::future<long>> fs;
+            for (size_t i = 1; i < ns; i++) {
+                const size_t s0 = i * part, len = std::min(n, s0 + part) - s0;
+                fs.push_back(std::async(std::launch::async,
+                                        [this, &b, have, s0, len]() { return pread_all(b.data() + have + s0, len, off + s0); }));
+            }
+            const long r0 = pread_all(b.data() + have, std::min(n, part), off);
+            std::vector<long> rs{r0};
+            for (auto& f : fs) rs.push_back(f.get());
+            if (r0 >= 0 || errno != ESPIPE) {
+                size_t got = 0;
+                for (size_t i = 0; i < rs.size(); i++) {
+                    if (rs[i] < 0) { b.resize(have); return false; }
+                    const size_t want = std::min(n, i * part + part) - i * part;
+                    got += (size_t)rs[i];
+                    if ((size_t)rs[i] < want) {   // end of file inside slice i
+                        eof = true;
+                        break;
+                    }
+                }
+                off += got;
+                b.resize(have + got);
+                return true;
+            }
+            seekable = false;   // a pipe: sequential reads below
+        }
         size_t got = 0;
         while (got < n && !eof) {
             long r;
@@ -147,6 +192,7 @@ struct Input {
             } else {
                 r = (long)::read(fd, b.data() + have + got, n - got);
                 if (r < 0 && errno == EINTR) continue;
+                if (r > 0) off += (uint64_t)r;
             }
             if (r < 0) { b.resize(have + got); return false; }
             if (r == 0) eof = true;
@@ -195,6 +241,29 @@ struct ParsedPool {
     }
 };
 
+// Text windows are recycled too: a fresh 25-50 MiB allocation per block is
+// mapped anew and faults in every page on the first read into it.
+struct TextPool {
+    std::mutex mu;
+    std::vector<Buf<uint8_t>> free;
+    Buf<uint8_t> get()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (free.empty()) return Buf<uint8_t>();
+        Buf<uint8_t> b = std::move(free.back());
+        free.pop_back();
+        b.n = 0;
+        return b;
+    }
+    void put(Buf<uint8_t>& b)
+    {
+        if (!b.cap) return;
+        std::lock_guard<std::mutex> g(mu);
+        free.push_back(std::move(b));
+        b.n = b.cap = 0;
+    }
+};
+
 struct Job {                     // one block between the reader and the writer
     Buf<uint8_t> t1, t2;          // its FASTQ text (freed once parsed)
     std::unique_ptr<Parsed> p;
@@ -213,7 +282,7 @@ int bare_plus(const Buf<uint8_t>& t)
     return nl[2] - nl[1] > 2 ? 0 : 1;
 }
 
-bool parse_job(Job& j, bool pe, ParsedPool& pool)
+bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts)
 {
     const uint64_t cap = j.t1.size() + j.t2.size() + 16;
     j.p = pool.get();
@@ -241,14 +310,15 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool)
     p.qual.n = sb;
     p.nl.n = p.nreads;
     p.sl.n = p.nreads;
-    j.t1.release();
-    j.t2.release();
+    texts.put(j.t1);
+    texts.put(j.t2);
     return true;
 }
 
 struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr;
-    bool compress = false, decompress = false, force = false, in_dir = false, share_device = false, verbose = false;
+    bool compress = false, decompress = false, force = false, in_dir = false, share_device = false, verbose = false,
+         host_only = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
 };
@@ -280,7 +350,8 @@ int compress(const Options& o)
                                      : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // contexts: K per device; every device's contexts share one front scratch
     std::vector<sa_ctx*> ctxs;
-    for (int d = 0; d < o.devices; d++) {
+    if (o.host_only) ctxs.assign((size_t)o.contexts, nullptr);
+    for (int d = 0; d < o.devices && !o.host_only; d++) {
         sa_ctx* first = nullptr;
         for (int k = 0; k < o.contexts; k++) {
             const int dev = o.device + (o.share_device ? 0 : d);
@@ -300,12 +371,14 @@ int compress(const Options& o)
 
     std::mutex mu;
     std::condition_variable cv;
-    ParsedPool pool;   // (declared before the jobs: outlives them)
+    ParsedPool pool;   // (declared before the jobs: outlive them)
+    TextPool texts;
     std::map<int64_t, std::unique_ptr<Job>> jobs;
     // -v: when the stages first / last did something (seconds from the start)
     auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     const double t_ctx = now_s();
     std::atomic<double> t_read_done{0}, t_first_enc{1e30}, t_last_enc{0}, enc_busy{0}, parse_busy{0};
+    double fill_busy = 0, cut_busy = 0;   // (reader thread only)
     std::deque<int64_t> to_parse;
     int64_t nread = 0, nblocks = -1, written = 0, next_batch = 0;
     bool failed = false, tmpl_ready = false;
@@ -334,6 +407,7 @@ int compress(const Options& o)
             }
             b1.reserve(want);
             if (pe) b2.reserve(want);
+            const double tf0 = now_s();
             {   // the two mate files are read concurrently
                 std::future<bool> r2;
                 if (pe && b2.size() < want && !in2.eof)
@@ -355,6 +429,8 @@ int compress(const Options& o)
                 first.assign(f0, nl ? (const uint8_t*)nl + 1 : f0 + b1.size());
                 plus_bare = bare_plus(pe ? b2 : b1);
             }
+            const double tc0 = now_s();
+            fill_busy += tc0 - tf0;
             uint64_t e1 = 0, e2 = 0;
             if (pe) {
                 if (sa_cut_next_pe(b1.data(), b1.size(), in1.eof, b2.data(), b2.size(), in2.eof, bs, first.data(),
@@ -365,9 +441,10 @@ int compress(const Options& o)
                 if (e < 0) return fail("block cut failed");
                 e1 = (uint64_t)e;
             }
+            cut_busy += now_s() - tc0;
             std::unique_ptr<Job> j(new Job());
             auto hand_over = [&](Buf<uint8_t>& b, Buf<uint8_t>& to, uint64_t e) {
-                Buf<uint8_t> carry;   // the bytes after the cut start the next window
+                Buf<uint8_t> carry = texts.get();   // the bytes after the cut start the next window
                 carry.reserve(want);
                 memcpy(carry.data(), b.data() + e, b.size() - e);
                 carry.n = b.size() - e;
@@ -408,7 +485,7 @@ int compress(const Options& o)
                     j = jobs[i].get();
                 }
                 const double tp = now_s();
-                if (!parse_job(*j, pe, pool)) return fail("parse failed");
+                if (!parse_job(*j, pe, pool, texts)) return fail("parse failed");
                 {
                     double cur = parse_busy.load();
                     while (!parse_busy.compare_exchange_weak(cur, cur + now_s() - tp)) {}
@@ -468,7 +545,9 @@ int compress(const Options& o)
                     double cur = t_first_enc.load();
                     while (te < cur && !t_first_enc.compare_exchange_weak(cur, te)) {}
                 }
-                if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
+                if (!ctx) {   // --host-only
+                    for (sa_out& x : outs) x.size = 0;
+                } else if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
                     return fail(std::string("encode failed: ") + sa_last_error(ctx));
                 {
                     const double tf = now_s();
@@ -528,7 +607,8 @@ int compress(const Options& o)
     reader.join();
     for (auto& t : parsers) t.join();
     for (auto& t : encoders) t.join();
-    for (sa_ctx* c : ctxs) sa_destroy(c);
+    for (sa_ctx* c : ctxs)
+        if (c) sa_destroy(c);
     if (failed) {
         fprintf(stderr, "seqarc_amd: %s\n", err.c_str());
         if (fo) fclose(fo);
@@ -550,9 +630,10 @@ int compress(const Options& o)
         if (o.verbose)
             fprintf(stderr,
                     "seqarc_amd: contexts ready %.3f s, input read %.3f s, first encode %.3f s, last encode "
-                    "done %.3f s; encode busy %.3f s over %zu contexts, parse busy %.3f s over %d threads\n",
+                    "done %.3f s; encode busy %.3f s over %zu contexts, parse busy %.3f s over %d threads; "
+                    "reader: fill %.3f s, cut %.3f s\n",
                     t_ctx, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
-                    parse_busy.load(), nparse);
+                    parse_busy.load(), nparse, fill_busy, cut_busy);
         fprintf(stderr, "seqarc_amd: %zu block(s), %llu -> %llu bytes (%.2fx), %.3f s, %.1f MB/s\n", info.size(),
                 (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
                 (double)total_in / (double)(16 + total + tl), secs, (double)total_in / secs / 1e6);
@@ -792,6 +873,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--batch")) { if (!ival(o.batch, 1)) return usage(); }
         else if (!strcmp(a, "--block-size")) { if (!ival(o.block_mib, 1)) return usage(); }
         else if (!strcmp(a, "--share-device")) o.share_device = true;
+        else if (!strcmp(a, "--host-only")) o.host_only = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (a[0] != '-') pos.push_back(a);
         else return usage();

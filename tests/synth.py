@@ -73,13 +73,15 @@ def _sparse(rng: np.random.Generator, total: int, rate: float) -> np.ndarray:
 
 
 def _chunk(args):
-    seed, ci, s, n, read_len, paired, genome_len = args
+    seed, ci, s, n, read_len, paired, genome_len, x_span = args
     genome = _genome(seed, genome_len)
     win = np.lib.stride_tricks.sliding_window_view(genome, read_len)
     rng = np.random.default_rng([seed, ci])
     start = rng.integers(0, genome_len - max(450, read_len), size=n)
     ins = rng.integers(250, 450, size=n)
     x = rng.integers(1000, 32000, size=n)
+    if x_span:   # (the draw stays: every other byte is the same for any x_span)
+        x = 1000 + (x - 1000) % x_span
     cells = n * read_len
 
     def quals():
@@ -106,10 +108,14 @@ def _chunk(args):
 
 
 def generate(n_reads: int, read_len: int = 150, paired: bool = False, seed: int = 12345,
-             genome_len: int = 5_000_000, chunk: int = 250_000, progress=None, workers: int = 1):
+             genome_len: int = 5_000_000, chunk: int = 250_000, progress=None, workers: int = 1,
+             x_span: int = 0):
     """Return (r1_bytes, r2_bytes or None) of n_reads records (pairs if paired).
-    workers > 1 draws the chunks in that many spawned processes (same bytes)."""
-    jobs = [(seed, ci, s, min(chunk, n_reads - s), read_len, paired, genome_len)
+    workers > 1 draws the chunks in that many spawned processes (same bytes).
+    x_span > 0 draws the header x coordinate from that many values (x_span = 8:
+    a 50 MiB PE block's name stream is ~60 kB, near SURVEY 8's 58.7 kB; the
+    default, uniform over 31000 values, gives ~195 kB)."""
+    jobs = [(seed, ci, s, min(chunk, n_reads - s), read_len, paired, genome_len, x_span)
             for ci, s in enumerate(range(0, n_reads, chunk))]
     out1: list[bytes] = []
     out2: list[bytes] = []
