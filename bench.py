@@ -183,7 +183,7 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int):
     os.remove(out + ".arc")
     return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
             "cli_clock_mb_s": clock, "cli_stages": stages, "fastq_bytes": in_bytes, "contexts": contexts, "batch_blocks": batch,
-            "parse_threads": threads, "leading_blocks_identical_to_bench": same,
+            "parse": "device (sa_stage_text from page-locked text windows)", "leading_blocks_identical_to_bench": same,
             "command": "seqarc_amd -c -1 r1.fq -2 r2.fq (FASTQ on disk, page cache warm)"}
 
 

@@ -58,6 +58,15 @@ class _SaDecoded(C.Structure):
                 ("nreads", C.c_uint32), ("md5_ok", C.c_int32)]
 
 
+class _SaTextBlock(C.Structure):
+    _fields_ = [("text1", C.c_void_p), ("len1", C.c_uint64), ("text2", C.c_void_p), ("len2", C.c_uint64)]
+
+
+class _SaTextInfo(C.Structure):
+    _fields_ = [("nreads", C.c_uint32), ("len_long", C.c_uint32), ("name_bytes", C.c_uint64),
+                ("seq_bytes", C.c_uint64), ("out_bound", C.c_uint64)]
+
+
 class _SaOut(C.Structure):
     _fields_ = [("data", C.c_void_p), ("cap", C.c_uint64), ("size", C.c_uint64)]
 
@@ -91,6 +100,7 @@ def load_library(path: str | None = None):
         "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
         "sa_decode_block": ([P, U64, P, P, I32, P], I64),
         "sa_host_register": ([P, U64], I32), "sa_host_unregister": ([P], I32),
+        "sa_stage_text": ([P, P, I32, P], I32), "sa_host_alloc": ([U64], P), "sa_host_free": ([P], None),
         "sa_hash_build": ([P, P, U64, C.c_uint32, C.c_uint32, C.c_uint32], P),
         "sa_hash_file_bytes": ([P], U64), "sa_hash_serialize": ([P, P, P, U64], I32),
         "sa_hash_genome_length": ([P], C.c_uint32), "sa_hash_destroy": ([P], None),
@@ -243,7 +253,7 @@ class Encoder:
                      else self._lib.sa_create(device))
         if not self._ctx:
             raise SeqArcError(f"no usable gfx950 device {device} (the HIP path is the only path)")
-        self._staged: list[Block] = []
+        self._staged: list[int] | None = []   # output bound of each staged block
 
     def close(self):
         if self._ctx:
@@ -264,10 +274,27 @@ class Encoder:
         self._lib.sa_set_timing(self._ctx, 1 if on else 0)
 
     def stage(self, blocks: list[Block]):
-        self._staged = list(blocks)
+        self._staged = [int(self._lib.sa_output_bound(C.byref(b._c()))) for b in blocks]
         arr = (_SaBlock * max(1, len(blocks)))(*[b._c() for b in blocks])
         if self._lib.sa_stage(self._ctx, arr, len(blocks)) != 0:
             self._err("sa_stage")
+
+    def stage_text(self, texts) -> list[dict]:
+        """sa_stage_text: blocks given as FASTQ text, [(text1, text2 or None)]
+        as the reader cut them, parsed on the device.  Returns per-block counts."""
+        keep = [(_as_u8(a), None if b is None else _as_u8(b)) for a, b in texts]
+        dummy = np.zeros(1, np.uint8)   # (an empty PE mate text still needs a non-NULL pointer)
+        arr = (_SaTextBlock * max(1, len(keep)))(*[
+            _SaTextBlock(_ptr(a) or dummy.ctypes.data, a.size,
+                         None if b is None else (_ptr(b) or dummy.ctypes.data), 0 if b is None else b.size)
+            for a, b in keep])
+        info = (_SaTextInfo * max(1, len(keep)))()
+        if self._lib.sa_stage_text(self._ctx, arr, len(keep), info) != 0:
+            self._staged = None
+            self._err("sa_stage_text")
+        self._staged = [int(info[i].out_bound) for i in range(len(keep))]
+        return [{"nreads": int(info[i].nreads), "len_long": int(info[i].len_long),
+                 "name_bytes": int(info[i].name_bytes), "seq_bytes": int(info[i].seq_bytes)} for i in range(len(keep))]
 
     def run(self, cfg: Config):
         c = cfg._c()
@@ -279,9 +306,7 @@ class Encoder:
             raise SeqArcError("fetch(): nothing staged (encode_blocks() fetched its own output; stage() or "
                               "run_input() first)")
         outs, keep = [], []
-        for b in self._staged:
-            cb = b._c()
-            cap = int(self._lib.sa_output_bound(C.byref(cb)))
+        for cap in self._staged:
             buf = np.empty(cap, dtype=np.uint8)
             keep.append(buf)
             outs.append(_SaOut(_ptr(buf), cap, 0))
@@ -313,7 +338,7 @@ class Encoder:
         c = cfg._c()
         if self._lib.sa_run_input(self._ctx, inp._h, C.byref(c)) != 0:
             self._err("sa_run_input")
-        self._staged = inp.blocks
+        self._staged = [int(self._lib.sa_output_bound(C.byref(b._c()))) for b in inp.blocks]
 
     def device_bytes(self) -> int:
         return int(self._lib.sa_device_bytes(self._ctx))

@@ -109,9 +109,14 @@ struct sa_input {
     DBuf d_names, d_seq, d_qual, d_read_block, d_name_off, d_name_len, d_seq_off, d_seq_len;
     std::vector<uint32_t> h_read_block, h_name_off, h_seq_off, h_seq_len;
     std::vector<uint16_t> h_name_len;
+    // sa_stage_text: the texts and the device parse's scratch (sa_parse.hip)
+    DBuf d_text, d_tile_text, d_tile_cnt, d_tile_base, d_ptexts, d_ntiles, d_text_nl, d_pblocks, d_btot, d_perr, d_nl,
+        d_src;
     ~sa_input()
     {
-        for (DBuf* b : {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off, &d_seq_len})
+        for (DBuf* b : {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off, &d_seq_len,
+                        &d_text, &d_tile_text, &d_tile_cnt, &d_tile_base, &d_ptexts, &d_ntiles, &d_text_nl, &d_pblocks,
+                        &d_btot, &d_perr, &d_nl, &d_src})
             b->release();
     }
 };
@@ -126,6 +131,7 @@ struct sa_ctx {
     bool serial_seq = false;
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
+    bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
     // pass-R placement (k_coder_rv): four chains per workgroup, one per SIMD, and
     // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
     // SA_CODER_LDS)
@@ -380,7 +386,7 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     }
     ck0.push_back((uint32_t)ck.size());
     const uint32_t nck = (uint32_t)ck.size(), nbk = (uint32_t)c->blocks.size();
-    SA_CHECK(c, c->d_qual_q.ensure(seq_bytes + 16));
+    SA_CHECK(c, c->d_qual_q.ensure(seq_bytes + 64));
     bv.qual_q = c->d_qual_q.as<uint8_t>();
     if (!nck) return 0;
     SA_CHECK(c, c->d_rb_chunks.ensure(sizeof(RbChunk) * nck));
@@ -794,8 +800,8 @@ int input_upload(sa_input* I, const sa_block* in, int n, hipStream_t st, std::st
         }
     }
     IN_CHECK(I->d_names.ensure(nb + 16));
-    IN_CHECK(I->d_seq.ensure(sb + 16));
-    IN_CHECK(I->d_qual.ensure(sb + 16));
+    IN_CHECK(I->d_seq.ensure(sb + 64));   // (k_prep_sq16 reads whole dwords past a read)
+    IN_CHECK(I->d_qual.ensure(sb + 64));
     const size_t nr4 = (size_t)std::max<uint32_t>(nr, 1) * 4;
     IN_CHECK(I->d_read_block.ensure(nr4));
     IN_CHECK(I->d_name_off.ensure(nr4));
@@ -975,8 +981,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     if (nr) {
         hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
                            F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(), d_err);
-        hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
-                           F->d_counts.as<uint32_t>(), d_err);
+        if (c->prep_wave)   // (SA_PREP_WAVE=1: the wave-per-read variant, for A/B)
+            hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
+                               F->d_counts.as<uint32_t>(), d_err);
+        else
+            hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
+                               F->d_counts.as<uint32_t>(), d_err);
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, F->d_counts.as<uint32_t>(),
                        c->d_totals.as<uint32_t>(), F->d_maxlen.as<uint16_t>());
@@ -1436,6 +1446,9 @@ int sa_encode_blocks(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, 
 }
 
 }  // extern "C"
+
+// FASTQ text parsed on the device (sa_stage_text)
+#include "sa_parse.hip"
 
 // the HASH reference-index path
 #include "sa_hash.hip"

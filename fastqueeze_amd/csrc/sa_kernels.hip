@@ -225,6 +225,147 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_prep_sq(const BatchView bv,
         prep_sq_read(bv, r, lane, stage[w], counts, err);
 }
 
+// k_prep_sq16: the same columns, one 16-lane row per read (four reads per
+// wave), each lane taking 16 bytes of the read per step with SWAR byte tests:
+// a 150 bp read is one step instead of three wave-wide steps of ballots.
+// Bytes are loaded as aligned dwords and funnel-shifted (the reads start at
+// any byte).  The gap statistics of reads with an N/IUPAC base (seq_stat's
+// second loop) run on the row's first lane.
+__device__ __forceinline__ uint32_t bytes_nonzero(uint32_t v)   // 0x80 in every non-zero byte
+{
+    return (((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v) & 0x80808080u;
+}
+
+__device__ __forceinline__ void load16(const uint8_t* p, uint32_t w[4])
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) d[k] = al[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t row_sum(uint32_t v)
+{
+#pragma unroll
+    for (int d = W / 2; d >= 1; d >>= 1) v += __shfl_xor(v, d, W);
+    return v;
+}
+template <int W>
+__device__ __forceinline__ uint32_t row_max(uint32_t v)
+{
+#pragma unroll
+    for (int d = W / 2; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d, W);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+template <int W>
+__device__ __forceinline__ uint32_t row_min(uint32_t v)
+{
+#pragma unroll
+    for (int d = W / 2; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(v, d, W);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+constexpr uint32_t PREP_ROW = 16;
+
+__global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ err)
+{
+    const uint32_t rl = threadIdx.x & (PREP_ROW - 1);
+    const uint32_t rows = gridDim.x * (blockDim.x / PREP_ROW);
+    const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / PREP_ROW;
+    const uint32_t nr = bv.nreads_total;
+    // wave-uniform trip count: every row of the wave loops while any row has a read
+    const uint32_t wrow0 = row0 & ~3u;
+    for (uint32_t base = wrow0; base < nr; base += rows) {
+        const uint32_t r = base + (row0 & 3u);
+        const bool live = r < nr;
+        uint32_t len = 0;
+        const uint8_t *s = nullptr, *q = nullptr, *qv = nullptr;
+        if (live) {
+            const DevBlock& blk = bv.blocks[bv.read_block[r]];
+            const uint64_t o = blk.seq_base + bv.seq_off[r];
+            s = bv.seq + o;
+            q = bv.qual + o;
+            qv = bv.qual_q + o;
+            len = bv.seq_len[r];
+        }
+        uint32_t valid = 0, nonascii = 0, lastnz = 0, firstbad = 0xffffffffu, maxq = 0, hasn = 0;
+        const uint32_t wlen = (uint32_t)wave_max_i32((int)len);   // (the wave's longest read)
+        for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * PREP_ROW) {
+            const uint32_t pos = i0 + 16 * rl;
+            if (pos < len) {
+                const uint32_t cnt = len - pos < 16 ? len - pos : 16;
+                uint32_t sw[4], qw[4], cw[4];
+                load16(s + pos, sw);
+                load16(q + pos, qw);
+                if (bv.lossy) load16(qv + pos, cw);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t nb = cnt > 4u * k ? (cnt - 4u * k < 4 ? cnt - 4u * k : 4) : 0;
+                    const uint32_t inm = nb >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * nb)) - 1u));
+                    const uint32_t x = sw[k] | 0x20202020u;
+                    const uint32_t acgt = ~(bytes_nonzero(x ^ 0x61616161u) & bytes_nonzero(x ^ 0x63636363u) &
+                                            bytes_nonzero(x ^ 0x67676767u) & bytes_nonzero(x ^ 0x74747474u)) & inm;
+                    valid += __popc(acgt);
+                    nonascii |= sw[k] & inm;
+                    const uint32_t nonb = ~acgt & inm;   // N / IUPAC bytes: max of their (signed) qualities
+                    if (nonb) {
+                        hasn = 1;
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (nonb & (0x80u << (8 * j))) {
+                                const int qi = (int)(int8_t)(qw[k] >> (8 * j));
+                                if (qi > (int)maxq) maxq = (uint32_t)qi;
+                            }
+                    }
+                    const uint32_t qc = bv.lossy ? cw[k] : qw[k];   // the QUAL stream's bytes
+                    const uint32_t nh = bytes_nonzero(qc ^ 0x23232323u) & inm;
+                    if (nh) lastnz = pos + 4 * k + (31 - __clz(nh)) / 8 + 1;
+                    const uint32_t lo = qc & 0x7f7f7f7fu;
+                    const uint32_t bad = ((qc & 0x80808080u) | (~(lo + 0x5f5f5f5fu) & 0x80808080u) |
+                                          ((lo + 0x01010101u) & 0x80808080u)) & inm;
+                    if (bad && firstbad == 0xffffffffu) firstbad = pos + 4 * k + (__ffs(bad) - 1) / 8;
+                }
+            }
+        }
+        valid = row_sum<PREP_ROW>(valid);
+        nonascii = row_max<PREP_ROW>(nonascii ? 1u : 0u);
+        lastnz = row_max<PREP_ROW>(lastnz);
+        firstbad = row_min<PREP_ROW>(firstbad);
+        maxq = row_max<PREP_ROW>(maxq);
+        hasn = row_max<PREP_ROW>(hasn);
+        if (live && rl == 0) {
+            SeqStat st{valid, len - valid, maxq & 0xffu, 0u, 0u, nonascii ? (uint32_t)E_NONASCII : 0u};
+            if (hasn) {   // seq_stat's second loop
+                uint32_t gap = 0;
+                for (uint32_t i = 0; i < len; i++) {
+                    if ((int)st.maxq < (int)(int8_t)q[i]) continue;
+                    if (base_code(s[i]) > 3) {
+                        gap++;
+                    } else {
+                        st.exc++;
+                        st.npos_syms += 1 + (uint32_t)nbits_u32(gap);
+                        gap = 0;
+                    }
+                }
+            }
+            const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, lastnz, st, firstbad < lastnz);
+            if (e) atomicOr(err, e);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // R-Block lossy pre-pass (rblock@0x426c10; sa_logic.h): speculative chunk
 // passes, one carry lane per block, chunk replay writing every run once.

@@ -14,6 +14,7 @@
 //   --batch B     blocks per encode, --block-size MiB (default 50)
 //   --share-device   all contexts on one GPU (tests of the multi-GPU gather)
 //   --host-only      read, cut and parse only (no device; measures the host pipeline)
+//   --host-parse     parse the blocks on host threads (default: on the device, sa_stage_text)
 //
 // Compression mirrors SeqArc-1.6 main@0x41fd40 -> SeqArcContext::doReadAndEncode
 // @0x41a4e0 as a stream: one reader thread cuts 50 MiB blocks as the input
@@ -82,17 +83,49 @@ bool may_write(const std::string& path, bool force)
 }
 
 // An uninitialised growable array (std::vector would zero-fill the tens of MB
-// of every block's buffers, which costs more than parsing them).
+// of every block's buffers, which costs more than parsing them).  `pinned`
+// (set while empty): page-locked storage (sa_host_alloc), so that staging the
+// text to the device is a DMA.
 template <class T>
 struct Buf {
-    std::unique_ptr<T[]> d;
+    T* d = nullptr;
     size_t n = 0, cap = 0;
+    bool pinned = false;
+    Buf() = default;
+    Buf(const Buf&) = delete;
+    Buf& operator=(const Buf&) = delete;
+    Buf(Buf&& o) noexcept { take(o); }
+    Buf& operator=(Buf&& o) noexcept
+    {
+        if (this != &o) {
+            release();
+            take(o);
+        }
+        return *this;
+    }
+    ~Buf() { release(); }
+    void take(Buf& o)
+    {
+        d = o.d;
+        n = o.n;
+        cap = o.cap;
+        pinned = o.pinned;
+        o.d = nullptr;
+        o.n = o.cap = 0;
+    }
     void reserve(size_t c)
     {
         if (c <= cap) return;
-        std::unique_ptr<T[]> nd(new T[c]);
-        if (n) memcpy(nd.get(), d.get(), n * sizeof(T));
-        d = std::move(nd);
+        T* nd;
+        if (pinned) {
+            nd = static_cast<T*>(sa_host_alloc(c * sizeof(T)));
+            if (!nd) throw std::bad_alloc();
+        } else {
+            nd = new T[c];
+        }
+        if (n) memcpy(nd, d, n * sizeof(T));
+        free_(d);
+        d = nd;
         cap = c;
     }
     void resize(size_t c)
@@ -100,15 +133,22 @@ struct Buf {
         reserve(c);
         n = c;
     }
+    void free_(T* p)
+    {
+        if (!p) return;
+        if (pinned) sa_host_free(p);
+        else delete[] p;
+    }
     void release()
     {
-        d.reset();
+        free_(d);
+        d = nullptr;
         n = cap = 0;
     }
     T& operator[](size_t i) { return d[i]; }
     const T& operator[](size_t i) const { return d[i]; }
-    T* data() { return d.get(); }
-    const T* data() const { return d.get(); }
+    T* data() { return d; }
+    const T* data() const { return d; }
     size_t size() const { return n; }
     bool empty() const { return n == 0; }
 };
@@ -246,10 +286,15 @@ struct ParsedPool {
 struct TextPool {
     std::mutex mu;
     std::vector<Buf<uint8_t>> free;
+    bool pinned = false;   // new windows in page-locked memory (device parse)
     Buf<uint8_t> get()
     {
         std::lock_guard<std::mutex> g(mu);
-        if (free.empty()) return Buf<uint8_t>();
+        if (free.empty()) {
+            Buf<uint8_t> b;
+            b.pinned = pinned;
+            return b;
+        }
         Buf<uint8_t> b = std::move(free.back());
         free.pop_back();
         b.n = 0;
@@ -265,8 +310,10 @@ struct TextPool {
 };
 
 struct Job {                     // one block between the reader and the writer
-    Buf<uint8_t> t1, t2;          // its FASTQ text (freed once parsed)
-    std::unique_ptr<Parsed> p;
+    Buf<uint8_t> t1, t2;          // its FASTQ text (recycled once parsed / staged)
+    uint64_t text1 = 0, text2 = 0;   // its text bytes in input 1 / 2
+    uint32_t nreads = 0, len_long = 0;
+    std::unique_ptr<Parsed> p;     // host parse (--host-parse; block 0 for the ID template)
     Buf<uint8_t> out;             // the encoded block
     int state = 0;                // 0 read, 1 parsed, 2 encoded
 };
@@ -282,7 +329,7 @@ int bare_plus(const Buf<uint8_t>& t)
     return nl[2] - nl[1] > 2 ? 0 : 1;
 }
 
-bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts)
+bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_text)
 {
     const uint64_t cap = j.t1.size() + j.t2.size() + 16;
     j.p = pool.get();
@@ -310,15 +357,19 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts)
     p.qual.n = sb;
     p.nl.n = p.nreads;
     p.sl.n = p.nreads;
-    texts.put(j.t1);
-    texts.put(j.t2);
+    j.nreads = p.nreads;
+    for (uint32_t r = 0; r < p.nreads; r++) j.len_long |= p.sl[r] > 0xffff;
+    if (!keep_text) {
+        texts.put(j.t1);
+        texts.put(j.t2);
+    }
     return true;
 }
 
 struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr;
     bool compress = false, decompress = false, force = false, in_dir = false, share_device = false, verbose = false,
-         host_only = false;
+         host_only = false, host_parse = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
 };
@@ -346,8 +397,9 @@ int compress(const Options& o)
     if (!may_write(path, o.force)) return 1;
 
     const uint64_t bs = (uint64_t)o.block_mib << 20;   // BlockSize(M), default 50 (param+0x1b78)
-    const int nparse = o.threads > 0 ? o.threads
-                                     : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int nparse = !o.host_parse && !o.host_only ? 1   // (device parse: block 0 only, for the ID template)
+                       : o.threads > 0 ? o.threads
+                                       : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // contexts: K per device; every device's contexts share one front scratch
     std::vector<sa_ctx*> ctxs;
     if (o.host_only) ctxs.assign((size_t)o.contexts, nullptr);
@@ -373,6 +425,13 @@ int compress(const Options& o)
     std::condition_variable cv;
     ParsedPool pool;   // (declared before the jobs: outlive them)
     TextPool texts;
+    // Device parse (default): the reader's text windows are page-locked, the
+    // encoder threads stage them with sa_stage_text (H2D DMA + parse in HBM)
+    // and recycle them at once; only block 0 is parsed here, for the ID
+    // template.  --host-parse / --host-only: -t parser threads build the SoA.
+    const bool dev_parse = !o.host_parse && !o.host_only;
+    texts.pinned = dev_parse;
+    std::atomic<double> stage_busy{0};
     std::map<int64_t, std::unique_ptr<Job>> jobs;
     // -v: when the stages first / last did something (seconds from the start)
     auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
@@ -380,7 +439,7 @@ int compress(const Options& o)
     std::atomic<double> t_read_done{0}, t_first_enc{1e30}, t_last_enc{0}, enc_busy{0}, parse_busy{0};
     double fill_busy = 0, cut_busy = 0;   // (reader thread only)
     std::deque<int64_t> to_parse;
-    int64_t nread = 0, nblocks = -1, written = 0, next_batch = 0;
+    int64_t nread = 0, nblocks = -1, written = 0, next_batch = 0, staged = 0;
     bool failed = false, tmpl_ready = false;
     std::string err;
     uint8_t tmpl[512] = {0};
@@ -396,13 +455,16 @@ int compress(const Options& o)
 
     // reader: cuts blocks as the input arrives
     std::thread reader([&]() {
-        Buf<uint8_t> b1, b2;
+        Buf<uint8_t> b1 = texts.get(), b2 = texts.get();
         std::vector<uint8_t> first;
         const uint64_t want = pe ? (uint64_t)((uint32_t)bs >> 1) : bs;
         for (int64_t i = 0;; i++) {
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return failed || (size_t)(nread - written) < max_inflight; });
+                // device parse: at most two batches of page-locked text ahead of the staging
+                cv.wait(lk, [&] {
+                    return failed || ((size_t)(nread - written) < max_inflight && (!dev_parse || nread - staged < 2 * B));
+                });
                 if (failed) return;
             }
             b1.reserve(want);
@@ -456,11 +518,14 @@ int compress(const Options& o)
             if (pe) hand_over(b2, j->t2, e2);
             const bool last = b1.empty() && b2.empty() && in1.eof && (!pe || in2.eof);
             if (last) t_read_done = now_s();
+            j->text1 = e1;
+            j->text2 = e2;
+            if (dev_parse && i > 0) j->state = 1;   // (parsed on the device when staged)
             {
                 std::lock_guard<std::mutex> g(mu);
                 total_in += e1 + e2;
                 jobs[i] = std::move(j);
-                to_parse.push_back(i);
+                if (!dev_parse || i == 0) to_parse.push_back(i);
                 nread = i + 1;
                 if (last) nblocks = nread;
             }
@@ -485,7 +550,7 @@ int compress(const Options& o)
                     j = jobs[i].get();
                 }
                 const double tp = now_s();
-                if (!parse_job(*j, pe, pool, texts)) return fail("parse failed");
+                if (!parse_job(*j, pe, pool, texts, dev_parse)) return fail("parse failed");
                 {
                     double cur = parse_busy.load();
                     while (!parse_busy.compare_exchange_weak(cur, cur + now_s() - tp)) {}
@@ -494,6 +559,7 @@ int compress(const Options& o)
                     const sa_block fb = j->p->view();
                     if (sa_analyze_ids(&fb, pe ? 0 : 1, tmpl) != 0) return fail("ID analysis failed");
                 }
+                if (dev_parse) pool.put(std::move(j->p));   // (only the template needed it)
                 {
                     std::lock_guard<std::mutex> g(mu);
                     j->state = 1;
@@ -532,23 +598,53 @@ int compress(const Options& o)
                     b1 = nblocks >= 0 ? std::min(nblocks, b0 + B) : b0 + B;
                     for (int64_t i = b0; i < b1; i++) js.push_back(jobs[i].get());
                 }
-                std::vector<sa_block> in(js.size());
                 std::vector<sa_out> outs(js.size());
-                for (size_t i = 0; i < js.size(); i++) {
-                    in[i] = js[i]->p->view();
-                    js[i]->out.resize(sa_output_bound(&in[i]));   // (uninitialised: only the real bytes are touched)
-                    outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
-                }
                 const sa_cfg c = cfg;
                 const double te = now_s();
                 {
                     double cur = t_first_enc.load();
                     while (te < cur && !t_first_enc.compare_exchange_weak(cur, te)) {}
                 }
-                if (!ctx) {   // --host-only
-                    for (sa_out& x : outs) x.size = 0;
-                } else if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
-                    return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                if (dev_parse) {
+                    std::vector<sa_text_block> tin(js.size());
+                    std::vector<sa_text_info> ti(js.size());
+                    for (size_t i = 0; i < js.size(); i++)
+                        tin[i] = sa_text_block{js[i]->t1.data(), js[i]->t1.size(), pe ? js[i]->t2.data() : nullptr,
+                                               pe ? js[i]->t2.size() : 0};
+                    if (sa_stage_text(ctx, tin.data(), (int)tin.size(), ti.data()) != 0)
+                        return fail(std::string("staging failed: ") + sa_last_error(ctx));
+                    {
+                        const double ts = now_s() - te;
+                        double cur = stage_busy.load();
+                        while (!stage_busy.compare_exchange_weak(cur, cur + ts)) {}
+                    }
+                    {
+                        std::lock_guard<std::mutex> g(mu);
+                        staged += (int64_t)js.size();
+                    }
+                    for (size_t i = 0; i < js.size(); i++) {
+                        texts.put(js[i]->t1);   // (the device holds the text now)
+                        texts.put(js[i]->t2);
+                        js[i]->nreads = ti[i].nreads;
+                        js[i]->len_long = ti[i].len_long;
+                        js[i]->out.resize(ti[i].out_bound);
+                        outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                    }
+                    cv.notify_all();   // (text windows are free for the reader)
+                    if (sa_run(ctx, &c) != 0 || sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
+                        return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                } else {
+                    std::vector<sa_block> in(js.size());
+                    for (size_t i = 0; i < js.size(); i++) {
+                        in[i] = js[i]->p->view();
+                        js[i]->out.resize(sa_output_bound(&in[i]));   // (uninitialised: only the real bytes are touched)
+                        outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                    }
+                    if (!ctx) {   // --host-only
+                        for (sa_out& x : outs) x.size = 0;
+                    } else if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
+                        return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                }
                 {
                     const double tf = now_s();
                     double cur = enc_busy.load();
@@ -589,15 +685,14 @@ int compress(const Options& o)
             j = std::move(jobs[i]);
             jobs.erase(i);
         }
-        uint32_t lng = 0;
-        for (uint32_t r = 0; r < j->p->nreads; r++) lng |= j->p->sl[r] > 0xffff;
+        const uint32_t lng = j->len_long;
         if (fwrite(j->out.data(), 1, j->out.size(), fo) != j->out.size()) {   // writeData@0x40e070: exit(1)
             fail("write error on " + path);
             break;
         }
-        info.push_back(sa_arc_block{(uint32_t)j->out.size(), lng, j->p->text1, j->p->text2});
+        info.push_back(sa_arc_block{(uint32_t)j->out.size(), lng, j->text1, j->text2});
         total += j->out.size();
-        pool.put(std::move(j->p));
+        if (j->p) pool.put(std::move(j->p));
         {
             std::lock_guard<std::mutex> g(mu);
             written = i + 1;
@@ -631,9 +726,10 @@ int compress(const Options& o)
             fprintf(stderr,
                     "seqarc_amd: contexts ready %.3f s, input read %.3f s, first encode %.3f s, last encode "
                     "done %.3f s; encode busy %.3f s over %zu contexts, parse busy %.3f s over %d threads; "
-                    "reader: fill %.3f s, cut %.3f s\n",
+                    "reader: fill %.3f s, cut %.3f s; stage %.3f s (%s parse)\n",
                     t_ctx, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
-                    parse_busy.load(), nparse, fill_busy, cut_busy);
+                    parse_busy.load(), nparse, fill_busy, cut_busy, stage_busy.load(),
+                    dev_parse ? "device" : "host");
         fprintf(stderr, "seqarc_amd: %zu block(s), %llu -> %llu bytes (%.2fx), %.3f s, %.1f MB/s\n", info.size(),
                 (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
                 (double)total_in / (double)(16 + total + tl), secs, (double)total_in / secs / 1e6);
@@ -874,6 +970,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--block-size")) { if (!ival(o.block_mib, 1)) return usage(); }
         else if (!strcmp(a, "--share-device")) o.share_device = true;
         else if (!strcmp(a, "--host-only")) o.host_only = true;
+        else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (a[0] != '-') pos.push_back(a);
         else return usage();

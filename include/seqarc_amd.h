@@ -80,6 +80,32 @@ int sa_encode_blocks(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, 
 
 /* ---- staged API (inputs resident in HBM; used by bench.py) ------------ */
 int sa_stage(sa_ctx *ctx, const sa_block *in, int n);     /* H2D copy of a batch   */
+/* FASTQ text of one block as the reader cut it (doReadPEJob@0x432d10 /
+ * cultPEbuf@0x432180 hand these to getBlockRead[PE]): file 1 and, for PE,
+ * file 2 (text2 = NULL: single-end). */
+typedef struct sa_text_block {
+    const uint8_t *text1;
+    uint64_t len1;
+    const uint8_t *text2;
+    uint64_t len2;
+} sa_text_block;
+typedef struct sa_text_info {   /* per block, written by sa_stage_text */
+    uint32_t nreads;
+    uint32_t len_long;          /* a read > 65535 bp (SeqArcMemBuf+0x2)     */
+    uint64_t name_bytes;
+    uint64_t seq_bytes;
+    uint64_t out_bound;         /* sa_output_bound of the parsed block      */
+} sa_text_info;
+/* Stages a batch given as FASTQ text: the texts are copied to HBM (a DMA when
+ * they are in sa_host_alloc memory) and parsed there into the batch sa_stage
+ * would upload -- getBlockRead@0x411b60 (SE) / getBlockReadPE@0x412920 (PE),
+ * byte for byte the blocks sa_parse_se / sa_parse_pe give.  info (optional, n
+ * entries) gets each block's counts.  Then sa_run / sa_fetch.  -1 and
+ * sa_last_error where sa_parse_* fail.  The texts may be reused on return. */
+int sa_stage_text(sa_ctx *ctx, const sa_text_block *in, int n, sa_text_info *info);
+/* page-locked host memory (hipHostMalloc) for the reader's text windows */
+void *sa_host_alloc(uint64_t bytes);
+void sa_host_free(void *p);
 int sa_run(sa_ctx *ctx, const sa_cfg *cfg);                /* encode the staged batch */
 int sa_fetch(sa_ctx *ctx, sa_out *out, int n);             /* D2H of the encaps     */
 /* per-phase device time (ms) of the last sa_run, measured with HIP events on

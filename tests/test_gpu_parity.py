@@ -274,9 +274,14 @@ def test_cli_multi_device_gather(tmp_path, test_pair):
     # the streaming pipeline with several contexts sharing a front, 2-block batches, 2 parser threads
     r4 = subprocess.run(base[:-1] + ["2", "--contexts", "3", "-t", "2", "-o", str(tmp_path / "four")],
                         capture_output=True, text=True, timeout=120)
+    # the blocks parsed on host threads (--host-parse) instead of on the device
+    r5 = subprocess.run(base[:-1] + ["2", "--contexts", "2", "--host-parse", "-t", "2", "-o", str(tmp_path / "five")],
+                        capture_output=True, text=True, timeout=120)
     assert r1.returncode == 0 and r3.returncode == 0 and r4.returncode == 0, (r1.stderr, r3.stderr, r4.stderr)
+    assert r5.returncode == 0, r5.stderr
     one = open(tmp_path / "one.arc", "rb").read()
     assert one == open(tmp_path / "three.arc", "rb").read() == open(tmp_path / "four.arc", "rb").read()
+    assert one == open(tmp_path / "five.arc", "rb").read()
     blocks = fq.blocks_from_fastq(*test_pair, 1 << 20)
     assert len(blocks) > 3
     tmpl = fq.analyze_ids(blocks[0], False)
@@ -362,3 +367,74 @@ def test_resident_inputs_concurrent_contexts(pe_full):
     assert not errs, errs
     for (i, rep), (which, outs) in got.items():
         assert outs == want[which], (i, rep)
+
+
+# ---- sa_stage_text: FASTQ text parsed on the device ------------------------------------------
+
+def _texts(t1, t2=None, bs=fq.BLOCK_SIZE):
+    a = fq._as_u8(t1)
+    if t2 is None:
+        return [(a[s:e], None) for s, e in fq.cut_se(a, bs)]
+    b = fq._as_u8(t2)
+    return [(a[s1:e1], b[s2:e2]) for (s1, e1), (s2, e2) in fq.cut_pe(a, b, bs)]
+
+
+def _check_text(enc, t1, t2, cfg, bs=fq.BLOCK_SIZE):
+    """Blocks staged as text (device parse) encode to the same bytes as the
+    host-parsed blocks (getBlockRead[PE] restated in fastq_host.cpp)."""
+    texts = _texts(t1, t2, bs)
+    blocks = fq.blocks_from_fastq(t1, t2, bs)
+    info = enc.stage_text(texts)
+    enc.run(cfg)
+    got = enc.fetch()
+    assert [i["nreads"] for i in info] == [b.nreads for b in blocks]
+    assert [i["name_bytes"] for i in info] == [b.names.size for b in blocks]
+    assert [i["seq_bytes"] for i in info] == [b.seq.size for b in blocks]
+    assert [i["len_long"] for i in info] == [int((b.seq_lens > 0xffff).any()) for b in blocks]
+    want = enc.encode(blocks, cfg)
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"block {k}: device-parsed {len(g)} B vs host-parsed {len(w)} B"
+    return got
+
+
+def test_stage_text_reference_pair(enc, test_pair):
+    tmpl = fq.analyze_ids(fq.blocks_from_fastq(*test_pair)[0], False)
+    _check_text(enc, *test_pair, fq.Config(bin_mode=int(tmpl[0])))
+    _check_text(enc, *test_pair, fq.Config(bin_mode=int(tmpl[0])), bs=1 << 20)   # several blocks per batch
+    _check_text(enc, test_pair[0], None, fq.Config(bin_mode=1), bs=300_000)
+
+
+def test_stage_text_edge_cases(enc):
+    _check_text(enc, synth.edge_cases(), None, fq.Config())
+    _check_text(enc, _long_read_fastq(91, 120), None, fq.Config(qlevel=3))
+    t_long, _ = synth.generate(6, seed=92, read_len=70000)             # len_long blocks
+    _check_text(enc, t_long, None, fq.Config())
+    a, _ = synth.generate(3000, paired=True, seed=93)
+    _, short = synth.generate(3000, paired=True, seed=94, read_len=90)  # mates of unequal length
+    _check_text(enc, a, short, fq.Config(), bs=400_000)
+    # no newline at the end of the file: the partial last line is dropped by both parsers
+    _check_text(enc, synth.edge_cases() + b"@tail", None, fq.Config())
+
+
+def test_stage_text_full_size_batch(enc):
+    """Three 50 MiB PE blocks (the bench's unit of work), staged as text."""
+    a, b = synth.generate(150_000, paired=True, seed=31)
+    _check_text(enc, a, b, fq.Config())
+
+
+@pytest.mark.parametrize("case", ["truncated_se", "qual_len_pe", "long_name", "qual_past_end"])
+def test_stage_text_rejects_what_the_host_parser_rejects(enc, case):
+    rec = b"@r\nACGT\n+\nIIII\n"
+    if case == "truncated_se":
+        t1, t2 = rec * 3 + b"@r\nACGT\n+\n", None
+    elif case == "qual_len_pe":
+        t1, t2 = rec * 2, rec + b"@r\nACGT\n+\nIII\n"
+    elif case == "long_name":
+        t1, t2 = rec + b"@" + b"n" * 70000 + b"\nACGT\n+\nIIII\n", None
+    else:   # SE copies the sequence's length of qualities: past the end of the block
+        t1, t2 = rec + b"@r\nACGTACGT\n+\nII\n", None
+    with pytest.raises(fq.SeqArcError):
+        fq.parse_se(t1) if t2 is None else fq.parse_pe(t1, t2)
+    with pytest.raises(fq.SeqArcError):
+        enc.stage_text([(t1, t2)])
+    _check_text(enc, rec * 5, None, fq.Config())   # the context stays usable
