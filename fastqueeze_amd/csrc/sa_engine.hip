@@ -132,6 +132,12 @@ struct sa_ctx {
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
+    // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
+    uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
+    // k_md5<true> reads the next block's words while the chain runs: 148 VGPRs instead
+    // of 60, which costs the co-resident front kernels more than it saves (r2x:
+    // 11.6 vs 12.9 GB/s), so SA_MD5_PIPE=1 only
+    bool md5_pipe = std::getenv("SA_MD5_PIPE") && std::atoi(std::getenv("SA_MD5_PIPE")) != 0;
     // pass-R placement (k_coder_rv): four chains per workgroup, one per SIMD, and
     // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
     // SA_CODER_LDS)
@@ -295,7 +301,7 @@ hipError_t sync_d2h(sa_ctx* c, hipStream_t st)
 // 8 workgroups per CU, fewer for a small batch
 uint32_t wave_grid(const sa_ctx* c, uint32_t nreads)
 {
-    return std::max<uint32_t>(1, std::min<uint32_t>((nreads + EMIT_WAVES - 1) / EMIT_WAVES, 8 * c->n_cu));
+    return std::max<uint32_t>(1, std::min<uint32_t>((nreads + EMIT_WAVES - 1) / EMIT_WAVES, c->wg_per_cu * c->n_cu));
 }
 
 // Digit widths of a sort over bits [lo, hi): the fewest passes of at most
@@ -964,7 +970,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         SA_CHECK(c, hipStreamWaitEvent(c->st2, c->ev_fork, 0));
         SA_CHECK(c, h2d(c, c->d_md5tasks.p, md5t.data(), sizeof(Md5Task) * md5t.size(), c->st2));
         ev_begin(c, PH_MD5, c->st2);
-        hipLaunchKernelGGL(k_md5, dim3((uint32_t)md5t.size()), dim3(128), 0, c->st2, c->d_md5tasks.as<Md5Task>(),
+        hipLaunchKernelGGL(c->md5_pipe ? k_md5<true> : k_md5<false>, dim3((uint32_t)md5t.size()), dim3(128), 0, c->st2,
+                           c->d_md5tasks.as<Md5Task>(),
                            (uint32_t)md5t.size(), c->d_digests.as<uint32_t>(), c->md5_prio);
         ev_finish(c, PH_MD5, c->st2);
         SA_CHECK(c, hipGetLastError());

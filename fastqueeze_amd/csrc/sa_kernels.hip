@@ -2088,6 +2088,7 @@ __device__ inline void md5_block_mk(uint32_t h[4], const uint4* __restrict__ w4)
 // word moves to an SGPR and the add of K rode the chain wave).
 constexpr uint32_t MD5_CHUNK_BLOCKS = 16;
 
+template <bool PIPE>
 __global__ __launch_bounds__(128) void k_md5(const Md5Task* __restrict__ tasks, uint32_t ntasks,
                                              uint32_t* __restrict__ digests, uint32_t prio)
 {
@@ -2125,22 +2126,26 @@ __global__ __launch_bounds__(128) void k_md5(const Md5Task* __restrict__ tasks, 
             // the next block's words are read while this block's chain runs (two
             // register sets; the scheduler barriers keep the reads ahead)
             const uint4(*blk)[16] = mk[c & 1];
-            uint4 qa[16], qb[16];
+            if (!PIPE) {   // (SA_MD5_PIPE=0: one block's reads at a time, for A/B)
+                for (uint32_t k = 0; k < nb; k++) md5_block_mk(h, blk[k]);
+            } else {
+                uint4 qa[16], qb[16];
 #pragma unroll
-            for (int i = 0; i < 16; i++) qa[i] = blk[0][i];
-            for (uint32_t k = 0; k < nb; k += 2) {
-                const uint32_t k1 = min(k + 1, nb - 1), k2 = min(k + 2, nb - 1);
+                for (int i = 0; i < 16; i++) qa[i] = blk[0][i];
+                for (uint32_t k = 0; k < nb; k += 2) {
+                    const uint32_t k1 = min(k + 1, nb - 1), k2 = min(k + 2, nb - 1);
 #pragma unroll
-                for (int i = 0; i < 16; i++) qb[i] = blk[k1][i];
-                __builtin_amdgcn_sched_barrier(0);
-                md5_block_q(h, qa);
-                __builtin_amdgcn_sched_barrier(0);
-                if (k + 1 >= nb) break;
+                    for (int i = 0; i < 16; i++) qb[i] = blk[k1][i];
+                    __builtin_amdgcn_sched_barrier(0);
+                    md5_block_q(h, qa);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (k + 1 >= nb) break;
 #pragma unroll
-                for (int i = 0; i < 16; i++) qa[i] = blk[k2][i];
-                __builtin_amdgcn_sched_barrier(0);
-                md5_block_q(h, qb);
-                __builtin_amdgcn_sched_barrier(0);
+                    for (int i = 0; i < 16; i++) qa[i] = blk[k2][i];
+                    __builtin_amdgcn_sched_barrier(0);
+                    md5_block_q(h, qb);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
         __syncthreads();

@@ -240,7 +240,8 @@ extern "C" {
 void* sa_host_alloc(uint64_t bytes)
 {
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    // portable: any device's contexts may stage from it (--devices N)
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
     return p;
 }
 

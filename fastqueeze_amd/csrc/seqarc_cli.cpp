@@ -91,6 +91,7 @@ struct Buf {
     T* d = nullptr;
     size_t n = 0, cap = 0;
     bool pinned = false;
+    bool external = false;   // d belongs to an arena (TextPool): never freed here
     Buf() = default;
     Buf(const Buf&) = delete;
     Buf& operator=(const Buf&) = delete;
@@ -110,8 +111,10 @@ struct Buf {
         n = o.n;
         cap = o.cap;
         pinned = o.pinned;
+        external = o.external;
         o.d = nullptr;
         o.n = o.cap = 0;
+        o.external = false;
     }
     void reserve(size_t c)
     {
@@ -127,6 +130,7 @@ struct Buf {
         free_(d);
         d = nd;
         cap = c;
+        external = false;
     }
     void resize(size_t c)
     {
@@ -135,7 +139,7 @@ struct Buf {
     }
     void free_(T* p)
     {
-        if (!p) return;
+        if (!p || external) return;
         if (pinned) sa_host_free(p);
         else delete[] p;
     }
@@ -144,6 +148,7 @@ struct Buf {
         free_(d);
         d = nullptr;
         n = cap = 0;
+        external = false;
     }
     T& operator[](size_t i) { return d[i]; }
     const T& operator[](size_t i) const { return d[i]; }
@@ -283,13 +288,39 @@ struct ParsedPool {
 
 // Text windows are recycled too: a fresh 25-50 MiB allocation per block is
 // mapped anew and faults in every page on the first read into it.
+//
+// Device parse: the windows are page-locked, carved from arena chunks of
+// kChunk windows each -- one hipHostMalloc per chunk, not per window (the
+// runtime serialises host allocations against the encoder threads' calls).
 struct TextPool {
+    static constexpr size_t kChunk = 16;
     std::mutex mu;
     std::vector<Buf<uint8_t>> free;
+    std::vector<void*> chunks;
     bool pinned = false;   // new windows in page-locked memory (device parse)
+    size_t win = 0;        // window bytes of the arena (set before the first get)
+    ~TextPool()
+    {
+        free.clear();
+        for (void* c : chunks) sa_host_free(c);
+    }
     Buf<uint8_t> get()
     {
         std::lock_guard<std::mutex> g(mu);
+        if (free.empty() && pinned && win) {
+            uint8_t* c = static_cast<uint8_t*>(sa_host_alloc(kChunk * win));
+            if (c) {
+                chunks.push_back(c);
+                for (size_t k = 0; k < kChunk; k++) {
+                    Buf<uint8_t> b;
+                    b.pinned = true;
+                    b.external = true;
+                    b.d = c + k * win;
+                    b.cap = win;
+                    free.push_back(std::move(b));
+                }
+            }
+        }
         if (free.empty()) {
             Buf<uint8_t> b;
             b.pinned = pinned;
@@ -414,6 +445,9 @@ int compress(const Options& o)
         }
         if (!first) break;
     }
+    if (o.verbose)
+        for (sa_ctx* c : ctxs)
+            if (c) sa_set_timing(c, 1);
     if (ctxs.empty()) {
         fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", o.device);
         return 1;
@@ -431,6 +465,7 @@ int compress(const Options& o)
     // template.  --host-parse / --host-only: -t parser threads build the SoA.
     const bool dev_parse = !o.host_parse && !o.host_only;
     texts.pinned = dev_parse;
+    texts.win = (pe ? (size_t)((uint32_t)bs >> 1) : (size_t)bs) + (64u << 10);   // a window + slack for the carry
     std::atomic<double> stage_busy{0};
     std::map<int64_t, std::unique_ptr<Job>> jobs;
     // -v: when the stages first / last did something (seconds from the start)
@@ -588,6 +623,7 @@ int compress(const Options& o)
             for (;;) {
                 int64_t k, b0, b1;
                 std::vector<Job*> js;
+                const double tw = now_s();
                 {
                     std::unique_lock<std::mutex> lk(mu);
                     if (failed) return;
@@ -631,8 +667,26 @@ int compress(const Options& o)
                         outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
                     }
                     cv.notify_all();   // (text windows are free for the reader)
-                    if (sa_run(ctx, &c) != 0 || sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
-                        return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                    const double tr = now_s();
+                    if (sa_run(ctx, &c) != 0) return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                    const double tf = now_s();
+                    if (sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
+                        return fail(std::string("fetch failed: ") + sa_last_error(ctx));
+                    if (o.verbose) {   // per batch: when it became ready, what each step took, device phases
+                        const char* pn[16];
+                        float pm[16];
+                        const int np = sa_phase_times(ctx, pn, pm, 16);
+                        std::string ph;
+                        for (int x = 0; x < np; x++) {
+                            char pb[48];
+                            snprintf(pb, sizeof pb, " %s %.0f", pn[x], pm[x]);
+                            ph += pb;
+                        }
+                        fprintf(stderr,
+                                "seqarc_amd: batch %lld (%zu blocks) context %p: asked %.3f s, ready %.3f s, stage %.3f s, "
+                                "run %.3f s, fetch %.3f s; device ms:%s\n",
+                                (long long)k, js.size(), (void*)ctx, tw, te, tr - te, tf - tr, now_s() - tf, ph.c_str());
+                    }
                 } else {
                     std::vector<sa_block> in(js.size());
                     for (size_t i = 0; i < js.size(); i++) {
