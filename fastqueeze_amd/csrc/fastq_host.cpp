@@ -188,8 +188,8 @@ int sa_cut_next_pe(const uint8_t* w1, uint64_t avail1, int eof1, const uint8_t* 
     // The same cut as sa_cut_pe (cultPEbuf@0x432180 over the newline arrays of
     // both windows) without materialising the arrays: the newline counts of
     // both windows (counted concurrently), then short walks back from their ends.
-    std::future<uint64_t> f2 = std::async(std::launch::async, [&]() { return count_nl_par(w2, a2, 3); });
-    const uint64_t k1 = count_nl_par(w1, a1, 3);
+    std::future<uint64_t> f2 = std::async(std::launch::async, [&]() { return count_nl_par(w2, a2, 2); });
+    const uint64_t k1 = count_nl_par(w1, a1, 2);
     const uint64_t k2 = f2.get();
     const uint64_t k = std::min(k1, k2);
     if (k < 2) return -1;

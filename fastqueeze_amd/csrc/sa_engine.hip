@@ -603,6 +603,14 @@ sa_ctx* sa_create(int device)
         return nullptr;
     }
     if (hipSetDevice(device) != hipSuccess) return nullptr;
+    // SA_SYNC=block: host waits sleep instead of spinning (the command line sets
+    // it: five encoder threads spinning on their streams took the CPU share the
+    // reader needs); only effective before the device's first use in the process
+    if (const char* e = std::getenv("SA_SYNC")) {
+        if (!std::strcmp(e, "block")) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
+        else if (!std::strcmp(e, "spin")) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        (void)hipGetLastError();   // (hipErrorSetOnActiveProcess when the device is in use already)
+    }
     sa_ctx* c = new sa_ctx();
     // pass-R placement knobs (k_coder_rv): waves per workgroup, unused LDS per workgroup
     if (const char* e = std::getenv("SA_CODER_WAVES")) {

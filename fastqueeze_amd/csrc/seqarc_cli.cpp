@@ -201,7 +201,9 @@ struct Input {
         b.resize(have + n);
         const size_t kSlice = 8u << 20;
         if (!is_gz && seekable && !eof && n >= 2 * kSlice) {
-            const size_t ns = std::min<size_t>(8, n / kSlice), part = (n + ns - 1) / ns;
+            // (four slices: the box's CPU share is a cgroup quota -- more copy
+            // threads throttle the whole process, encoder threads included)
+            const size_t ns = std::min<size_t>(4, n / kSlice), part = (n + ns - 1) / ns;
             std::vector<std::future<long>> fs;
             for (size_t i = 1; i < ns; i++) {
                 const size_t s0 = i * part, len = std::min(n, s0 + part) - s0;
@@ -993,6 +995,7 @@ int decompress(const Options& o)
 
 int main(int argc, char** argv)
 {
+    setenv("SA_SYNC", "block", 0);   // encoder threads sleep on their streams (sa_create)
     Options o;
     std::vector<const char*> pos;
     for (int i = 1; i < argc; i++) {
