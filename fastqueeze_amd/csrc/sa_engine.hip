@@ -342,10 +342,16 @@ void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const ui
 
 // sorts keys by bits [lo, hi) (bits below lo ride along); the result is in
 // keys[result_buf] / vals[result_buf]
+// index_vals: the input values are each element's index in its segment and are
+// not read (the first pass computes them)
 int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
-             DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf)
+             DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf, bool index_vals = false)
 {
     result_buf = 0;
+    if (plan.total && hi <= lo && index_vals) {
+        c->err = "internal: a sort without passes over implicit values";
+        return -1;
+    }
     if (plan.total == 0 || hi <= lo) return 0;
     SortView sv{};
     sv.segs = segs.as<SortSeg>();
@@ -357,7 +363,7 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     int cur = 0, shift = lo;
     for (const int db : sort_digits(lo, hi)) {
         const uint32_t* kin = keys[cur]->as<uint32_t>();
-        const uint32_t* vin = vals[cur]->as<uint32_t>();
+        const uint32_t* vin = index_vals && shift == lo ? nullptr : vals[cur]->as<uint32_t>();
         uint32_t* kout = keys[cur ^ 1]->as<uint32_t>();
         uint32_t* vout = vals[cur ^ 1]->as<uint32_t>();
         if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
@@ -1121,10 +1127,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
                            c->d_totals.as<uint32_t>(), F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(),
                            F->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                           akb[0]->as<uint32_t>(), avb[0]->as<uint32_t>(), d_err);
+                           akb[0]->as<uint32_t>(), nullptr, d_err);   // (AUX values: the index, run_sort)
         hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                            F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                           akb[0]->as<uint32_t>(), avb[0]->as<uint32_t>());
+                           akb[0]->as<uint32_t>(), nullptr);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);
@@ -1161,7 +1167,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_SORT_AUX, st);
     if (run_sort(c, st, pa, F->d_segs_aux, F->d_tile_aux, F->d_hist_aux, akb, avb, AUX_SYM_BITS,
-                 AUX_SYM_BITS + aux_bits, aux_sorted_buf))
+                 AUX_SYM_BITS + aux_bits, aux_sorted_buf, true))
         return -1;
     ev_finish(c, PH_SORT_AUX, st);
     ev_begin(c, PH_REPLAY_AUX, st);

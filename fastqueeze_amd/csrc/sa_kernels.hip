@@ -553,7 +553,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
             if (nz) n = i0 + 64 - (uint32_t)__builtin_clzll(nz);
         }
         uint32_t* K = aux_key + blk.aux_sym_base;
-        uint32_t* V = aux_val + blk.aux_sym_base;
+        uint32_t* V = aux_val ? aux_val + blk.aux_sym_base : nullptr;
         const uint32_t pos0 = blk.sbase[ST_QUAL] + off[C_QUAL];
         const int ql = bv.qlevel;
         uint32_t p1 = 0, p2 = 0, ctx_c = 0;   // sym i0-1, sym i0-2, the context after i0-1
@@ -576,7 +576,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
             const uint32_t last = lane >= 1 ? uc : ctx_c;
             if (i < n) {
                 K[pos0 + i] = ((M_QUAL + last) << AUX_SYM_BITS) | sym;
-                V[pos0 + i] = pos0 + i;
+                if (aux_val) V[pos0 + i] = pos0 + i;
             }
             const int tail = (int)(n - i0 < 64 ? n - i0 : 64) - 1;   // last lane of the step
             p1 = __builtin_amdgcn_readlane(sym, tail);
@@ -586,7 +586,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
         }
         if (n != len && lane == 0) {
             K[pos0 + n] = ((M_QUAL + ctx_c) << AUX_SYM_BITS) | 94u;
-            V[pos0 + n] = pos0 + n;
+            if (aux_val) V[pos0 + n] = pos0 + n;
         }
     }
 }
@@ -791,7 +791,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
         k[r] = kin[wbase + (size_t)r * 64 + lane];
-        v[r] = vin[wbase + (size_t)r * 64 + lane];
+        // vin = nullptr: the values are the index in the segment (the AUX
+        // space's first pass: the emitters leave the values out)
+        v[r] = vin ? vin[wbase + (size_t)r * 64 + lane]
+                   : lt * SORT_TILE + w * (64 * SORT_ITEMS) + (uint32_t)r * 64 + lane;
     }
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 #pragma unroll

@@ -82,7 +82,7 @@ struct AuxEmit {
     SA_HD void operator()(uint32_t model, uint32_t s)
     {
         key[pos] = (model << AUX_SYM_BITS) | s;
-        val[pos] = pos;
+        if (val) val[pos] = pos;   // (the device leaves the AUX values out: they are the index)
         pos++;
     }
 };
@@ -137,7 +137,7 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
             ctx = ((ctx << 2) + cd) & mask;
         }
     }
-    AuxEmit em{aux_key + blk.aux_sym_base, aux_val + blk.aux_sym_base, 0};
+    AuxEmit em{aux_key + blk.aux_sym_base, aux_val ? aux_val + blk.aux_sym_base : nullptr, 0};
     // lengths (encode_len_short@0x4239a0; last_len stays 0)
     em.pos = blk.sbase[ST_LEN] + off[C_LEN];
     if (len == 0) {
