@@ -78,7 +78,8 @@ def parse_args(argv=None):
     ap.add_argument("--gen-workers", type=int, default=0, help="generator processes (0: the CPU share)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--e2e-batches", type=int, default=-1,
-                    help="batches written as FASTQ files for the end-to-end seqarc_amd -c run (-1: all, 0: skip)")
+                    help="batches written as FASTQ files for the end-to-end seqarc_amd -c run (-1: all at one "
+                         "rank, none with more; 0: skip)")
     ap.add_argument("--e2e-repeat", type=int, default=0,
                     help="the end-to-end files hold the e2e batches this many times over (a longer stream, so "
                          "pipeline fill and drain weigh less; 0: 3 at one rank, 1 with more ranks)")
@@ -89,8 +90,8 @@ def parse_args(argv=None):
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
                          "(scripts/pmc_traffic.py), committed under profiles/")
     a = ap.parse_args(argv)
-    if a.e2e_batches < 0:
-        a.e2e_batches = a.batches
+    if a.e2e_batches < 0:   # (one rank only by default: N ranks would each write their own files to /dev/shm)
+        a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 0
     if a.dry_run:
         a.pairs = min(a.pairs, 3000)
         a.block_size = min(a.block_size, 300_000)

@@ -11,6 +11,7 @@
 #include <memory>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -78,7 +79,12 @@ enum { PH_PREP, PH_EMIT, PH_SORT_SEQ, PH_SORT_AUX, PH_REPLAY_SEQ, PH_REPLAY_AUX,
 // recorded after the previous front's last kernel.
 struct FrontShare {
     int refs = 0;
+    // the front is taken in arrival order (a ticket lock): std::mutex lets a
+    // returning thread barge in, and in the command line's pipeline some
+    // contexts waited 2+ s for their turn while others went again (r3b trace)
     std::mutex mu;
+    std::condition_variable turn_cv;
+    uint64_t next_ticket = 0, serving = 0;
     hipEvent_t ev_free = nullptr;
     bool have_ev = false;
     DBuf d_counts, d_name_p, d_name_s, d_maxlen, d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
@@ -97,6 +103,30 @@ struct FrontShare {
     }
 };
 std::mutex g_share_mu;   // FrontShare::refs
+
+// RAII turn on a FrontShare's front (FIFO)
+struct FrontTurn {
+    FrontShare* F = nullptr;
+    bool held = false;
+    explicit FrontTurn(FrontShare* f) : F(f)
+    {
+        std::unique_lock<std::mutex> lk(F->mu);
+        const uint64_t t = F->next_ticket++;
+        F->turn_cv.wait(lk, [&] { return F->serving == t; });
+        held = true;
+    }
+    void unlock()
+    {
+        if (!held) return;
+        {
+            std::lock_guard<std::mutex> g(F->mu);
+            F->serving++;
+        }
+        F->turn_cv.notify_all();
+        held = false;
+    }
+    ~FrontTurn() { unlock(); }
+};
 
 // A batch of parsed blocks resident in HBM (names, bases, qualities and the
 // per-read offsets), read-only while it is encoded: any number of contexts of
@@ -935,7 +965,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     const uint32_t nr = I->nreads;
     FrontShare* F = c->fs;
     // the front (up to the short model runs) holds the device's front scratch
-    std::unique_lock<std::mutex> front_lock(F->mu);
+    FrontTurn front_lock(F);
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));

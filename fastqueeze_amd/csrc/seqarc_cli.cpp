@@ -1052,5 +1052,13 @@ int main(int argc, char** argv)
         o.out = p;
     }
     if (!o.f1 || !o.out) return usage();
+    // one hardware queue per stream (four per context): with the runtime's
+    // default of four queues, the contexts' streams share queues and a front
+    // waits behind another context's range coder (set before the device is used)
+    {
+        char q[16];
+        snprintf(q, sizeof q, "%d", std::min(32, 4 * o.contexts * o.devices + 4));
+        setenv("GPU_MAX_HW_QUEUES", q, 0);
+    }
     return compress(o);
 }
