@@ -67,6 +67,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-share", action="store_true", help="contexts with their own front scratch (A/B)")
     ap.add_argument("--pairs", type=int, default=5_000_000, help="mate pairs per batch (reads with --se)")
     ap.add_argument("--se", action="store_true", help="single-end reads (configs[1] shape) instead of PE")
+    ap.add_argument("--ont", action="store_true",
+                    help="configs[4] shape: SE long reads of 10, 20, 30, 40 and 50 kbp (--pairs = reads per batch, "
+                         "default 60000: ~3.6 GB of FASTQ); use with --lossy 1.15")
+    ap.add_argument("--lossy", type=float, default=0.0, help="-l R: R-Block lossy qualities (rblock@0x426c10)")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--x-span", type=int, default=8,
                     help="header x coordinates drawn from this many values (8: ~60 kB name stream per block, "
@@ -90,6 +94,10 @@ def parse_args(argv=None):
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
                          "(scripts/pmc_traffic.py), committed under profiles/")
     a = ap.parse_args(argv)
+    if a.ont:
+        a.se = True
+        if a.pairs == 5_000_000:
+            a.pairs = 60_000
     if a.e2e_batches < 0:   # (one rank only by default: N ranks would each write their own files to /dev/shm)
         a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 0
     if a.dry_run:
@@ -143,8 +151,14 @@ def make_batch(gid: int, args, workers: int, files=None):
     import synth
     import fastqueeze_amd as fq
     paired = not args.se
-    t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers,
-                            x_span=args.x_span)
+    if args.ont:   # five read lengths, a fifth of the reads each, chunks small enough for the generator's arrays
+        parts = [synth.generate(args.pairs // 5, read_len=L, seed=1000 + 10 * gid + k, workers=workers,
+                                chunk=1000, x_span=args.x_span)[0]
+                 for k, L in enumerate((10_000, 20_000, 30_000, 40_000, 50_000))]
+        t1, t2 = b"".join(parts), None
+    else:
+        t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers,
+                                x_span=args.x_span)
     if files:
         for path, t in zip(files, (t1, t2)):
             if t is not None:
@@ -322,14 +336,14 @@ def main():
         log(f"[rank {rank}] batch {g}: {len(batches[-1])} blocks, "
             f"{sum(b.text_bytes for b in batches[-1]) / 1e9:.2f} GB ({time.time() - t0:.1f}s)")
     tmpl = fq.analyze_ids(batches[0][0], args.se)
-    cfg = fq.Config(slevel=args.slevel, qlevel=args.qlevel, bin_mode=int(tmpl[0]))
+    cfg = fq.Config(slevel=args.slevel, qlevel=args.qlevel, bin_mode=int(tmpl[0]), lossy=args.lossy)
     batch_bytes = [sum(b.text_bytes for b in bl) for bl in batches]
 
     if args.dry_run:
         import oracle_py
         local_out = []
         for g, bl in zip(gids, batches):
-            outs = [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode) for b in bl]
+            outs = [oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode, cfg.lossy) for b in bl]
             local_out.append((g, b"".join(hashlib.sha256(o).digest() for o in outs)))
         allb = gather_blocks(local_out, world * args.batches) if world > 1 else [o for _, o in local_out]
         if rank == 0:
@@ -378,9 +392,9 @@ def main():
         import oracle_py
         for i in sorted({0, len(vb) - 1}):
             b = vb[i]
-            if outs[i] != oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode):
+            if outs[i] != oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode, cfg.lossy):
                 raise SystemExit(f"bench output of block {i} differs from the CPU restatement")
-            if not cfg.bin_mode:
+            if not cfg.bin_mode and not cfg.lossy:   # (lossy: the qualities do not come back)
                 nm, nl, sq, sl, ql, ok = oracle_py.decode_block(outs[i], b.nreads, b.names.size, b.seq.size,
                                                                cfg.slevel, cfg.qlevel, cfg.md5)
                 if not (ok and np.array_equal(sq, b.seq) and np.array_equal(ql, b.qual)
@@ -414,7 +428,7 @@ def main():
         import oracle_py
         from concurrent.futures import ThreadPoolExecutor
         blocks = keep["cpu"]
-        enc1 = lambda b: oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode)  # noqa: E731
+        enc1 = lambda b: oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode, cfg.lossy)  # noqa: E731
         t0 = time.perf_counter()
         nb = nbytes = 0
         for b in blocks:
@@ -459,10 +473,12 @@ def main():
         "dtype": "u8",
         "data": "synthetic (SURVEY.md 8(d) generator, tests/synth.py, seed 1000 + global batch id), "
                 "inputs resident in HBM",
-        "config": {"workload": f"synthetic {args.pairs/1e6:g}M x {args.read_len} bp "
-                               f"{'SE reads' if args.se else 'PE mate pairs (interleaved r1,r2)'} per batch, "
-                               f"{args.batches} distinct batches per GPU, no-ref, Slevel {args.slevel} "
-                               f"(order-{args.slevel + 7}), Qlevel {args.qlevel}, 50 MiB blocks, MD5 on",
+        "config": {"workload": (f"synthetic {args.pairs} SE long reads of 10/20/30/40/50 kbp" if args.ont else
+                                f"synthetic {args.pairs/1e6:g}M x {args.read_len} bp "
+                                f"{'SE reads' if args.se else 'PE mate pairs (interleaved r1,r2)'}")
+                               + f" per batch, {args.batches} distinct batches per GPU, no-ref, Slevel {args.slevel} "
+                               f"(order-{args.slevel + 7}), Qlevel {args.qlevel}, 50 MiB blocks, MD5 on"
+                               + (f", -l {args.lossy} (R-Block lossy qualities)" if args.lossy else ""),
                    "blocks_per_batch": len(keep["verify"]), "fastq_bytes_per_batch": in0,
                    "contexts_per_gpu": args.contexts, "batches_per_gpu": args.batches,
                    "parallelism": f"block-shard x{world} (batches dealt by shard_indices)"},
