@@ -183,7 +183,8 @@ struct sa_ctx {
     // in flight then); D2H copies land in it and reach their destination at the
     // next sync_d2h
     uint8_t* mail = nullptr;
-    size_t mail_cap = 0, mail_used = 0, mail_high = 0;
+    size_t mail_cap = 0, mail_used = 0, mail_high = 16u << 20;   // (16 MiB from the first run on)
+    std::vector<uint8_t*> mail_retired;   // outgrown mailboxes, freed in the destructor
     struct Pending {
         void* dst;
         const void* src;
@@ -251,6 +252,7 @@ struct sa_ctx {
         for (hipEvent_t e : {ev_fork, ev_fork_seq, ev_md5_done, ev_r[0], ev_r[1], ev_seq_done, ev_long_done})
             if (e) (void)hipEventDestroy(e);
         if (mail) (void)hipHostFree(mail);
+        for (uint8_t* m : mail_retired) (void)hipHostFree(m);
         if (st) (void)hipStreamDestroy(st);
         if (st2) (void)hipStreamDestroy(st2);
         if (st3) (void)hipStreamDestroy(st3);
@@ -278,7 +280,9 @@ int mail_reset(sa_ctx* c)
     c->mail_used = 0;
     const size_t want = std::max<size_t>(c->mail_high + c->mail_high / 8, 1u << 20);
     if (want > c->mail_cap) {
-        if (c->mail) (void)hipHostFree(c->mail);
+        // the old one is retired, not freed: hipHostFree waits for the whole
+        // device, i.e. for every other context's work in flight
+        if (c->mail) c->mail_retired.push_back(c->mail);
         c->mail = nullptr;
         c->mail_cap = 0;
         if (hipHostMalloc(reinterpret_cast<void**>(&c->mail), want, hipHostMallocDefault) != hipSuccess) {

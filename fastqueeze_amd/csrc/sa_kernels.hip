@@ -345,21 +345,71 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
         firstbad = row_min<PREP_ROW>(firstbad);
         maxq = row_max<PREP_ROW>(maxq);
         hasn = row_max<PREP_ROW>(hasn);
-        if (live && rl == 0) {
-            SeqStat st{valid, len - valid, maxq & 0xffu, 0u, 0u, nonascii ? (uint32_t)E_NONASCII : 0u};
-            if (hasn) {   // seq_stat's second loop
-                uint32_t gap = 0;
-                for (uint32_t i = 0; i < len; i++) {
-                    if ((int)st.maxq < (int)(int8_t)q[i]) continue;
-                    if (base_code(s[i]) > 3) {
+        // seq_stat's second loop, row-parallel (long reads carry N / IUPAC bases
+        // in nearly every read): over the positions with quality <= maxq, an
+        // ACGT base adds 1 + bits(gap) symbols, gap = the eligible non-ACGT
+        // bases since the previous eligible ACGT base.  Each lane summarises its
+        // 16 bytes as (g, h) = (eligible non-ACGT after its last eligible ACGT,
+        // has one); a row scan gives each lane the gap entering it.
+        uint32_t exc = 0, nsym = 0;
+        if (__ballot(hasn != 0)) {   // (rows without such a base take no bytes: cnt = 0)
+            uint32_t cg = 0;         // the row's carry from the previous step: gap after its last eligible ACGT
+            const int mq = (int)(maxq & 0xffu);
+            for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * PREP_ROW) {
+                const uint32_t pos = i0 + 16 * rl;
+                uint32_t sw[4] = {0, 0, 0, 0}, qw[4] = {0, 0, 0, 0}, cnt = 0;
+                if (hasn && pos < len) {
+                    cnt = len - pos < 16 ? len - pos : 16;
+                    load16(s + pos, sw);
+                    load16(q + pos, qw);
+                }
+                // the lane's summary
+                uint32_t g = 0, h = 0;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    const int qi = (int)(int8_t)(qw[j >> 2] >> (8 * (j & 3)));
+                    if (qi > mq) continue;
+                    if (base_code((uint8_t)(sw[j >> 2] >> (8 * (j & 3)))) > 3) {
+                        g++;
+                    } else {
+                        g = 0;
+                        h = 1;
+                    }
+                }
+                // inclusive row scan of (g, h): (A then B) = (hB ? gB : gA + gB, hA | hB)
+                uint32_t ig = g, ih = h;
+#pragma unroll
+                for (int d = 1; d < (int)PREP_ROW; d <<= 1) {
+                    const uint32_t pg = __shfl_up(ig, d, PREP_ROW), ph = __shfl_up(ih, d, PREP_ROW);
+                    if ((int)rl >= d) {
+                        ig = ih ? ig : pg + ig;
+                        ih |= ph;
+                    }
+                }
+                uint32_t eg = __shfl_up(ig, 1, PREP_ROW), eh = __shfl_up(ih, 1, PREP_ROW);
+                if (rl == 0) eg = eh = 0;
+                // the gap entering this lane: the carry, then the lanes before it
+                uint32_t gap = eh ? eg : cg + eg;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    const int qi = (int)(int8_t)(qw[j >> 2] >> (8 * (j & 3)));
+                    if (qi > mq) continue;
+                    if (base_code((uint8_t)(sw[j >> 2] >> (8 * (j & 3)))) > 3) {
                         gap++;
                     } else {
-                        st.exc++;
-                        st.npos_syms += 1 + (uint32_t)nbits_u32(gap);
+                        exc++;
+                        nsym += 1 + (uint32_t)nbits_u32(gap);
                         gap = 0;
                     }
                 }
+                // the row's total (lane 15's inclusive value) continues the carry
+                const uint32_t tg = __shfl(ig, PREP_ROW - 1, PREP_ROW), th = __shfl(ih, PREP_ROW - 1, PREP_ROW);
+                cg = th ? tg : cg + tg;
             }
+            exc = row_sum<PREP_ROW>(exc);
+            nsym = row_sum<PREP_ROW>(nsym);
+        }
+        if (live && rl == 0) {
+            SeqStat st{valid, len - valid, maxq & 0xffu, hasn ? exc : 0u, hasn ? nsym : 0u,
+                       nonascii ? (uint32_t)E_NONASCII : 0u};
             const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, lastnz, st, firstbad < lastnz);
             if (e) atomicOr(err, e);
         }
