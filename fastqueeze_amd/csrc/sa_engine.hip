@@ -89,11 +89,12 @@ struct FrontShare {
     bool have_ev = false;
     DBuf d_counts, d_name_p, d_name_s, d_maxlen, d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux, d_seq_longs, d_nseq_long, d_short_at;
+    DBuf d_dege_maxq;   // per read: maxq of the N / IUPAC side streams (k_prep_sq16 -> k_emit, k_emit_sq)
     std::vector<DBuf*> buffers()
     {
         return {&d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1],
                 &d_auxs_k, &d_auxs_v, &d_hist_seq, &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux,
-                &d_seq_longs, &d_nseq_long, &d_short_at};
+                &d_seq_longs, &d_nseq_long, &d_short_at, &d_dege_maxq};
     }
     uint64_t held_bytes()
     {
@@ -974,6 +975,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
     SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
+    SA_CHECK(c, F->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
+    uint8_t* dege_maxq = c->prep_wave ? nullptr : F->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
     SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
     SA_CHECK(c, F->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
     SA_CHECK(c, F->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
@@ -1041,7 +1044,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
                                F->d_counts.as<uint32_t>(), d_err);
         else
             hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                               F->d_counts.as<uint32_t>(), d_err);
+                               F->d_counts.as<uint32_t>(), d_err, F->d_dege_maxq.as<uint8_t>());
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, F->d_counts.as<uint32_t>(),
                        c->d_totals.as<uint32_t>(), F->d_maxlen.as<uint16_t>());
@@ -1161,10 +1164,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
                            c->d_totals.as<uint32_t>(), F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(),
                            F->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                           akb[0]->as<uint32_t>(), nullptr, d_err);   // (AUX values: the index, run_sort)
+                           akb[0]->as<uint32_t>(), nullptr, d_err, dege_maxq);   // (AUX values: the index, run_sort)
         hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                            F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                           akb[0]->as<uint32_t>(), nullptr);
+                           akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);

@@ -279,7 +279,7 @@ __device__ __forceinline__ uint32_t row_min(uint32_t v)
 constexpr uint32_t PREP_ROW = 16;
 
 __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t* __restrict__ counts,
-                                                   uint32_t* __restrict__ err)
+                                                   uint32_t* __restrict__ err, uint8_t* __restrict__ dege_maxq)
 {
     const uint32_t rl = threadIdx.x & (PREP_ROW - 1);
     const uint32_t rows = gridDim.x * (blockDim.x / PREP_ROW);
@@ -412,6 +412,7 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
                        nonascii ? (uint32_t)E_NONASCII : 0u};
             const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, lastnz, st, firstbad < lastnz);
             if (e) atomicOr(err, e);
+            dege_maxq[r] = (uint8_t)st.maxq;   // (k_emit / k_emit_sq: the side streams)
         }
     }
 }
@@ -522,11 +523,12 @@ __global__ void k_emit(const BatchView bv, const uint32_t* __restrict__ counts, 
                        const uint16_t* __restrict__ name_maxlen,
                        uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
                        uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
-                       uint32_t* __restrict__ err)
+                       uint32_t* __restrict__ err, const uint8_t* __restrict__ dege_maxq)
 {
     uint32_t e = 0;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < bv.nreads_total; r += gridDim.x * blockDim.x)
-        e |= emit_read(bv, r, counts, totals, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key, aux_val, false);
+        e |= emit_read(bv, r, counts, totals, name_p, name_s, name_maxlen, seq_key, seq_val, aux_key, aux_val, false,
+                       dege_maxq);
     if (e) atomicOr(err, e);
 }
 
@@ -548,7 +550,8 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
                                              uint32_t (&comp)[64], uint8_t (&stg)[2][EMIT_STAGE],
                                              const uint32_t* __restrict__ counts, uint32_t* __restrict__ seq_key,
                                              uint32_t* __restrict__ seq_val, uint32_t* __restrict__ aux_key,
-                                             uint32_t* __restrict__ aux_val)
+                                             uint32_t* __restrict__ aux_val, const uint32_t* __restrict__ totals,
+                                             const uint8_t* __restrict__ dege_maxq)
 {
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
@@ -639,19 +642,71 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
             if (aux_val) V[pos0 + n] = pos0 + n;
         }
     }
+    // N / IUPAC side streams (DegeInfoProcess@0x433a10), 64 positions per step,
+    // when k_prep_sq16 left the read's maxq (long reads carry such bases in
+    // nearly every read; k_emit's serial loops took four passes per read):
+    // the CH codes in order, and per eligible ACGT base (quality <= maxq, the
+    // original qualities) the kModel symbols of the gap before it -- a wave
+    // scan of (gap, has-ACGT) gives each lane its gap, an exclusive scan of the
+    // symbol counts its slots.
+    if (dege_maxq && read_col_count(bv, counts, totals, r, C_CH)) {
+        const int mq = (int)dege_maxq[r];
+        const uint8_t* qo = bv.qual + blk.seq_base + bv.seq_off[r];
+        uint32_t* K = aux_key + blk.aux_sym_base;
+        uint32_t pch = blk.sbase[ST_CH] + off[C_CH];
+        uint32_t pnp = blk.sbase[ST_NPOS] + off[C_NPOS];
+        uint32_t gcarry = 0;   // eligible non-ACGT bases since the last eligible ACGT base
+        const uint64_t below = (1ull << lane) - 1ull;
+        for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool in = i < len;
+            const uint32_t cd = in ? base_code(S(i)) : 0u;
+            const bool isn = in && cd > 3;
+            const uint64_t nm = __ballot(isn);
+            if (isn) K[pch + (uint32_t)__popcll(nm & below)] = (M_CH << AUX_SYM_BITS) | (cd - 4);
+            pch += (uint32_t)__popcll(nm);
+            const bool elig = in && (int)(int8_t)(i < EMIT_STAGE && !bv.lossy ? stg[1][i] : qo[i]) <= mq;
+            uint32_t g = elig && isn ? 1u : 0u, h = elig && !isn ? 1u : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {   // inclusive scan: (A then B) = (hB ? gB : gA + gB, hA | hB)
+                const uint32_t pg = (uint32_t)__shfl_up((int)g, d, 64), ph = (uint32_t)__shfl_up((int)h, d, 64);
+                if (lane >= (uint32_t)d) {
+                    g = h ? g : pg + g;
+                    h |= ph;
+                }
+            }
+            uint32_t eg = (uint32_t)__shfl_up((int)g, 1, 64), eh = (uint32_t)__shfl_up((int)h, 1, 64);
+            if (lane == 0) eg = eh = 0;
+            const uint32_t gap = eh ? eg : gcarry + eg;
+            const bool emit = elig && !isn;
+            const uint32_t nb = emit ? (uint32_t)nbits_u32(gap) : 0u;
+            const uint32_t cnt = emit ? 1 + nb : 0u;
+            const uint32_t incl = wave_incl_scan_dpp(cnt);
+            if (emit) {
+                uint32_t at = pnp + incl - cnt;
+                K[at++] = (M_KBITS << AUX_SYM_BITS) | nb;
+                for (uint32_t k = 0; k < nb; k++) K[at++] = ((M_KBIT0 + k) << AUX_SYM_BITS) | ((gap >> k) & 1u);
+            }
+            pnp += (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+            const uint32_t tg = (uint32_t)__builtin_amdgcn_readlane(g, 63), th = (uint32_t)__builtin_amdgcn_readlane(h, 63);
+            gcarry = th ? tg : gcarry + tg;
+        }
+    }
 }
 
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv, const uint32_t* __restrict__ counts,
                                                               uint32_t* __restrict__ seq_key,
                                                               uint32_t* __restrict__ seq_val,
                                                               uint32_t* __restrict__ aux_key,
-                                                              uint32_t* __restrict__ aux_val)
+                                                              uint32_t* __restrict__ aux_val,
+                                                              const uint32_t* __restrict__ totals,
+                                                              const uint8_t* __restrict__ dege_maxq)
 {
     __shared__ uint32_t comp[EMIT_WAVES][64];
     __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
-        emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val);
+        emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals, dege_maxq);
 }
 
 // SORT_PAD into the key slots no symbol is written to: each segment's tail up to

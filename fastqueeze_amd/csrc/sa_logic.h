@@ -110,7 +110,8 @@ SA_HD uint32_t read_col_count(const BatchView& bv, const uint32_t* counts, const
 // (k_emit_sq writes those one wave per read).
 SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts, const uint32_t* totals,
                          const int16_t* name_p, const int16_t* name_s, const uint16_t* name_maxlen,
-                         uint32_t* seq_key, uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val, bool bulk)
+                         uint32_t* seq_key, uint32_t* seq_val, uint32_t* aux_key, uint32_t* aux_val, bool bulk,
+                         const uint8_t* dege_maxq = nullptr)
 {
     uint32_t e = 0;
     const uint32_t b = bv.read_block[r];
@@ -198,7 +199,12 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
         em.pos = blk.sbase[ST_TIP] + off[C_TIP];
         const uint32_t nch = read_col_count(bv, counts, totals, r, C_CH);   // from k_prep
         em(M_TIP, nch ? 1u : 0u);
-        if (nch) {
+        if (nch && dege_maxq) {   // device: k_prep_sq16 kept maxq; the CH / NPOS streams are k_emit_sq's
+            em.pos = blk.sbase[ST_MAXQ] + off[C_MAXQ];
+            em(M_MAXQ, (uint8_t)(dege_maxq[r] - 33));
+            em.pos = blk.sbase[ST_NCNT] + off[C_NCNT];
+            emit_kmodel(em, read_col_count(bv, counts, totals, r, C_NPOSV));
+        } else if (nch) {
             const SeqStat st = seq_stat(s, q, len);
             em.pos = blk.sbase[ST_CH] + off[C_CH];
             for (uint32_t i = 0; i < len; i++) {
