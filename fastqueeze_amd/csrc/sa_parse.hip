@@ -262,11 +262,14 @@ int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
     sa_input* I = &c->own;
     hipStream_t st = c->st;
     if (mail_reset(c)) return -1;
-    I->nblocks = (uint32_t)n;
-    I->blocks.assign((size_t)n, DevBlock{});
+    // (the input is empty until the whole batch is staged: a failed staging
+    // leaves nothing for sa_run to encode)
+    I->nblocks = 0;
+    I->blocks.clear();
     I->nreads = 0;
     I->names_bytes = I->seq_bytes = I->text_bytes = 0;
     if (n == 0) return 0;
+    std::vector<DevBlock> dblocks((size_t)n, DevBlock{});
 
     // ---- text layout: every text starts on a tile ----
     std::vector<ParseText> texts;
@@ -420,7 +423,7 @@ int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
             c->err = "block too large (a reference block is 50 MiB of FASTQ)";
             return -1;
         }
-        DevBlock& d = I->blocks[(size_t)b];
+        DevBlock& d = dblocks[(size_t)b];
         d.nreads = p.nreads;
         d.read0 = p.read0;
         d.name_base = nb;
@@ -462,6 +465,8 @@ int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
     // (sa_run's kernels follow on this stream; the texts on the host are free
     // once this returns)
     SA_CHECK(c, hipStreamSynchronize(st));
+    I->blocks = std::move(dblocks);
+    I->nblocks = (uint32_t)n;
     return 0;
 }
 

@@ -119,18 +119,15 @@ struct Buf {
     void reserve(size_t c)
     {
         if (c <= cap) return;
-        T* nd;
-        if (pinned) {
-            nd = static_cast<T*>(sa_host_alloc(c * sizeof(T)));
-            if (!nd) throw std::bad_alloc();
-        } else {
-            nd = new T[c];
-        }
+        T* nd = pinned ? static_cast<T*>(sa_host_alloc(c * sizeof(T))) : nullptr;
+        const bool got_pinned = nd != nullptr;
+        if (!nd) nd = new T[c];   // (pageable when page-locked memory runs out: staging is then a slower copy)
         if (n) memcpy(nd, d, n * sizeof(T));
         free_(d);
         d = nd;
         cap = c;
         external = false;
+        pinned = got_pinned;
     }
     void resize(size_t c)
     {
