@@ -154,3 +154,26 @@ def test_streaming_cut_equals_whole_buffer_cut(pair, step):
     _, short = synth.generate(3000, paired=True, seed=62, read_len=90)   # mates of unequal length
     assert _stream_cut(a, short, bs, step) == [tuple(map(tuple, x)) for x in fq.cut_pe(a, short, bs)]
     assert _stream_cut(a, b, bs, step) == [tuple(map(tuple, x)) for x in fq.cut_pe(a, b, bs)]
+
+
+def test_host_only_reader_matches_the_cut(tmp_path):
+    """-c --host-only: the streaming reader (parallel pread slices once a window
+    is >= 16 MiB, counted PE cut, recycled windows) and the host parser, with no
+    device: the block count and bytes read equal the whole-buffer cut's, for
+    several block sizes, PE and SE."""
+    a, b = synth.generate(70_000, paired=True, seed=63)   # ~2 x 25 MB: full 25 MiB PE windows
+    pa, pb = tmp_path / "h_1.fq", tmp_path / "h_2.fq"
+    pa.write_bytes(a)
+    pb.write_bytes(b)
+    for mib in (1, 8, 50):
+        r = _run(["-c", "-f", "--host-only", "--block-size", str(mib), "-1", str(pa), "-2", str(pb), "-o",
+                  str(tmp_path / "h")], tmp_path)
+        assert r.returncode == 0, r.stderr
+        want = len(fq.cut_pe(a, b, mib << 20))
+        line = [ln for ln in r.stderr.decode().splitlines() if "block(s)" in ln][0]
+        assert line.split()[1] == str(want) and f" {len(a) + len(b)} -> " in line, (mib, line)
+        r = _run(["-c", "-f", "--host-only", "--block-size", str(mib), "-1", str(pa), "-o", str(tmp_path / "s")],
+                 tmp_path)
+        assert r.returncode == 0, r.stderr
+        line = [ln for ln in r.stderr.decode().splitlines() if "block(s)" in ln][0]
+        assert line.split()[1] == str(len(fq.cut_se(a, mib << 20))) and f" {len(a)} -> " in line, (mib, line)
