@@ -347,10 +347,12 @@ std::vector<int> sort_digits(int lo, int hi)
 {
     std::vector<int> w;
     if (hi <= lo) return w;
+    static const int min_db = std::getenv("SA_SORT_MIN_DB") ? std::max(7, std::min(9, std::atoi(std::getenv("SA_SORT_MIN_DB"))))
+                                                           : SORT_MIN_DB;
     const int bits = hi - lo, passes = (bits + SORT_MAX_DB - 1) / SORT_MAX_DB;
     for (int p = 0, done = 0; p < passes; p++) {
         const int d = (bits - done + (passes - p) - 1) / (passes - p);
-        w.push_back(std::max(d, SORT_MIN_DB));
+        w.push_back(std::max(d, min_db));
         done += d;
     }
     return w;
@@ -359,7 +361,7 @@ std::vector<int> sort_digits(int lo, int hi)
 // histogram words per tile of a sort over bits [lo, hi)
 uint64_t sort_hist_per_tile(int lo, int hi)
 {
-    int m = SORT_MIN_DB;
+    int m = 0;
     for (int d : sort_digits(lo, hi)) m = std::max(m, d);
     return 1ull << m;
 }
@@ -401,7 +403,8 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
         const uint32_t* vin = index_vals && shift == lo ? nullptr : vals[cur]->as<uint32_t>();
         uint32_t* kout = keys[cur ^ 1]->as<uint32_t>();
         uint32_t* vout = vals[cur ^ 1]->as<uint32_t>();
-        if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
+        if (db == 7) sort_pass<7>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
+        else if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
         else sort_pass<9>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
         shift += db;
         cur ^= 1;

@@ -743,13 +743,13 @@ __global__ __launch_bounds__(256) void k_pad_keys(const SortView sv, uint32_t* _
 constexpr uint32_t HIST_TILES = 2;
 // (10-bit digits measured slower than 8: a 4096-key tile scatters ~4 keys per
 // digit run, too short for coalesced writes)
-constexpr int SORT_MIN_DB = 8, SORT_MAX_DB = 9;
+constexpr int SORT_MIN_DB = 7, SORT_MAX_DB = 9;   // (SA_SORT_MIN_DB=8: round 1's floor, for A/B)
 
 template <int DB>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, const uint32_t* __restrict__ keys,
                                                             uint32_t shift)
 {
-    constexpr uint32_t ND = 1u << DB, PER = ND / SORT_THREADS;
+    constexpr uint32_t ND = 1u << DB;
     // HIST_TILES consecutive tiles per workgroup (amortises the per-workgroup
     // prologue; each tile's counts still go to its own row)
     __shared__ uint32_t h[HIST_TILES][ND];
@@ -758,8 +758,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, c
 #pragma unroll
     for (int j = 0; j < HIST_TILES; j++) {
         const uint32_t t = blockIdx.x * HIST_TILES + j;
-#pragma unroll
-        for (uint32_t p = 0; p < PER; p++) h[j][threadIdx.x + p * SORT_THREADS] = 0;
+        for (uint32_t i = threadIdx.x; i < ND; i += SORT_THREADS) h[j][i] = 0;   // (ND may be < the threads)
         sgp[j] = t < sv.ntiles ? &sv.segs[sv.tile_seg[t]] : nullptr;
     }
 #pragma unroll
@@ -782,9 +781,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, c
     for (int j = 0; j < HIST_TILES; j++)   // one coalesced row per tile
         if (sgp[j]) {
             const uint32_t t = blockIdx.x * HIST_TILES + j;
-#pragma unroll
-            for (uint32_t p = 0; p < PER; p++)
-                sv.hist[(size_t)t * ND + threadIdx.x + p * SORT_THREADS] = h[j][threadIdx.x + p * SORT_THREADS];
+            for (uint32_t i = threadIdx.x; i < ND; i += SORT_THREADS) sv.hist[(size_t)t * ND + i] = h[j][i];
         }
 }
 
@@ -881,7 +878,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
                                                                uint32_t* __restrict__ kout,
                                                                uint32_t* __restrict__ vout, uint32_t shift)
 {
-    constexpr uint32_t ND = 1u << DB, NW = SORT_THREADS / 64, C = ND / SORT_THREADS;
+    constexpr uint32_t ND = 1u << DB, NW = SORT_THREADS / 64, C = ND >= SORT_THREADS ? ND / SORT_THREADS : 1;
     __shared__ uint32_t wc[NW][ND];   // per wave and digit: count, then the wave's slot base in the tile
     __shared__ uint32_t gstart[ND], dsum[NW];
     __shared__ uint32_t sk[SORT_TILE], svl[SORT_TILE];
@@ -926,11 +923,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         for (uint32_t c = 0; c < C; c++) {
             const uint32_t d = threadIdx.x * C + c;
             uint32_t acc = 0;
+            if (d < ND) {   // (7-bit digits: half the threads own none)
 #pragma unroll
-            for (uint32_t ww = 0; ww < NW; ww++) {
-                const uint32_t tcount = wc[ww][d];
-                wc[ww][d] = acc;
-                acc += tcount;
+                for (uint32_t ww = 0; ww < NW; ww++) {
+                    const uint32_t tcount = wc[ww][d];
+                    wc[ww][d] = acc;
+                    acc += tcount;
+                }
             }
             cnt[c] = acc;
             s += acc;
@@ -940,9 +939,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 #pragma unroll
         for (uint32_t c = 0; c < C; c++) {
             const uint32_t d = threadIdx.x * C + c;
+            if (d < ND) {
 #pragma unroll
-            for (uint32_t ww = 0; ww < NW; ww++) wc[ww][d] += ex;
-            gstart[d] = sv.hist[(size_t)t * ND + d] - ex;
+                for (uint32_t ww = 0; ww < NW; ww++) wc[ww][d] += ex;
+                gstart[d] = sv.hist[(size_t)t * ND + d] - ex;
+            }
             ex += cnt[c];
         }
     }
