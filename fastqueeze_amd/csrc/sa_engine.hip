@@ -163,6 +163,7 @@ struct sa_ctx {
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
+    bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
     // k_md5<true> reads the next block's words while the chain runs: 148 VGPRs instead
@@ -968,6 +969,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     const int k = cfg->slevel + 7;
     const uint32_t ns = 1u << ((2 * k) & 31);
     const int seq_bits = (2 * k) & 31;   // NS = 1 << seq_bits (x86 shl masks the count)
+    // k <= 14: the SEQ key carries the base in its low two bits and the values
+    // are the stream position, i.e. the index (the emitter writes no values, the
+    // first sort pass computes them); k = 15 fills all 32 key bits (a key could
+    // equal the sort pad) and order 0 has no sort pass, so they keep values
+    // position << 2 | base (SA_SEQ_PACK=0: always)
+    const uint32_t seq_sh = (ns > 1 && seq_bits <= 28 && !c->seq_unpacked) ? 2u : 0u;
     const int aux_bits = cfg->qlevel > 2 ? 21 : 17;
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
@@ -1115,7 +1122,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     const uint64_t max_short = std::max<uint64_t>(std::min<uint64_t>(pa.total, (uint64_t)nbk << aux_bits), 1);
     SA_CHECK(c, F->d_short_at.ensure(max_short * 8));
     SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.tile_seg.size(), 1) * 4 *
-                                     sort_hist_per_tile(0, ns > 1 ? seq_bits : 0)));
+                                     sort_hist_per_tile((int)seq_sh, ns > 1 ? (int)seq_sh + seq_bits : 0)));
     SA_CHECK(c, F->d_hist_aux.ensure(std::max<uint64_t>(pa.tile_seg.size(), 1) * 4 *
                                      sort_hist_per_tile(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits)));
     SA_CHECK(c, F->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
@@ -1170,7 +1177,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
                            akb[0]->as<uint32_t>(), nullptr, d_err, dege_maxq);   // (AUX values: the index, run_sort)
         hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                            F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                           akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq);
+                           akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);
@@ -1188,8 +1195,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     //      records the long runs have not written yet (k_coder_r) ----
     SA_CHECK(c, hipMemsetAsync(c->d_prs_aux.p, 0, atot * sizeof(PRec), st));
     ev_begin(c, PH_SORT_SEQ, st);
-    if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, 0, ns > 1 ? seq_bits : 0,
-                 seq_sorted_buf))
+    if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, (int)seq_sh,
+                 ns > 1 ? (int)seq_sh + seq_bits : 0, seq_sorted_buf, seq_sh != 0))
         return -1;
     ev_finish(c, PH_SORT_SEQ, st);
     ev_begin(c, PH_REPLAY_SEQ, st);
@@ -1197,11 +1204,11 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         SA_CHECK(c, hipMemsetAsync(F->d_nseq_long.p, 0, 4, st));
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,
                            F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
-                           sink_seq, F->d_seq_longs.as<uint64_t>(), F->d_nseq_long.as<uint32_t>());
+                           sink_seq, F->d_seq_longs.as<uint64_t>(), F->d_nseq_long.as<uint32_t>(), seq_sh);
         hipLaunchKernelGGL(k_replay_seq_long, dim3((uint32_t)std::min<uint64_t>(max_seq_long, 2048)), dim3(128), 0,
                            st, svs, F->d_seq_k[seq_sorted_buf].as<uint32_t>(),
                            F->d_seq_v[seq_sorted_buf].as<uint32_t>(), sink_seq, F->d_seq_longs.as<uint64_t>(),
-                           F->d_nseq_long.as<uint32_t>(), d_err);
+                           F->d_nseq_long.as<uint32_t>(), d_err, seq_sh);
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_SEQ, st);

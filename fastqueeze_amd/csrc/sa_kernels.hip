@@ -551,7 +551,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
                                              const uint32_t* __restrict__ counts, uint32_t* __restrict__ seq_key,
                                              uint32_t* __restrict__ seq_val, uint32_t* __restrict__ aux_key,
                                              uint32_t* __restrict__ aux_val, const uint32_t* __restrict__ totals,
-                                             const uint8_t* __restrict__ dege_maxq)
+                                             const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh)
 {
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
@@ -589,9 +589,13 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
             x |= shfl_up0(x, 4) << 8;
             x |= shfl_up0(x, 8) << 16;
             const uint32_t ctx = ((lane < 16 ? carry << (2 * lane) : 0u) | x) & mask;
-            if (lane < nv) {
-                K[d + lane] = ctx;
-                V[d + lane] = ((d + lane) << 2) | c;
+            if (lane < nv) {   // seq_sh = 2: the base rides in the key, the value is the index (implicit)
+                if (seq_sh) {
+                    K[d + lane] = (ctx << 2) | c;
+                } else {
+                    K[d + lane] = ctx;
+                    V[d + lane] = ((d + lane) << 2) | c;
+                }
             }
             if (nv) carry = __builtin_amdgcn_readlane(((ctx << 2) + c) & mask, (int)nv - 1);
             d += nv;
@@ -700,13 +704,14 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
                                                               uint32_t* __restrict__ aux_key,
                                                               uint32_t* __restrict__ aux_val,
                                                               const uint32_t* __restrict__ totals,
-                                                              const uint8_t* __restrict__ dege_maxq)
+                                                              const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh)
 {
     __shared__ uint32_t comp[EMIT_WAVES][64];
     __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
-        emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals, dege_maxq);
+        emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals, dege_maxq,
+                     seq_sh);
 }
 
 // SORT_PAD into the key slots no symbol is written to: each segment's tail up to
@@ -999,10 +1004,12 @@ __device__ inline uint32_t sum16(uint64_t c)
            (uint32_t)(c >> 48);
 }
 
+// sh = 2: keys are context << 2 | base and values the stream position (k <= 14);
+// sh = 0: keys are the context and values position << 2 | base
 __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, const uint32_t* __restrict__ keys,
                                                              const uint32_t* __restrict__ vals, const SymSink rec,
                                                              uint64_t* __restrict__ long_runs,
-                                                             uint32_t* __restrict__ nlong)
+                                                             uint32_t* __restrict__ nlong, const uint32_t sh)
 {
     __shared__ SegCnt part[SORT_THREADS / 64];
     __shared__ uint64_t carry_cnt;
@@ -1031,13 +1038,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
     if (tid < 64) {
         uint64_t cc = 0;
         const uint32_t key0 = keys[tile0];
-        if (lt > 0 && before_tile == key0 && key0 != SORT_PAD) {
+        if (lt > 0 && (before_tile >> sh) == (key0 >> sh) && key0 != SORT_PAD) {
             for (uint32_t back = 0; back < SEQ_HALVE_J + 64; back += 64) {
                 const size_t at = tile0 - 1 - back - tid;
-                const bool ok = at >= sg.base && at < tile0 && keys[at] == key0;
+                const bool ok = at >= sg.base && at < tile0 && (keys[at] >> sh) == (key0 >> sh);
                 const uint64_t miss = ~__ballot(ok);
                 const uint64_t lead = miss ? ((1ull << __builtin_ctzll(miss)) - 1ull) : ~0ull;
-                if ((lead >> tid) & 1ull) cc += onehot16(vals[at] & 3u);
+                if ((lead >> tid) & 1ull) cc += onehot16((sh ? keys[at] : vals[at]) & 3u);
                 if (miss) break;
             }
 #pragma unroll
@@ -1052,11 +1059,11 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
     uint32_t pk = prev_key;
 #pragma unroll
     for (int e = 0; e < SORT_ITEMS; e++) {
-        if (k[e] != pk) {
+        if ((k[e] >> sh) != (pk >> sh)) {
             acc.cnt = 0;
             acc.head = 1;
         }
-        if (k[e] != SORT_PAD) acc.cnt += onehot16(v[e] & 3u);
+        if (k[e] != SORT_PAD) acc.cnt += onehot16((sh ? k[e] : v[e]) & 3u);
         pk = k[e];
     }
     // block-wide exclusive segmented scan of the aggregates: a wave scan
@@ -1082,10 +1089,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
     const SymSink out{rec.prs + sg.base, nullptr};   // packed SEQ records
 #pragma unroll
     for (int e = 0; e < SORT_ITEMS; e++) {
-        if (k[e] != pk) cnt = 0;
+        if ((k[e] >> sh) != (pk >> sh)) cnt = 0;
         pk = k[e];
         if (k[e] == SORT_PAD) continue;
-        const uint32_t b = v[e] & 3u, pos = v[e] >> 2;
+        const uint32_t b = (sh ? k[e] : v[e]) & 3u, pos = sh ? v[e] : v[e] >> 2;
         const uint32_t j = sum16(cnt);
         if (j < SEQ_HALVE_J) {
             const uint32_t c0 = 3u + (uint32_t)(cnt & 0xffff), c1 = 3u + (uint32_t)((cnt >> 16) & 0xffff);
@@ -1653,7 +1660,7 @@ __global__ __launch_bounds__(128) void k_replay_aux_long(const RunLists rl, cons
 // exceeds 253 (that symbol halves first, at the start of the next step).  Only
 // the in-run indices >= SEQ_HALVE_J are written (k_replay_seq wrote the rest).
 // ---------------------------------------------------------------------------
-__device__ void replay_seq_long_run(const LongRun& lr, const SymSink& rec, RunRing& rg, bool& bad)
+__device__ void replay_seq_long_run(const LongRun& lr, const SymSink& rec, RunRing& rg, bool& bad, uint32_t sh)
 {
     const uint32_t lane = threadIdx.x;
     uint32_t c0 = 3, c1 = 3, c2 = 3, c3 = 3;   // wave-uniform model state
@@ -1673,7 +1680,7 @@ __device__ void replay_seq_long_run(const LongRun& lr, const SymSink& rec, RunRi
         }
         const uint32_t slot = (rel + lane) % RING_LEN;
         const uint32_t key = rg.key[slot], val = rg.val[slot];
-        const uint64_t outm = ~__ballot(key == lr.model);
+        const uint64_t outm = ~__ballot((key >> sh) == lr.model);
         uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(outm ? (int)__builtin_ctzll(outm) : 64);
         if (c == 0) break;
         uint32_t T = c0 + c1 + c2 + c3;
@@ -1686,7 +1693,7 @@ __device__ void replay_seq_long_run(const LongRun& lr, const SymSink& rec, RunRi
         }
         if (c > 254u - T) c = 254u - T;
         const bool act = lane < c;
-        const uint32_t b = val & 3u;
+        const uint32_t b = (sh ? key : val) & 3u;
         const uint64_t m0 = __ballot(act && b == 0), m1 = __ballot(act && b == 1), m2 = __ballot(act && b == 2),
                        m3 = __ballot(act && b == 3);
         const uint32_t n0 = c0 + lanes_below(m0), n1 = c1 + lanes_below(m1), n2 = c2 + lanes_below(m2),
@@ -1694,7 +1701,7 @@ __device__ void replay_seq_long_run(const LongRun& lr, const SymSink& rec, RunRi
         if (act && rel + lane >= SEQ_HALVE_J) {
             const uint32_t cum = (b > 0 ? n0 : 0u) + (b > 1 ? n1 : 0u) + (b > 2 ? n2 : 0u);
             const uint32_t f = b == 0 ? n0 : b == 1 ? n1 : b == 2 ? n2 : n3;
-            sink_put(rec, val >> 2, cum, f, T + lane);
+            sink_put(rec, sh ? val : val >> 2, cum, f, T + lane);
         }
         c0 += (uint32_t)__popcll(m0);
         c1 += (uint32_t)__popcll(m1);
@@ -1713,7 +1720,7 @@ __global__ __launch_bounds__(128) void k_replay_seq_long(const SortView sv, cons
                                                          const uint32_t* __restrict__ vals, const SymSink rec_all,
                                                          const uint64_t* __restrict__ long_runs,
                                                          const uint32_t* __restrict__ nlong,
-                                                         uint32_t* __restrict__ err)
+                                                         uint32_t* __restrict__ err, const uint32_t sh)
 {
     __shared__ RunRing rg;
     const uint32_t n = *nlong;
@@ -1721,15 +1728,15 @@ __global__ __launch_bounds__(128) void k_replay_seq_long(const SortView sv, cons
     for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
         const size_t i = long_runs[r];
         const SortSeg& sg = sv.segs[sv.tile_seg[i / SORT_TILE]];
-        const LongRun lr{i, sg.base + sg.count, sg.base, keys[i], 0};
+        const LongRun lr{i, sg.base + sg.count, sg.base, keys[i] >> sh, 0};
         if (threadIdx.x == 0) {
             rg.filled = 0;
             rg.consumed = 0;
             rg.done = 0;
         }
         __syncthreads();
-        if (threadIdx.x >= 64) run_loader(lr, keys, vals, rg, 0);
-        else replay_seq_long_run(lr, SymSink{rec_all.prs + sg.base, nullptr}, rg, bad);
+        if (threadIdx.x >= 64) run_loader(lr, keys, vals, rg, sh);
+        else replay_seq_long_run(lr, SymSink{rec_all.prs + sg.base, nullptr}, rg, bad, sh);
         __syncthreads();
     }
     if (threadIdx.x < 64 && __ballot(bad) && threadIdx.x == 0) atomicOr(err, (uint32_t)E_CODER);
