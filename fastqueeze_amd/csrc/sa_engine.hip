@@ -213,7 +213,7 @@ struct sa_ctx {
     DBuf d_longs, d_huge_sorted, d_nlong;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
-    DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry;   // -l (rblock)
+    DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess;   // -l (rblock)
 
     // last run
     std::vector<uint64_t> final_base, final_len;
@@ -224,7 +224,7 @@ struct sa_ctx {
         return {&d_blocks, &d_totals, &d_err, &d_auxp_k, &d_auxp_v, &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux,
                 &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
                 &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_first_sq,
+                &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_first_sq,
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1]};
     }
     uint64_t held_bytes()
@@ -445,13 +445,17 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     SA_CHECK(c, c->d_rb_opens.ensure(4ull * RB_WORDS * nck));
     SA_CHECK(c, c->d_rb_spec.ensure(sizeof(RbRun) * nck));
     SA_CHECK(c, c->d_rb_entry.ensure(sizeof(RbRun) * nck));
+    SA_CHECK(c, c->d_rb_guess.ensure(sizeof(RbRun) * nck));
     SA_CHECK(c, h2d(c, c->d_rb_chunks.p, ck.data(), sizeof(RbChunk) * nck, st));
     SA_CHECK(c, h2d(c, c->d_rb_ck0.p, ck0.data(), 4ull * (nbk + 1), st));
     const RbChunk* dck = c->d_rb_chunks.as<RbChunk>();
     hipLaunchKernelGGL(k_rb_spec, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, dck, nck, ratio,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>());
+    hipLaunchKernelGGL(k_rb_guess, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, dck, nck, ratio,
+                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>());
     hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk,
-                       ratio, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_entry.as<RbRun>());
+                       ratio, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
+                       c->d_rb_entry.as<RbRun>());
     hipLaunchKernelGGL(k_rb_apply, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck, nck,
                        ratio, c->d_rb_entry.as<RbRun>());
     SA_CHECK(c, hipGetLastError());
