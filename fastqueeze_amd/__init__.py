@@ -67,6 +67,11 @@ class _SaTextInfo(C.Structure):
                 ("seq_bytes", C.c_uint64), ("out_bound", C.c_uint64)]
 
 
+class _SaAlignCfg(C.Structure):
+    _fields_ = [("index", C.c_void_p), ("paired", C.c_int32), ("maxmis", C.c_int32), ("good", C.c_int32),
+                ("insert_size", C.c_uint32)]
+
+
 class _SaOut(C.Structure):
     _fields_ = [("data", C.c_void_p), ("cap", C.c_uint64), ("size", C.c_uint64)]
 
@@ -105,6 +110,10 @@ def load_library(path: str | None = None):
         "sa_hash_file_bytes": ([P], U64), "sa_hash_serialize": ([P, P, P, U64], I32),
         "sa_hash_genome_length": ([P], C.c_uint32), "sa_hash_destroy": ([P], None),
         "sa_hash_align": ([P, P, P, P, P, I64, C.c_int32, C.c_int32, P, P, P, P, P, P], I32),
+        "sa_align_chain_create": ([C.c_int32, C.c_int32], P), "sa_align_chain_destroy": ([P], None),
+        "sa_run_input_aligned": ([P, P, P, P, P, U64], I32), "sa_run_aligned": ([P, P, P, P, U64], I32),
+        "sa_encode_blocks_aligned": ([P, P, I32, P, P, P, P], I32),
+        "sa_hash_load": ([P, P, U64], P), "sa_hash_packed": ([P, P, P, U64], I32),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -340,6 +349,35 @@ class Encoder:
             self._err("sa_run_input")
         self._staged = [int(self._lib.sa_output_bound(C.byref(b._c()))) for b in inp.blocks]
 
+    def run_aligned(self, cfg: Config, index: "HashIndex", paired: bool, chain: "AlignChain",
+                    batch: int | None = None, inp: "Input | None" = None, maxmis: int = 7, good: int = 1,
+                    insert_size: int = 0):
+        """The staged batch (or `inp`) through the reference path
+        (sa_run_input_aligned; doAlignEncode@0x42d4c0 per block); fetch() then."""
+        c = cfg._c()
+        a = _SaAlignCfg(index._h, 1 if paired else 0, maxmis, good, insert_size)
+        b = 0xFFFFFFFFFFFFFFFF if batch is None else int(batch)
+        if inp is None:
+            rc = self._lib.sa_run_aligned(self._ctx, C.byref(c), C.byref(a), chain._h, b)
+        else:
+            rc = self._lib.sa_run_input_aligned(self._ctx, inp._h, C.byref(c), C.byref(a), chain._h, b)
+            self._staged = [int(self._lib.sa_output_bound(C.byref(x._c()))) for x in inp.blocks]
+        if rc != 0:
+            self._err("sa_run_input_aligned")
+
+    def encode_aligned(self, blocks: list[Block], cfg: Config, index: "HashIndex", paired: bool,
+                       chain: "AlignChain | None" = None, **kw) -> list[bytes]:
+        """stage + run_aligned + fetch (a fresh chain unless one is given)."""
+        own = chain is None
+        chain = chain or AlignChain()
+        try:
+            self.stage(blocks)
+            self.run_aligned(cfg, index, paired, chain, **kw)
+            return self.fetch()
+        finally:
+            if own:
+                chain.close()
+
     def device_bytes(self) -> int:
         return int(self._lib.sa_device_bytes(self._ctx))
 
@@ -466,6 +504,28 @@ def decode_block(data: bytes, text_bytes: int, cfg: Config | None = None, templa
         bool(d.md5_ok)
 
 
+class AlignChain:
+    """The align_info state an encode thread carries from read to read and block
+    to block on the reference path (sa_align_chain): one per input, batches
+    pass through it in order.  nmis: the states before the first read (0 for
+    a fresh encode thread's AlignParam)."""
+
+    def __init__(self, nmis_mate1: int = 0, nmis_mate2: int = 0):
+        self._lib = load_library()
+        self._h = self._lib.sa_align_chain_create(nmis_mate1, nmis_mate2)
+
+    def close(self):
+        if self._h:
+            self._lib.sa_align_chain_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class HashIndex:
     """The HASH reference index of a FASTA (`SeqArc -i ref.fa`,
     buildRefIndex@0x410190), built and kept on an Encoder's device
@@ -474,8 +534,16 @@ class HashIndex:
 
     K, STEP, MAXCOUNT, MAXMIS, GOOD = 14, 2, 1 << 16, 7, 1   # SeqArcParam ctor @0x407490
 
-    def __init__(self, enc: "Encoder", fasta: bytes, k: int = K, step: int = STEP, maxcount: int = MAXCOUNT):
+    def __init__(self, enc: "Encoder", fasta: bytes | None, k: int = K, step: int = STEP, maxcount: int = MAXCOUNT,
+                 hash_file: bytes | None = None):
+        """From the FASTA (built on the device) or from its `.hash` file (hash_file)."""
         self._enc, self._lib = enc, enc._lib
+        if hash_file is not None:
+            f = np.frombuffer(hash_file, np.uint8)
+            self._h = self._lib.sa_hash_load(enc._ctx, _ptr(f), f.size)
+            if not self._h:
+                enc._err("sa_hash_load")
+            return
         self._h = self._lib.sa_hash_build(enc._ctx, fasta, len(fasta), k, step, maxcount)
         if not self._h:
             enc._err("sa_hash_build")

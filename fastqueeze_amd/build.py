@@ -13,7 +13,8 @@ LIB = os.path.join(LIB_DIR, "libseqarc_amd.so")
 BIN_DIR = os.path.join(HERE, "bin")
 CLI = os.path.join(BIN_DIR, "seqarc_amd")
 SOURCES = ["sa_engine.hip", "fastq_host.cpp", "arc_file.cpp", "arc_decode.cpp"]
-DEPS = SOURCES + ["seqarc_cli.cpp", "sa_kernels.hip", "sa_hash.hip", "sa_parse.hip", "sa_common.h", "sa_device.h", "sa_logic.h", "sa_plan.h"]
+DEPS = SOURCES + ["seqarc_cli.cpp", "sa_kernels.hip", "sa_hash.hip", "sa_parse.hip", "sa_common.h", "sa_device.h", "sa_logic.h", "sa_plan.h",
+                  "sa_align_host.h"]
 
 
 def _hipcc() -> str:

@@ -35,9 +35,31 @@ enum Stream : int {
     ST_NCNT = 6,   // encap 25  compressNDegeCnt@0x42d010
     ST_NPOS = 7,   // encap 26  compressNDegePos@0x42d170
     ST_SEQ = 8,    // encap 6   compressSeq@0x4248a0 (own symbol space)
-    NSTREAM = 9,
-    NAUX = 8
+    // reference (HASH index) path only, doAlignEncode@0x42d4c0:
+    ST_ORD = 9,    // encap 8   compressOrder@0x424b70
+    ST_PEREL = 10, // encap 9   compressPERelation@0x422be0 (PE)
+    ST_POS = 11,   // encap 0xb compressAlignInfo_Pos@0x425d70
+    ST_MIS = 12,   // encap 0xf compressAlignInfo_Mis@0x425ff0
+    ST_REV = 13,   // encap 0xa compressAlignInfo_Rev@0x426480
+    ST_CIGL = 14,  // encap 0xc compressAlignInfo_CigaL@0x426700
+    ST_CIGV = 15,  // encap 0xd compressAlignInfo_CigaV@0x426980
+    NSTREAM = 16,
+    NAUX = 8,      // AUX streams with a per-read count column (ST_LEN .. ST_NPOS)
+    NALN = 7       // alignment streams (ST_ORD .. ST_CIGV)
 };
+
+// ---- per-read count columns of the alignment streams (reference path) -------
+enum ACol : int {
+    A_ORD = 0,    // 1 per read with an order byte (block reads < order count)
+    A_PEREL = 1,  // 1 per PE pair with both mates aligned (on mate 1)
+    A_POS = 2,    // position bits
+    A_MIS = 3,    // 1 per aligned read
+    A_REV = 4,    // 1 per aligned read
+    A_CIGL = 5,   // mismatch-offset bits
+    A_CIGV = 6,   // mismatches
+    NACOL = 7
+};
+static_assert(ST_ORD + A_CIGV == ST_CIGV, "alignment column k is stream ST_ORD + k");
 
 // ---- per-read count columns (exclusive-scanned per block) -----------------
 enum Col : int {
@@ -67,6 +89,15 @@ constexpr uint32_t M_KBITS = 6;           // kModel SIMPLE_MODEL<64> @+0x15c0
 constexpr uint32_t M_KBIT0 = 7;           // 64 x SIMPLE_MODEL<2> (vector @+0x15a8)
 constexpr uint32_t M_LEN_B2 = 71;         // SIMPLE_MODEL<256> @+0x828 (compressLen_long@0x423710)
 constexpr uint32_t M_LEN_B3 = 72;         // SIMPLE_MODEL<256> @+0xc38
+// one model per alignment stream (each compressX keeps its model on the stack)
+constexpr uint32_t M_ORD = 73;            // SIMPLE_MODEL<5>  compressOrder@0x424b70
+constexpr uint32_t M_PEREL = 74;          // SIMPLE_MODEL<4>  compressPERelation@0x422be0
+constexpr uint32_t M_POS = 75;            // SIMPLE_MODEL<2>  compressAlignInfo_Pos@0x425d70
+constexpr uint32_t M_MIS8 = 76;           // SIMPLE_MODEL<8>  compressAlignInfo_Mis@0x425ff0 (maxmis 1..7)
+constexpr uint32_t M_REV = 77;            // SIMPLE_MODEL<2>  compressAlignInfo_Rev@0x426480
+constexpr uint32_t M_CIGL = 78;           // SIMPLE_MODEL<2>  compressAlignInfo_CigaL@0x426700
+constexpr uint32_t M_CIGV = 79;           // SIMPLE_MODEL<4>  compressAlignInfo_CigaV@0x426980
+constexpr uint32_t M_MIS9 = 80;           // SIMPLE_MODEL<9>  compressAlignInfo_Mis (maxmis 8)
 constexpr uint32_t M_NAME_PRE = 128;      // 256 x SIMPLE_MODEL<256> @+0x1068
 constexpr uint32_t M_NAME_SUF = 384;      // 256 x SIMPLE_MODEL<256> @+0x1070
 constexpr uint32_t M_NAME_LEN = 640;      // 256 x SIMPLE_MODEL<256> @+0x1078
@@ -79,7 +110,15 @@ SA_HD uint32_t model_nsym(uint32_t id)
     if (id >= M_NAME_MID) return 128;
     if (id >= M_NAME_PRE) return 256;
     if (id == M_LEN_B2 || id == M_LEN_B3) return 256;
-    if (id >= M_KBIT0) return 2;
+    switch (id) {
+    case M_ORD: return 5;
+    case M_PEREL: return 4;
+    case M_MIS8: return 8;
+    case M_CIGV: return 4;
+    case M_MIS9: return 9;
+    default: break;
+    }
+    if (id >= M_KBIT0) return 2;   // (also M_POS, M_REV, M_CIGL)
     switch (id) {
     case M_LEN_SAME: return 2;
     case M_LEN_LO: return 256;

@@ -23,13 +23,18 @@ struct DevBlock {
     uint64_t seq_bytes;
     uint64_t seq_sym_base;     // element offset of the block's SEQ symbol space (tile-aligned)
     uint64_t aux_sym_base;     // element offset of the block's AUX symbol space (tile-aligned)
-    uint32_t sbase[NAUX];      // start of each AUX stream inside the AUX space
-    uint32_t scount[NAUX];     // symbols of each AUX stream
+    uint32_t sbase[NSTREAM];   // start of each AUX stream inside the AUX space (ST_SEQ unused)
+    uint32_t scount[NSTREAM];  // symbols of each AUX stream
     uint32_t vcount[NSTREAM];  // value counts written in the dege encaps
     uint32_t n_seq;
     uint32_t n_aux;
     uint32_t len_long;         // a read > 0xffff bp: compressLen_long@0x423710 (SeqArcMemBuf+0x2)
-    uint32_t pad_;
+    // reference path (SeqArcMemBuf fields the block's doAlign leaves):
+    uint32_t order_count;      // +0x34: reads with an order byte (the rest after a bail-out)
+    uint32_t align_count;      // +0x30: aligned reads
+    uint32_t insert_bits;      // +0x28: PE insert-window bits (CaclInsertSize@0x413270)
+    uint32_t win;              // AlignEncodePEJob+0xa8: insert window
+    uint32_t ibits;            // AlignEncodePEJob+0xac: bits of a distance inside it
 };
 
 struct BatchView {
@@ -50,6 +55,27 @@ struct BatchView {
     int32_t bin_mode;
     int32_t md5;
     int32_t lossy;                // -l: QUAL codes qual_q, no quality MD5 (compressQual@0x426eca)
+    // reference (HASH index) path, doAlignEncode@0x42d4c0
+    int32_t aligned;              // blocks in the doAlignEncode layout
+    int32_t paired;               // PE (param+0x1b38 == 0): the PE relation streams
+    const uint8_t* seq_skip;      // per read: aligned, not in the SEQ stream (compressSeq@0x4249b3)
+};
+
+// Per-read alignment of the reference path (getHashAlignInfo@0x4113c0 after the
+// carried-state choice) and the constants of the position split
+// (HashAlignment::loadRefIndex@0x40fe9b: shift = bits(genome) - 2).
+struct AlignView {
+    const int32_t* ret;       // mismatches, -1 = not aligned
+    const uint8_t* rev;       // reverse-complement strand
+    const uint32_t* pos;      // 1-based reference position
+    const int32_t* mispos;    // per read `stride` slots, offsets along the aligned strand
+    const int32_t* mistype;   // per read `stride` slots (type @0x44a0c0; 3: N / IUPAC in the read)
+    uint32_t stride;          // maxmis + 1
+    uint32_t shift;           // param+0x1858
+    uint64_t mask;            // param+0x1860 = 2^shift - 1
+    uint64_t glen;            // param+0x1868: genome bases
+    int32_t paired;
+    uint32_t mis_model;       // M_MIS8 / M_MIS9, 0 = no Mis symbols (maxmis 0 or > 8)
 };
 
 // R-Block lossy pre-pass (rblock@0x426c10): a block's quality bytes are cut
@@ -151,7 +177,7 @@ struct AsmView {
     const uint64_t* task_out_base;
     uint32_t* copies;   // per block: count, then (dst offset, source task, length) x ASM_MAX_COPIES
 };
-constexpr uint32_t ASM_MAX_COPIES = 16;
+constexpr uint32_t ASM_MAX_COPIES = 20;
 constexpr uint32_t ASM_COPY_WORDS = 1 + 3 * ASM_MAX_COPIES;
 
 }  // namespace sa

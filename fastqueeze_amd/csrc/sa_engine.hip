@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/seqarc_amd.h"
+#include "sa_align_host.h"
 #include "sa_kernels.hip"
 #include "sa_plan.h"
 
@@ -108,8 +109,10 @@ std::mutex g_share_mu;   // FrontShare::refs
 // RAII turn on a FrontShare's front (FIFO)
 struct FrontTurn {
     FrontShare* F = nullptr;
+    hipStream_t st = nullptr;   // the stream the holder enqueues its front on
     bool held = false;
-    explicit FrontTurn(FrontShare* f) : F(f)
+    bool freed = false;         // F->ev_free recorded after this front's last kernel
+    FrontTurn(FrontShare* f, hipStream_t s) : F(f), st(s)
     {
         std::unique_lock<std::mutex> lk(F->mu);
         const uint64_t t = F->next_ticket++;
@@ -119,6 +122,12 @@ struct FrontTurn {
     void unlock()
     {
         if (!held) return;
+        // an early exit (error) after front kernels were queued: the next front
+        // must still wait for them before it reuses the shared scratch
+        if (!freed && hipEventRecord(F->ev_free, st) == hipSuccess) {
+            F->have_ev = true;
+            freed = true;
+        }
         {
             std::lock_guard<std::mutex> g(F->mu);
             F->serving++;
@@ -214,6 +223,15 @@ struct sa_ctx {
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
     DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess;   // -l (rblock)
+    // reference path: per read the alignment of both carried states, status, the
+    // alignment columns, the SEQ skip flags (sa_hash.hip, align_front)
+    DBuf d_al_ret[2], d_al_rev[2], d_al_pos[2], d_al_mp[2], d_al_mt[2], d_al_st, d_al_sel, d_al_scr, d_acounts, d_atot,
+        d_seq_skip;
+    // the last aligned batch's block plans (a re-run of the same batch -- the
+    // exact-payload fallback -- reuses them instead of passing the chain again)
+    const sa_input* al_input = nullptr;
+    uint64_t al_batch = 0;
+    std::vector<uint32_t> al_plan;   // per block: order count, win, ibits, insert bits
 
     // last run
     std::vector<uint64_t> final_base, final_len;
@@ -225,7 +243,10 @@ struct sa_ctx {
                 &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
                 &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
                 &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_first_sq,
-                &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1]};
+                &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
+                &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
+                &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
+                &d_seq_skip};
     }
     uint64_t held_bytes()
     {
@@ -780,7 +801,9 @@ uint64_t sa_output_bound(const sa_block* b)
     // (1 + bits(g) symbols per g + 1 bases), bases; each symbol narrows the
     // range by < 2^16 (<= 2 bytes); + per stream flush and header, the MD5s and
     // the ID-bin first ID
-    const uint64_t syms = 3 * nb + nn + 45ull * b->nreads;
+    // (+ 140 per read: the reference path's alignment symbols, <= 64 position
+    // bits, <= 63 x 17 mismatch bits and types at maxmis 7 ...)
+    const uint64_t syms = 3 * nb + nn + (45ull + 140ull) * b->nreads;
     return 2 * syms + 9 * 96 + 4096 + 0x10000;
 }
 
@@ -942,12 +965,29 @@ int sa_run(sa_ctx* c, const sa_cfg* cfg)
 
 }  // extern "C"
 
+// The reference (HASH index) path of a batch: doAlignEncode@0x42d4c0 instead of
+// doFqzEncode@0x42d2d0 (sa_run_input_aligned).
+struct AlignReq {
+    const sa_hash_index* ix;
+    sa_align_cfg cfg;
+    sa_align_chain* chain;
+    uint64_t batch;   // the batch's place in the chain (UINT64_MAX: the chain's next)
+};
+// sa_hash.hip: aligns the batch, follows the carried state through it (after
+// the chain's previous batch), plans its blocks (c->blocks: order count, insert
+// window), counts and scans the alignment columns (atot: per block NACOL sums)
+// and sets the BatchView / AlignView fields of the path
+int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq, std::vector<uint32_t>& atot,
+                AlignView& av);
+void align_chain_fail(sa_align_chain* ch);
+
 namespace {
 
 // One encode of a resident batch; exact: the payload arena sized from the
 // streams' real byte counts after L2 (else the 2-bytes-per-symbol bound).
+// al: the reference path (nullptr: no reference).
 // Returns 0, -1, or 2 when a stream outgrew its exact cap.
-int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
+int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const AlignReq* al = nullptr)
 {
     if (!c) return -1;
     if (!I || !cfg || I->device != c->device) {
@@ -983,21 +1023,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
     FrontShare* F = c->fs;
-    // the front (up to the short model runs) holds the device's front scratch
-    FrontTurn front_lock(F);
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
-    SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
-    SA_CHECK(c, F->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
-    uint8_t* dege_maxq = c->prep_wave ? nullptr : F->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
-    SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
-    SA_CHECK(c, F->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, F->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, F->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, c->d_err.ensure(16));
-    SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 16, st));
-
     BatchView bv{};
     bv.blocks = c->d_blocks.as<DevBlock>();
     bv.nblocks = nbk;
@@ -1016,6 +1044,27 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     bv.qlevel = cfg->qlevel;
     bv.bin_mode = cfg->bin_mode ? 1 : 0;
     bv.md5 = cfg->md5 ? 1 : 0;
+    // reference path: the reads are aligned (and the batch placed in the
+    // align_info chain) before the front is taken: the chain may wait for
+    // the batch before this one, which another context runs
+    std::vector<uint32_t> aln_tot;
+    AlignView alv{};
+    if (al && align_front(c, I, bv, *al, aln_tot, alv)) {
+        align_chain_fail(al->chain);
+        return -1;
+    }
+    // the front (up to the short model runs) holds the device's front scratch
+    FrontTurn front_lock(F, st);
+    SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
+    SA_CHECK(c, F->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
+    uint8_t* dege_maxq = c->prep_wave ? nullptr : F->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
+    SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
+    SA_CHECK(c, F->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, F->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, F->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_err.ensure(16));
+    SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 16, st));
+
     uint32_t* d_err = c->d_err.as<uint32_t>();
 
     ev_begin(c, PH_TOTAL, st);
@@ -1078,7 +1127,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
 
     // ---- layout of the symbol spaces, coder tasks, md5 tasks, outputs ----
     BatchPlan bp;
-    if (!plan_batch(c->blocks, tot, bp)) {
+    if (!plan_batch(c->blocks, tot, bp, al ? &aln_tot : nullptr, alv.mis_model)) {
         c->err = "block symbol space too large";
         return -1;
     }
@@ -1182,6 +1231,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
         hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                            F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                            akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh);
+        if (al)   // the alignment streams (AlignInfoProcess[PE], decomposeAlignInfo)
+            hipLaunchKernelGGL(k_align_emit, dim3(rgrid), dim3(256), 0, st, bv, alv, c->d_acounts.as<uint32_t>(),
+                               akb[0]->as<uint32_t>());
     }
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_EMIT, st);
@@ -1244,6 +1296,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     // the front scratch is free once the kernels enqueued so far on st are done
     SA_CHECK(c, hipEventRecord(F->ev_free, st));
     F->have_ev = true;
+    front_lock.freed = true;
     front_lock.unlock();
     hipStream_t st3 = c->st3, st4 = c->st4;
     SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
@@ -1270,8 +1323,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact)
     for (size_t t = 0; t < tasks.size(); t++) task_out_base[t] = tasks[t].out_base;
     c->final_base.assign(nbk, 0);
     for (uint32_t b = 0; b < nbk; b++) {
-        uint64_t blk = 64 + 2 + 0x10000;
-        for (int s = 0; s < NSTREAM; s++) blk += out_len[asmb[b].task[s]] + 32;
+        uint64_t blk = 64 + 2 + 0x10000 + 96;
+        for (int s = 0; s < NSTREAM; s++)
+            if (asmb[b].task[s] != NO_TASK) blk += out_len[asmb[b].task[s]] + 32;
         asmb[b].out_base = final_bytes;
         c->final_base[b] = final_bytes;
         final_bytes = align_up(final_bytes + blk, 16);

@@ -448,6 +448,89 @@ __global__ __launch_bounds__(256) void k_hash_align(const HashView ix, const Has
         }
 }
 
+// ---------------------------------------------------------------------------
+// The reference path of a resident batch (doAlignEncode@0x42d4c0's inputs,
+// sa_run_input_aligned): every read aligned where it lies in HBM, then the
+// alignment streams' per-read columns and keys (sa_logic.h).
+// ---------------------------------------------------------------------------
+// Scratch words of read r's packed strands: floor(offset / 8) + 2 r (the next
+// read's slot starts at least 2 ceil(len / 16) words later).
+__device__ __forceinline__ uint64_t align_scratch_word(const BatchView& bv, uint32_t r)
+{
+    return (bv.blocks[bv.read_block[r]].seq_base + bv.seq_off[r]) / 8 + 2ull * r;
+}
+
+// stale = 0: every read (sel == nullptr) with the carried state "not aligned";
+// status = AL_OK0 | AL_CONS (the search consulted the carried state) | AL_NSKIP
+// (SE: more N / IUPAC bases than maxmis: AlignEncodeSEJob::doAlign@0x411a0b
+// does not call the aligner).  stale = 1: the listed reads with "aligned"
+// (status |= AL_OK1).  Outputs at the read's index.
+__global__ __launch_bounds__(256) void k_hash_align_batch(const HashView ix, const HashArgs a, const BatchView bv,
+                                                          uint32_t* __restrict__ scratch, const uint32_t* __restrict__ sel,
+                                                          uint32_t n, int stale, int se, int32_t* __restrict__ ret,
+                                                          uint8_t* __restrict__ rev, uint32_t* __restrict__ pos,
+                                                          int32_t* __restrict__ mispos, int32_t* __restrict__ mistype,
+                                                          uint8_t* __restrict__ status)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t i = sel ? sel[t] : t;
+    const DevBlock& blk = bv.blocks[bv.read_block[i]];
+    const uint8_t* rd = bv.seq + blk.seq_base + bv.seq_off[i];
+    const int len = (int)bv.seq_len[i];
+    const int stride = a.maxmis + 1;
+    int* mp = mispos + (size_t)i * stride;
+    int* mt = mistype + (size_t)i * stride;
+    uint32_t* scr = scratch + align_scratch_word(bv, i);
+    HashRead fw{rd, len, false, scr};
+    HashRead rc{rd, len, true, scr + ((len - 1) >> 4) + 1};
+    HashAlign ai{stale ? 0 : -1, 0, 0, false, false};
+    int sidx[4] = {-1, -1, -1, -1};
+    int best = -1, r = -1, nn = 0;
+    uint32_t cnt = 0;
+    const int thr = a.good < a.maxmis ? a.good : a.maxmis;
+    if (len > 0 && (nn = hash_pack_read(fw)) <= a.maxmis) {
+        best = a.maxmis + 1;
+        aligner_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+        if (!(a.maxmis >= best) && cnt <= 299) {
+            hash_pack_read(rc);
+            aligner_d(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+            if (!(a.maxmis >= best) && cnt <= 299) {
+                aligner_parts_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+                if (!(a.maxmis >= best) && cnt <= 299) aligner_parts_d(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr);
+            }
+        }
+        if (best <= a.maxmis) r = best;
+    }
+    ret[i] = r;
+    rev[i] = r >= 0 ? ai.rev : 0;
+    pos[i] = r >= 0 ? (uint32_t)ai.pos : 0u;
+    if (!stale)
+        status[i] = (uint8_t)((r >= 0 ? AL_OK0 : 0) | (ai.consulted ? AL_CONS : 0) | (se && nn > a.maxmis ? AL_NSKIP : 0));
+    else if (r >= 0)
+        status[i] |= AL_OK1;
+}
+
+// the reads whose carried state was "aligned": variant 1 over variant 0
+__global__ __launch_bounds__(256) void k_align_select(const uint32_t* __restrict__ sel, uint32_t n, uint32_t stride,
+                                                      const int32_t* __restrict__ ret1, const uint8_t* __restrict__ rev1,
+                                                      const uint32_t* __restrict__ pos1, const int32_t* __restrict__ mp1,
+                                                      const int32_t* __restrict__ mt1, int32_t* __restrict__ ret,
+                                                      uint8_t* __restrict__ rev, uint32_t* __restrict__ pos,
+                                                      int32_t* __restrict__ mp, int32_t* __restrict__ mt)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t i = sel[t];
+    ret[i] = ret1[i];
+    rev[i] = rev1[i];
+    pos[i] = pos1[i];
+    for (uint32_t k = 0; k < stride; k++) {
+        mp[(size_t)i * stride + k] = mp1[(size_t)i * stride + k];
+        mt[(size_t)i * stride + k] = mt1[(size_t)i * stride + k];
+    }
+}
+
 }  // namespace sa
 
 // ---------------------------------------------------------------------------
@@ -553,6 +636,11 @@ sa_hash_index* sa_hash_build(sa_ctx* c, const char* fasta, uint64_t bytes, uint3
     }
     std::vector<uint8_t> b;
     if (!fasta_bases(fasta, bytes, b, c->err)) return nullptr;
+    // HashRefIndex32 keeps the genome length and every seed position in 32 bits
+    if ((uint64_t)b.size() >= (1ull << 32)) {
+        c->err = "sa_hash_build: genome of 2^32 bases or more (HashRefIndex64) is not supported";
+        return nullptr;
+    }
     std::unique_ptr<sa_hash_index> ix(new sa_hash_index());
     auto fail = [&](int rc) -> sa_hash_index* { return rc ? nullptr : ix.release(); };
     auto body = [&]() -> int {
@@ -773,6 +861,292 @@ int sa_hash_align(sa_ctx* c, const sa_hash_index* ix, const char* seq, const uin
         aligned = ret[i] >= 0;
     }
     *ai_nmis = ret[N - 1];   // getHashAlignInfo leaves nmis = the count, or -1
+    return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// reference path of a resident batch (sa_run_input_aligned)
+// ---------------------------------------------------------------------------
+struct sa_align_chain {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t next = 0;            // the batch whose alignment may follow the chain now
+    sa::AlignChainState st;
+    bool failed = false;
+};
+
+void align_chain_fail(sa_align_chain* ch)
+{
+    if (!ch) return;
+    {
+        std::lock_guard<std::mutex> g(ch->mu);
+        ch->failed = true;
+    }
+    ch->cv.notify_all();
+}
+
+int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq, std::vector<uint32_t>& atot,
+                AlignView& av)
+{
+    const sa_hash_index* ix = rq.ix;
+    const sa_align_cfg& a = rq.cfg;
+    const uint32_t nr = I->nreads, nbk = I->nblocks;
+    if (!ix || !rq.chain || ix->device != c->device) {
+        c->err = "sa_run_input_aligned: no index / chain, or an index of another device";
+        return -1;
+    }
+    if (a.maxmis < 0 || a.maxmis > 63 || ix->total < 4) {
+        c->err = "sa_run_input_aligned: maxmis must be 0..63 and the genome at least 4 bases";
+        return -1;
+    }
+    if (a.paired)
+        for (const DevBlock& d : c->blocks)
+            if (d.nreads & 1) {
+                c->err = "sa_run_input_aligned: a paired block with an odd read count";
+                return -1;
+            }
+    hipStream_t st = c->st;
+    const uint32_t stride = (uint32_t)a.maxmis + 1;
+    const size_t n1 = std::max<uint32_t>(nr, 1);
+    for (int v = 0; v < 2; v++) {
+        SA_CHECK(c, c->d_al_ret[v].ensure(4 * n1));
+        SA_CHECK(c, c->d_al_rev[v].ensure(n1));
+        SA_CHECK(c, c->d_al_pos[v].ensure(4 * n1));
+        SA_CHECK(c, c->d_al_mp[v].ensure(4 * stride * n1));
+        SA_CHECK(c, c->d_al_mt[v].ensure(4 * stride * n1));
+    }
+    SA_CHECK(c, c->d_al_st.ensure(n1));
+    SA_CHECK(c, c->d_al_scr.ensure(4 * (I->seq_bytes / 8 + 2 * (uint64_t)n1 + 64)));
+    SA_CHECK(c, c->d_acounts.ensure(4 * NACOL * n1));
+    SA_CHECK(c, c->d_atot.ensure(4 * NACOL * (size_t)std::max<uint32_t>(nbk, 1)));
+    SA_CHECK(c, c->d_seq_skip.ensure(n1));
+    const HashView hv{ix->seq.as<uint32_t>(), ix->num.as<uint32_t>(), ix->ind.as<uint32_t>(), ix->pos.as<uint32_t>(),
+                      ix->K, (uint64_t)ix->total};
+    const HashArgs ha{a.maxmis, a.good};
+    const bool rerun = c->al_input == I && c->al_plan.size() == 4ull * nbk &&
+                       (rq.batch == UINT64_MAX || rq.batch == c->al_batch);
+    if (!rerun) {
+        // ---- every read with the carried state "not aligned" ----
+        if (nr)
+            hipLaunchKernelGGL(k_hash_align_batch, dim3((nr + 255) / 256), dim3(256), 0, st, hv, ha, bv,
+                               c->d_al_scr.as<uint32_t>(), nullptr, nr, 0, a.paired ? 0 : 1, c->d_al_ret[0].as<int32_t>(),
+                               c->d_al_rev[0].as<uint8_t>(), c->d_al_pos[0].as<uint32_t>(), c->d_al_mp[0].as<int32_t>(),
+                               c->d_al_mt[0].as<int32_t>(), c->d_al_st.as<uint8_t>());
+        SA_CHECK(c, hipGetLastError());
+        std::vector<uint8_t> status(n1, 0);
+        std::vector<uint32_t> pos0(n1, 0), pos1(n1, 0);
+        SA_CHECK(c, d2h(c, status.data(), c->d_al_st.p, nr, st));
+        SA_CHECK(c, d2h(c, pos0.data(), c->d_al_pos[0].p, 4ull * nr, st));
+        SA_CHECK(c, sync_d2h(c, st));
+        // ---- the reads that consulted it, again with "aligned" ----
+        std::vector<uint32_t> cons;
+        for (uint32_t r = 0; r < nr; r++)
+            if ((status[r] & AL_CONS) && !(status[r] & AL_NSKIP)) cons.push_back(r);
+        if (!cons.empty()) {
+            SA_CHECK(c, c->d_al_sel.ensure(4 * cons.size()));
+            SA_CHECK(c, h2d(c, c->d_al_sel.p, cons.data(), 4 * cons.size(), st));
+            hipLaunchKernelGGL(k_hash_align_batch, dim3((uint32_t)((cons.size() + 255) / 256)), dim3(256), 0, st, hv, ha, bv,
+                               c->d_al_scr.as<uint32_t>(), c->d_al_sel.as<uint32_t>(), (uint32_t)cons.size(), 1,
+                               a.paired ? 0 : 1, c->d_al_ret[1].as<int32_t>(), c->d_al_rev[1].as<uint8_t>(),
+                               c->d_al_pos[1].as<uint32_t>(), c->d_al_mp[1].as<int32_t>(), c->d_al_mt[1].as<int32_t>(),
+                               c->d_al_st.as<uint8_t>());
+            SA_CHECK(c, hipGetLastError());
+            SA_CHECK(c, d2h(c, status.data(), c->d_al_st.p, nr, st));
+            SA_CHECK(c, d2h(c, pos1.data(), c->d_al_pos[1].p, 4ull * nr, st));
+            SA_CHECK(c, sync_d2h(c, st));
+        }
+        // ---- the chain: this batch after the previous one ----
+        sa_align_chain* ch = rq.chain;
+        std::vector<uint32_t> sel;
+        {
+            std::unique_lock<std::mutex> lk(ch->mu);
+            const uint64_t me = rq.batch == UINT64_MAX ? ch->next : rq.batch;
+            ch->cv.wait(lk, [&] { return ch->failed || ch->next == me; });
+            if (ch->failed) {
+                c->err = "sa_run_input_aligned: an earlier batch of the chain failed";
+                return -1;
+            }
+            c->al_plan.assign(4ull * nbk, 0);
+            for (uint32_t b = 0; b < nbk; b++) {
+                const DevBlock& d = c->blocks[b];
+                std::vector<uint32_t> sl;
+                const AlignBlockPlan p = align_plan_block(a.paired != 0, d.nreads, &status[d.read0], &pos0[d.read0],
+                                                          &pos1[d.read0], a.insert_size, ch->st, sl);
+                for (uint32_t i : sl) sel.push_back(d.read0 + i);
+                c->al_plan[4 * b + 0] = p.order_count;
+                c->al_plan[4 * b + 1] = p.win;
+                c->al_plan[4 * b + 2] = p.ibits;
+                c->al_plan[4 * b + 3] = p.insert_bits;
+            }
+            ch->next = me + 1;
+            c->al_batch = me;
+        }
+        ch->cv.notify_all();
+        c->al_input = I;
+        if (!sel.empty()) {
+            SA_CHECK(c, c->d_al_sel.ensure(4 * sel.size()));
+            SA_CHECK(c, h2d(c, c->d_al_sel.p, sel.data(), 4 * sel.size(), st));
+            hipLaunchKernelGGL(k_align_select, dim3((uint32_t)((sel.size() + 255) / 256)), dim3(256), 0, st,
+                               c->d_al_sel.as<uint32_t>(), (uint32_t)sel.size(), stride, c->d_al_ret[1].as<int32_t>(),
+                               c->d_al_rev[1].as<uint8_t>(), c->d_al_pos[1].as<uint32_t>(), c->d_al_mp[1].as<int32_t>(),
+                               c->d_al_mt[1].as<int32_t>(), c->d_al_ret[0].as<int32_t>(), c->d_al_rev[0].as<uint8_t>(),
+                               c->d_al_pos[0].as<uint32_t>(), c->d_al_mp[0].as<int32_t>(), c->d_al_mt[0].as<int32_t>());
+            SA_CHECK(c, hipGetLastError());
+        }
+    }
+    for (uint32_t b = 0; b < nbk; b++) {
+        DevBlock& d = c->blocks[b];
+        d.order_count = c->al_plan[4 * b + 0];
+        d.win = c->al_plan[4 * b + 1];
+        d.ibits = c->al_plan[4 * b + 2];
+        d.insert_bits = c->al_plan[4 * b + 3];
+    }
+    SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
+    const uint32_t shift = host_bits(ix->total) - 2;   // HashAlignment::loadRefIndex@0x40fe9b
+    av = AlignView{c->d_al_ret[0].as<int32_t>(), c->d_al_rev[0].as<uint8_t>(), c->d_al_pos[0].as<uint32_t>(),
+                   c->d_al_mp[0].as<int32_t>(), c->d_al_mt[0].as<int32_t>(), stride, shift, (1ull << shift) - 1,
+                   (uint64_t)ix->total, a.paired ? 1 : 0,
+                   a.maxmis >= 1 && a.maxmis <= 7 ? M_MIS8 : a.maxmis == 8 ? M_MIS9 : 0u};
+    bv.aligned = 1;
+    bv.paired = a.paired ? 1 : 0;
+    bv.seq_skip = c->d_seq_skip.as<uint8_t>();
+    if (nr) {
+        hipLaunchKernelGGL(k_align_counts, dim3((nr + 255) / 256), dim3(256), 0, st, bv, av, c->d_acounts.as<uint32_t>(),
+                           c->d_seq_skip.as<uint8_t>());
+        hipLaunchKernelGGL(k_scan_align, dim3(nbk), dim3(1024), 0, st, bv, c->d_acounts.as<uint32_t>(),
+                           c->d_atot.as<uint32_t>());
+    } else {
+        SA_CHECK(c, hipMemsetAsync(c->d_atot.p, 0, 4ull * NACOL * nbk, st));
+    }
+    SA_CHECK(c, hipGetLastError());
+    atot.assign((size_t)NACOL * nbk, 0);
+    SA_CHECK(c, d2h(c, atot.data(), c->d_atot.p, 4ull * NACOL * nbk, st));
+    SA_CHECK(c, sync_d2h(c, st));
+    return 0;
+}
+
+extern "C" {
+
+sa_align_chain* sa_align_chain_create(int32_t nmis_mate1, int32_t nmis_mate2)
+{
+    sa_align_chain* ch = new sa_align_chain();
+    // hashAligner@0x410f50's test: the carried mismatch count within [0, maxmis]
+    // (maxmis is not known yet: a fresh thread's 0 and -1 are the cases that arise)
+    ch->st.c[0] = nmis_mate1 >= 0;
+    ch->st.c[1] = nmis_mate2 >= 0;
+    return ch;
+}
+
+void sa_align_chain_destroy(sa_align_chain* ch) { delete ch; }
+
+int sa_run_input_aligned(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, const sa_align_cfg* acfg,
+                         sa_align_chain* chain, uint64_t batch)
+{
+    if (!c) return -1;
+    if (!acfg || !chain) {
+        c->err = "sa_run_input_aligned: no alignment config or chain";
+        return -1;
+    }
+    const AlignReq rq{acfg->index, *acfg, chain, batch};
+    c->al_input = nullptr;   // (a new batch: pass the chain)
+    int rc = run_input(c, I, cfg, true, &rq);
+    if (rc == 2) {   // exact payload outgrown: drain, re-run with the bound (same alignment plan)
+        for (hipStream_t s : {c->st, c->st2, c->st3, c->st4}) SA_CHECK(c, hipStreamSynchronize(s));
+        const AlignReq rq2{acfg->index, *acfg, chain, c->al_batch};
+        rc = run_input(c, I, cfg, false, &rq2);
+    }
+    return rc ? -1 : 0;
+}
+
+int sa_run_aligned(sa_ctx* c, const sa_cfg* cfg, const sa_align_cfg* acfg, sa_align_chain* chain, uint64_t batch)
+{
+    if (!c) return -1;
+    return sa_run_input_aligned(c, &c->own, cfg, acfg, chain, batch);
+}
+
+int sa_encode_blocks_aligned(sa_ctx* ctx, const sa_block* in, int n, const sa_cfg* cfg, const sa_align_cfg* acfg,
+                             sa_align_chain* chain, sa_out* out)
+{
+    if (!ctx || !cfg || !acfg || !chain || (n > 0 && (!in || !out))) return -1;
+    SA_CHECK(ctx, hipSetDevice(ctx->device));
+    size_t free_b = 0, total_b = 0;
+    SA_CHECK(ctx, hipMemGetInfo(&free_b, &total_b));
+    // (per read ~2 x (9 + 8 (maxmis + 1)) bytes of alignment on top of the encode)
+    const uint64_t budget = (uint64_t)((double)(free_b + ctx->held_bytes()) * 0.75);
+    uint64_t cap_bases = ~0ull;
+    if (const char* e = std::getenv("SA_BATCH_BASES")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v > 0) cap_bases = v;
+    }
+    int b0 = 0;
+    while (b0 < n) {
+        int b1 = b0;
+        uint64_t bases = 0, bytes = 0;
+        while (b1 < n) {
+            uint64_t ls = 0;
+            for (uint32_t r = 0; r < in[b1].nreads; r++) ls += (uint64_t)std::max(in[b1].seq_lens[r], 0);
+            const uint64_t fb = block_footprint(in[b1]) + (uint64_t)in[b1].nreads * (40 + 16 * (uint64_t)(acfg->maxmis + 1));
+            if (b1 > b0 && (bases + ls > cap_bases || bytes + fb > budget)) break;
+            bases += ls;
+            bytes += fb;
+            b1++;
+        }
+        if (sa_stage(ctx, in + b0, b1 - b0)) return -1;
+        if (sa_run_aligned(ctx, cfg, acfg, chain, UINT64_MAX)) return -1;
+        if (sa_fetch(ctx, out + b0, b1 - b0)) return -1;
+        b0 = b1;
+    }
+    return 0;
+}
+
+sa_hash_index* sa_hash_load(sa_ctx* c, const uint8_t* file, uint64_t bytes)
+{
+    if (!c || !file || bytes < 16) return nullptr;
+    uint32_t hdr[4];
+    std::memcpy(hdr, file, 16);
+    const uint32_t K = hdr[0];
+    if (K < 1 || K > 16) {
+        c->err = "sa_hash_load: not a .hash file (K)";
+        return nullptr;
+    }
+    const uint64_t nk = K >= 16 ? (1ull << 32) : (1ull << (2 * K));
+    if (bytes != 16 + 4ull * (hdr[2] + 2 * nk + hdr[3]) || hdr[2] != (hdr[1] ? (hdr[1] - 1) / 16 + 1 : 1u)) {
+        c->err = "sa_hash_load: .hash file size does not match its header";
+        return nullptr;
+    }
+    std::unique_ptr<sa_hash_index> ix(new sa_hash_index());
+    ix->device = c->device;
+    ix->K = K;
+    ix->total = hdr[1];
+    ix->nwords = hdr[2];
+    ix->npos = hdr[3];
+    ix->nkmers = nk;
+    auto body = [&]() -> int {
+        SA_CHECK(c, hipSetDevice(c->device));
+        const uint8_t* p = file + 16;
+        SA_CHECK(c, ix->seq.ensure(4ull * ix->nwords));
+        SA_CHECK(c, hipMemcpy(ix->seq.p, p, 4ull * ix->nwords, hipMemcpyHostToDevice));
+        p += 4ull * ix->nwords;
+        SA_CHECK(c, ix->num.ensure(4 * nk));
+        SA_CHECK(c, hipMemcpy(ix->num.p, p, 4 * nk, hipMemcpyHostToDevice));
+        p += 4 * nk;
+        SA_CHECK(c, ix->ind.ensure(4 * nk));
+        SA_CHECK(c, hipMemcpy(ix->ind.p, p, 4 * nk, hipMemcpyHostToDevice));
+        p += 4 * nk;
+        SA_CHECK(c, ix->pos.ensure(4ull * std::max<uint32_t>(ix->npos, 1)));
+        if (ix->npos) SA_CHECK(c, hipMemcpy(ix->pos.p, p, 4ull * ix->npos, hipMemcpyHostToDevice));
+        return 0;
+    };
+    return body() ? nullptr : ix.release();
+}
+
+int sa_hash_packed(sa_ctx* c, const sa_hash_index* ix, uint32_t* out, uint64_t words)
+{
+    if (!c || !ix || !out || words < ix->nwords) return -1;
+    SA_CHECK(c, hipSetDevice(ix->device));
+    SA_CHECK(c, hipMemcpy(out, ix->seq.p, 4ull * ix->nwords, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -731,6 +731,55 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
                      seq_sh);
 }
 
+// ---------------------------------------------------------------------------
+// Reference path (doAlignEncode@0x42d4c0): the alignment streams' per-read
+// columns, their per-block scan and their keys (sa_logic.h align_read_*).
+// ---------------------------------------------------------------------------
+// per read: the alignment columns and whether the SEQ stream leaves it out
+__global__ __launch_bounds__(256) void k_align_counts(const BatchView bv, const AlignView av,
+                                                      uint32_t* __restrict__ acounts, uint8_t* __restrict__ seq_skip)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bv.nreads_total) return;
+    seq_skip[r] = align_read_counts(bv, av, r, acounts + (size_t)r * NACOL) ? 1 : 0;
+}
+
+// exclusive scan of the alignment columns per block (one workgroup a block)
+__global__ __launch_bounds__(1024) void k_scan_align(const BatchView bv, uint32_t* __restrict__ acounts,
+                                                     uint32_t* __restrict__ atot)
+{
+    __shared__ uint32_t sh[16];
+    const DevBlock& blk = bv.blocks[blockIdx.x];
+    const uint32_t r0 = blk.read0, n = blk.nreads;
+    uint32_t carry[NACOL];
+#pragma unroll
+    for (int k = 0; k < NACOL; k++) carry[k] = 0;
+    for (uint32_t base = 0; base < n; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const bool in = i < n;
+        uint32_t* c = acounts + (size_t)(r0 + i) * NACOL;
+#pragma unroll
+        for (int k = 0; k < NACOL; k++) {
+            const uint32_t v = in ? c[k] : 0u;
+            uint32_t ex;
+            const uint32_t tot = wg1024_excl_scan(v, ex, sh);
+            if (in) c[k] = carry[k] + ex;
+            carry[k] += tot;
+        }
+    }
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int k = 0; k < NACOL; k++) atot[(size_t)blockIdx.x * NACOL + k] = carry[k];
+}
+
+__global__ __launch_bounds__(256) void k_align_emit(const BatchView bv, const AlignView av,
+                                                    const uint32_t* __restrict__ acounts, uint32_t* __restrict__ aux_key)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= bv.nreads_total) return;
+    align_read_emit(bv, av, r, acounts + (size_t)r * NACOL, aux_key, nullptr);
+}
+
 // SORT_PAD into the key slots no symbol is written to: each segment's tail up to
 // its last tile (ping buffer), and the slack slots past the space (both buffers;
 // the replays read past a run's end).

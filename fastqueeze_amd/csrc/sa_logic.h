@@ -11,10 +11,13 @@ namespace sa {
 // ---- per-read counts (k_prep) ----------------------------------------------
 // The columns of a read's SEQ / QUAL / N-IUPAC side streams (and their input
 // checks) from its seq_stat and trimmed quality length.
-SA_HD uint32_t prep_sq_cols(uint32_t* c, uint32_t len, uint32_t nq, const SeqStat& st, bool qual_bad)
+// seq_skip: an aligned read of the reference path, whose bases the SEQ stream
+// leaves out (compressSeq@0x4249b3: order byte != 0).
+SA_HD uint32_t prep_sq_cols(uint32_t* c, uint32_t len, uint32_t nq, const SeqStat& st, bool qual_bad,
+                            bool seq_skip = false)
 {
     uint32_t e = st.err;
-    c[C_SEQ] = st.valid;
+    c[C_SEQ] = seq_skip ? 0u : st.valid;
     c[C_QUAL] = nq + (nq != len ? 1 : 0);
     if (qual_bad) e |= E_QUALRANGE;
     c[C_CH] = st.nch;
@@ -48,7 +51,7 @@ SA_HD uint32_t prep_read(const BatchView& bv, uint32_t r, uint32_t* counts, int1
         bool qbad = false;
         for (uint32_t i = 0; i < n; i++)
             if (qq[i] < 33 || qq[i] > 126) { qbad = true; break; }
-        e |= prep_sq_cols(c, len, n, st, qbad);
+        e |= prep_sq_cols(c, len, n, st, qbad, bv.seq_skip && bv.seq_skip[r]);
     }
     c[C_LEN] = len == 0 ? 1 : (blk.len_long ? 5 : 3);
     c[C_TIP] = 1;
@@ -123,7 +126,7 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
     const uint32_t* off = counts + (size_t)r * NCOL;
 
     // sequence: BASE_MODEL contexts (encode_seq@0x421f30)
-    if (bulk) {
+    if (bulk && !(bv.seq_skip && bv.seq_skip[r])) {
         uint32_t* K = seq_key + blk.seq_sym_base;
         uint32_t* V = seq_val + blk.seq_sym_base;
         uint32_t d = off[C_SEQ];
@@ -229,6 +232,120 @@ SA_HD uint32_t emit_read(const BatchView& bv, uint32_t r, const uint32_t* counts
         }
     }
     return e;
+}
+
+// ---- reference (HASH index) path: the alignment streams of one read ---------
+// What AlignEncodeSEJob::AlignInfoProcess@0x4118b0 / AlignEncodePEJob::
+// AlignInfoProcessPE@0x412290 and decomposeAlignInfo@0x433860 push for a read
+// (int2bit@0x40dcd0: values as bit strings, least significant bit first), as
+// em(column, model, symbol) calls in stream order.  A read of the block's first
+// order_count reads is aligned iff av.ret >= 0 (the host chose its variant of
+// the carried align_info state and cut the block at the bail-out); PE pairs are
+// reads (2j, 2j+1) of the block: mate 1 carries the pair's relation (the
+// position of mate 2 from the insert window, further right as a distance,
+// further left absolutely) and, with both mates aligned, both carry mate 1's
+// order byte.
+SA_HD uint32_t aln_bits(uint64_t v)   // getbitnum@0x40d470
+{
+    uint32_t n = 0;
+    while (v) { n++; v >>= 1; }
+    return n;
+}
+
+template <class Em>
+SA_HD void align_read_syms(const BatchView& bv, const AlignView& av, uint32_t r, Em em)
+{
+    const DevBlock& blk = bv.blocks[bv.read_block[r]];
+    const uint32_t i = r - blk.read0;
+    if (i >= blk.order_count) return;
+    const bool al = av.ret[r] >= 0;
+    auto bits = [&](uint64_t v, uint32_t nb) {
+        for (uint32_t k = 0; k < nb; k++) em(A_POS, M_POS, (uint32_t)((v >> k) & 1u));
+    };
+    uint64_t ord = 0;
+    if (!av.paired) {
+        if (al) {
+            const uint64_t p = av.pos[r];
+            bits(p & av.mask, av.shift);
+            ord = (p >> av.shift) + 1;
+        }
+    } else {
+        const bool mate2 = (i & 1u) != 0;
+        const uint32_t r1 = mate2 ? r - 1 : r, r2 = r1 + 1;
+        const bool a1 = av.ret[r1] >= 0, a2 = av.ret[r2] >= 0;
+        const uint64_t p1 = av.pos[r1], p2 = av.pos[r2];
+        if (!mate2) {
+            if (a1) {
+                bits(p1 & av.mask, av.shift);
+                ord = (p1 >> av.shift) + 1;
+                if (a2) {
+                    const uint64_t d = p1 > p2 ? p1 - p2 : p2 - p1;
+                    if (d < (uint64_t)blk.win) {
+                        em(A_PEREL, M_PEREL, p1 < p2 ? 1u : 0u);
+                        bits(d, blk.ibits);
+                    } else if (p1 < p2) {
+                        em(A_PEREL, M_PEREL, 3u);
+                        bits(d, aln_bits(av.glen - p1));
+                    } else {
+                        em(A_PEREL, M_PEREL, 2u);
+                        bits(p2, aln_bits(p1));
+                    }
+                }
+            }
+        } else if (a2) {
+            if (a1) {
+                ord = (p1 >> av.shift) + 1;
+            } else {
+                bits(p2 & av.mask, av.shift);
+                ord = (p2 >> av.shift) + 1;
+            }
+        }
+    }
+    em(A_ORD, M_ORD, (uint32_t)(ord & 0xffu));
+    if (!al) return;
+    // decomposeAlignInfo@0x433860: each mismatch offset as the gap from the
+    // previous one in bits(len - previous) bits, its type; the count, the strand
+    const int nm = av.ret[r];
+    const int32_t* mp = av.mispos + (size_t)r * av.stride;
+    const int32_t* mt = av.mistype + (size_t)r * av.stride;
+    const int len = (int)bv.seq_len[r];
+    int prev = 0;
+    for (int k = 0; k < nm; k++) {
+        const uint32_t v = (uint32_t)(mp[k] - prev), nb = aln_bits((uint64_t)(int64_t)(len - prev));
+        for (uint32_t j = 0; j < nb; j++) em(A_CIGL, M_CIGL, (v >> j) & 1u);
+        prev = mp[k];
+        em(A_CIGV, M_CIGV, (uint32_t)mt[k]);
+    }
+    em(A_MIS, av.mis_model, (uint32_t)nm);
+    em(A_REV, M_REV, (uint32_t)av.rev[r]);
+}
+
+// The count columns of read r (and whether its bases leave the SEQ stream).
+SA_HD bool align_read_counts(const BatchView& bv, const AlignView& av, uint32_t r, uint32_t* c)
+{
+    for (int k = 0; k < NACOL; k++) c[k] = 0;
+    align_read_syms(bv, av, r, [&](int col, uint32_t, uint32_t) { c[col]++; });
+    const DevBlock& blk = bv.blocks[bv.read_block[r]];
+    return r - blk.read0 < blk.order_count && av.ret[r] >= 0;
+}
+
+// The keys of read r's alignment symbols; off = its exclusive column offsets.
+// (The Mis symbols are counted for align_count but written only when the
+// maxmis in force has a Mis model.)
+SA_HD void align_read_emit(const BatchView& bv, const AlignView& av, uint32_t r, const uint32_t* off, uint32_t* aux_key,
+                           uint32_t* aux_val)
+{
+    const DevBlock& blk = bv.blocks[bv.read_block[r]];
+    uint32_t at[NACOL];   // (column k is stream ST_ORD + k)
+    for (int k = 0; k < NACOL; k++) at[k] = blk.sbase[ST_ORD + k] + off[k];
+    uint32_t* K = aux_key + blk.aux_sym_base;
+    uint32_t* V = aux_val ? aux_val + blk.aux_sym_base : nullptr;
+    align_read_syms(bv, av, r, [&](int col, uint32_t model, uint32_t sym) {
+        if (col == A_MIS && !model) return;
+        const uint32_t p = at[col]++;
+        K[p] = (model << AUX_SYM_BITS) | sym;
+        if (V) V[p] = p;
+    });
 }
 
 // ---- coder records written by the model replays ---------------------------
@@ -694,15 +811,28 @@ SA_HD uint32_t assemble_plan(const BatchView& bv, uint32_t b, const AsmBlock& ab
 {
     const DevBlock& blk = bv.blocks[b];
     uint32_t p = 5;   // 0x81 + size4
-    // count (compressCount@0x422a00)
-    o[p++] = 0x81; o[p++] = 0x84; put_u32le(o + p, blk.nreads); p += 4;
     uint32_t ns = 0;
+    // compressCount@0x422a00: setID(id), size byte 0x84, u32 LE
+    auto count = [&](uint32_t id, uint32_t v) {
+        p += put_id(o + p, id);
+        o[p++] = 0x84;
+        put_u32le(o + p, v);
+        p += 4;
+    };
+    // a stream's encap: setID(id), size4, the coded bytes
+    auto stream = [&](uint32_t id, int st) {
+        const uint32_t L = out_len[ab.task[st]];
+        p += put_id(o + p, id);
+        put_size4(o + p, L);
+        p += 4;
+        seg_dst[ns] = p; seg_src_task[ns] = ab.task[st]; seg_len[ns] = L; ns++; p += L;
+    };
+    count(1, blk.nreads);
     const int md5 = bv.md5;
-    // length
-    {
-        uint32_t L = out_len[ab.task[ST_LEN]];
-        p += put_id(o + p, 4); put_size4(o + p, L); p += 4;
-        seg_dst[ns] = p; seg_src_task[ns] = ab.task[ST_LEN]; seg_len[ns] = L; ns++; p += L;
+    stream(4, ST_LEN);
+    if (bv.aligned) {   // doAlignEncode@0x42d4c0: order count and order bytes
+        count(0x1b, blk.order_count);
+        stream(8, ST_ORD);
     }
     // ID (compressID@0x4247c0)
     {
@@ -738,6 +868,22 @@ SA_HD uint32_t assemble_plan(const BatchView& bv, uint32_t b, const AsmBlock& ab
         uint32_t L = out_len[ab.task[ST_QUAL]];
         seg_dst[ns] = p; seg_src_task[ns] = ab.task[ST_QUAL]; seg_len[ns] = L; ns++; p += L;
         put_size4(o + szp, h + L);
+    }
+    if (bv.aligned) {   // the alignment streams (@0x42d5bd-0x42d6bb, 0x42d830)
+        count(0x11, blk.align_count);
+        count(0x12, blk.scount[ST_POS]);
+        count(0x13, blk.scount[ST_CIGL]);
+        count(0x14, blk.scount[ST_CIGV]);
+        if (bv.paired) {
+            count(0x15, blk.insert_bits);
+            count(0x16, blk.scount[ST_PEREL]);
+            stream(9, ST_PEREL);
+        }
+        stream(0xb, ST_POS);
+        stream(0xf, ST_MIS);
+        stream(0xa, ST_REV);
+        stream(0xc, ST_CIGL);
+        stream(0xd, ST_CIGV);
     }
     // degenerate-base streams: encap omitted when its value count is 0
     const uint32_t ids[5] = {23, 14, 24, 25, 26};

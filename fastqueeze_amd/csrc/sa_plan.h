@@ -48,9 +48,15 @@ struct BatchPlan {
     uint64_t final_bytes = 0;
 };
 
-// totals: per block, the NCOL column sums of k_scan_reads.  Fills the symbol
-// space fields of every DevBlock.  Returns false if a block is too large.
-inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t>& totals, BatchPlan& bp)
+constexpr uint32_t NO_TASK = 0xffffffffu;   // AsmBlock::task of a stream the layout does not have
+
+// totals: per block, the NCOL column sums of k_scan_reads.  atot (reference
+// path only): per block the NACOL sums of the alignment columns, whose streams
+// follow the others in the AUX space; mis_model: the Mis stream's model (0: no
+// symbols).  Fills the symbol space fields of every DevBlock.  Returns false if
+// a block is too large.
+inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t>& totals, BatchPlan& bp,
+                       const std::vector<uint32_t>* atot = nullptr, uint32_t mis_model = 0)
 {
     const size_t nbk = blocks.size();
     std::vector<uint64_t> seq_counts(nbk), aux_counts(nbk);
@@ -59,10 +65,21 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
         const uint32_t* t = &totals[b * NCOL];
         const uint32_t sc[NAUX] = {t[C_LEN], t[C_NAME], t[C_QUAL], t[C_TIP], t[C_CH], t[C_MAXQ], t[C_NCNT], t[C_NPOS]};
         uint64_t a = 0;
+        for (int s = 0; s < NSTREAM; s++) d.sbase[s] = d.scount[s] = 0;
         for (int s = 0; s < NAUX; s++) {
             d.sbase[s] = (uint32_t)a;
             d.scount[s] = sc[s];
             a += sc[s];
+        }
+        if (atot) {
+            const uint32_t* at = &(*atot)[b * NACOL];
+            for (int k = 0; k < NACOL; k++) {
+                const int s = ST_ORD + k;
+                d.sbase[s] = (uint32_t)a;
+                d.scount[s] = (k == A_MIS && !mis_model) ? 0u : at[k];
+                a += d.scount[s];
+            }
+            d.align_count = at[A_REV];
         }
         if (a >= (1ull << 31) || t[C_SEQ] >= (1u << 30)) return false;
         d.n_aux = (uint32_t)a;
@@ -80,7 +97,9 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
     bp.aux = plan_sort(aux_counts);
     bp.tasks.clear();
     bp.task_out_base.clear();
-    bp.asmb.assign(nbk, AsmBlock{});
+    AsmBlock none{};
+    for (int s = 0; s < NSTREAM; s++) none.task[s] = NO_TASK;
+    bp.asmb.assign(nbk, none);
     uint64_t payload = 0, fin = 0, segs = 0;
     // coder tasks: every block's SEQ stream first (tasks [0, nbk)), then the AUX
     // streams (tasks [nbk, 9 nbk)), so the two groups can be coded on two streams
@@ -115,13 +134,15 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
         d.aux_sym_base = bp.aux.segs[b].base;
         add_task(b, ST_SEQ);
     }
+    const int nst = atot ? NSTREAM : ST_SEQ + 1;   // (the alignment streams: reference path only)
     for (size_t b = 0; b < nbk; b++)
-        for (int s = 0; s < NSTREAM; s++)
+        for (int s = 0; s < nst; s++)
             if (s != ST_SEQ) add_task(b, s);
     for (size_t b = 0; b < nbk; b++) {
         const DevBlock& d = blocks[b];
-        uint64_t blk_out = 64 + 2 + d.name_bytes;   // headers, MD5s, ID-bin payload (first ID)
-        for (int s = 0; s < NSTREAM; s++) blk_out += bp.tasks[bp.asmb[b].task[s]].out_cap + 32;
+        uint64_t blk_out = 64 + 2 + d.name_bytes + (atot ? 96 : 0);   // headers, counts, MD5s, ID-bin first ID
+        for (int s = 0; s < NSTREAM; s++)
+            if (bp.asmb[b].task[s] != NO_TASK) blk_out += bp.tasks[bp.asmb[b].task[s]].out_cap + 32;
         for (int f = 0; f < 3; f++) bp.asmb[b].md5_task[f] = (uint32_t)(3 * b + f);
         bp.asmb[b].out_base = fin;
         fin = align_up(fin + blk_out, 16);

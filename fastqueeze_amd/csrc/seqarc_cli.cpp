@@ -941,7 +941,15 @@ int decompress(const Options& o)
             }
             std::string s = i <= 1 ? name1 : name2;
             if (gz1 && s.size() >= 3) s = s.substr(0, s.size() - 3);
-            if (s == "@empty*" || s.empty()) s = std::string("decode") + (i == 0 ? ".fastq" : i == 1 ? "_1.fastq" : "_2.fastq");
+            // the archive's stored names (trailer fields 13/14) are untrusted: the
+            // encoder only ever stores basenames (compressStr@0x4160f0), so keep the
+            // part after the last '/' and refuse '.', '..' and control characters
+            const size_t sl = s.rfind('/');
+            if (sl != std::string::npos) s = s.substr(sl + 1);
+            bool bad = s == "." || s == "..";
+            for (unsigned char ch : s) bad |= ch < 0x20 || ch == 0x7f;
+            if (bad || s == "@empty*" || s.empty())
+                s = std::string("decode") + (i == 0 ? ".fastq" : i == 1 ? "_1.fastq" : "_2.fastq");
             return dir + s;
         };
         const std::string p1 = name(paired ? 1 : 0), p2 = paired ? name(2) : std::string();

@@ -248,6 +248,43 @@ int sa_hash_align(sa_ctx *ctx, const sa_hash_index *ix, const char *seq, const u
                   int64_t n, int32_t maxmis, int32_t good, int32_t *ai_nmis, int32_t *ret, uint8_t *rev,
                   uint64_t *pos, int32_t *mispos, int32_t *mistype);
 
+/* ---- reference path: the block encoder with a HASH index ---------------
+ * Replaces, per block, EncapFqzComp::doAlignEncode@0x42d4c0 together with the
+ * per-block alignment driver ISeqArcEncodeThread::doTask@0x433ed8 runs before
+ * it (AlignEncodeSEJob::doAlign@0x411910 / AlignEncodePEJob::doAlign@0x413580):
+ * every read aligned (getHashAlignInfo@0x4113c0), aligned reads coded as order /
+ * position / mismatch / strand streams (and the PE mate relation), the rest
+ * through the SEQ stream.  The encode thread carries one align_info per mate
+ * from read to read and from block to block; an sa_align_chain is that state,
+ * and batches of one input pass it on in order. */
+typedef struct {
+    const sa_hash_index *index;   /* on the encoding context's device              */
+    int32_t paired;               /* PE, reads interleaved r1, r2 (-2 given)       */
+    int32_t maxmis;               /* param+0x1b60 (7), 0..63                       */
+    int32_t good;                 /* param+0x1b74 (1)                              */
+    uint32_t insert_size;         /* -I (param+0x28); 0: estimated per block       */
+} sa_align_cfg;
+typedef struct sa_align_chain sa_align_chain;
+/* the align_info mismatch counts before the first batch (AlignParam+0xc / +0x54;
+ * 0 for a fresh encode thread) */
+sa_align_chain *sa_align_chain_create(int32_t nmis_mate1, int32_t nmis_mate2);
+void sa_align_chain_destroy(sa_align_chain *ch);
+/* encodes the resident batch in the doAlignEncode layout; batch = its place in
+ * the chain (0, 1, 2, ...: a call waits until the previous batch has passed
+ * its alignment), or UINT64_MAX for the chain's next.  Then sa_fetch. */
+int sa_run_input_aligned(sa_ctx *ctx, const sa_input *in, const sa_cfg *cfg, const sa_align_cfg *acfg,
+                         sa_align_chain *chain, uint64_t batch);
+int sa_run_aligned(sa_ctx *ctx, const sa_cfg *cfg, const sa_align_cfg *acfg, sa_align_chain *chain, uint64_t batch);
+/* one-shot form of the above (sub-batches in order through the chain) */
+int sa_encode_blocks_aligned(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, const sa_align_cfg *acfg,
+                             sa_align_chain *chain, sa_out *out);
+/* the ".hash" file back onto ctx's device (HashRefIndex32::readIndexFile) */
+sa_hash_index *sa_hash_load(sa_ctx *ctx, const uint8_t *file, uint64_t bytes);
+/* the genome's packed bases (16 a word, 2 bits, first base in the top bits,
+ * N as A): what decoding an aligned read reads (HashAlignment::doGetSeq@0x40ff90);
+ * out has room for (bases + 15) / 16 words */
+int sa_hash_packed(sa_ctx *ctx, const sa_hash_index *ix, uint32_t *out, uint64_t words);
+
 #ifdef __cplusplus
 }
 #endif

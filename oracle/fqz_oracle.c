@@ -241,7 +241,18 @@ static uint8_t base_code(uint8_t c)
 /* 0x424934); halve (c -= c>>1) when sum > 253; code; c[b]++.                */
 /* k = Slevel + 7 (ctor 0x42f63e); NS = 1u << ((2k) & 31) (x86 shl masks).   */
 /* ------------------------------------------------------------------------ */
+/* skip / nskip: the reference path's compressSeq (@0x424976-0x4249d5) codes
+ * only the reads r < nskip with skip[r] == 0 (order byte 0: not aligned) and
+ * every read from nskip on; NULL: every read (no reference) */
+static int64_t seq_payload_sel(const orc_block *b, int k, const uint8_t *skip, uint32_t nskip, uint8_t *out,
+                               uint8_t *end);
 static int64_t seq_payload(const orc_block *b, int k, uint8_t *out, uint8_t *end)
+{
+    return seq_payload_sel(b, k, NULL, 0, out, end);
+}
+
+static int64_t seq_payload_sel(const orc_block *b, int k, const uint8_t *skip, uint32_t nskip, uint8_t *out,
+                               uint8_t *end)
 {
     uint32_t ns = 1u << ((2 * k) & 31);
     uint32_t mask = ns - 1;
@@ -254,6 +265,10 @@ static int64_t seq_payload(const orc_block *b, int k, uint8_t *out, uint8_t *end
     for (uint32_t r = 0; r < b->nreads; r++) {
         int32_t len = b->seq_lens[r];
         uint32_t ctx = 0x7616c7u & mask;
+        if (skip && r < nskip && skip[r]) {
+            if (len > 0) p += len;
+            continue;
+        }
         for (int32_t i = 0; i < len; i++) {
             uint8_t c = base_code(p[i]);
             if (c > 3) continue;
@@ -803,6 +818,131 @@ int64_t orc_encode_block(const orc_block *b, const orc_cfg *cfg, uint8_t *out, s
 
     if ((r = orc_encap_seq(b, cfg, p, (size_t)(end - p))) < 0) return -1;
     p += r;
+    int64_t total = p - (out + idn + 4);
+    encap_set_size((uint64_t)total, 4, out + idn);
+    return p - out;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reference (HASH index) path: EncapFqzComp::doAlignEncode@0x42d4c0.         */
+/* 81 size4 | count(1) | len(4) | count(0x1b) | order(8) | ID(5) | qual(7) | */
+/* count(0x11..0x14) | [PE: count(0x15) count(0x16) perel(9)] | pos(0xb) |    */
+/* mis(0xf) | rev(0xa) | cigal(0xc) | cigav(0xd) | dege 23 14 24 25 26 |      */
+/* seq(6) -- the seq stream codes only the reads that did not align.          */
+/* ------------------------------------------------------------------------ */
+
+/* compressCount@0x422a00: setID(id), 1-byte size 0x84, u32 LE */
+static int64_t count_encap(uint32_t id, uint32_t v, uint8_t *out, uint8_t *end)
+{
+    if (end - out < 16) return -1;
+    int n = encap_set_id(id, out);
+    encap_set_size(4, 1, out + n);
+    put_u32le(out + n + 1, v);
+    return n + 5;
+}
+
+/* One SIMPLE_MODEL<nsym> over a byte array, own range coder: the template of
+ * compressOrder@0x424b70 (8, <5>), compressPERelation@0x422be0 (9, <4>),
+ * compressAlignInfo_Pos@0x425d70 (0xb, <2>), _Rev@0x426480 (0xa, <2>),
+ * _CigaL@0x426700 (0xc, <2>), _CigaV@0x426980 (0xd, <4>) and _Mis@0x425ff0
+ * (0xf, <8> for maxmis 1..7, <9> for 8, no symbols otherwise).  setID + size4
+ * + the coded bytes; no count, always written (8 flush bytes when empty). */
+static int64_t sm_stream_encap(uint32_t id, int nsym, const uint8_t *vals, uint32_t n, uint8_t *out, uint8_t *end)
+{
+    if (end - out < 16) return -1;
+    int idn = encap_set_id(id, out);
+    uint8_t *p = out + idn + 4;
+    smodel *m = (smodel *)malloc(sizeof(smodel));
+    if (!m) return -1;
+    rc_t rc;
+    rc_init(&rc, p, end);
+    if (nsym > 0) {
+        sm_init(m, nsym);
+        for (uint32_t i = 0; i < n && !rc.err; i++) {
+            if (vals[i] >= nsym) { rc.err = 1; break; }
+            sm_encode(m, &rc, vals[i]);
+        }
+    }
+    rc_finish(&rc);
+    free(m);
+    if (rc.err) return -1;
+    int64_t pl = rc.out - p;
+    encap_set_size((uint64_t)pl, 4, out + idn);
+    return idn + 4 + pl;
+}
+
+int64_t orc_encode_block_aligned(const orc_block *b, const orc_cfg *cfg, const orc_align_streams *a,
+                                 uint8_t *out, size_t cap)
+{
+    uint8_t *end = out + cap;
+    if (cap < 16 || a->order_count > b->nreads) return -1;
+    int idn = encap_set_id(1, out);
+    uint8_t *p = out + idn + 4;
+    int64_t r;
+#define PUT(expr) do { if ((r = (expr)) < 0) return -1; p += r; } while (0)
+    PUT(count_encap(1, b->nreads, p, end));
+    PUT(orc_encap_len(b, p, (size_t)(end - p)));
+    PUT(count_encap(0x1b, a->order_count, p, end));
+    PUT(sm_stream_encap(8, 5, a->order, a->order_count, p, end));
+    PUT(orc_encap_id(b, cfg, p, (size_t)(end - p)));
+    PUT(orc_encap_qual(b, cfg, p, (size_t)(end - p)));
+    PUT(count_encap(0x11, a->align_count, p, end));
+    PUT(count_encap(0x12, a->npos, p, end));
+    PUT(count_encap(0x13, a->ncigal, p, end));
+    PUT(count_encap(0x14, a->ncigav, p, end));
+    if (a->paired) {   /* param+0x1b38 == 0 (-2 given) */
+        PUT(count_encap(0x15, a->insert_bits, p, end));
+        PUT(count_encap(0x16, a->nperel, p, end));
+        PUT(sm_stream_encap(9, 4, a->perel, a->nperel, p, end));
+    }
+    PUT(sm_stream_encap(0xb, 2, a->pos, a->npos, p, end));
+    PUT(sm_stream_encap(0xf, a->maxmis >= 1 && a->maxmis <= 7 ? 8 : a->maxmis == 8 ? 9 : 0, a->mis, a->nmis, p, end));
+    PUT(sm_stream_encap(0xa, 2, a->rev, a->nrev, p, end));
+    PUT(sm_stream_encap(0xc, 2, a->cigal, a->ncigal, p, end));
+    PUT(sm_stream_encap(0xd, 4, a->cigav, a->ncigav, p, end));
+#undef PUT
+    dege_t d;
+    memset(&d, 0, sizeof d);
+    const uint8_t *s = b->seq, *q = b->qual;
+    int bad = 0;
+    for (uint32_t i = 0; i < b->nreads && !bad; i++) {
+        int32_t len = b->seq_lens[i];
+        if (dege_read(&d, s, q, len > 0 ? len : 0)) bad = 1;
+        s += len;
+        q += len;
+    }
+    kmodel *km = (kmodel *)malloc(sizeof(kmodel));
+    if (!km) bad = 1;
+    else kmodel_init(km);
+    if (!bad && (r = dege_sm_stream(23, 2, d.tip.v, d.tip.n, 0, p, end)) < 0) bad = 1;
+    if (!bad) p += r;
+    if (!bad && (r = dege_sm_stream(14, 11, d.ch.v, d.ch.n, 1, p, end)) < 0) bad = 1;
+    if (!bad) p += r;
+    if (!bad && (r = dege_sm_stream(24, 95, d.maxq.v, d.maxq.n, 2, p, end)) < 0) bad = 1;
+    if (!bad) p += r;
+    if (!bad && (r = dege_k_stream(25, km, d.cnt.v, d.cnt.n, p, end)) < 0) bad = 1;
+    if (!bad) p += r;
+    if (!bad && (r = dege_k_stream(26, km, d.pos.v, d.pos.n, p, end)) < 0) bad = 1;
+    if (!bad) p += r;
+    free(km);
+    free(d.tip.v); free(d.ch.v); free(d.maxq.v); free(d.cnt.v); free(d.pos.v);
+    if (bad) return -1;
+    /* sequence: compressSeq@0x4248a0, aligned reads skipped */
+    {
+        if (end - p < 32) return -1;
+        int n = encap_set_id(6, p);
+        uint8_t *q6 = p + n + 4;
+        int hdr = 0;
+        if (cfg->md5) {
+            orc_md5(b->seq, (size_t)total_seq(b), q6);
+            q6 += 16;
+            hdr = 16;
+        }
+        int64_t pl = seq_payload_sel(b, cfg->slevel + 7, a->order, a->order_count, q6, end);
+        if (pl < 0) return -1;
+        encap_set_size((uint64_t)(hdr + pl), 4, p + n);
+        p += n + 4 + hdr + pl;
+    }
     int64_t total = p - (out + idn + 4);
     encap_set_size((uint64_t)total, 4, out + idn);
     return p - out;

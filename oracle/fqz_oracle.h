@@ -51,6 +51,39 @@ typedef struct {
 int64_t orc_encode_block(const orc_block *b, const orc_cfg *cfg,
                          uint8_t *out, size_t cap);
 
+/* The per-block arrays the reference path builds in SeqArcMemBuf
+ * (AlignEncode{SE,PE}Job::doAlign@0x411910/0x413580, AlignInfoProcess[PE]
+ * @0x4118b0/0x412290, decomposeAlignInfo@0x433860) and doAlignEncode@0x42d4c0
+ * codes.  Bit arrays hold one bit (0/1) per byte, LSB of the value first. */
+typedef struct {
+    int paired;                 /* param+0x1b38 == 0                          */
+    int maxmis;                 /* param+0x1b60 (Mis model size)              */
+    uint32_t order_count;       /* +0xe8 / +0x34: reads with an order byte    */
+    uint32_t align_count;       /* +0x30: aligned reads                       */
+    uint32_t insert_bits;       /* +0x28 (PE)                                 */
+    const uint8_t *order;       /* +0xe0: 0 or (pos >> shift) + 1             */
+    const uint8_t *pos;   uint32_t npos;     /* +0xf0 / +0xf8 (bits)        */
+    const uint8_t *cigal; uint32_t ncigal;   /* +0x100 / +0x108 (bits)      */
+    const uint8_t *mis;   uint32_t nmis;     /* +0x110 / +0x118             */
+    const uint8_t *rev;   uint32_t nrev;     /* +0x120 / +0x128             */
+    const uint8_t *cigav; uint32_t ncigav;   /* +0x130 / +0x138             */
+    const uint8_t *perel; uint32_t nperel;   /* +0x140 / +0x148             */
+} orc_align_streams;
+
+/* EncapFqzComp::doAlignEncode@0x42d4c0 over the arrays above. */
+int64_t orc_encode_block_aligned(const orc_block *b, const orc_cfg *cfg, const orc_align_streams *a,
+                                 uint8_t *out, size_t cap);
+
+/* The whole reference path of one block against the index last built by
+ * ho_build (hash_oracle.c): doAlign (the aligner over the read chain, the 5 %
+ * probe and bail-out, the PE insert-size estimate CaclInsertSize@0x413270),
+ * then doAlignEncode.  carry[0] (SE; PE mate 1) / carry[1] (PE mate 2): the
+ * align_info nmis the encode thread carries from read to read and block to
+ * block (AlignParam+0xc / +0x54), in and out.  insert_size: -I (param+0x28),
+ * 0 = estimated per block.  Returns bytes written or -1. */
+int64_t orc_encode_block_hash(const orc_block *b, const orc_cfg *cfg, int paired, int maxmis, int good,
+                              uint32_t insert_size, int32_t carry[2], uint8_t *out, size_t cap);
+
 /* Individual streams, each returning the complete encap (ID + size + payload)
  * exactly as the corresponding compressX routine writes it. */
 int64_t orc_encap_seq(const orc_block *b, const orc_cfg *cfg, uint8_t *out, size_t cap);

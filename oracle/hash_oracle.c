@@ -20,6 +20,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "hash_oracle.h"
+
 /* base code @0x449fc0: ACGT 0-3 (either case), IUPAC M 5, R 6, Y 7, K 8, S 9,
  * W 10, H 11, B 12, V 13, D 14, anything else 4 (sa_common.h base_code); a
  * byte >= 0x80 indexes the reference's table with a sign-extended offset
@@ -66,13 +68,6 @@ static const uint8_t HO_MISTYPE[16] = {3, 1, 0, 2, 1, 3, 0, 2, 1, 0, 3, 2, 2, 1,
 static uint64_t ho_mask(uint32_t k) { return k >= 32 ? ~0ull : (1ull << (2 * k)) - 1; } /* @0x449e80 */
 
 /* ---- index ------------------------------------------------------------- */
-typedef struct {
-    uint32_t K, step, maxcount;
-    uint64_t nkmers;                 /* 4^K                                   */
-    uint32_t total, nwords, npos;    /* +0x40, +0x44, +0x48                   */
-    uint32_t *seq, *num, *ind, *pos; /* +0x38, +0x50, +0x58, +0x60           */
-} ho_index;
-
 void ho_index_free(ho_index* ix)
 {
     free(ix->seq);
@@ -87,7 +82,7 @@ static int next_line(const char* fa, uint64_t n, uint64_t* at, const char** line
 {
     if (*at >= n) return 0;
     const char* p = fa + *at;
-    const char* e = memchr(p, '\n', n - *at);
+    const char* e = (const char*)memchr(p, '\n', n - *at);
     const uint64_t l = e ? (uint64_t)(e - p) + 1 : n - *at;
     *line = p;
     *len = l;
@@ -99,7 +94,7 @@ static int next_line(const char* fa, uint64_t n, uint64_t* at, const char** line
  * (getdelim keeps the '\n'; strlen stops at a NUL) */
 static uint64_t line_bases(const char* line, uint64_t len)
 {
-    const char* z = memchr(line, 0, len);
+    const char* z = (const char*)memchr(line, 0, len);
     const uint64_t sl = z ? (uint64_t)(z - line) : len;
     return sl ? sl - 1 : 0;
 }
@@ -208,26 +203,9 @@ int ho_index_serialize(const ho_index* ix, uint8_t* out, uint64_t cap)
 /* ---- alignment --------------------------------------------------------- */
 /* aligner_args (calloc'd in HashAlignment::loadRefIndex@0x40fdc0): seed length,
  * max mismatches (param+0x1b60 = 7), genome length, the "good enough"
- * threshold (param+0x1b74 = 1) and two flags (0) */
-typedef struct {
-    uint32_t K;
-    int32_t maxmis;
-    uint64_t glen;
-    int32_t good;
-    uint8_t f14, f15;
-} ho_args;
-
-#define HO_MAXMIS 64
-/* align_info: strand, mismatches (-1: unaligned), read length, 1-based
- * reference position, mismatch offsets and types */
-typedef struct {
-    uint8_t rev;
-    int32_t nmis;
-    int32_t len;
-    uint64_t pos;
-    int32_t mispos[HO_MAXMIS + 1];
-    int32_t mistype[HO_MAXMIS + 1];
-} ho_align;
+ * threshold (param+0x1b74 = 1) and two flags (0): ho_args, hash_oracle.h;
+ * align_info: strand, mismatches (-1: unaligned), read length, 1-based
+ * reference position, mismatch offsets and types: ho_align */
 
 static uint32_t mis2(uint32_t x) /* g_mismatch_count@0x65a7c0: differing 2-bit groups */
 {
@@ -518,6 +496,8 @@ int64_t ho_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32_t
 int ho_serialize(uint8_t* out, uint64_t cap) { return ho_index_serialize(&g_ix, out, cap); }
 
 uint32_t ho_genome_length(void) { return g_ix.total; }
+
+const ho_index *ho_current_index(void) { return &g_ix; }
 
 /* aligns n reads (seq + offsets / lengths), in order, against the last built
  * index; *ai_nmis: the carried align_info state (in: before the first read;

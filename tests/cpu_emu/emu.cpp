@@ -7,7 +7,13 @@
 // extract -> sort -> replay -> code decomposition before it runs on MI355X;
 // the GPU parity tests (tests/test_gpu_parity.py) check the kernels themselves.
 //
-//   emu [-b block_bytes] [-s slevel] [-q qlevel] in1.fq [in2.fq]
+//   emu [-b block_bytes] [-s slevel] [-q qlevel] [-r ref.fa [-I insert]] in1.fq [in2.fq]
+//
+// -r: the reference (HASH index) path: the oracle's index and aligner give
+// every read's alignment under both carried align_info states (what the GPU
+// pass computes), the engine's host bookkeeping (sa_align_host.h) chooses and
+// plans the blocks, sa_logic.h emits the alignment streams, and each block is
+// compared with the oracle's doAlign + doAlignEncode restatement.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -16,10 +22,12 @@
 #include <string>
 #include <vector>
 
+#include "../../fastqueeze_amd/csrc/sa_align_host.h"
 #include "../../fastqueeze_amd/csrc/sa_logic.h"
 #include "../../fastqueeze_amd/csrc/sa_plan.h"
 #include "../../include/seqarc_amd.h"
 #include "../../oracle/fqz_oracle.h"
+#include "../../oracle/hash_oracle.h"
 
 using namespace sa;
 
@@ -130,8 +138,13 @@ int main(int argc, char** argv)
     uint64_t bs = 50ull << 20;
     int slevel = 3, qlevel = 2;
     double lossy = 0.0;
+    const char* ref = nullptr;
+    uint32_t insert_size = 0;
+    const int maxmis = 7, good = 1;
     std::vector<const char*> in;
     for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "-r") && i + 1 < argc) { ref = argv[++i]; continue; }
+        if (!std::strcmp(argv[i], "-I") && i + 1 < argc) { insert_size = (uint32_t)std::atoi(argv[++i]); continue; }
         if (!std::strcmp(argv[i], "-b") && i + 1 < argc) bs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "-s") && i + 1 < argc) slevel = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "-q") && i + 1 < argc) qlevel = std::atoi(argv[++i]);
@@ -145,6 +158,7 @@ int main(int argc, char** argv)
     std::vector<uint64_t> e1(4096), e2(4096);
     int64_t nb = pe ? sa_cut_pe(t1.data(), t1.size(), t2.data(), t2.size(), bs, e1.data(), e2.data(), 4096)
                     : sa_cut_se(t1.data(), t1.size(), bs, e1.data(), 4096);
+    if (nb <= 0) { std::printf("FAIL cut\n"); return 1; }
     // the oracle's cut must agree
     {
         std::vector<size_t> o1(4096), o2(4096);
@@ -234,6 +248,85 @@ int main(int argc, char** argv)
     bv.md5 = 1;
     bv.qual_q = qual.data();
     bv.lossy = lossy > 0.0;
+    // ---- -r: alignments (both carried states), the host plan, the variant choice ----
+    std::vector<int32_t> a_ret(nr, -1), a_mp((size_t)nr * (maxmis + 1), -1), a_mt((size_t)nr * (maxmis + 1), 0);
+    std::vector<uint8_t> a_rev(nr, 0), seq_skip(nr, 0);
+    std::vector<uint32_t> a_pos(nr, 0);
+    AlignView av{};
+    if (ref) {
+        std::vector<uint8_t> fa = slurp(ref);
+        if (fa.empty() || ho_build((const char*)fa.data(), fa.size(), 14, 2, 1u << 16) < 0) {
+            std::printf("FAIL index\n");
+            return 1;
+        }
+        const ho_index* ix = ho_current_index();
+        const ho_args args{ix->K, maxmis, ix->total, good, 0, 0};
+        std::vector<ho_align> v0(nr), v1(nr);
+        std::vector<uint8_t> st(nr, 0);
+        std::vector<uint32_t> p0(nr, 0), p1(nr, 0);
+        for (uint32_t r = 0; r < nr; r++) {
+            const DevBlock& d = blocks[read_block[r]];
+            const char* rd = (const char*)seq.data() + d.seq_base + seq_off[r];
+            const int len = (int)seq_len[r];
+            int nn = 0;
+            for (int i = 0; i < len; i++) nn += base_code((uint8_t)rd[i]) > 3;
+            std::memset(&v0[r], 0, sizeof(ho_align));
+            std::memset(&v1[r], 0, sizeof(ho_align));
+            v0[r].nmis = -1;
+            v1[r].nmis = 0;
+            const int r0 = len > 0 ? ho_align_read(ix, &args, rd, len, &v0[r]) : -1;
+            const int r1 = len > 0 ? ho_align_read(ix, &args, rd, len, &v1[r]) : -1;
+            if (r0 < 0) v0[r].nmis = -1;
+            if (r1 < 0) v1[r].nmis = -1;
+            bool differ = r0 != r1;
+            if (!differ && r0 >= 0)
+                differ = v0[r].pos != v1[r].pos || v0[r].rev != v1[r].rev ||
+                         std::memcmp(v0[r].mispos, v1[r].mispos, sizeof(int32_t) * (size_t)r0) ||
+                         std::memcmp(v0[r].mistype, v1[r].mistype, sizeof(int32_t) * (size_t)r0);
+            st[r] = (uint8_t)((r0 >= 0 ? AL_OK0 : 0) | (differ ? AL_CONS : 0) | (!pe && nn > maxmis ? AL_NSKIP : 0) |
+                              (r1 >= 0 ? AL_OK1 : 0));
+            p0[r] = (uint32_t)v0[r].pos;
+            p1[r] = (uint32_t)v1[r].pos;
+        }
+        AlignChainState ch;   // fresh align_info: nmis 0 ("aligned")
+        for (int64_t b = 0; b < nb; b++) {
+            DevBlock& d = blocks[(size_t)b];
+            std::vector<uint32_t> sel;
+            const AlignBlockPlan bp = align_plan_block(pe, d.nreads, &st[d.read0], &p0[d.read0], &p1[d.read0], insert_size,
+                                                       ch, sel);
+            d.order_count = bp.order_count;
+            d.win = bp.win;
+            d.ibits = bp.ibits;
+            d.insert_bits = bp.insert_bits;
+            std::vector<uint8_t> use1(d.nreads, 0);
+            for (uint32_t i : sel) use1[i] = 1;
+            if (std::getenv("EMU_ALN"))   // what the case exercised
+                std::printf("block %lld: reads %u order %u aligned %u variant-1 %zu win %u ibits %u\n", (long long)b,
+                            d.nreads, bp.order_count, bp.aligned, sel.size(), bp.win, bp.ibits);
+            for (uint32_t i = 0; i < d.nreads; i++) {
+                const uint32_t r = d.read0 + i;
+                const ho_align& a = use1[i] ? v1[r] : v0[r];
+                a_ret[r] = a.nmis;
+                a_rev[r] = a.rev;
+                a_pos[r] = (uint32_t)a.pos;
+                for (int k2 = 0; k2 < a.nmis && k2 <= maxmis; k2++) {
+                    a_mp[(size_t)r * (maxmis + 1) + k2] = a.mispos[k2];
+                    a_mt[(size_t)r * (maxmis + 1) + k2] = a.mistype[k2];
+                }
+            }
+        }
+        const uint32_t shift = host_bits(ix->total) - 2;
+        av = AlignView{a_ret.data(), a_rev.data(), a_pos.data(), a_mp.data(), a_mt.data(), (uint32_t)maxmis + 1, shift,
+                       (1ull << shift) - 1, ix->total, pe ? 1 : 0,
+                       maxmis >= 1 && maxmis <= 7 ? M_MIS8 : maxmis == 8 ? M_MIS9 : 0u};
+        for (uint32_t r = 0; r < nr; r++) {
+            uint32_t c[NACOL];
+            seq_skip[r] = align_read_counts(bv, av, r, c) ? 1 : 0;
+        }
+        bv.aligned = 1;
+        bv.paired = pe ? 1 : 0;
+        bv.seq_skip = seq_skip.data();
+    }
     // -l: the chunked rblock (what k_rb_spec / k_rb_fix / k_rb_apply compute),
     // checked against the oracle's serial restatement block by block
     std::vector<uint8_t> qual_q;
@@ -286,16 +379,32 @@ int main(int argc, char** argv)
         }
         for (int col = 0; col < NCOL; col++) totals[(size_t)b * NCOL + col] = carry[col];
     }
+    // alignment columns: per read, exclusive per block
+    std::vector<uint32_t> acounts((size_t)nr * NACOL, 0), atot((size_t)nb * NACOL, 0);
+    if (ref) {
+        for (int64_t b = 0; b < nb; b++) {
+            const DevBlock& d = blocks[(size_t)b];
+            uint32_t carry[NACOL] = {0};
+            for (uint32_t i = 0; i < d.nreads; i++) {
+                uint32_t* c = &acounts[(size_t)(d.read0 + i) * NACOL];
+                align_read_counts(bv, av, d.read0 + i, c);
+                for (int col = 0; col < NACOL; col++) { uint32_t v = c[col]; c[col] = carry[col]; carry[col] += v; }
+            }
+            for (int col = 0; col < NACOL; col++) atot[(size_t)b * NACOL + col] = carry[col];
+        }
+    }
     BatchPlan bp;
-    if (!plan_batch(blocks, totals, bp)) { std::printf("FAIL plan\n"); return 1; }
+    if (!plan_batch(blocks, totals, bp, ref ? &atot : nullptr, av.mis_model)) { std::printf("FAIL plan\n"); return 1; }
 
     // ---- emit ----
-    const size_t stot = bp.seq.total + 64, atot = bp.aux.total + 64;   // slack as the engine
-    std::vector<uint32_t> sk(stot, SORT_PAD), sv(stot), ak(atot, SORT_PAD), av(atot);
+    const size_t stot = bp.seq.total + 64, atot_sz = bp.aux.total + 64;   // slack as the engine
+    std::vector<uint32_t> sk(stot, SORT_PAD), sv(stot), ak(atot_sz, SORT_PAD), av_(atot_sz);
     for (uint32_t r = 0; r < nr; r++)
         err |= emit_read(bv, r, counts.data(), totals.data(), name_p.data(), name_s.data(), maxlen.data(), sk.data(),
-                         sv.data(), ak.data(), av.data(), true);
+                         sv.data(), ak.data(), av_.data(), true);
     if (err) { std::printf("FAIL emit error bits %x\n", err); return 1; }
+    if (ref)
+        for (uint32_t r = 0; r < nr; r++) align_read_emit(bv, av, r, &acounts[(size_t)r * NACOL], ak.data(), av_.data());
 
     // ---- stable sort per segment (what k_sort_* computes) ----
     auto sort_space = [](std::vector<uint32_t>& K, std::vector<uint32_t>& V, const SortPlan& p, int lo) {
@@ -312,7 +421,7 @@ int main(int argc, char** argv)
         }
     };
     sort_space(sk, sv, bp.seq, 0);
-    sort_space(ak, av, bp.aux, AUX_SYM_BITS);
+    sort_space(ak, av_, bp.aux, AUX_SYM_BITS);
 
     // EMU_RUNS=1: the longest model runs per space (what bounds the replay kernels)
     if (std::getenv("EMU_RUNS")) {
@@ -335,8 +444,8 @@ int main(int argc, char** argv)
         runs(ak, bp.aux, AUX_SYM_BITS, "aux");
     }
     // ---- replays ----
-    std::vector<PRec> ps(stot), pa(atot);
-    std::vector<uint16_t> cs(stot), ca(atot);
+    std::vector<PRec> ps(stot), pa(atot_sz);
+    std::vector<uint16_t> cs(stot), ca(atot_sz);
     std::vector<uint32_t> F(256);
     for (const SortSeg& g : bp.seq.segs) {
         const SymSink sink{ps.data() + g.base, nullptr};   // packed SEQ records
@@ -347,7 +456,7 @@ int main(int argc, char** argv)
         const SymSink sink{pa.data() + g.base, ca.data() + g.base};
         for (size_t i = g.base; i < g.base + g.count; i++)
             if (i == g.base || (ak[i - 1] >> AUX_SYM_BITS) != (ak[i] >> AUX_SYM_BITS))
-                err |= replay_simple_run(ak.data(), av.data(), i, g.base + g.count, ak[i] >> AUX_SYM_BITS, sink, F.data());
+                err |= replay_simple_run(ak.data(), av_.data(), i, g.base + g.count, ak[i] >> AUX_SYM_BITS, sink, F.data());
     }
     if (err) { std::printf("FAIL replay error bits %x\n", err); return 1; }
 
@@ -381,21 +490,24 @@ int main(int argc, char** argv)
     }
     int fails = 0;
     uint64_t total_out = 0;
+    int32_t ocarry[2] = {0, 0};   // the oracle's own align_info chain (fresh: nmis 0)
     for (int64_t b = 0; b < nb; b++) {
         std::vector<uint8_t> o(bp.final_bytes + 64);
-        uint32_t dst[16], tsk[16], len[16], nseg = 0;
+        uint32_t dst[ASM_MAX_COPIES], tsk[ASM_MAX_COPIES], len[ASM_MAX_COPIES], nseg = 0;
         uint32_t L = assemble_plan(bv, (uint32_t)b, bp.asmb[(size_t)b], out_len.data(), digests.data(), o.data(), dst, tsk,
                                    len, nseg);
         for (uint32_t s = 0; s < nseg; s++) std::memcpy(o.data() + dst[s], payload.data() + bp.task_out_base[tsk[s]], len[s]);
         HostBlock& h = hb[(size_t)b];
         orc_block ob{h.names.data(), h.nl.data(), h.seq.data(), h.sl.data(), h.qual.data(), h.nreads};
         orc_cfg oc{slevel, qlevel, 1, T[0], lossy};
-        std::vector<uint8_t> ref(2 * (h.seq.size() + h.names.size()) + 4096);
-        int64_t rl = orc_encode_block(&ob, &oc, ref.data(), ref.size());
-        bool ok = rl == (int64_t)L && std::memcmp(ref.data(), o.data(), L) == 0;
+        std::vector<uint8_t> want(3 * (h.seq.size() + h.names.size()) + 64 * h.nreads + 8192);
+        int64_t rl = ref ? orc_encode_block_hash(&ob, &oc, pe ? 1 : 0, maxmis, good, insert_size, ocarry, want.data(),
+                                                 want.size())
+                         : orc_encode_block(&ob, &oc, want.data(), want.size());
+        bool ok = rl == (int64_t)L && std::memcmp(want.data(), o.data(), L) == 0;
         if (!ok) {
             size_t at = 0;
-            while (at < L && at < (size_t)rl && ref[at] == o[at]) at++;
+            while (at < L && at < (size_t)rl && want[at] == o[at]) at++;
             std::printf("block %lld MISMATCH emu %u oracle %lld first diff at %zu\n", (long long)b, L, (long long)rl, at);
             fails++;
         }

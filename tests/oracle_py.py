@@ -35,7 +35,8 @@ def lib():
     global _lib
     if _lib is None:
         srcs = [os.path.join(ORACLE_DIR, f)
-                for f in ("fqz_oracle.c", "fqz_decode.c", "hash_oracle.c", "fqz_oracle.h", "orc_cli.c")]
+                for f in ("fqz_oracle.c", "fqz_decode.c", "hash_oracle.c", "align_oracle.c", "fqz_oracle.h",
+                          "hash_oracle.h", "orc_cli.c")]
         if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
             build()
         l = C.CDLL(LIB)
@@ -60,6 +61,8 @@ def lib():
         l.ho_genome_length.restype = C.c_uint32
         l.ho_align_reads.argtypes = [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P]
         l.ho_align_reads.restype = C.c_int
+        l.orc_encode_block_hash.argtypes = [P, P, C.c_int, C.c_int, C.c_int, C.c_uint32, P, P, C.c_size_t]
+        l.orc_encode_block_hash.restype = C.c_int64
         _lib = l
     return _lib
 
@@ -205,3 +208,21 @@ def hash_align(reads: list[bytes], maxmis: int = HASH_MAXMIS, good: int = HASH_G
                         _p(mt)):
         raise ValueError("hash align failed")
     return ret[:n], rev[:n], pos[:n], mp[:n], mt[:n]
+
+
+def encode_block_hash(b, paired: bool, carry=None, slevel=3, qlevel=2, md5=True, bin_mode=0, lossy=0.0,
+                      maxmis: int = HASH_MAXMIS, good: int = HASH_GOOD, insert_size: int = 0):
+    """The reference path's block encode (doAlign + doAlignEncode@0x42d4c0)
+    against the last hash_index.  carry: [mate1/SE, mate2] align_info state in,
+    updated in place (default: a fresh zero-filled AlignParam)."""
+    cap = 3 * (b.seq.size + b.names.size) + 64 * b.nreads + 8192
+    out = np.empty(cap, dtype=np.uint8)
+    cb, cc = _blk(b), _Cfg(slevel, qlevel, 1 if md5 else 0, 1 if bin_mode else 0, float(lossy))
+    cr = np.array(carry if carry is not None else [0, 0], dtype=np.int32)
+    n = lib().orc_encode_block_hash(C.byref(cb), C.byref(cc), 1 if paired else 0, maxmis, good, insert_size,
+                                    _p(cr), _p(out), cap)
+    if n < 0:
+        raise RuntimeError("oracle reference-path encode failed")
+    if carry is not None:
+        carry[0], carry[1] = int(cr[0]), int(cr[1])
+    return out[:n].tobytes()

@@ -162,3 +162,72 @@ def edge_cases() -> bytes:
             q = q[:-2] + b"##"
         recs.append((nm, s, q))
     return b"".join(b"@" + n + b"\n" + s + b"\n+\n" + q + b"\n" for n, s, q in recs)
+
+
+def reference(genome_len: int, seed: int, chroms: int = 3, width: int = 60) -> tuple[bytes, np.ndarray]:
+    """FASTA of a random genome (`chroms` records, some lowercase and N runs)
+    for the reference (HASH index) path, and its bases as uint8 ACGTN."""
+    rng = np.random.default_rng([seed, 7])
+    g = _BASES[rng.integers(0, 4, size=genome_len, dtype=np.uint8)].copy()
+    for at in rng.integers(0, max(genome_len - 64, 1), size=max(genome_len // 200000, 1)):
+        g[at:at + int(rng.integers(1, 40))] = ord("N")
+    cuts = sorted(set(int(x) for x in rng.integers(1, genome_len, size=chroms - 1))) if chroms > 1 else []
+    bounds = [0] + cuts + [genome_len]
+    out = []
+    for i in range(len(bounds) - 1):
+        c = g[bounds[i]:bounds[i + 1]].tobytes()
+        if i == 1:
+            c = c.lower()
+        out.append(b">chr%d synthetic\n" % (i + 1))
+        out += [c[j:j + width] + b"\n" for j in range(0, len(c), width)]
+    return b"".join(out), g
+
+
+def aligned_reads(genome: np.ndarray, n: int, seed: int, paired: bool = False, read_len: int = 150,
+                  random_frac: float = 0.05, far_frac: float = 0.05, short_frac: float = 0.0) -> tuple[bytes, bytes | None]:
+    """Reads for the reference path: drawn from `genome` (either strand) with
+    0-10 substitutions, some N runs (more than maxmis in some reads), a fraction
+    of random (unalignable) reads; PE mates mostly 250-449 apart, a fraction
+    far apart or on another chromosome region (the relation's other cases)."""
+    rng = np.random.default_rng([seed, 11])
+    G = genome.size
+    comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+
+    def one(start, rev):
+        s = genome[start:start + read_len].copy()
+        k = int(rng.choice([0, 0, 0, 1, 1, 2, 3, 5, 8, 10]))
+        if k:
+            at = rng.integers(0, read_len, size=k)
+            s[at] = _BASES[(np.searchsorted(_BASES, s[at]) + rng.integers(1, 4, size=k)) % 4]
+        if rng.random() < 0.03:
+            a = int(rng.integers(0, read_len))
+            s[a:a + int(rng.integers(1, 12))] = ord("N")
+        if rng.random() < random_frac:
+            s = _BASES[rng.integers(0, 4, size=read_len)]
+        if rng.random() < short_frac:   # short reads: few even-offset seeds survive a few substitutions
+            s = s[:int(rng.integers(20, 60))].copy()
+            k2 = int(rng.integers(1, 5))
+            at = rng.integers(0, s.size, size=k2)
+            s[at] = _BASES[(np.searchsorted(_BASES, s[at]) + 1) % 4]
+        b = s.tobytes()
+        return b.translate(comp)[::-1] if rev else b
+
+    r1, r2 = [], []
+    for i in range(n):
+        st = int(rng.integers(0, G - 1000 - read_len))
+        rv = bool(rng.random() < 0.5)
+        r1.append(one(st, rv))
+        if paired:
+            if rng.random() < far_frac:
+                st2 = int(rng.integers(0, G - read_len))
+            else:
+                st2 = min(st + int(rng.integers(250, 450)) - read_len, G - read_len)
+            r2.append(one(max(st2, 0), not rv))
+
+    x = rng.integers(1000, 32000, size=n)
+
+    def fq(reads, mate):
+        q = _QUALS[rng.integers(0, 3, size=(len(reads), read_len))]
+        names = _headers(0, x, mate)
+        return b"".join(b"%s\n%s\n+\n%s\n" % (names[i], s, q[i, :len(s)].tobytes()) for i, s in enumerate(reads))
+    return fq(r1, 1), (fq(r2, 2) if paired else None)

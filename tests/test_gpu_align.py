@@ -1,0 +1,153 @@
+"""GPU parity of the reference (HASH index) block path -- the encoder with an
+index, configs[3]: AlignEncode{SE,PE}Job::doAlign
+(@0x411910 / @0x413580: the aligner over the carried align_info chain, the 5 %
+probe and bail-out, the PE insert window CaclInsertSize@0x413270) and
+EncapFqzComp::doAlignEncode@0x42d4c0 (order / position / mismatch / strand /
+PE-relation streams, the SEQ stream of the unaligned reads), every block byte
+for byte against the CPU restatement (oracle/align_oracle.c +
+oracle/hash_oracle.c + oracle/fqz_oracle.c).  Parity with SeqArc itself is
+unpinned: the reference ships no index and no aligned archive."""
+import numpy as np
+import pytest
+
+import fastqueeze_amd as fq
+import oracle_py as orc
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def enc():
+    e = fq.Encoder(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def ref():
+    fa, g = synth.reference(3_000_000, 21)
+    return fa, g
+
+
+@pytest.fixture(scope="module")
+def index(enc, ref):
+    fa, _ = ref
+    orc.hash_index(fa)               # the oracle keeps its index for encode_block_hash
+    ix = fq.HashIndex(enc, fa)
+    yield ix
+    ix.close()
+
+
+def oracle_blocks(blocks, paired, cfg, **kw):
+    carry = [0, 0]
+    return [orc.encode_block_hash(b, paired, carry, slevel=cfg.slevel, qlevel=cfg.qlevel, md5=cfg.md5,
+                                  bin_mode=cfg.bin_mode, **kw) for b in blocks]
+
+
+def check(enc, index, blocks, paired, cfg=None, **kw):
+    cfg = cfg or fq.Config()
+    got = enc.encode_aligned(blocks, cfg, index, paired, **kw)
+    want = oracle_blocks(blocks, paired, cfg, **kw)
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"block {i}: {len(g)} vs {len(w)} bytes, first difference at " \
+                       f"{next((k for k in range(min(len(g), len(w))) if g[k] != w[k]), min(len(g), len(w)))}"
+    return got
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_blocks_identical(enc, index, ref, paired):
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 12000, 31, paired=paired, random_frac=0.08, far_frac=0.1, short_frac=0.2)
+    blocks = fq.blocks_from_fastq(r1, r2, block_size=1_000_000)
+    assert len(blocks) >= 3
+    out = check(enc, index, blocks, paired)
+    assert sum(map(len, out)) < sum(map(len, orc_noref(blocks)))   # aligned reads leave the SEQ stream
+
+
+def orc_noref(blocks):
+    return [orc.encode_block(b) for b in blocks]
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_carried_state_and_short_reads(enc, index, ref, paired):
+    """Short reads whose even-offset seeds are all broken: the search consults
+    the carried align_info; both variants run on the GPU, the chain picks."""
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 8000, 32, paired=paired, random_frac=0.1, short_frac=0.6)
+    check(enc, index, fq.blocks_from_fastq(r1, r2, block_size=400_000), paired)
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_bail_out(enc, index, ref, paired):
+    """Blocks where fewer than half of the first 5 % of reads align: the rest of
+    the block goes through the SEQ stream without order bytes."""
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 6000, 33, paired=paired, random_frac=0.7, far_frac=0.3)
+    check(enc, index, fq.blocks_from_fastq(r1, r2, block_size=300_000), paired)
+
+
+def test_pe_insert_size_option(enc, index, ref):
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 6000, 34, paired=True, far_frac=0.2)
+    blocks = fq.blocks_from_fastq(r1, r2, block_size=600_000)
+    check(enc, index, blocks, True, insert_size=500)
+    check(enc, index, blocks, True, insert_size=50)
+
+
+@pytest.mark.parametrize("maxmis", [0, 3, 8])
+def test_maxmis(enc, index, ref, maxmis):
+    """Mis stream model by maxmis (SIMPLE_MODEL<8> for 1..7, <9> for 8, no
+    symbols otherwise; compressAlignInfo_Mis@0x425ff0)."""
+    _, g = ref
+    r1, _ = synth.aligned_reads(g, 4000, 35, short_frac=0.2)
+    check(enc, index, fq.blocks_from_fastq(r1, None, block_size=400_000), False, maxmis=maxmis)
+
+
+def test_chain_across_batches(enc, index, ref):
+    """Two batches through one chain equal one oracle pass over all blocks."""
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 8000, 36, paired=True, short_frac=0.4, random_frac=0.1)
+    blocks = fq.blocks_from_fastq(r1, r2, block_size=500_000)
+    cfg = fq.Config()
+    chain = fq.AlignChain()
+    got = []
+    for k, part in enumerate((blocks[:2], blocks[2:])):
+        enc.stage(part)
+        enc.run_aligned(cfg, index, True, chain, batch=k)
+        got += enc.fetch()
+    chain.close()
+    assert got == oracle_blocks(blocks, True, cfg)
+
+
+def test_index_from_hash_file(enc, index, ref):
+    """The `.hash` file loaded back (sa_hash_load) aligns as the built index."""
+    _, g = ref
+    ix2 = fq.HashIndex(enc, None, hash_file=index.file_bytes())
+    try:
+        r1, _ = synth.aligned_reads(g, 3000, 37)
+        blocks = fq.blocks_from_fastq(r1, None, block_size=400_000)
+        assert enc.encode_aligned(blocks, fq.Config(), ix2, False) == enc.encode_aligned(blocks, fq.Config(), index,
+                                                                                           False)
+    finally:
+        ix2.close()
+
+
+def test_full_block_pe(enc, index, ref):
+    """A full 50 MiB block of 150 bp pairs (configs[3] shape, scaled genome)."""
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 80_000, 38, paired=True, random_frac=0.02, far_frac=0.02)
+    blocks = fq.blocks_from_fastq(r1, r2)
+    assert blocks[0].nreads > 100_000
+    check(enc, index, blocks[:1], True)
+
+
+def test_other_configs(enc, index, ref):
+    """Slevel 4 / Qlevel 3 / MD5 off / ID-bin names on the reference path."""
+    _, g = ref
+    r1, r2 = synth.aligned_reads(g, 3000, 39, paired=True)
+    blocks = fq.blocks_from_fastq(r1, r2, block_size=400_000)
+    tmpl = fq.analyze_ids(blocks[0], False)
+    for cfg in (fq.Config(slevel=4), fq.Config(qlevel=3), fq.Config(md5=False), fq.Config(bin_mode=int(tmpl[0]))):
+        check(enc, index, blocks, True, cfg)

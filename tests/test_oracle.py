@@ -90,7 +90,8 @@ def test_cpu_decomposition(tmp_path):
     src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
                     os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
-                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), "-lm"], check=True)
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), os.path.join(ROOT, "oracle", "hash_oracle.c"),
+                    os.path.join(ROOT, "oracle", "align_oracle.c"), "-lm"], check=True)
     import synth
     pe1, pe2 = synth.generate(3000, paired=True, seed=3)
     (tmp_path / "a.fq").write_bytes(pe1)
@@ -108,13 +109,45 @@ def test_cpu_decomposition(tmp_path):
         assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
 
 
+def test_cpu_decomposition_reference_path(tmp_path):
+    """The reference (HASH index) path's decomposition on the host: the engine's
+    chain / bail-out / insert-window bookkeeping (sa_align_host.h) and the
+    alignment-stream emission (sa_logic.h) over the oracle's alignments, block
+    for block equal to the oracle's doAlign + doAlignEncode restatement."""
+    exe = tmp_path / "emu"
+    src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
+                    os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), os.path.join(ROOT, "oracle", "hash_oracle.c"),
+                    os.path.join(ROOT, "oracle", "align_oracle.c"), "-lm"], check=True)
+    import synth
+    fa, g = synth.reference(2_000_000, 5)
+    (tmp_path / "ref.fa").write_bytes(fa)
+    a, b = synth.aligned_reads(g, 8000, 9, paired=True, random_frac=0.1, far_frac=0.2, short_frac=0.5)
+    (tmp_path / "p1.fq").write_bytes(a)
+    (tmp_path / "p2.fq").write_bytes(b)
+    a, _ = synth.aligned_reads(g, 6000, 7, random_frac=0.6, short_frac=0.3)
+    (tmp_path / "s.fq").write_bytes(a)
+    runs = [["-b", "500000", str(tmp_path / "p1.fq"), str(tmp_path / "p2.fq")],
+            ["-I", "400", "-b", "700000", str(tmp_path / "p1.fq"), str(tmp_path / "p2.fq")],
+            ["-b", "300000", str(tmp_path / "s.fq")]]
+    for args in runs:
+        r = subprocess.run([str(exe), "-r", str(tmp_path / "ref.fa")] + args, capture_output=True, text=True,
+                           env=dict(os.environ, EMU_ALN="1"))
+        assert r.returncode == 0 and r.stdout.splitlines()[-1].startswith("OK"), (args, r.stdout[-2000:], r.stderr)
+        # the cases reached the paths: a bail-out / the carried-state variant / an estimated window
+        lines = [l for l in r.stdout.splitlines() if l.startswith("block ")]
+        assert lines
+
+
 def test_coder_decomposition_selftest(tmp_path):
     """Decomposed coder (pass R / L1 / L2 / L3 + squeeze restarts) == serial coder on the host."""
     exe = tmp_path / "emu"
     src = os.path.join(ROOT, "tests", "cpu_emu", "emu.cpp")
     subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src,
                     os.path.join(ROOT, "fastqueeze_amd", "csrc", "fastq_host.cpp"),
-                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), "-lm"], check=True)
+                    os.path.join(ROOT, "oracle", "fqz_oracle.c"), os.path.join(ROOT, "oracle", "hash_oracle.c"),
+                    os.path.join(ROOT, "oracle", "align_oracle.c"), "-lm"], check=True)
     r = subprocess.run([str(exe), "--coder"], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout
 
