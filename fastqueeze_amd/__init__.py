@@ -49,7 +49,8 @@ class _SaArcBlock(C.Structure):
 
 class _SaArcInfo(C.Structure):
     _fields_ = [("file1", C.c_char_p), ("file2", C.c_char_p), ("paired", C.c_int32), ("gz1", C.c_int32),
-                ("bare_plus", C.c_int32), ("md5", C.c_int32), ("lossy", C.c_int32), ("id_template", C.c_void_p)]
+                ("bare_plus", C.c_int32), ("md5", C.c_int32), ("lossy", C.c_int32), ("id_template", C.c_void_p),
+                ("ref_md5", C.c_void_p), ("insert_size", C.c_uint32)]
 
 
 class _SaDecoded(C.Structure):
@@ -72,6 +73,11 @@ class _SaAlignCfg(C.Structure):
                 ("insert_size", C.c_uint32)]
 
 
+class _SaRef(C.Structure):
+    _fields_ = [("genome", C.c_void_p), ("bases", C.c_uint64), ("paired", C.c_int32), ("maxmis", C.c_int32),
+                ("insert_size", C.c_uint32)]
+
+
 class _SaOut(C.Structure):
     _fields_ = [("data", C.c_void_p), ("cap", C.c_uint64), ("size", C.c_uint64)]
 
@@ -84,6 +90,8 @@ def load_library(path: str | None = None):
     if path is None:
         path = _build.LIB
         if _build.needs_build():
+            if os.environ.get("SA_NO_BUILD"):   # (GPU runs: the library travels prebuilt)
+                raise SeqArcError("libseqarc_amd.so is older than its sources and SA_NO_BUILD is set")
             _build.build()
     if not os.path.exists(path):
         raise SeqArcError(f"libseqarc_amd.so not found at {path}")
@@ -114,6 +122,7 @@ def load_library(path: str | None = None):
         "sa_run_input_aligned": ([P, P, P, P, P, U64], I32), "sa_run_aligned": ([P, P, P, P, U64], I32),
         "sa_encode_blocks_aligned": ([P, P, I32, P, P, P, P], I32),
         "sa_hash_load": ([P, P, U64], P), "sa_hash_packed": ([P, P, P, U64], I32),
+        "sa_decode_block_ref": ([P, U64, P, P, I32, P, P], I64),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -458,7 +467,7 @@ def bare_plus(text) -> int:
 
 def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str | None = None,
                 template: np.ndarray | None = None, cfg: Config | None = None, gz1: bool = False,
-                plus_bare: int = 1) -> bytes:
+                plus_bare: int = 1, ref_md5: bytes | None = None, insert_size: int = 0) -> bytes:
     """The .arc file around encoded blocks (header, blocks in input order, trailer):
     SeqArcFile::writeFileInfo@0x4171b0 / writeParam@0x416450 / writeBlockLenArry (arc_file.cpp)."""
     lib = load_library()
@@ -468,8 +477,10 @@ def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str
         lng = 1 if b.nreads and int(b.seq_lens.max()) > 0xffff else 0
         recs[i] = _SaArcBlock(len(e), lng, b.text1 or b.text_bytes, b.text2)
     tmpl = np.zeros(512, np.uint8) if template is None else np.ascontiguousarray(template, dtype=np.uint8)
+    rm = None if ref_md5 is None else np.frombuffer(ref_md5, np.uint8)
     info = _SaArcInfo(file1.encode(), (file2 or "").encode(), 1 if file2 else 0, 1 if gz1 else 0, int(plus_bare),
-                      1 if cfg.md5 else 0, 1 if cfg.lossy > 0 else 0, _ptr(tmpl))
+                      1 if cfg.md5 else 0, 1 if cfg.lossy > 0 else 0, _ptr(tmpl), None if rm is None else _ptr(rm),
+                      int(insert_size))
     cap = 4096 + 40 * len(encaps)
     tr = np.empty(cap, np.uint8)
     n = lib.sa_arc_trailer(C.byref(info), recs, len(encaps), _ptr(tr), cap)
@@ -480,11 +491,19 @@ def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str
     return hdr.tobytes() + b"".join(encaps) + tr[:n].tobytes()
 
 
+def hash_file_genome(hash_file: bytes) -> tuple[np.ndarray, int]:
+    """(packed genome words, bases) of a `.hash` file (HashRefIndex32 layout:
+    K, bases, words, positions, then the words)."""
+    K, bases, nwords, npos = np.frombuffer(hash_file[:16], np.uint32)
+    return np.frombuffer(hash_file, np.uint32, count=int(nwords), offset=16).copy(), int(bases)
+
+
 def decode_block(data: bytes, text_bytes: int, cfg: Config | None = None, template: np.ndarray | None = None,
-                 long_reads: bool = False) -> tuple[Block, bool]:
+                 long_reads: bool = False, ref: tuple | None = None) -> tuple[Block, bool]:
     """Host decode of one encoded block (sa_decode_block; doFqzDecode@0x42c680):
     (the block's reads, stored MD5s match).  text_bytes bounds the arrays
-    (the block's FASTQ size, from the archive's block table)."""
+    (the block's FASTQ size, from the archive's block table).  ref = (genome
+    words, bases, paired, maxmis[, insert_size]): a block of the reference path."""
     lib = load_library()
     cfg = cfg or Config()
     cap = int(text_bytes) + 64
@@ -495,7 +514,13 @@ def decode_block(data: bytes, text_bytes: int, cfg: Config | None = None, templa
     src = np.frombuffer(data, np.uint8)
     tmpl = np.zeros(512, np.uint8) if template is None else np.ascontiguousarray(template, dtype=np.uint8)
     c = cfg._c()
-    n = lib.sa_decode_block(_ptr(src), src.size, C.byref(c), _ptr(tmpl), 1 if long_reads else 0, C.byref(d))
+    if ref is None:
+        n = lib.sa_decode_block(_ptr(src), src.size, C.byref(c), _ptr(tmpl), 1 if long_reads else 0, C.byref(d))
+    else:
+        words = np.ascontiguousarray(ref[0], dtype=np.uint32)
+        r = _SaRef(_ptr(words), int(ref[1]), 1 if ref[2] else 0, int(ref[3]), int(ref[4]) if len(ref) > 4 else 0)
+        n = lib.sa_decode_block_ref(_ptr(src), src.size, C.byref(c), _ptr(tmpl), 1 if long_reads else 0, C.byref(r),
+                                    C.byref(d))
     if n < 0:
         raise SeqArcError("sa_decode_block: malformed block")
     n = int(n)

@@ -309,10 +309,48 @@ bool bin_names(const uint8_t* first, int flen, const uint8_t T[512], const int32
 
 const char kIupac[] = "NMRYKSWHBVD";   // base codes 4..14 (seq_val_table@0x44b800)
 
-}  // namespace
+// one SIMPLE_MODEL<nsym> stream of `n` symbols (compressOrder@0x424b70 and
+// the compressAlignInfo_* family): setID(id), size4, the coded bytes
+bool sm_stream(Cursor& c, int id, int nsym, uint32_t n, std::vector<uint8_t>& out)
+{
+    if (!c.id(id)) return false;
+    const uint32_t sz = c.size4();
+    if (c.bad) return false;
+    out.assign(n, 0);
+    if (nsym > 0) {
+        SModel m;
+        m.reset(nsym);
+        RangeIn rc(c.p, c.p + sz);
+        for (uint32_t i = 0; i < n; i++) out[i] = (uint8_t)m.decode(rc);
+        if (rc.bad) return false;
+    }
+    c.p += sz;
+    return true;
+}
 
-extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_cfg* cfg, const uint8_t tmpl[512],
-                                   int32_t long_reads, sa_decoded* o)
+bool count_encap(Cursor& c, int id, uint32_t& v)   // compressCount@0x422a00
+{
+    if (!c.id(id) || c.end - c.p < 5 || c.p[0] != 0x84) return false;
+    v = le32(c.p + 1);
+    c.p += 5;
+    return true;
+}
+
+// the read type the encoder wrote for a substitution (@0x44a0c0, [ref * 4 + read])
+const uint8_t kMisType[16] = {3, 1, 0, 2, 1, 3, 0, 2, 1, 0, 3, 2, 2, 1, 0, 3};
+
+// mapvar2base@0x40db20: the read base of mismatch type t over reference base b
+// (type 3: an N / IUPAC base, restored from the side streams)
+uint32_t var2base(uint32_t b, uint32_t t)
+{
+    if (t >= 3) return 4;
+    for (uint32_t x = 0; x < 4; x++)
+        if (x != b && kMisType[b * 4 + x] == t) return x;
+    return 4;
+}
+
+int64_t decode_block(const uint8_t* in, uint64_t in_len, const sa_cfg* cfg, const uint8_t tmpl[512],
+                     int32_t long_reads, const sa_ref* ref, sa_decoded* o)
 {
     if (!in || !cfg || !o) return -1;
     Cursor c{in, in + in_len};
@@ -351,6 +389,12 @@ extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_
     uint64_t total = 0;
     for (uint32_t r = 0; r < n; r++) { o->seq_lens[r] = (int32_t)len[r]; total += len[r]; }
     if (total > o->seq_cap) return -1;
+    // reference path: order count and bytes (doAlignEncode@0x42d4c0)
+    uint32_t norder = 0;
+    std::vector<uint8_t> order;
+    if (ref) {
+        if (!count_encap(c, 0x1b, norder) || norder > n || !sm_stream(c, 8, 5, norder, order)) return -1;
+    }
 
     uint64_t name_total = 0;
     {   // IDs: compressID@0x4247c0
@@ -413,6 +457,24 @@ extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_
         }
         if (rc.bad) return -1;
         c.p += sz;
+    }
+
+    // reference path: the alignment streams (counts, PE relation, position bits,
+    // mismatch counts, strands, mismatch offset bits and types)
+    uint32_t nalign = 0, npos = 0, ncigl = 0, ncigv = 0, ibits = 0, nperel = 0;
+    std::vector<uint8_t> perel, posb, mis, rev, cigl, cigv;
+    if (ref) {
+        if (!count_encap(c, 0x11, nalign) || !count_encap(c, 0x12, npos) || !count_encap(c, 0x13, ncigl) ||
+            !count_encap(c, 0x14, ncigv))
+            return -1;
+        if (ref->paired && (!count_encap(c, 0x15, ibits) || !count_encap(c, 0x16, nperel) ||
+                            !sm_stream(c, 9, 4, nperel, perel)))
+            return -1;
+        const int mis_nsym = ref->maxmis >= 1 && ref->maxmis <= 7 ? 8 : ref->maxmis == 8 ? 9 : 0;
+        if (!sm_stream(c, 0xb, 2, npos, posb) || !sm_stream(c, 0xf, mis_nsym, nalign, mis) ||
+            !sm_stream(c, 0xa, 2, nalign, rev) || !sm_stream(c, 0xc, 2, ncigl, cigl) ||
+            !sm_stream(c, 0xd, 4, ncigv, cigv))
+            return -1;
     }
 
     // N / IUPAC side streams (DegeInfoProcess@0x433a10): 23 tip, 14 chars,
@@ -509,7 +571,66 @@ extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_
         // with -l a misplaced N shifts the base stream (see above): the rest of
         // the block decodes as 'N' and the sequence MD5 reports it
         const bool lenient = cfg->lossy > 0.0;
+        // reference path: decompressSeq@0x42e390 rebuilds the reads with an order
+        // byte from the genome (getRealPos@0x42de30: the position from the order
+        // byte and low bits, or for a PE mate 2 after an aligned mate 1 from the
+        // relation; AlignInfoToSeq@0x42e020: the segment, its mismatches, the
+        // strand), the N / IUPAC bases then from the side streams
+        size_t ip = 0, ia = 0, il = 0, iv = 0, ir = 0;
+        if (ref && !ibits && ref->insert_size)   // -I: the encoder used bits(I), the block says 0
+            for (uint32_t v = ref->insert_size; v; v >>= 1) ibits++;
+        uint64_t last_pos = 0;
+        const uint32_t shift = ref && ref->bases ? (uint32_t)(64 - __builtin_clzll(ref->bases)) - 2 : 0;
+        auto take_bits = [&](uint32_t nb, const std::vector<uint8_t>& v, size_t& at, bool& ok) {
+            uint64_t x = 0;
+            for (uint32_t k = 0; k < nb; k++) {
+                if (at >= v.size()) { ok = false; return x; }
+                x |= (uint64_t)v[at++] << k;
+            }
+            return x;
+        };
+        auto nbits = [](uint64_t v) { uint32_t k = 0; while (v) { k++; v >>= 1; } return k; };
         for (uint32_t r = 0; r < n && (!rc.bad || lenient); r++) {
+            if (ref && r < norder && order[r]) {
+                bool ok = true;
+                uint64_t pos;
+                if (ref->paired && (r & 1) && order[r - 1]) {
+                    const uint8_t rl = ir < perel.size() ? perel[ir++] : 0xff;
+                    if (rl == 1) pos = last_pos + take_bits(ibits, posb, ip, ok);
+                    else if (rl == 0) pos = last_pos - take_bits(ibits, posb, ip, ok);
+                    else if (rl == 2) pos = take_bits(nbits(last_pos), posb, ip, ok);
+                    else if (rl == 3) pos = last_pos + take_bits(nbits(ref->bases - last_pos), posb, ip, ok);
+                    else return -1;
+                } else {
+                    pos = ((uint64_t)(order[r] - 1) << shift) + take_bits(shift, posb, ip, ok);
+                }
+                last_pos = pos;
+                if (ia >= mis.size() || ia >= rev.size()) return -1;
+                const uint32_t nm = mis[ia], rv = rev[ia];
+                ia++;
+                const uint32_t L = len[r];
+                if (!ok || pos == 0 || pos - 1 + L > ref->bases) return -1;
+                std::vector<uint8_t> seg(L);
+                for (uint32_t i = 0; i < L; i++) {   // doGetSeq@0x40ff90: 2-bit codes (N read as A)
+                    const uint64_t q = pos - 1 + i;
+                    seg[i] = (uint8_t)((ref->genome[q >> 4] >> (30 - 2 * (q & 15))) & 3u);
+                }
+                uint32_t prev = 0;
+                for (uint32_t k = 0; k < nm; k++) {
+                    const uint32_t at2 = prev + (uint32_t)take_bits(nbits(L - prev), cigl, il, ok);
+                    if (!ok || at2 >= L || iv >= cigv.size()) return -1;
+                    seg[at2] = (uint8_t)var2base(seg[at2], cigv[iv++]);
+                    prev = at2;
+                }
+                for (uint32_t i = 0; i < L; i++) {   // getch@0x40dc50
+                    uint32_t b = seg[rv ? L - 1 - i : i];
+                    if (b < 4 && rv) b = 3 - b;
+                    S[i] = isn[at + i] ? isn[at + i] : (uint8_t)(b < 4 ? "ACGT"[b] : 'N');
+                }
+                S += L;
+                at += L;
+                continue;
+            }
             uint32_t ctx = 0x7616c7u & mask;
             for (uint32_t i = 0; i < len[r]; i++) {
                 if (isn[at + i]) { S[i] = isn[at + i]; continue; }
@@ -549,4 +670,21 @@ extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_
         if (memcmp(dg, dg_s, 16)) o->md5_ok = 0;
     }
     return (int64_t)n;
+}
+
+}  // namespace
+
+extern "C" void sa_md5(const uint8_t* data, uint64_t len, uint8_t digest[16]) { md5(data, (size_t)len, digest); }
+
+extern "C" int64_t sa_decode_block(const uint8_t* in, uint64_t in_len, const sa_cfg* cfg, const uint8_t tmpl[512],
+                                   int32_t long_reads, sa_decoded* o)
+{
+    return decode_block(in, in_len, cfg, tmpl, long_reads, nullptr, o);
+}
+
+extern "C" int64_t sa_decode_block_ref(const uint8_t* in, uint64_t in_len, const sa_cfg* cfg, const uint8_t tmpl[512],
+                                       int32_t long_reads, const sa_ref* ref, sa_decoded* o)
+{
+    if (!ref || !ref->genome || ref->bases < 4) return -1;
+    return decode_block(in, in_len, cfg, tmpl, long_reads, ref, o);
 }

@@ -9,8 +9,9 @@
 //            writeParam@0x416450 (ID 1, size2: fields 1-18) +
 //            writeBlockLenArry{SE,PE}@0x416d60/0x416e90 (ID 7, size4, the raw
 //            32-byte _tagBlockInfoSE / 40-byte _tagBlockInfoPE records)
-// writeMd5 (reference-index MD5, param+0x3 clear), writeModel (usemodel,
-// param+0x8) and writeFileList (-m, param+0xd) are not written on this path.
+// writeMd5@0x416b10 (reference-index MD5, ID 8, when param+0x3 is clear: the
+// reference path) follows the params; writeModel (usemodel, param+0x8) and
+// writeFileList (-m, param+0xd) are not written.
 #include <stdint.h>
 #include <string.h>
 
@@ -122,7 +123,7 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     if (!ph) return -1;
     put_id(1, ph);
     uint8_t* pbeg = o.p;
-    field_bool(o, 1, 1);                        // param+0x3: no reference index
+    field_bool(o, 1, in->ref_md5 ? 0 : 1);      // param+0x3: no reference index
     field_bool(o, 2, in->bare_plus);            // param+0x4: '+' lines carry no ID (getFirstLine@0x431eb0)
     field_bool(o, 3, in->paired ? 0 : 1);       // param+0x5: single-end (set by -1, cleared by -2: parseOptFromCmd@0x40b460)
     field_bool(o, 4, in->gz1);                  // param+0x6: getFileType@0x40d9f0 of input 1
@@ -131,7 +132,7 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     field_bool(o, 7, 0);                        // param+0xc
     field_uint(o, 8, 2, 1);                     // param+0x10 (1)
     field_uint(o, 9, 2, 6);                     // param+0x14 (6)
-    field_uint(o, 10, 2, 0);                    // param+0x28 (-I)
+    field_uint(o, 10, 2, in->insert_size);      // param+0x28 (-I)
     field_uint(o, 11, 4, n);                    // param+0x20: block count
     field_uint(o, 12, 4, 0);                    // param+0x24
     field_str(o, 13, in->file1);                // param+0x430
@@ -150,6 +151,13 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     field_bool(o, 18, 0);                       // param+0xd: file list (-m)
     if (!o.ok) return -1;
     put_size((uint64_t)(o.p - pbeg), 2, ph + 1);
+    if (in->ref_md5) {   // writeMd5@0x416b10: setID(8), 1-byte size 0x10, the 16 bytes
+        uint8_t* d = o.take(1 + 1 + 16);
+        if (!d) return -1;
+        put_id(8, d);
+        put_size(16, 1, d + 1);
+        memcpy(d + 2, in->ref_md5, 16);
+    }
     // ---- writeBlockLenArry: ID 7, size4, raw block records ----
     const uint32_t rec = in->paired ? 40u : 32u;
     uint8_t* bh = o.take(1 + 4);

@@ -1,8 +1,14 @@
 // seqarc_amd -- the SeqArc command line over libseqarc_amd (host C++).
 //
-//   seqarc_amd -c [options] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)     -> OUT.arc
-//   seqarc_amd -d [options] ARCHIVE.arc [PREFIX] [-o PREFIX]
+//   seqarc_amd -i ref.fa                                                   -> ref.fa.hash, ref.fa.md5
+//   seqarc_amd -c [options] [ref.fa] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)  -> OUT.arc
+//   seqarc_amd -d [options] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]
 //
+//   ref.fa     the HASH index path (SeqArcContext::doBuildIndex@0x419db0 /
+//              HashAlignment::buildRefIndex@0x410190 for -i; with -c the blocks
+//              take EncapFqzComp::doAlignEncode@0x42d4c0, aligned on the GPU;
+//              the index is read from ref.fa.hash, or built on the GPU if absent)
+//   -I N       max insert size of PE alignment (param+0x28), --maxmis M (param+0x1b60, 7)
 //   -t N       host threads that parse (-c) or decode (-d) blocks
 //   -l R       R-Block lossy qualities (rblock@0x426c10)      -n  no per-block MD5
 //   -f         overwrite existing outputs ("%s has exist!" otherwise, .rodata +0x877)
@@ -59,8 +65,86 @@ int usage()
             "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
             "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
             "                  [--block-size MiB] [--device D] [--share-device]\n"
-            "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] ARCHIVE.arc [PREFIX] [-o PREFIX]\n");
+            "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
+            "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
+            "       (-c / -d with ref.fa: the reference path; -I N insert size, --maxmis M)\n");
     return 2;
+}
+
+bool slurp(const std::string& path, std::vector<uint8_t>& out)
+{
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n >= 0 && fread(out.data(), 1, out.size(), f) == out.size();
+    fclose(f);
+    return ok;
+}
+
+bool spill(const std::string& path, const uint8_t* p, size_t n)
+{
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const bool ok = fwrite(p, 1, n, f) == n;
+    return fclose(f) == 0 && ok;
+}
+
+bool is_fasta_name(const std::string& s)
+{
+    for (const char* e : {".fa", ".fasta", ".fna"}) {
+        const size_t l = strlen(e);
+        if (s.size() > l && s.compare(s.size() - l, l, e) == 0) return true;
+    }
+    return false;
+}
+
+// The genome the index packs (k_hash_pack, buildRefIndex@0x410190: every
+// line not starting with '>', up to strlen - 1 characters), 16 bases a word,
+// 2 bits a base (code & 3: N reads as A), the last word left-aligned
+bool pack_fasta(const std::vector<uint8_t>& fa, std::vector<uint32_t>& words, uint64_t& bases)
+{
+    words.clear();
+    bases = 0;
+    uint32_t w = 0;
+    bool header = false;
+    for (size_t at = 0; at < fa.size();) {
+        const uint8_t* p = fa.data() + at;
+        const uint8_t* e = (const uint8_t*)memchr(p, '\n', fa.size() - at);
+        const size_t len = e ? (size_t)(e - p) + 1 : fa.size() - at;
+        at += len;
+        if (p[0] == '>') { header = true; continue; }
+        const uint8_t* z = (const uint8_t*)memchr(p, 0, len);
+        const size_t sl = z ? (size_t)(z - p) : len;
+        if (sl <= 1) continue;
+        if (!header) return false;
+        for (size_t i = 0; i + 1 < sl; i++) {
+            uint32_t c;
+            switch (p[i] | 0x20) {
+            case 'c': c = 1; break;
+            case 'g': c = 2; break;
+            case 't': c = 3; break;
+            case 'm': c = 1; break;   // IUPAC codes 5..14, & 3
+            case 'r': c = 2; break;
+            case 'y': c = 3; break;
+            case 'k': c = 0; break;
+            case 's': c = 1; break;
+            case 'w': c = 2; break;
+            case 'h': c = 3; break;
+            case 'b': c = 0; break;
+            case 'v': c = 1; break;
+            case 'd': c = 2; break;
+            default: c = 0;   // A, N and anything else
+            }
+            w = (w << 2) | c;
+            if (++bases % 16 == 0) { words.push_back(w); w = 0; }
+        }
+    }
+    if (bases % 16) words.push_back(w << (2 * (16 - bases % 16)));
+    if (words.empty()) words.push_back(0);
+    return header;
 }
 
 std::string dir_of(const std::string& p)
@@ -397,12 +481,81 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_tex
 }
 
 struct Options {
-    const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr;
-    bool compress = false, decompress = false, force = false, in_dir = false, share_device = false, verbose = false,
-         host_only = false, host_parse = false;
-    int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50;
+    const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
+    bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
+         verbose = false, host_only = false, host_parse = false;
+    int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
+    int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
 };
+
+// ---- SeqArc -i ref.fa: the HASH index (HashAlignment::buildRefIndex@0x410190,
+//      HashRefIndex32::writeIndexFile@0x41ed00 -> "<ref>.hash"; MD5File@0x405950 of
+//      the FASTA -> "<ref>.md5", 16 bytes) ----
+int build_index(const Options& o)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint8_t> fa;
+    if (!slurp(o.ref, fa) || fa.empty()) {
+        fprintf(stderr, "Error:The file %s may be not exist or empty!\n", o.ref);
+        return 1;
+    }
+    sa_ctx* c = sa_create(o.device);
+    if (!c) {
+        fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", o.device);
+        return 1;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    sa_hash_index* ix = sa_hash_build(c, (const char*)fa.data(), fa.size(), 14, 2, 1u << 16);
+    if (!ix) {
+        fprintf(stderr, "seqarc_amd: index build failed: %s\n", sa_last_error(c));
+        sa_destroy(c);
+        return 1;
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    std::vector<uint8_t> file(sa_hash_file_bytes(ix));
+    int rc = sa_hash_serialize(c, ix, file.data(), file.size());
+    uint8_t md[16];
+    sa_md5(fa.data(), fa.size(), md);
+    if (rc || !spill(std::string(o.ref) + ".hash", file.data(), file.size()) ||
+        !spill(std::string(o.ref) + ".md5", md, 16)) {
+        fprintf(stderr, "seqarc_amd: cannot write the index files of %s\n", o.ref);
+        rc = 1;
+    }
+    const double s_load = std::chrono::duration<double>(t1 - t0).count(),
+                 s_build = std::chrono::duration<double>(t2 - t1).count(),
+                 s_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "seqarc_amd: index of %u bases (%s.hash, %zu bytes): read %.3f s, build %.3f s, total %.3f s\n",
+            sa_hash_genome_length(ix), o.ref, file.size(), s_load, s_build, s_all);
+    sa_hash_destroy(ix);
+    sa_destroy(c);
+    return rc;
+}
+
+// The reference of -c / -d: its index file (or the FASTA to build it from) and
+// the MD5 the archive records (getMd5@0x416810 reads "<ref>.md5")
+struct RefFiles {
+    std::vector<uint8_t> hash, fasta;
+    uint8_t md5[16] = {0};
+};
+
+bool load_ref(const char* ref, bool need_fasta, RefFiles& rf)
+{
+    const std::string r(ref);
+    const bool have_hash = slurp(r + ".hash", rf.hash) && rf.hash.size() > 16;
+    if (!have_hash) rf.hash.clear();
+    std::vector<uint8_t> m;
+    const bool have_md5 = slurp(r + ".md5", m) && m.size() == 16;
+    if (!have_hash || !have_md5 || need_fasta) {
+        if (!slurp(r, rf.fasta) || rf.fasta.empty()) {
+            fprintf(stderr, "Error:The file %s may be not exist or empty!\n", ref);
+            return false;
+        }
+    }
+    if (have_md5) memcpy(rf.md5, m.data(), 16);
+    else sa_md5(rf.fasta.data(), rf.fasta.size(), rf.md5);
+    return true;
+}
 
 // ---- compression: the streaming pipeline ------------------------------------
 int compress(const Options& o)
@@ -450,6 +603,36 @@ int compress(const Options& o)
     if (ctxs.empty()) {
         fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", o.device);
         return 1;
+    }
+    // reference path: the index on every device in use, one align_info chain
+    // through all batches in input order (the reference's -t 1 thread)
+    RefFiles rf;
+    std::map<sa_ctx*, sa_align_cfg> acfg;
+    std::vector<sa_hash_index*> indexes;
+    sa_align_chain* chain = nullptr;
+    if (o.ref && !o.host_only) {
+        if (!load_ref(o.ref, false, rf)) return 1;
+        const double ti = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        sa_ctx* owner = nullptr;
+        sa_hash_index* ix = nullptr;
+        for (size_t k = 0; k < ctxs.size(); k++) {
+            if (k % (size_t)o.contexts == 0 && !(o.share_device && ix)) {   // the first context of a device
+                owner = ctxs[k];
+                ix = !rf.hash.empty() ? sa_hash_load(owner, rf.hash.data(), rf.hash.size())
+                                      : sa_hash_build(owner, (const char*)rf.fasta.data(), rf.fasta.size(), 14, 2, 1u << 16);
+                if (!ix) {
+                    fprintf(stderr, "seqarc_amd: reference index: %s\n", sa_last_error(owner));
+                    return 1;
+                }
+                indexes.push_back(ix);
+            }
+            acfg[ctxs[k]] = sa_align_cfg{ix, pe ? 1 : 0, o.maxmis, 1, (uint32_t)o.insert};
+        }
+        chain = sa_align_chain_create(0, 0);   // a fresh encode thread's AlignParam (nmis 0)
+        if (o.verbose)
+            fprintf(stderr, "seqarc_amd: reference %s: index %s in %.3f s\n", o.ref,
+                    rf.hash.empty() ? "built" : "loaded",
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() - ti);
     }
     const int64_t B = std::max(1, o.batch);
     const size_t max_inflight = (size_t)B * (ctxs.size() + 2);   // blocks read but not yet written
@@ -667,7 +850,8 @@ int compress(const Options& o)
                     }
                     cv.notify_all();   // (text windows are free for the reader)
                     const double tr = now_s();
-                    if (sa_run(ctx, &c) != 0) return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                    if ((chain ? sa_run_aligned(ctx, &c, &acfg[ctx], chain, (uint64_t)k) : sa_run(ctx, &c)) != 0)
+                        return fail(std::string("encode failed: ") + sa_last_error(ctx));
                     const double tf = now_s();
                     if (sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
                         return fail(std::string("fetch failed: ") + sa_last_error(ctx));
@@ -695,6 +879,11 @@ int compress(const Options& o)
                     }
                     if (!ctx) {   // --host-only
                         for (sa_out& x : outs) x.size = 0;
+                    } else if (chain) {   // (the batch's place in the chain: k)
+                        if (sa_stage(ctx, in.data(), (int)in.size()) != 0 ||
+                            sa_run_aligned(ctx, &c, &acfg[ctx], chain, (uint64_t)k) != 0 ||
+                            sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
+                            return fail(std::string("encode failed: ") + sa_last_error(ctx));
                     } else if (sa_encode_blocks(ctx, in.data(), (int)in.size(), &c, outs.data()) != 0)
                         return fail(std::string("encode failed: ") + sa_last_error(ctx));
                 }
@@ -758,6 +947,8 @@ int compress(const Options& o)
     const double t_joined = now_s();
     // (releasing five contexts' ~200 GB of buffers takes ~1.4 s; leaving them to
     // the process exit moves the same time there, r3k)
+    for (sa_hash_index* ix : indexes) sa_hash_destroy(ix);
+    if (chain) sa_align_chain_destroy(chain);
     for (sa_ctx* c : ctxs)
         if (c) sa_destroy(c);
     if (o.verbose) fprintf(stderr, "seqarc_amd: encoders done %.3f s, contexts released %.3f s\n", t_joined, now_s());
@@ -767,7 +958,7 @@ int compress(const Options& o)
         return 1;
     }
     sa_arc_info ai{o.f1, pe ? o.f2 : nullptr, pe ? 1 : 0, in1.is_gz ? 1 : 0, plus_bare, cfg.md5,
-                   cfg.lossy > 0.0 ? 1 : 0, tmpl};
+                   cfg.lossy > 0.0 ? 1 : 0, tmpl, o.ref ? rf.md5 : nullptr, (uint32_t)o.insert};
     std::vector<uint8_t> tr(4096 + 40 * info.size());
     const int64_t tl = sa_arc_trailer(&ai, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
     if (tl < 0) {
@@ -879,8 +1070,8 @@ int decompress(const Options& o)
     t += 2;
     const uint8_t* pend = t + psz;
     uint8_t tmpl[512] = {0};
-    int bare = 1, paired = 0, lossy = 0, md5 = 1, gz1 = 0;
-    uint32_t nblocks = 0;
+    int bare = 1, paired = 0, lossy = 0, md5 = 1, gz1 = 0, noref = 1;
+    uint32_t nblocks = 0, insert = 0;
     std::string name1, name2;
     while (t < pend) {
         const uint64_t id = vint(t, pend, w);
@@ -890,7 +1081,9 @@ int decompress(const Options& o)
         const uint64_t ln = be(t, sw) & ((1ull << (7 * sw)) - 1);
         t += sw;
         if (t + ln > pend) return 1;
-        if (id == 2) bare = t[0];
+        if (id == 1) noref = t[0];
+        else if (id == 10 && ln >= 2) insert = (uint32_t)(t[0] | t[1] << 8);
+        else if (id == 2) bare = t[0];
         else if (id == 4) gz1 = t[0];
         else if (id == 11 && ln >= 4) nblocks = (uint32_t)(t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24);
         else if (id == 13) name1.assign((const char*)t, ln);
@@ -900,6 +1093,48 @@ int decompress(const Options& o)
         else if (id == 17) md5 = t[0];
         t += ln;
     }
+    // writeMd5@0x416b10: the reference FASTA's MD5 (ID 8), archives made with one
+    uint8_t arc_md5[16] = {0};
+    bool have_md5 = false;
+    if (vint(t, end, w) == 8 && w) {
+        t += w;
+        if (t + 17 > end || (be(t, 1) & 0x7f) != 16) return 1;
+        memcpy(arc_md5, t + 1, 16);
+        have_md5 = true;
+        t += 17;
+    }
+    // the genome of an archive made with a reference (Decompress::loadRef: the
+    // index's packed bases, or the FASTA packed the same way)
+    RefFiles rf;
+    std::vector<uint32_t> gwords;
+    uint64_t gbases = 0;
+    if (!noref) {
+        if (!o.ref) {
+            fprintf(stderr, "seqarc_amd: %s was made with a reference: give ref.fa\n", o.arc);
+            return 1;
+        }
+        if (!load_ref(o.ref, false, rf)) return 1;
+        if (have_md5 && memcmp(arc_md5, rf.md5, 16)) {   // checkMd5@0x416c40
+            fprintf(stderr, "seqarc_amd: the reference %s is not the one %s was made with (MD5)\n", o.ref, o.arc);
+            return 1;
+        }
+        if (!rf.hash.empty()) {   // K, bases, words, positions; words follow
+            uint32_t hdr[4];
+            memcpy(hdr, rf.hash.data(), 16);
+            if (16 + 4ull * hdr[2] > rf.hash.size()) {
+                fprintf(stderr, "seqarc_amd: %s.hash is truncated\n", o.ref);
+                return 1;
+            }
+            gbases = hdr[1];
+            gwords.resize(hdr[2]);
+            memcpy(gwords.data(), rf.hash.data() + 16, 4ull * hdr[2]);
+            rf.hash.clear();
+        } else if (!pack_fasta(rf.fasta, gwords, gbases)) {
+            fprintf(stderr, "seqarc_amd: %s: not a FASTA file\n", o.ref);
+            return 1;
+        }
+    }
+    const sa_ref gref{gwords.data(), gbases, paired, o.maxmis, insert};
     if (vint(t, end, w) != 7 || !w) return 1;
     t += w;
     const uint64_t bt = be(t, 4) & 0x0fffffff;
@@ -980,7 +1215,8 @@ int decompress(const Options& o)
                 d.nl.resize(cap / 4 + 8); d.sl.resize(cap / 4 + 8);
                 d.d = sa_decoded{d.names.data(), d.nl.data(), d.seq.data(), d.sl.data(), d.qual.data(), cap, cap,
                                  (uint32_t)(cap / 4 + 8), 0, 0};
-                d.rc = sa_decode_block(a.data() + bk.off, bk.size, &cfg, tmpl, (int32_t)bk.lng, &d.d);
+                d.rc = noref ? sa_decode_block(a.data() + bk.off, bk.size, &cfg, tmpl, (int32_t)bk.lng, &d.d)
+                             : sa_decode_block_ref(a.data() + bk.off, bk.size, &cfg, tmpl, (int32_t)bk.lng, &gref, &d.d);
             });
         for (auto& x : th) x.join();
         for (uint32_t i = 0; i < n && !rc; i++) {
@@ -1038,12 +1274,28 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--host-only")) o.host_only = true;
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
+        else if (!strcmp(a, "-i")) { o.index = true; if (!(o.ref = val())) return usage(); }
+        else if (!strcmp(a, "-q")) {   // -q -i: the minimizer index (MINI_INDEX) is not part of this build
+            fprintf(stderr, "seqarc_amd: -q (minimizer index) is not part of this build; the HASH index is\n");
+            return 2;
+        }
+        else if (!strcmp(a, "-I")) { if (!ival(o.insert, 0)) return usage(); o.insert = std::min(o.insert, 65535); }
+        else if (!strcmp(a, "--maxmis")) { if (!ival(o.maxmis, 0)) return usage(); o.maxmis = std::min(o.maxmis, 63); }
         else if (a[0] != '-') pos.push_back(a);
         else return usage();
     }
+    if (o.index) {
+        if (o.compress || o.decompress || !pos.empty()) return usage();
+        return build_index(o);
+    }
     if (o.compress == o.decompress) return usage();
-    if (o.decompress) {
-        // SeqArc -d [ref.fa] ARCHIVE [PREFIX]: a reference index is not part of this build
+    // the first positional argument is the reference when it names a FASTA
+    // (SeqArcParam::parseOptFromCmd@0x40b460: the argument before the inputs)
+    if (!pos.empty() && is_fasta_name(pos[0])) {
+        o.ref = pos[0];
+        pos.erase(pos.begin());
+    }
+    if (o.decompress) {   // SeqArc -d [ref.fa] ARCHIVE [PREFIX]
         if (pos.empty() || pos.size() > 2) return usage();
         o.arc = pos[0];
         if (pos.size() == 2 && !o.out) o.out = pos[1];
@@ -1051,12 +1303,6 @@ int main(int argc, char** argv)
     }
     // SeqArc -c [ref.fa] -1 A [-2 B] OUT
     for (const char* p : pos) {
-        const std::string s(p);
-        const std::string ext = s.size() > 3 ? s.substr(s.rfind('.') == std::string::npos ? s.size() : s.rfind('.')) : "";
-        if (ext == ".fa" || ext == ".fasta" || ext == ".fna") {
-            fprintf(stderr, "seqarc_amd: reference-index compression (%s) is not part of this build\n", p);
-            return 2;
-        }
         if (o.out) return usage();
         o.out = p;
     }

@@ -193,6 +193,11 @@ typedef struct {
     int32_t md5;                   /* param+0x1880                                       */
     int32_t lossy;                 /* param+0x1870 (-l)                                  */
     const uint8_t *id_template;    /* 512 B, param+0x18a4 (sa_analyze_ids)               */
+    /* reference path (-c ref.fa): param+0x3 clear, -I in field 10, and the
+     * index MD5 encap writeMd5@0x416b10 (ID 8: the 16 bytes of "<ref.fa>.md5",
+     * the MD5 of the FASTA file, getMd5@0x416810) */
+    const uint8_t *ref_md5;        /* NULL: no reference                                 */
+    uint32_t insert_size;          /* param+0x28 (-I)                                    */
 } sa_arc_info;
 
 /* ---- block decoder (SeqArc -d; host) ------------------------------------ */
@@ -215,6 +220,24 @@ typedef struct {
  * record's flag bit (compressLen_long). */
 int64_t sa_decode_block(const uint8_t *in, uint64_t len, const sa_cfg *cfg, const uint8_t tmpl[512],
                         int32_t long_reads, sa_decoded *out);
+
+/* The reference path's blocks (doAlignEncode@0x42d4c0 layout): aligned reads are
+ * rebuilt from the genome (EncapFqzComp::decompressSeq@0x42e390 ->
+ * getRealPos@0x42de30, AlignInfoToSeq@0x42e020). */
+typedef struct {
+    const uint32_t *genome;   /* packed bases: sa_hash_packed / the .hash file's words */
+    uint64_t bases;           /* genome length (param+0x1868)                          */
+    int32_t paired;           /* the archive is PE (the mate relation streams)         */
+    int32_t maxmis;           /* param+0x1b60 the archive was made with (Mis model)    */
+    uint32_t insert_size;     /* -I (trailer field 10): the mate distances' bits when  */
+                              /* the block's insert-bits count is 0 (the reference's   */
+                              /* own decoder reads 0 bits there)                       */
+} sa_ref;
+int64_t sa_decode_block_ref(const uint8_t *in, uint64_t len, const sa_cfg *cfg, const uint8_t tmpl[512],
+                            int32_t long_reads, const sa_ref *ref, sa_decoded *out);
+
+/* RFC 1321 MD5 (MD5File@0x405950 of the reference FASTA, the block digests) */
+void sa_md5(const uint8_t *data, uint64_t len, uint8_t digest[16]);
 
 /* 16-byte header; block_bytes = sum of the blocks' sizes. Returns 0. */
 int sa_arc_header(uint64_t block_bytes, uint8_t out[16]);

@@ -3,6 +3,7 @@ output naming of SeqArcParam::getDecodeFile@0x405f70) on archives built from
 the CPU restatement's blocks, and the streaming block cut the -c reader uses
 (sa_cut_next_se / sa_cut_next_pe) against the whole-buffer cut."""
 import ctypes as C
+import hashlib
 import os
 import subprocess
 
@@ -92,15 +93,54 @@ def test_decode_names_force_and_dir(tmp_path, pair):
 
 
 def test_compress_usage_errors(tmp_path):
-    """-c argument checks that need no GPU: missing / empty input, a reference
-    index (not part of this build)."""
+    """-c argument checks that need no GPU: missing / empty input, -q (the
+    minimizer index, not part of this build), a missing reference."""
     r = _run(["-c", "-1", str(tmp_path / "missing.fq"), "-o", "x"], tmp_path)
     assert r.returncode == 1 and b"may be not exist or empty" in r.stderr
     (tmp_path / "e.fq").write_bytes(b"")
     r = _run(["-c", "-1", str(tmp_path / "e.fq"), "x"], tmp_path)
     assert r.returncode == 1
-    r = _run(["-c", "ref.fa", "-1", str(tmp_path / "e.fq"), "x"], tmp_path)
+    r = _run(["-q", "-i", "ref.fa"], tmp_path)
     assert r.returncode == 2
+    r = _run(["-i", str(tmp_path / "missing.fa")], tmp_path)
+    assert r.returncode == 1 and b"may be not exist" in r.stderr
+
+
+@pytest.mark.parametrize("paired,with_hash", [(False, True), (True, False), (True, True)])
+def test_decode_with_reference(tmp_path, paired, with_hash):
+    """SeqArc -d ref.fa ARCHIVE PREFIX on an archive of the reference path
+    (blocks from the oracle's doAlignEncode restatement, trailer field 1 = 0,
+    the FASTA's MD5 after the params, writeMd5@0x416b10): the genome from
+    ref.fa.hash or, without it, packed from ref.fa; the MD5 checked
+    (checkMd5@0x416c40); no reference or another one: refused."""
+    fa, g = synth.reference(800_000, 71, chroms=2)
+    fa = fa.upper()
+    hfile = oracle_py.hash_index(fa)
+    (tmp_path / "ref.fa").write_bytes(fa)
+    if with_hash:
+        (tmp_path / "ref.fa.hash").write_bytes(hfile)
+    r1, r2 = synth.aligned_reads(g, 2500, 72, paired=paired, random_frac=0.2, far_frac=0.3, short_frac=0.2)
+    blocks = fq.blocks_from_fastq(r1, r2, block_size=150_000)
+    assert len(blocks) >= 3
+    tmpl = fq.analyze_ids(blocks[0], not paired)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    carry = [0, 0]
+    ins = 400 if paired and with_hash else 0
+    enc = [oracle_py.encode_block_hash(b, paired, carry, bin_mode=cfg.bin_mode, insert_size=ins) for b in blocks]
+    data = fq.arc_archive(enc, blocks, "a_1.fq", "a_2.fq" if paired else None, tmpl, cfg,
+                          plus_bare=fq.bare_plus(r1), ref_md5=hashlib.md5(fa).digest(), insert_size=ins)
+    (tmp_path / "a.arc").write_bytes(data)
+    r = _run(["-d", "-t", "3", "ref.fa", "a.arc", "back"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    if paired:
+        assert (tmp_path / "back_1.fastq").read_bytes() == r1 and (tmp_path / "back_2.fastq").read_bytes() == r2
+    else:
+        assert (tmp_path / "back.fastq").read_bytes() == r1
+    r = _run(["-d", "-f", "a.arc", "x"], tmp_path)
+    assert r.returncode == 1 and b"made with a reference" in r.stderr
+    (tmp_path / "other.fa").write_bytes(fa.replace(b"ACGT", b"ACGA", 1))
+    r = _run(["-d", "-f", "other.fa", "a.arc", "x"], tmp_path)
+    assert r.returncode == 1 and b"MD5" in r.stderr
 
 
 def _stream_cut(t1, t2, bs, step):

@@ -151,3 +151,56 @@ def test_other_configs(enc, index, ref):
     tmpl = fq.analyze_ids(blocks[0], False)
     for cfg in (fq.Config(slevel=4), fq.Config(qlevel=3), fq.Config(md5=False), fq.Config(bin_mode=int(tmpl[0]))):
         check(enc, index, blocks, True, cfg)
+
+
+def test_cli_reference_path(tmp_path):
+    """seqarc_amd -i ref.fa / -c ref.fa / -d ref.fa (README.md:19-26, 55-93): the
+    index files equal the restatement's, the archive equals the oracle's blocks
+    in the restated container (the align_info chain through 1 MiB blocks in
+    2-block batches over two contexts), with the index loaded from ref.fa.hash
+    or built from ref.fa, -I, SE on the host parser; -d brings the reads back."""
+    import hashlib
+    import os
+    import subprocess
+    from fastqueeze_amd import build
+    fa, g = synth.reference(1_500_000, 51, chroms=2)
+    fa = fa.upper()   # (aligned bases come back from the genome in upper case)
+    (tmp_path / "ref.fa").write_bytes(fa)
+    run = lambda args: subprocess.run([build.CLI] + args, capture_output=True, cwd=tmp_path, timeout=300)
+    r = run(["-i", "ref.fa"])
+    assert r.returncode == 0, r.stderr
+    hfile = orc.hash_index(fa)
+    assert (tmp_path / "ref.fa.hash").read_bytes() == hfile
+    assert (tmp_path / "ref.fa.md5").read_bytes() == hashlib.md5(fa).digest()
+    r1, r2 = synth.aligned_reads(g, 14000, 52, paired=True, random_frac=0.1, far_frac=0.1, short_frac=0.2)
+    (tmp_path / "a_1.fq").write_bytes(r1)
+    (tmp_path / "a_2.fq").write_bytes(r2)
+    (tmp_path / "s.fq").write_bytes(r1)
+
+    def want(paired, ins=0):
+        blocks = fq.blocks_from_fastq(r1, r2 if paired else None, 1 << 20)
+        assert len(blocks) >= 3
+        tmpl = fq.analyze_ids(blocks[0], not paired)
+        cfg = fq.Config(bin_mode=int(tmpl[0]))
+        carry = [0, 0]
+        enc = [orc.encode_block_hash(b, paired, carry, bin_mode=cfg.bin_mode, insert_size=ins) for b in blocks]
+        return fq.arc_archive(enc, blocks, "a_1.fq" if paired else "s.fq", "a_2.fq" if paired else None, tmpl, cfg,
+                              plus_bare=fq.bare_plus(r1), ref_md5=hashlib.md5(fa).digest(), insert_size=ins)
+
+    base = ["-c", "-f", "--block-size", "1", "--batch", "2"]
+    r = run(base + ["--contexts", "2", "ref.fa", "-1", "a_1.fq", "-2", "a_2.fq", "pe"])
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "pe.arc").read_bytes() == want(True)
+    r = run(["-d", "ref.fa", "pe.arc", "back"])
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "back_1.fastq").read_bytes() == r1 and (tmp_path / "back_2.fastq").read_bytes() == r2
+    r = run(base + ["--host-parse", "ref.fa", "-1", "s.fq", "se"])
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "se.arc").read_bytes() == want(False)
+    os.remove(tmp_path / "ref.fa.hash")   # the index built on the device from the FASTA
+    r = run(base + ["-I", "300", "ref.fa", "-1", "a_1.fq", "-2", "a_2.fq", "pi"])
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "pi.arc").read_bytes() == want(True, 300)
+    r = run(["-d", "ref.fa", "pi.arc", "bi"])
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "bi_1.fastq").read_bytes() == r1
