@@ -284,6 +284,47 @@ class Workers:
         if errs:
             raise errs[0]
 
+    def verify_shared(self, probe=None):
+        """Every batch encoded by the contexts together (sharing the front scratch,
+        as in the timed region), outputs fetched per step; then each batch by
+        context 0 alone.  Per-batch digests must agree.  probe(s, outs): an extra
+        check on a batch's outputs from the shared run.  Returns {batch: context}."""
+        lock = threading.Lock()
+        nxt = [0]
+        errs, shared, who = [], {}, {}
+
+        def worker(k, enc):
+            try:
+                while True:
+                    with lock:
+                        s = nxt[0]
+                        if s >= len(self.inputs):
+                            return
+                        nxt[0] += 1
+                    enc.run_input(self.inputs[s], self.cfg)
+                    outs = enc.fetch()
+                    if probe:
+                        probe(s, outs)
+                    with lock:
+                        shared[s] = hashlib.sha256(b"".join(hashlib.sha256(o).digest() for o in outs)).digest()
+                        who[s] = k
+            except Exception as e:
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(k, e)) for k, e in enumerate(self.encs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        for s, inp in enumerate(self.inputs):
+            self.encs[0].run_input(inp, self.cfg)
+            outs = self.encs[0].fetch()
+            if hashlib.sha256(b"".join(hashlib.sha256(o).digest() for o in outs)).digest() != shared[s]:
+                raise SystemExit(f"batch {s}: the shared-front run (context {who[s]}) differs from context 0 alone")
+        return who
+
 
 def main():
     argv = sys.argv[1:]
@@ -354,7 +395,7 @@ def main():
         return
 
     # ---- resident inputs, encoder contexts ----
-    keep = {"verify": batches[0], "cpu": batches[0]}
+    keep = {"verify": batches[0], "cpu": batches[0], "last": batches[-1]}
     inputs = [fq.Input(bl, local) for bl in batches]
     del batches
     encs = [fq.Encoder(local)]
@@ -401,6 +442,20 @@ def main():
                         and np.array_equal(nm, b.names)):
                     raise SystemExit(f"bench output of block {i} does not decode back to its input")
         log("[rank 0] spot-check: first and last block of batch 0 bit-identical to the oracle, decode back")
+    # every batch again with the contexts sharing the front (as timed) against
+    # context 0 alone; the last block of the last batch against the oracle
+    if not args.no_verify:
+        import oracle_py
+        lb = keep["last"]
+
+        def probe(s, outs):
+            if s == len(inputs) - 1 and outs[-1] != oracle_py.encode_block(lb[-1], cfg.slevel, cfg.qlevel, cfg.md5,
+                                                                              cfg.bin_mode, cfg.lossy):
+                raise SystemExit(f"bench output of the last block of batch {s} differs from the CPU restatement")
+        who = W.verify_shared(probe)
+        log(f"[rank {rank}] shared-front outputs of every batch identical to context 0 alone "
+            f"(batch -> context {who}); last block of batch {len(inputs) - 1} bit-identical to the oracle")
+    del keep["last"]
     digest = hashlib.sha256(b"".join(hashlib.sha256(o).digest() for o in outs)).digest()
     if world > 1:
         digs = gather_blocks([(rank, digest)], world)

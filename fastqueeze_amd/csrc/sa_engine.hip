@@ -1053,8 +1053,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         align_chain_fail(al->chain);
         return -1;
     }
+    const bool trace = al && std::getenv("SA_ALN_TRACE");
     // the front (up to the short model runs) holds the device's front scratch
     FrontTurn front_lock(F, st);
+    if (trace) fprintf(stderr, "[align] front turn taken\n");
     SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
     SA_CHECK(c, F->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
     uint8_t* dege_maxq = c->prep_wave ? nullptr : F->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
@@ -1363,6 +1365,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             (void)hipEventElapsedTime(&c->ph_ms[i], c->ev_beg[i], c->ev_end[i]);
         }
     }
+    if (trace) fprintf(stderr, "[align] batch queued\n");
     c->have_output = true;
     return 0;
 }

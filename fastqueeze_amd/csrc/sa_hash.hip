@@ -869,6 +869,20 @@ int sa_hash_align(sa_ctx* c, const sa_hash_index* ix, const char* seq, const uin
 // ---------------------------------------------------------------------------
 // reference path of a resident batch (sa_run_input_aligned)
 // ---------------------------------------------------------------------------
+// SA_ALN_TRACE=1: the reference path's host steps on stderr
+static bool aln_trace()
+{
+    static const bool on = std::getenv("SA_ALN_TRACE") != nullptr;
+    return on;
+}
+#define ATRACE(...)                                  \
+    do {                                             \
+        if (aln_trace()) {                           \
+            std::fprintf(stderr, "[align] " __VA_ARGS__); \
+            std::fflush(stderr);                     \
+        }                                            \
+    } while (0)
+
 struct sa_align_chain {
     std::mutex mu;
     std::condition_variable cv;
@@ -927,6 +941,7 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
     const HashArgs ha{a.maxmis, a.good};
     const bool rerun = c->al_input == I && c->al_plan.size() == 4ull * nbk &&
                        (rq.batch == UINT64_MAX || rq.batch == c->al_batch);
+    ATRACE("front: %u reads, %u blocks, rerun %d\n", nr, nbk, (int)rerun);
     if (!rerun) {
         // ---- every read with the carried state "not aligned" ----
         if (nr)
@@ -940,6 +955,7 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
         SA_CHECK(c, d2h(c, status.data(), c->d_al_st.p, nr, st));
         SA_CHECK(c, d2h(c, pos0.data(), c->d_al_pos[0].p, 4ull * nr, st));
         SA_CHECK(c, sync_d2h(c, st));
+        ATRACE("variant 0 done\n");
         // ---- the reads that consulted it, again with "aligned" ----
         std::vector<uint32_t> cons;
         for (uint32_t r = 0; r < nr; r++)
@@ -957,6 +973,7 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
             SA_CHECK(c, d2h(c, pos1.data(), c->d_al_pos[1].p, 4ull * nr, st));
             SA_CHECK(c, sync_d2h(c, st));
         }
+        ATRACE("variant 1 done (%zu reads)\n", cons.size());
         // ---- the chain: this batch after the previous one ----
         sa_align_chain* ch = rq.chain;
         std::vector<uint32_t> sel;
@@ -984,6 +1001,7 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
             c->al_batch = me;
         }
         ch->cv.notify_all();
+        ATRACE("chain passed, %zu reads take variant 1\n", sel.size());
         c->al_input = I;
         if (!sel.empty()) {
             SA_CHECK(c, c->d_al_sel.ensure(4 * sel.size()));
@@ -1024,6 +1042,10 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
     atot.assign((size_t)NACOL * nbk, 0);
     SA_CHECK(c, d2h(c, atot.data(), c->d_atot.p, 4ull * NACOL * nbk, st));
     SA_CHECK(c, sync_d2h(c, st));
+    for (uint32_t b = 0; b < nbk && aln_trace(); b++)
+        ATRACE("block %u: order_count %u win %u ibits %u; columns %u %u %u %u %u %u %u\n", b, c->blocks[b].order_count,
+               c->blocks[b].win, c->blocks[b].ibits, atot[NACOL * b], atot[NACOL * b + 1], atot[NACOL * b + 2],
+               atot[NACOL * b + 3], atot[NACOL * b + 4], atot[NACOL * b + 5], atot[NACOL * b + 6]);
     return 0;
 }
 

@@ -209,7 +209,7 @@ __device__ __forceinline__ void prep_sq_read(const BatchView& bv, const uint32_t
         }
     }
     if (lane == 0) {
-        const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, n, st, qbad);
+        const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, n, st, qbad, bv.seq_skip && bv.seq_skip[r]);
         if (e) atomicOr(err, e);
     }
 }
@@ -410,7 +410,8 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
         if (live && rl == 0) {
             SeqStat st{valid, len - valid, maxq & 0xffu, hasn ? exc : 0u, hasn ? nsym : 0u,
                        nonascii ? (uint32_t)E_NONASCII : 0u};
-            const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, lastnz, st, firstbad < lastnz);
+            const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, lastnz, st, firstbad < lastnz,
+                                            bv.seq_skip && bv.seq_skip[r]);
             if (e) atomicOr(err, e);
             dege_maxq[r] = (uint8_t)st.maxq;   // (k_emit / k_emit_sq: the side streams)
         }
@@ -579,7 +580,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
     stage_read(s, q, len, stg);
     auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[0][i] : s[i]; };
     auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[1][i] : q[i]; };
-    {
+    if (!(bv.seq_skip && bv.seq_skip[r])) {   // (reference path: aligned reads leave the SEQ stream)
         uint32_t* K = seq_key + blk.seq_sym_base;
         uint32_t* V = seq_val + blk.seq_sym_base;
         uint32_t d = off[C_SEQ];

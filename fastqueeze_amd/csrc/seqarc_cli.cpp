@@ -1222,6 +1222,9 @@ int decompress(const Options& o)
         for (uint32_t i = 0; i < n && !rc; i++) {
             Dec& d = ds[i];
             if (d.rc < 0) { fprintf(stderr, "seqarc_amd: block %u does not decode\n", b0 + i); rc = 1; break; }
+            if (!d.d.md5_ok)   // (-l archives: a range-coder desync fills the rest of the block with N)
+                fprintf(stderr, "seqarc_amd: block %u: Name/Seq/Qual md5 unequal%s\n", b0 + i,
+                        lossy ? " (made with -l: its bases past a desync are N)" : "");
             bad_md5 |= !d.d.md5_ok;
             write_reads(o1, o2, d.names, d.nl, d.seq, d.sl, d.qual, d.d.nreads, paired, mate, bare);
         }
@@ -1289,6 +1292,9 @@ int main(int argc, char** argv)
         return build_index(o);
     }
     if (o.compress == o.decompress) return usage();
+    if (o.compress && o.cfg.lossy > 0.0)   // (the reference's R-Block decoder loses sync on N / IUPAC bases)
+        fprintf(stderr, "seqarc_amd: warning: -l: blocks with N / IUPAC bases may not decode back to their "
+                        "bases (as in SeqArc 1.6); -d reports such blocks\n");
     // the first positional argument is the reference when it names a FASTA
     // (SeqArcParam::parseOptFromCmd@0x40b460: the argument before the inputs)
     if (!pos.empty() && is_fasta_name(pos[0])) {
