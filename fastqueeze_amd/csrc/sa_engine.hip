@@ -172,6 +172,7 @@ struct sa_ctx {
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
+    bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;   // k_emit_sq's SEQ / QUAL instead of k_emit_sq16
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -1127,6 +1128,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         return -1;
     }
 
+    uint64_t n_ch = 0;   // N / IUPAC bases in the batch
+    for (uint32_t b = 0; b < nbk; b++) n_ch += tot[(size_t)b * NCOL + C_CH];
+
     // ---- layout of the symbol spaces, coder tasks, md5 tasks, outputs ----
     BatchPlan bp;
     if (!plan_batch(c->blocks, tot, bp, al ? &aln_tot : nullptr, alv.mis_model)) {
@@ -1230,9 +1234,21 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                            c->d_totals.as<uint32_t>(), F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(),
                            F->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                            akb[0]->as<uint32_t>(), nullptr, d_err, dege_maxq);   // (AUX values: the index, run_sort)
-        hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
-                           F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                           akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh);
+        if (c->emit_wave) {   // (SA_EMIT_WAVE=1: round 2's wave-per-read SEQ / QUAL, for A/B)
+            hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
+                               F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
+                               akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh,
+                               (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE));
+        } else {
+            hipLaunchKernelGGL(k_emit_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
+                               F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
+                               akb[0]->as<uint32_t>(), nullptr, seq_sh);
+            if (dege_maxq && n_ch)   // the N / IUPAC side streams of the reads that have such bases
+                hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
+                                   F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
+                                   F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr,
+                                   c->d_totals.as<uint32_t>(), dege_maxq, seq_sh, (uint32_t)EMIT_DEGE);
+        }
         if (al)   // the alignment streams (AlignInfoProcess[PE], decomposeAlignInfo)
             hipLaunchKernelGGL(k_align_emit, dim3(rgrid), dim3(256), 0, st, bv, alv, c->d_acounts.as<uint32_t>(),
                                akb[0]->as<uint32_t>());

@@ -114,6 +114,7 @@ __global__ void k_prep(const BatchView bv, uint32_t* __restrict__ counts,
 }
 
 constexpr uint32_t EMIT_WAVES = 4;
+enum : uint32_t { EMIT_SEQ = 1, EMIT_QUAL = 2, EMIT_DEGE = 4 };   // k_emit_sq parts
 constexpr uint32_t EMIT_STAGE = 256;   // bases / quals of a read staged in LDS up front
 
 // Stages the first EMIT_STAGE bases and quals of a read in LDS: every load is
@@ -569,7 +570,8 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
                                              const uint32_t* __restrict__ counts, uint32_t* __restrict__ seq_key,
                                              uint32_t* __restrict__ seq_val, uint32_t* __restrict__ aux_key,
                                              uint32_t* __restrict__ aux_val, const uint32_t* __restrict__ totals,
-                                             const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh)
+                                             const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh,
+                                             const uint32_t parts)
 {
     const uint32_t b = bv.read_block[r];
     const DevBlock& blk = bv.blocks[b];
@@ -580,7 +582,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
     stage_read(s, q, len, stg);
     auto S = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[0][i] : s[i]; };
     auto Q = [&](uint32_t i) __attribute__((always_inline)) { return i < EMIT_STAGE ? stg[1][i] : q[i]; };
-    if (!(bv.seq_skip && bv.seq_skip[r])) {   // (reference path: aligned reads leave the SEQ stream)
+    if ((parts & EMIT_SEQ) && !(bv.seq_skip && bv.seq_skip[r])) {   // (reference path: aligned reads leave the SEQ stream)
         uint32_t* K = seq_key + blk.seq_sym_base;
         uint32_t* V = seq_val + blk.seq_sym_base;
         uint32_t d = off[C_SEQ];
@@ -619,7 +621,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
             d += nv;
         }
     }
-    {
+    if (parts & EMIT_QUAL) {
         // trailing '#' are not coded (qual_nonhash); one symbol 94 marks them
         uint32_t n = 0;
         for (uint32_t i0 = 0; i0 < len; i0 += 64) {
@@ -671,7 +673,7 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
     // original qualities) the kModel symbols of the gap before it -- a wave
     // scan of (gap, has-ACGT) gives each lane its gap, an exclusive scan of the
     // symbol counts its slots.
-    if (dege_maxq && read_col_count(bv, counts, totals, r, C_CH)) {
+    if ((parts & EMIT_DEGE) && dege_maxq && read_col_count(bv, counts, totals, r, C_CH)) {
         const int mq = (int)dege_maxq[r];
         const uint8_t* qo = bv.qual + blk.seq_base + bv.seq_off[r];
         uint32_t* K = aux_key + blk.aux_sym_base;
@@ -722,14 +724,248 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
                                                               uint32_t* __restrict__ aux_key,
                                                               uint32_t* __restrict__ aux_val,
                                                               const uint32_t* __restrict__ totals,
-                                                              const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh)
+                                                              const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh,
+                                                              const uint32_t parts)
 {
     __shared__ uint32_t comp[EMIT_WAVES][64];
     __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
+    for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES) {
+        // (parts = EMIT_DEGE: only the reads with N / IUPAC bases have work)
+        if (parts == EMIT_DEGE && !read_col_count(bv, counts, totals, r, C_CH)) continue;
         emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals, dege_maxq,
-                     seq_sh);
+                     seq_sh, parts);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_emit_sq16: the SEQ and QUAL symbols of every read, one 16-lane row per read
+// (four reads per wave, grid-stride like k_prep_sq16), each lane 16 consecutive
+// bytes per step (256 bytes of a read per step: a 150 bp read is one step
+// instead of k_emit_sq's three dependent wave steps per stream).
+//   SEQ: a lane packs the codes of its ACGT bases (2 bits each, the last 16);
+//   a row scan concatenates them, so each lane knows the codes of the <= 16
+//   ACGT bases before its first one (the context, encode_seq@0x421f30, seed
+//   0x7616c7); the lane then walks its bytes.
+//   QUAL (encode_qual@0x422180): the context after symbol i needs symbols
+//   i-1, i-2 (from the previous lane's last two) and the running sum of drops
+//   (a row scan of the lanes' drop sums).
+// Keys are staged per row in LDS and written out row-contiguous.  The N /
+// IUPAC side streams stay in k_emit_sq (parts = EMIT_DEGE).
+// ---------------------------------------------------------------------------
+constexpr uint32_t ER = 16;              // lanes per row
+constexpr uint32_t ER_STEP = 16 * ER;    // bytes of a read per step
+
+__device__ __forceinline__ uint32_t cat_codes(uint32_t a, uint32_t b, uint32_t nb)   // a's codes, then nb codes b
+{
+    return nb >= 16 ? b : (a << (2 * nb)) | b;
+}
+
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[4], uint32_t j)
+{
+    return (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+}
+
+__global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
+                                                   uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
+                                                   const uint32_t seq_sh)
+{
+    __shared__ uint32_t stk[256 / ER][ER_STEP];
+    __shared__ uint32_t stv[256 / ER][ER_STEP];
+    const uint32_t rl = threadIdx.x & (ER - 1), rw = threadIdx.x / ER;
+    const uint32_t rows = gridDim.x * (blockDim.x / ER);
+    const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / ER;
+    const uint32_t nr = bv.nreads_total;
+    const uint32_t mask = bv.seq_mask;
+    const int ql = bv.qlevel;
+    uint32_t* sk = stk[rw];
+    uint32_t* sv = stv[rw];
+    auto sync_row = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    };
+    const uint32_t wrow0 = row0 & ~3u;   // wave-uniform trip count (rows of a wave shuffle together)
+    for (uint32_t base = wrow0; base < nr; base += rows) {
+        const uint32_t r = base + (row0 & 3u);
+        const bool live = r < nr;
+        uint32_t len = 0;
+        const uint8_t *s = nullptr, *q = nullptr;
+        uint32_t* KS = nullptr;
+        uint32_t* VS = nullptr;
+        uint32_t* KA = nullptr;
+        uint32_t* VA = nullptr;
+        uint32_t dseq = 0, pos0 = 0;
+        bool skip = true;
+        if (live) {
+            const DevBlock& blk = bv.blocks[bv.read_block[r]];
+            const uint64_t o = blk.seq_base + bv.seq_off[r];
+            s = bv.seq + o;
+            q = bv.qual_q + o;   // QUAL stream only (rblock output with -l)
+            len = bv.seq_len[r];
+            const uint32_t* off = counts + (size_t)r * NCOL;
+            KS = seq_key + blk.seq_sym_base;
+            VS = seq_val + blk.seq_sym_base;
+            KA = aux_key + blk.aux_sym_base;
+            VA = aux_val ? aux_val + blk.aux_sym_base : nullptr;
+            dseq = off[C_SEQ];
+            pos0 = blk.sbase[ST_QUAL] + off[C_QUAL];
+            skip = bv.seq_skip && bv.seq_skip[r];
+        }
+        const uint32_t wlen = (uint32_t)wave_max_i32((int)len);
+        // ---- SEQ ----
+        uint32_t carry = 0x7616c7u;   // the packed codes before the step (seed, masked at use)
+        for (uint32_t i0 = 0; i0 < wlen; i0 += ER_STEP) {
+            const uint32_t pos = i0 + 16 * rl;
+            const uint32_t cnt = !skip && pos < len ? (len - pos < 16 ? len - pos : 16) : 0u;
+            uint32_t sw[4] = {0, 0, 0, 0};
+            if (cnt) load16(s + pos, sw);
+            uint32_t P = 0, nv = 0, vmask = 0, codes = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++) {
+                const uint32_t c = j < cnt ? base_code((uint8_t)byte_at(sw, j)) : 4u;
+                if (c <= 3) {
+                    P = (P << 2) | c;
+                    nv++;
+                    vmask |= 1u << j;
+                    codes |= c << (2 * j);
+                }
+            }
+            uint32_t ip = P, in = nv;   // inclusive row scan of (codes, count): concatenation
+#pragma unroll
+            for (uint32_t d = 1; d < ER; d <<= 1) {
+                const uint32_t pp = __shfl_up(ip, d, ER), pn = __shfl_up(in, d, ER);
+                if (rl >= d) {
+                    ip = cat_codes(pp, ip, in);
+                    in += pn;
+                }
+            }
+            uint32_t ep = __shfl_up(ip, 1, ER), en = __shfl_up(in, 1, ER);
+            if (rl == 0) ep = en = 0;
+            uint32_t ctx = cat_codes(carry, ep, en);
+            uint32_t k = en;
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++) {
+                if (vmask & (1u << j)) {
+                    const uint32_t c = (codes >> (2 * j)) & 3u;
+                    const uint32_t cm = ctx & mask;
+                    if (seq_sh) {
+                        sk[k] = (cm << 2) | c;
+                    } else {
+                        sk[k] = cm;
+                        sv[k] = ((dseq + k) << 2) | c;
+                    }
+                    ctx = (ctx << 2) | c;
+                    k++;
+                }
+            }
+            const uint32_t tp = __shfl(ip, ER - 1, ER), tn = __shfl(in, ER - 1, ER);
+            carry = cat_codes(carry, tp, tn);
+            sync_row();
+            for (uint32_t t = rl; t < tn; t += ER) {
+                KS[dseq + t] = sk[t];
+                if (!seq_sh) VS[dseq + t] = sv[t];
+            }
+            dseq += tn;
+            sync_row();
+        }
+        // ---- QUAL: trailing '#' are not coded (qual_nonhash); one symbol 94 marks them ----
+        uint32_t n = 0;
+        for (uint32_t i0 = 0; i0 < wlen; i0 += ER_STEP) {
+            const uint32_t pos = i0 + 16 * rl;
+            const uint32_t cnt = pos < len ? (len - pos < 16 ? len - pos : 16) : 0u;
+            uint32_t qw[4] = {0, 0, 0, 0};
+            if (cnt) load16(q + pos, qw);
+            uint32_t last = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++)
+                if (j < cnt && byte_at(qw, j) != '#') last = pos + j + 1;
+            last = row_max<ER>(last);
+            n = last > n ? last : n;
+        }
+        const uint32_t nw = (uint32_t)wave_max_i32((int)n);
+        uint32_t p1 = 0, p2 = 0, ctx_c = 0;   // symbols i0-1, i0-2, the context after i0-1
+        int delta_c = 5;
+        for (uint32_t i0 = 0; i0 < nw; i0 += ER_STEP) {
+            const uint32_t pos = i0 + 16 * rl;
+            const uint32_t cnt = pos < n ? (n - pos < 16 ? n - pos : 16) : 0u;
+            uint32_t qw[4] = {0, 0, 0, 0};
+            if (cnt) load16(q + pos, qw);
+            // entering symbols: the previous lane's last two (every earlier lane of a step holds 16)
+            const uint32_t l2 = (byte_at(qw, 15) - 33u) & 0xffu, l1 = (byte_at(qw, 14) - 33u) & 0xffu;
+            const uint32_t u = __shfl_up(l2 | l1 << 8, 1, ER);
+            uint32_t q1 = rl ? (u & 0xffu) : p1, q2 = rl ? (u >> 8) : p2;
+            uint32_t dsum = 0;
+            {
+                uint32_t a1 = q1;
+#pragma unroll
+                for (uint32_t j = 0; j < 16; j++)
+                    if (j < cnt) {
+                        const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
+                        dsum += a1 > sym ? a1 - sym : 0u;
+                        a1 = sym;
+                    }
+            }
+            uint32_t id = dsum;   // inclusive row scan of the drop sums
+#pragma unroll
+            for (uint32_t d = 1; d < ER; d <<= 1) {
+                const uint32_t pd = __shfl_up(id, d, ER);
+                if (rl >= d) id += pd;
+            }
+            int delta = delta_c + (int)(id - dsum);
+            uint32_t ctxs[16];
+            uint32_t cl = 0;   // the context after the lane's last symbol
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++) {
+                if (j < cnt) {
+                    const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
+                    const uint32_t i = pos + j;
+                    delta += (int)(q1 > sym ? q1 - sym : 0u);
+                    uint32_t cx = (((q1 > q2 ? q1 : q2) << 6) + sym) & 0xfffu;
+                    if (ql > 1) {
+                        cx += q1 == q2 ? 0x1000u : 0u;
+                        cx += (uint32_t)(((delta <= 56 ? delta : 56) & 0xf8) << 10);
+                        if (ql > 2) cx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
+                    }
+                    ctxs[j] = cx;
+                    cl = cx;
+                    q2 = q1;
+                    q1 = sym;
+                }
+            }
+            uint32_t prev = __shfl_up(cl, 1, ER);
+            if (rl == 0) prev = ctx_c;
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++)
+                if (j < cnt) {
+                    const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
+                    sk[16 * rl + j] = ((M_QUAL + prev) << AUX_SYM_BITS) | sym;
+                    prev = ctxs[j];
+                }
+            // the step's last symbol: its lane carries the state on
+            const uint32_t tot = n > i0 ? (n - i0 < ER_STEP ? n - i0 : ER_STEP) : 0u;
+            const uint32_t src = tot ? (tot - 1) / 16 : 0u;
+            const uint32_t dl = (uint32_t)(delta_c + (int)id);   // (the lane's delta after its symbols)
+            const uint32_t n1 = __shfl(q1, src, ER), n2 = __shfl(q2, src, ER), nc = __shfl(cl, src, ER),
+                           nd = __shfl(dl, src, ER);
+            if (tot) {   // (a row whose read ended: its carry stays)
+                p1 = n1;
+                p2 = n2;
+                ctx_c = nc;
+                delta_c = (int)nd;
+            }
+            sync_row();
+            for (uint32_t t = rl; t < tot; t += ER) {
+                KA[pos0 + i0 + t] = sk[t];
+                if (VA) VA[pos0 + i0 + t] = pos0 + i0 + t;
+            }
+            sync_row();
+        }
+        if (live && n != len && rl == 0) {
+            KA[pos0 + n] = ((M_QUAL + ctx_c) << AUX_SYM_BITS) | 94u;
+            if (VA) VA[pos0 + n] = pos0 + n;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -332,6 +332,34 @@ def test_full_size_block_slevel8(enc, pe_full):
     _check(enc, pe_full[:1], fq.Config(slevel=8))
 
 
+@pytest.mark.parametrize("slevel", [8, 9])
+def test_full_size_se_block_high_order(enc, slevel):
+    """configs[1]'s unit of work: a full 50 MiB SE block of 150 bp reads at
+    Slevel 8 / 9 (k = 15 / 16, the README's "16-order" model; ctor@0x42f63e)."""
+    a, _ = synth.generate(150_000, seed=8)
+    blocks = fq.blocks_from_fastq(a)
+    assert blocks[0].text_bytes > 50_000_000
+    _check(enc, blocks[:1], fq.Config(slevel=slevel))
+
+
+@pytest.fixture(scope="module")
+def ont_full():
+    """configs[4]'s shape: 10/20/30/40/50 kbp SE reads with N / IUPAC bases
+    (the bench's --ont generator), the first full 50 MiB block."""
+    parts = [synth.generate(180, read_len=L, seed=700 + k, chunk=1000)[0]
+             for k, L in enumerate((10_000, 20_000, 30_000, 40_000, 50_000))]
+    blocks = fq.blocks_from_fastq(b"".join(parts))
+    assert blocks[0].text_bytes > 50_000_000 and blocks[0].nreads > 500
+    return blocks[:1]
+
+
+@pytest.mark.parametrize("lossy", [0.0, 1.15])
+def test_full_size_ont_block(enc, ont_full, lossy):
+    """The ONT block lossless and at -l 1.15 (rblock@0x426c10; lengths through
+    compressLen_short, every read < 65536 bp)."""
+    _check(enc, ont_full, fq.Config(lossy=lossy))
+
+
 def test_resident_inputs_concurrent_contexts(pe_full):
     """sa_input_create / sa_run_input: two resident batches encoded by two contexts
     sharing one front scratch (sa_create_shared) from two host threads at once
