@@ -1240,9 +1240,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                                akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh,
                                (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE));
         } else {
-            hipLaunchKernelGGL(k_emit_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                               F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
-                               akb[0]->as<uint32_t>(), nullptr, seq_sh);
+            hipLaunchKernelGGL(seq_sh ? k_emit_sq16<2> : k_emit_sq16<0>, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0,
+                               st, bv, F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
+                               F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr);
             if (dege_maxq && n_ch)   // the N / IUPAC side streams of the reads that have such bases
                 hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                    F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),

@@ -766,13 +766,14 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[4], uint32_t j)
     return (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
 }
 
+template <uint32_t SH>   // seq_sh: 2 = the base in the SEQ key, values implicit; 0 = values position << 2 | base
 __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
-                                                   uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
-                                                   const uint32_t seq_sh)
+                                                   uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val)
 {
+    constexpr uint32_t seq_sh = SH;
     __shared__ uint32_t stk[256 / ER][ER_STEP];
-    __shared__ uint32_t stv[256 / ER][ER_STEP];
+    __shared__ uint32_t stv[SH ? 1 : 256 / ER][SH ? 1 : ER_STEP];
     const uint32_t rl = threadIdx.x & (ER - 1), rw = threadIdx.x / ER;
     const uint32_t rows = gridDim.x * (blockDim.x / ER);
     const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / ER;
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
     const uint32_t mask = bv.seq_mask;
     const int ql = bv.qlevel;
     uint32_t* sk = stk[rw];
-    uint32_t* sv = stv[rw];
+    uint32_t* sv = stv[SH ? 0 : rw];
     auto sync_row = [&]() __attribute__((always_inline)) {
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
@@ -849,7 +850,7 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
                 if (vmask & (1u << j)) {
                     const uint32_t c = (codes >> (2 * j)) & 3u;
                     const uint32_t cm = ctx & mask;
-                    if (seq_sh) {
+                    if constexpr (SH != 0) {
                         sk[k] = (cm << 2) | c;
                     } else {
                         sk[k] = cm;
@@ -864,7 +865,7 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
             sync_row();
             for (uint32_t t = rl; t < tn; t += ER) {
                 KS[dseq + t] = sk[t];
-                if (!seq_sh) VS[dseq + t] = sv[t];
+                if constexpr (SH == 0) VS[dseq + t] = sv[t];
             }
             dseq += tn;
             sync_row();

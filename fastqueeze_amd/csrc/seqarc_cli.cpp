@@ -483,7 +483,7 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_tex
 struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
-         verbose = false, host_only = false, host_parse = false;
+         verbose = false, host_only = false, host_parse = false, ingest_only = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -585,8 +585,10 @@ int compress(const Options& o)
                                        : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // contexts: K per device; every device's contexts share one front scratch
     std::vector<sa_ctx*> ctxs;
-    if (o.host_only) ctxs.assign((size_t)o.contexts, nullptr);
-    for (int d = 0; d < o.devices && !o.host_only; d++) {
+    // --ingest-only: the reader and the block cut alone, feeding devices x
+    // contexts consumers that take batches as the device parse would (no device)
+    if (o.host_only || o.ingest_only) ctxs.assign((size_t)o.contexts * (o.ingest_only ? o.devices : 1), nullptr);
+    for (int d = 0; d < o.devices && !o.host_only && !o.ingest_only; d++) {
         sa_ctx* first = nullptr;
         for (int k = 0; k < o.contexts; k++) {
             const int dev = o.device + (o.share_device ? 0 : d);
@@ -610,7 +612,7 @@ int compress(const Options& o)
     std::map<sa_ctx*, sa_align_cfg> acfg;
     std::vector<sa_hash_index*> indexes;
     sa_align_chain* chain = nullptr;
-    if (o.ref && !o.host_only) {
+    if (o.ref && !o.host_only && !o.ingest_only) {
         if (!load_ref(o.ref, false, rf)) return 1;
         const double ti = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
         sa_ctx* owner = nullptr;
@@ -646,7 +648,7 @@ int compress(const Options& o)
     // and recycle them at once; only block 0 is parsed here, for the ID
     // template.  --host-parse / --host-only: -t parser threads build the SoA.
     const bool dev_parse = !o.host_parse && !o.host_only;
-    texts.pinned = dev_parse;
+    texts.pinned = dev_parse && !o.ingest_only;
     texts.win = (pe ? (size_t)((uint32_t)bs >> 1) : (size_t)bs) + (64u << 10);   // a window + slack for the carry
     std::atomic<double> stage_busy{0};
     std::map<int64_t, std::unique_ptr<Job>> jobs;
@@ -823,7 +825,18 @@ int compress(const Options& o)
                     double cur = t_first_enc.load();
                     while (te < cur && !t_first_enc.compare_exchange_weak(cur, te)) {}
                 }
-                if (dev_parse) {
+                if (dev_parse && !ctx) {   // --ingest-only: the batch is taken, its windows recycled
+                    {
+                        std::lock_guard<std::mutex> g(mu);
+                        staged += (int64_t)js.size();
+                    }
+                    for (size_t i = 0; i < js.size(); i++) {
+                        texts.put(js[i]->t1);
+                        texts.put(js[i]->t2);
+                        outs[i] = sa_out{nullptr, 0, 0};
+                    }
+                    cv.notify_all();
+                } else if (dev_parse) {
                     std::vector<sa_text_block> tin(js.size());
                     std::vector<sa_text_info> ti(js.size());
                     for (size_t i = 0; i < js.size(); i++)
@@ -1275,6 +1288,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--block-size")) { if (!ival(o.block_mib, 1)) return usage(); }
         else if (!strcmp(a, "--share-device")) o.share_device = true;
         else if (!strcmp(a, "--host-only")) o.host_only = true;
+        else if (!strcmp(a, "--ingest-only")) o.ingest_only = true;
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (!strcmp(a, "-i")) { o.index = true; if (!(o.ref = val())) return usage(); }

@@ -217,3 +217,25 @@ def test_host_only_reader_matches_the_cut(tmp_path):
         assert r.returncode == 0, r.stderr
         line = [ln for ln in r.stderr.decode().splitlines() if "block(s)" in ln][0]
         assert line.split()[1] == str(len(fq.cut_se(a, mib << 20))) and f" {len(a)} -> " in line, (mib, line)
+
+
+def test_ingest_only_eight_way(tmp_path, capsys):
+    """The -c reader and block cut alone (--ingest-only) feeding 8 devices x 1
+    context of consumers, as a whole-node run deals batches: the block count and
+    bytes equal the whole-buffer cut, and the ingest MB/s is reported."""
+    a, b = synth.generate(60_000, paired=True, seed=64)
+    pa, pb = tmp_path / "i_1.fq", tmp_path / "i_2.fq"
+    pa.write_bytes(a)
+    pb.write_bytes(b)
+    want = len(fq.cut_pe(a, b, 1 << 20))
+    rates = {}
+    for dev in (1, 8):
+        r = _run(["-c", "-f", "--ingest-only", "--devices", str(dev), "--contexts", "1", "--batch", "2",
+                  "--block-size", "1", "-1", str(pa), "-2", str(pb), "-o", str(tmp_path / "g")], tmp_path)
+        assert r.returncode == 0, r.stderr
+        line = [ln for ln in r.stderr.decode().splitlines() if "block(s)" in ln][0]
+        assert line.split()[1] == str(want) and f" {len(a) + len(b)} -> " in line, line
+        rates[dev] = float(line.split()[-2])
+    with capsys.disabled():
+        print(f"\n[ingest] reader + PE cut, 1 MiB blocks: 1 consumer {rates[1]:.0f} MB/s, "
+              f"8 consumers {rates[8]:.0f} MB/s")
