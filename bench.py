@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import argparse
 import hashlib
+import shutil
 import json
 import os
 import socket
@@ -83,10 +84,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--e2e-batches", type=int, default=-1,
                     help="batches written as FASTQ files for the end-to-end seqarc_amd -c run (-1: all at one "
-                         "rank, none with more; 0: skip)")
+                         "rank; rank 0's first with more ranks, run once through seqarc_amd --devices N; 0: skip)")
     ap.add_argument("--e2e-repeat", type=int, default=0,
                     help="the end-to-end files hold the e2e batches this many times over (a longer stream, so "
-                         "pipeline fill and drain weigh less; 0: 3 at one rank, 1 with more ranks)")
+                         "pipeline fill and drain weigh less; 0: 3 at one rank, 2 x N with N ranks)")
+    ap.add_argument("--e2e-batch", type=int, default=0, help="blocks per CLI batch in the e2e run (0: the bench's)")
     ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--e2e-log", default=None, help="write the CLI's stderr (-v stage lines, SA_TRACE) here")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
@@ -98,8 +100,8 @@ def parse_args(argv=None):
         a.se = True
         if a.pairs == 5_000_000:
             a.pairs = 60_000
-    if a.e2e_batches < 0:   # (one rank only by default: N ranks would each write their own files to /dev/shm)
-        a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 0
+    if a.e2e_batches < 0:   # (N ranks: rank 0's first batch, N x 2 times over, one seqarc_amd --devices N run)
+        a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 1
     if a.dry_run:
         a.pairs = min(a.pairs, 3000)
         a.block_size = min(a.block_size, 300_000)
@@ -167,16 +169,20 @@ def make_batch(gid: int, args, workers: int, files=None):
     return fq.blocks_from_fastq(t1, t2, args.block_size)
 
 
-def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int):
+def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, devices: int = 1,
+               ingest_only: bool = False):
     """`seqarc_amd -c` (the streaming reader / parser / encoder / writer
     pipeline) on the FASTQ files on disk: wall time of the whole process, and
     its own clock (device init to the closed .arc).  The archive's blocks must
-    be the bench's blocks of the same input, byte for byte."""
+    be the bench's blocks of the same input, byte for byte.  devices > 1: the
+    whole node in one process (batches dealt over devices x contexts);
+    ingest_only: the reader and the block cut alone (--dry-run: no device)."""
     from fastqueeze_amd import build
     out = os.path.join(os.path.dirname(files[0]), "e2e")
     cmd = [build.CLI, "-c", "-f", "-v", "-t", str(threads), "-1", files[0]] + (["-2", files[1]] if len(files) > 1 else []) \
         + ["-o", out, "--contexts", str(contexts), "--batch", str(batch), "--slevel", str(args.slevel),
-           "--qlevel", str(args.qlevel)]
+           "--qlevel", str(args.qlevel), "--block-size", str(max(1, args.block_size >> 20))] \
+        + (["--devices", str(devices)] if devices > 1 else []) + (["--ingest-only"] if ingest_only else [])
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     wall = time.perf_counter() - t0
@@ -188,7 +194,8 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int):
     in_bytes = sum(os.path.getsize(f) for f in files)
     with open(out + ".arc", "rb") as f:
         arc = f.read()
-    same = arc[16:16 + len(expect)] == expect   # (the batch's last, short block merges with the next batch's text)
+    same = None if ingest_only else arc[16:16 + len(expect)] == expect   # (a batch's last, short block merges
+    #                                                                          with the next batch's text)
     clock, stages = None, None
     for ln in r.stderr.splitlines():
         if "MB/s" in ln:
@@ -197,9 +204,25 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int):
             stages = ln.split(": ", 1)[1]
     os.remove(out + ".arc")
     return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
-            "cli_clock_mb_s": clock, "cli_stages": stages, "fastq_bytes": in_bytes, "contexts": contexts, "batch_blocks": batch,
-            "parse": "device (sa_stage_text from page-locked text windows)", "leading_blocks_identical_to_bench": same,
-            "command": "seqarc_amd -c -1 r1.fq -2 r2.fq (FASTQ on disk, page cache warm)"}
+            "cli_clock_mb_s": clock, "cli_stages": stages, "fastq_bytes": in_bytes, "devices": devices,
+            "contexts": contexts, "batch_blocks": batch,
+            "parse": "none (--ingest-only)" if ingest_only else "device (sa_stage_text from page-locked text windows)",
+            "leading_blocks_identical_to_bench": same,
+            "command": " ".join(os.path.basename(c) if i == 0 else c for i, c in enumerate(cmd))}
+
+
+def replicate(files, times: int):
+    """Append each file to itself until it holds its content `times` over."""
+    for f in files:
+        size0 = os.path.getsize(f)
+        with open(f, "ab") as dst:
+            for _ in range(times - 1):
+                with open(f, "rb") as src:
+                    left = size0
+                    while left > 0:
+                        chunk = src.read(min(left, 256 << 20))
+                        dst.write(chunk)
+                        left -= len(chunk)
 
 
 def stream_sizes(block: bytes) -> dict:
@@ -363,7 +386,7 @@ def main():
     t0 = time.time()
     batches = []
     e2e_files = None
-    if args.e2e_batches > 0 and not args.dry_run:
+    if args.e2e_batches > 0 and rank == 0:
         d = os.path.join(args.e2e_dir, f"seqarc_bench_{os.getpid()}")
         os.makedirs(d, exist_ok=True)
         e2e_files = [os.path.join(d, "r1.fq")] + ([] if args.se else [os.path.join(d, "r2.fq")])
@@ -388,8 +411,16 @@ def main():
             local_out.append((g, b"".join(hashlib.sha256(o).digest() for o in outs)))
         allb = gather_blocks(local_out, world * args.batches) if world > 1 else [o for _, o in local_out]
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "batches": len(allb),
-                              "blocks_digest": hashlib.sha256(b"".join(allb)).hexdigest()}), flush=True)
+            line = {"dry_run": True, "n_gpus": world, "batches": len(allb),
+                    "blocks_digest": hashlib.sha256(b"".join(allb)).hexdigest()}
+            if e2e_files:   # the whole-node host path without a device: reader + cut dealt to N x C consumers
+                try:
+                    replicate(e2e_files, args.e2e_repeat or 2 * world)
+                    line["end_to_end"] = end_to_end(args, e2e_files, args.contexts, b"", len(batches[0]), 1,
+                                                    devices=world, ingest_only=True)
+                finally:
+                    shutil.rmtree(os.path.dirname(e2e_files[0]), True)
+            print(json.dumps(line), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -559,36 +590,24 @@ def main():
         e.close()
     for i in inputs:
         i.close()
+    # the whole host path: the CLI reads the FASTQ from disk (HBM of every rank's
+    # contexts released above).  One rank: its batches, 3 times over.  N ranks:
+    # rank 0's first batch 2 N times over through one seqarc_amd --devices N
+    # (the whole node in one process, the reference's one reader feeding every
+    # encoder); the other ranks wait
+    barrier()
     if e2e_files:
-        # the whole host path: the CLI reads the FASTQ from disk (HBM of the bench's
-        # contexts released above); per rank, then max over ranks
-        barrier()
         expect = b"".join(outs if args.e2e_batches == 1 else outs[:-1])
-        rep = args.e2e_repeat or (3 if world == 1 else 1)
-        for f in e2e_files:   # the same FASTQ again, appended (rep - 1) times
-            size0 = os.path.getsize(f)
-            with open(f, "ab") as dst:
-                for _ in range(rep - 1):
-                    with open(f, "rb") as src:
-                        left = size0
-                        while left > 0:
-                            chunk = src.read(min(left, 256 << 20))
-                            dst.write(chunk)
-                            left -= len(chunk)
+        replicate(e2e_files, args.e2e_repeat or (3 if world == 1 else 2 * world))
         try:
             # batches of the bench's size (69 blocks): pass R of a batch takes as long for 28 blocks as
             # for 69, so smaller batches lose the coder's parallelism
-            e2e = end_to_end(args, e2e_files, args.contexts, expect, len(keep["verify"]),
-                             max(1, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
+            e2e = end_to_end(args, e2e_files, args.contexts, expect, args.e2e_batch or len(keep["verify"]),
+                             share["usable"], devices=world)
         finally:
             shutil.rmtree(os.path.dirname(e2e_files[0]), True)
-        if world > 1:
-            t = torch.tensor([e2e["wall_s"], float(e2e["fastq_bytes"])], dtype=torch.float64)
-            tm = t.clone()
-            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            e2e["value"] = round(float(t[1]) / float(tm[0]) / 1e6, 1)
         res["end_to_end"] = e2e
+    barrier()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

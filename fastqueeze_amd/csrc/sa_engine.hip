@@ -88,14 +88,12 @@ struct FrontShare {
     uint64_t next_ticket = 0, serving = 0;
     hipEvent_t ev_free = nullptr;
     bool have_ev = false;
-    DBuf d_counts, d_name_p, d_name_s, d_maxlen, d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
+    DBuf d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux, d_seq_longs, d_nseq_long, d_short_at;
-    DBuf d_dege_maxq;   // per read: maxq of the N / IUPAC side streams (k_prep_sq16 -> k_emit, k_emit_sq)
     std::vector<DBuf*> buffers()
     {
-        return {&d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1],
-                &d_auxs_k, &d_auxs_v, &d_hist_seq, &d_hist_aux, &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux,
-                &d_seq_longs, &d_nseq_long, &d_short_at, &d_dege_maxq};
+        return {&d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_auxs_k, &d_auxs_v, &d_hist_seq, &d_hist_aux,
+                &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_seq_longs, &d_nseq_long, &d_short_at};
     }
     uint64_t held_bytes()
     {
@@ -226,6 +224,10 @@ struct sa_ctx {
     DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess;   // -l (rblock)
     // reference path: per read the alignment of both carried states, status, the
     // alignment columns, the SEQ skip flags (sa_hash.hip, align_front)
+    // per-read counts of every column (k_prep, k_prep_sq16 -> k_scan_reads ->
+    // the emitters), name prefix / suffix, the per-block running name maximum,
+    // the N / IUPAC maxq: this context's own (the prep runs before its front turn)
+    DBuf d_counts, d_name_p, d_name_s, d_maxlen, d_dege_maxq;
     DBuf d_al_ret[2], d_al_rev[2], d_al_pos[2], d_al_mp[2], d_al_mt[2], d_al_st, d_al_sel, d_al_scr, d_acounts, d_atot,
         d_seq_skip;
     // the last aligned batch's block plans (a re-run of the same batch -- the
@@ -247,7 +249,7 @@ struct sa_ctx {
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
-                &d_seq_skip};
+                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq};
     }
     uint64_t held_bytes()
     {
@@ -1055,16 +1057,15 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         return -1;
     }
     const bool trace = al && std::getenv("SA_ALN_TRACE");
-    // the front (up to the short model runs) holds the device's front scratch
-    FrontTurn front_lock(F, st);
-    if (trace) fprintf(stderr, "[align] front turn taken\n");
-    SA_CHECK(c, F->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
-    SA_CHECK(c, F->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
-    uint8_t* dege_maxq = c->prep_wave ? nullptr : F->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
+    // per-read counts and their scan run before the front turn (this
+    // context's own buffers): the turn starts at the emitters
+    SA_CHECK(c, c->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
+    SA_CHECK(c, c->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
+    uint8_t* dege_maxq = c->prep_wave ? nullptr : c->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
     SA_CHECK(c, c->d_totals.ensure((size_t)nbk * NCOL * 4));
-    SA_CHECK(c, F->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, F->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, F->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
+    SA_CHECK(c, c->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
     SA_CHECK(c, c->d_err.ensure(16));
     SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 16, st));
 
@@ -1096,24 +1097,23 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     } else {
         SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
     }
-    if (F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));   // the previous front is done with it
     ev_begin(c, PH_PREP, st);
     if (lossy && run_rblock(c, cfg->lossy, I->seq_bytes, bv)) return -1;
     // thread-per-read kernels: one thread per read (a grid-stride variant with
     // 8 workgroups per CU measured slower: k_prep 1.2 -> 1.7 ms, k_emit 6.8 -> 9.4)
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
-        hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
-                           F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(), d_err);
+        hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                           c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
         if (c->prep_wave)   // (SA_PREP_WAVE=1: the wave-per-read variant, for A/B)
             hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
-                               F->d_counts.as<uint32_t>(), d_err);
+                               c->d_counts.as<uint32_t>(), d_err);
         else
             hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                               F->d_counts.as<uint32_t>(), d_err, F->d_dege_maxq.as<uint8_t>());
+                               c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>());
     }
-    hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, F->d_counts.as<uint32_t>(),
-                       c->d_totals.as<uint32_t>(), F->d_maxlen.as<uint16_t>());
+    hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
+                       c->d_totals.as<uint32_t>(), c->d_maxlen.as<uint16_t>());
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_PREP, st);
     std::vector<uint32_t> tot((size_t)nbk * NCOL);
@@ -1146,6 +1146,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         c->total_stream_syms += tk.n;
     }
     std::vector<AsmBlock> asmb = bp.asmb;
+
+    // ---- the front (emitters, sorts, replays up to the short model runs) holds
+    //      the device's front scratch ----
+    FrontTurn front_lock(F, st);
+    if (trace) fprintf(stderr, "[align] front turn taken\n");
+    if (F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));   // the previous front is done with it
 
     // ---- device buffers ----
     // slack: the replay loops read up to 2 chunks past a run's end, pass R one
@@ -1230,22 +1236,22 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     }
     SA_CHECK(c, hipMemsetAsync(c->d_first_sq.p, 0xff, 4 * tasks.size(), st));
     if (nr) {
-        hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, F->d_counts.as<uint32_t>(),
-                           c->d_totals.as<uint32_t>(), F->d_name_p.as<int16_t>(), F->d_name_s.as<int16_t>(),
-                           F->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
+        hipLaunchKernelGGL(k_emit, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                           c->d_totals.as<uint32_t>(), c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(),
+                           c->d_maxlen.as<uint16_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                            akb[0]->as<uint32_t>(), nullptr, d_err, dege_maxq);   // (AUX values: the index, run_sort)
         if (c->emit_wave) {   // (SA_EMIT_WAVE=1: round 2's wave-per-read SEQ / QUAL, for A/B)
             hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
-                               F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
+                               c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                                akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh,
                                (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE));
         } else {
             hipLaunchKernelGGL(seq_sh ? k_emit_sq16<2> : k_emit_sq16<0>, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0,
-                               st, bv, F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
+                               st, bv, c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
                                F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr);
             if (dege_maxq && n_ch)   // the N / IUPAC side streams of the reads that have such bases
                 hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
-                                   F->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
+                                   c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
                                    F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr,
                                    c->d_totals.as<uint32_t>(), dege_maxq, seq_sh, (uint32_t)EMIT_DEGE);
         }

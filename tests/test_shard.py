@@ -42,3 +42,8 @@ def test_bench_gpus2_launches_two_gloo_ranks_and_gathers_in_order():
     assert one["batches"] == two["batches"] == 4
     # the same global batches, encoded on two ranks and gathered in order
     assert one["blocks_digest"] == two["blocks_digest"]
+    # the whole-node end-to-end leg: rank 0's first batch, 2 x 2 times over, through one
+    # seqarc_amd --devices 2 (here --ingest-only: the reader and the cut dealing batches)
+    e2e = two["end_to_end"]
+    assert e2e["devices"] == 2 and "--devices 2" in e2e["command"] and e2e["fastq_bytes"] > 0
+    assert e2e["value"] > 0 and "block(s)" not in e2e["cli_stages"]
