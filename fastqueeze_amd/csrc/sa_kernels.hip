@@ -771,7 +771,6 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
                                                    uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
                                                    uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val)
 {
-    constexpr uint32_t seq_sh = SH;
     __shared__ uint32_t stk[256 / ER][ER_STEP];
     __shared__ uint32_t stv[SH ? 1 : 256 / ER][SH ? 1 : ER_STEP];
     const uint32_t rl = threadIdx.x & (ER - 1), rw = threadIdx.x / ER;

@@ -239,12 +239,250 @@ struct Buf {
     bool empty() const { return n == 0; }
 };
 
+// ---- gzip input -------------------------------------------------------------
+// The reference inflates with gzread on its reader thread.  Here a producer
+// thread per input inflates ahead of the block cut into a bounded queue of
+// chunks.  BGZF files (bgzip: gzip members of <= 64 KiB with the 'BC' extra
+// field giving each member's size) are inflated in parallel: the producer reads
+// a slab of members, `workers` threads inflate them into their places (each
+// member's ISIZE gives its output size) and check their CRCs.  Other gzip files
+// (one member, or several concatenated) inflate on the producer thread.
+struct GzStream {
+    int fd = -1;
+    int workers = 1;
+    bool bgzf = false;
+    std::thread prod;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::vector<uint8_t>> q;
+    size_t q_bytes = 0;
+    bool done = false, failed = false, stop = false;
+    std::vector<uint8_t> cur;
+    size_t cur_at = 0;
+    static constexpr size_t kMaxQueued = 512u << 20;
+
+    bool start(int f, int w)
+    {
+        fd = f;
+        workers = std::max(1, w);
+        uint8_t h[18];
+        const ssize_t r = ::pread(fd, h, sizeof h, 0);
+        bgzf = r == 18 && h[0] == 0x1f && h[1] == 0x8b && h[2] == 8 && (h[3] & 4) && h[10] == 6 && h[11] == 0 &&
+               h[12] == 'B' && h[13] == 'C' && h[14] == 2 && h[15] == 0;
+        prod = std::thread([this]() {
+            const bool ok = bgzf ? run_bgzf() : run_plain();
+            std::lock_guard<std::mutex> g(mu);
+            failed = !ok;
+            done = true;
+            cv.notify_all();
+        });
+        return true;
+    }
+    bool push(std::vector<uint8_t>&& v)   // false: the reader went away
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || q_bytes < kMaxQueued; });
+        if (stop) return false;
+        q_bytes += v.size();
+        q.push_back(std::move(v));
+        cv.notify_all();
+        return true;
+    }
+    long readn(uint8_t* dst, size_t n, uint64_t& at)
+    {
+        size_t got = 0;
+        while (got < n) {
+            const ssize_t r = ::pread(fd, dst + got, n - got, (off_t)(at + got));
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0) return -1;
+            if (r == 0) break;
+            got += (size_t)r;
+        }
+        at += got;
+        return (long)got;
+    }
+    // one member or several concatenated (gzread's reading of them)
+    bool run_plain()
+    {
+        z_stream z{};
+        if (inflateInit2(&z, 15 + 16) != Z_OK) return false;
+        std::vector<uint8_t> in(4u << 20);
+        uint64_t at = 0;
+        bool eof = false, member_end = false;
+        std::vector<uint8_t> out(8u << 20);
+        size_t have = 0;
+        for (;;) {
+            if (z.avail_in == 0 && !eof) {
+                const long r = readn(in.data(), in.size(), at);
+                if (r < 0) { inflateEnd(&z); return false; }
+                if (r == 0) eof = true;
+                z.next_in = in.data();
+                z.avail_in = (uInt)r;
+            }
+            if (z.avail_in == 0 && eof) break;
+            if (member_end) {   // the next member, if it is one (trailing bytes otherwise end the stream)
+                if (z.avail_in < 2 && !eof) {
+                    // (rare: a member boundary at the end of a read slab) keep the byte, read more
+                    memmove(in.data(), z.next_in, z.avail_in);
+                    const long r = readn(in.data() + z.avail_in, in.size() - z.avail_in, at);
+                    if (r < 0) { inflateEnd(&z); return false; }
+                    if (r == 0) eof = true;
+                    z.next_in = in.data();
+                    z.avail_in += (uInt)r;
+                }
+                if (z.avail_in < 2 || z.next_in[0] != 0x1f || z.next_in[1] != 0x8b) break;
+                inflateReset(&z);
+                member_end = false;
+            }
+            z.next_out = out.data() + have;
+            z.avail_out = (uInt)(out.size() - have);
+            const int rc = inflate(&z, Z_NO_FLUSH);
+            have = out.size() - z.avail_out;
+            if (rc == Z_STREAM_END) member_end = true;
+            else if (rc != Z_OK && rc != Z_BUF_ERROR) { inflateEnd(&z); return false; }
+            else if (rc == Z_BUF_ERROR && z.avail_in == 0 && eof) { inflateEnd(&z); return false; }   // truncated
+            if (have == out.size() || (member_end && have > (6u << 20))) {
+                out.resize(have);
+                if (!push(std::move(out))) { inflateEnd(&z); return true; }
+                out.assign(8u << 20, 0);
+                have = 0;
+            }
+        }
+        inflateEnd(&z);
+        if (!member_end && at > 0) return false;   // ended inside a member
+        out.resize(have);
+        if (have && !push(std::move(out))) return true;
+        return true;
+    }
+    // BGZF: slabs of whole members, inflated in parallel; the next slab is read
+    // while the workers inflate this one
+    bool run_bgzf()
+    {
+        const size_t kSlab = 32u << 20;
+        std::vector<uint8_t> slabs[2] = {std::vector<uint8_t>(kSlab), std::vector<uint8_t>(kSlab)};
+        int cs = 0;
+        size_t carry = 0;
+        uint64_t at = 0;
+        bool eof = false;
+        struct Mem { size_t off, len; uint64_t out; uint32_t crc, isize; };
+        auto fill_slab = [&](std::vector<uint8_t>& sl) -> bool {   // after the carry
+            const long r = readn(sl.data() + carry, kSlab - carry, at);
+            if (r < 0) return false;
+            if ((size_t)r < kSlab - carry) eof = true;
+            carry += (size_t)r;
+            return true;
+        };
+        if (!fill_slab(slabs[0])) return false;
+        while (carry) {
+            std::vector<uint8_t>& slab = slabs[cs];
+            std::vector<Mem> ms;
+            size_t p = 0;
+            uint64_t total = 0;
+            while (p + 18 <= carry) {
+                const uint8_t* h = slab.data() + p;
+                if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return false;
+                const size_t xlen = h[10] | (size_t)h[11] << 8;
+                size_t bsize = 0;
+                for (size_t x = 12; x + 4 <= 12 + xlen && p + x + 4 <= carry;) {   // the 'BC' subfield
+                    const size_t sl = h[x + 2] | (size_t)h[x + 3] << 8;
+                    if (h[x] == 'B' && h[x + 1] == 'C' && sl == 2) bsize = (h[x + 4] | (size_t)h[x + 5] << 8) + 1;
+                    x += 4 + sl;
+                }
+                if (!bsize || bsize < 12 + xlen + 8) return false;   // not BGZF after all
+                if (p + bsize > carry) break;                      // the member continues in the next slab
+                const uint8_t* t = h + bsize - 8;
+                Mem m{p + 12 + xlen, bsize - 12 - xlen - 8, total,
+                      (uint32_t)(t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24),
+                      (uint32_t)(t[4] | t[5] << 8 | t[6] << 16 | (uint32_t)t[7] << 24)};
+                total += m.isize;
+                ms.push_back(m);
+                p += bsize;
+            }
+            if (ms.empty()) return false;   // a truncated or oversized member
+            std::vector<uint8_t> out(total);
+            std::atomic<size_t> next{0};
+            std::atomic<bool> bad{false};
+            auto work = [&]() {
+                z_stream z{};
+                if (inflateInit2(&z, -15) != Z_OK) { bad = true; return; }
+                for (size_t i; (i = next.fetch_add(1)) < ms.size();) {
+                    const Mem& m = ms[i];
+                    if (m.isize == 0) {   // (the BGZF end-of-file marker: an empty member)
+                        if (m.crc != 0) bad = true;
+                        continue;
+                    }
+                    inflateReset(&z);
+                    z.next_in = slab.data() + m.off;
+                    z.avail_in = (uInt)m.len;
+                    z.next_out = out.data() + m.out;
+                    z.avail_out = (uInt)m.isize;
+                    const int rc = inflate(&z, Z_FINISH);
+                    if (rc != Z_STREAM_END || z.avail_out != 0 || crc32(0L, out.data() + m.out, (uInt)m.isize) != m.crc)
+                        bad = true;
+                }
+                inflateEnd(&z);
+            };
+            std::vector<std::thread> th;
+            for (int k = 0; k < workers; k++) th.emplace_back(work);
+            // the next slab: this one's partial last member, then fresh bytes
+            std::vector<uint8_t>& nx = slabs[cs ^ 1];
+            const size_t rest = carry - p;
+            memcpy(nx.data(), slab.data() + p, rest);
+            carry = rest;
+            const bool rd = eof || fill_slab(nx);
+            for (auto& x : th) x.join();
+            if (bad || !rd) return false;
+            if (!out.empty() && !push(std::move(out))) return true;
+            cs ^= 1;
+            if (eof && carry && carry == rest && rest < 18) return false;   // trailing bytes that are no member
+        }
+        return true;
+    }
+    // up to n bytes into dst; 0 at the end; -1 on a gzip error
+    long read(uint8_t* dst, size_t n)
+    {
+        size_t got = 0;
+        while (got < n) {
+            if (cur_at == cur.size()) {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !q.empty() || done; });
+                if (q.empty()) {
+                    if (failed) return -1;
+                    break;
+                }
+                cur = std::move(q.front());
+                q.pop_front();
+                q_bytes -= cur.size();
+                cur_at = 0;
+                cv.notify_all();
+            }
+            const size_t k = std::min(n - got, cur.size() - cur_at);
+            memcpy(dst + got, cur.data() + cur_at, k);
+            cur_at += k;
+            got += k;
+        }
+        return (long)got;
+    }
+    ~GzStream()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        if (prod.joinable()) prod.join();
+    }
+};
+
 // ---- input ---------------------------------------------------------------
-// getFileType@0x40d9f0 (gzip magic); plain files are read with read(2), gzip
-// through zlib's gzread.
+// getFileType@0x40d9f0 (gzip magic); plain files are read with read(2) /
+// parallel pread slices, gzip through a GzStream (inflated ahead, BGZF in
+// parallel).
+int g_gz_workers = 8;   // inflate threads per BGZF input (-t / 2 for PE)
+
 struct Input {
     int fd = -1;
-    gzFile gz = nullptr;
+    std::unique_ptr<GzStream> gz;
     bool is_gz = false, eof = false, seekable = true;
     uint64_t off = 0;   // file offset of the next byte (plain files)
     bool open(const char* path)
@@ -254,10 +492,8 @@ struct Input {
         unsigned char m[2] = {0, 0};
         is_gz = ::pread(fd, m, 2, 0) == 2 && m[0] == 0x1f && m[1] == 0x8b;
         if (is_gz) {
-            gz = gzdopen(fd, "rb");
-            if (!gz) return false;
-            gzbuffer(gz, 1 << 20);
-            fd = -1;
+            gz.reset(new GzStream());
+            gz->start(fd, g_gz_workers);
         }
         return true;
     }
@@ -315,8 +551,7 @@ struct Input {
         while (got < n && !eof) {
             long r;
             if (is_gz) {
-                const unsigned want = (unsigned)std::min<size_t>(n - got, 1u << 30);
-                r = gzread(gz, b.data() + have + got, want);
+                r = gz->read(b.data() + have + got, n - got);
             } else {
                 r = (long)::read(fd, b.data() + have + got, n - got);
                 if (r < 0 && errno == EINTR) continue;
@@ -331,7 +566,7 @@ struct Input {
     }
     ~Input()
     {
-        if (gz) gzclose(gz);
+        gz.reset();
         if (fd >= 0) ::close(fd);
     }
 };
@@ -430,6 +665,7 @@ struct Job {                     // one block between the reader and the writer
     std::unique_ptr<Parsed> p;     // host parse (--host-parse; block 0 for the ID template)
     Buf<uint8_t> out;             // the encoded block
     int state = 0;                // 0 read, 1 parsed, 2 encoded
+    uint32_t crc = 0;             // --ingest-only: CRC-32 of t1 then t2 (the writer folds them in order)
 };
 
 // getFirstLine@0x431eb0: the '+' line of the first record carries no ID
@@ -562,6 +798,8 @@ int compress(const Options& o)
 {
     const auto t_start = std::chrono::steady_clock::now();
     const bool pe = o.f2 && *o.f2;
+    // inflate threads per BGZF input: the -t share (the device parse leaves the host threads free)
+    g_gz_workers = std::max(2, (o.threads > 0 ? o.threads : 16) / (pe ? 2 : 1));
     Input in1, in2;
     struct stat sb;
     for (const char* f : {o.f1, pe ? o.f2 : nullptr}) {
@@ -831,6 +1069,9 @@ int compress(const Options& o)
                         staged += (int64_t)js.size();
                     }
                     for (size_t i = 0; i < js.size(); i++) {
+                        uint32_t c = (uint32_t)crc32(0L, js[i]->t1.data(), (uInt)js[i]->t1.size());
+                        if (pe) c = (uint32_t)crc32(c, js[i]->t2.data(), (uInt)js[i]->t2.size());
+                        js[i]->crc = c;
                         texts.put(js[i]->t1);
                         texts.put(js[i]->t2);
                         outs[i] = sa_out{nullptr, 0, 0};
@@ -923,6 +1164,7 @@ int compress(const Options& o)
     int rc = 0;
     std::vector<sa_arc_block> info;
     uint64_t total = 0;
+    uint32_t text_crc = 0;
     uint8_t hdr[16] = {0};
     if (!fo) {
         fail("cannot write " + path);
@@ -946,6 +1188,7 @@ int compress(const Options& o)
             break;
         }
         info.push_back(sa_arc_block{(uint32_t)j->out.size(), lng, j->text1, j->text2});
+        text_crc = (uint32_t)crc32_combine(text_crc, j->crc, (z_off_t)(j->text1 + j->text2));
         total += j->out.size();
         if (j->p) pool.put(std::move(j->p));
         {
@@ -991,6 +1234,7 @@ int compress(const Options& o)
                     t_ctx, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
                     parse_busy.load(), nparse, fill_busy, cut_busy, stage_busy.load(),
                     dev_parse ? "device" : "host");
+        if (o.ingest_only) fprintf(stderr, "seqarc_amd: ingest text crc32 %08x\n", text_crc);
         fprintf(stderr, "seqarc_amd: %zu block(s), %llu -> %llu bytes (%.2fx), %.3f s, %.1f MB/s\n", info.size(),
                 (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
                 (double)total_in / (double)(16 + total + tl), secs, (double)total_in / secs / 1e6);

@@ -239,3 +239,51 @@ def test_ingest_only_eight_way(tmp_path, capsys):
     with capsys.disabled():
         print(f"\n[ingest] reader + PE cut, 1 MiB blocks: 1 consumer {rates[1]:.0f} MB/s, "
               f"8 consumers {rates[8]:.0f} MB/s")
+
+
+def _bgzf(data: bytes, level: int = 1) -> bytes:
+    """bgzip's format: gzip members of <= 64 KiB input with the 'BC' extra field
+    (the member size), then the 28-byte empty end-of-file member."""
+    import struct
+    import zlib
+    out = bytearray()
+    for i in range(0, len(data), 65280):
+        chunk = data[i:i + 65280]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        cd = c.compress(chunk) + c.flush()
+        out += b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00"
+        out += struct.pack("<H", 18 + len(cd) + 8 - 1) + cd + struct.pack("<II", zlib.crc32(chunk), len(chunk))
+    return bytes(out) + bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def test_gzip_ingest_plain_multimember_bgzf(tmp_path, capsys):
+    """gzip inputs through the inflate-ahead reader: one member, concatenated
+    members and BGZF (members inflated in parallel) give the same blocks and
+    the same text (CRC-32 over every block's text in order) as the plain file;
+    a truncated gzip file is an error.  The ingest MB/s of each is reported."""
+    import gzip
+    a, b = synth.generate(40_000, paired=True, seed=65)
+    files = {"plain": (a, b), "gz": (gzip.compress(a, 1), gzip.compress(b, 1)),
+             "multi": (gzip.compress(a[:len(a) // 3], 1) + gzip.compress(a[len(a) // 3:], 1),
+                       gzip.compress(b[:7], 1) + gzip.compress(b[7:], 1)),
+             "bgzf": (_bgzf(a), _bgzf(b))}
+    got = {}
+    for k, (x, y) in files.items():
+        p1, p2 = tmp_path / f"{k}_1.fq", tmp_path / f"{k}_2.fq"
+        p1.write_bytes(x)
+        p2.write_bytes(y)
+        r = _run(["-c", "-f", "--ingest-only", "--devices", "2", "--contexts", "2", "--batch", "2", "--block-size",
+                  "1", "-t", "8", "-1", str(p1), "-2", str(p2), "-o", str(tmp_path / k)], tmp_path)
+        assert r.returncode == 0, (k, r.stderr)
+        err = r.stderr.decode()
+        crc = [ln for ln in err.splitlines() if "crc32" in ln][0].split()[-1]
+        line = [ln for ln in err.splitlines() if "block(s)" in ln][0]
+        got[k] = (crc, line.split()[1], line.split(" -> ")[0].split()[-1], float(line.split()[-2]))
+    assert len({v[:3] for v in got.values()}) == 1, got
+    assert got["plain"][1] == str(len(fq.cut_pe(a, b, 1 << 20)))
+    bad = tmp_path / "bad_1.fq"
+    bad.write_bytes(files["gz"][0][: len(files["gz"][0]) // 2])
+    r = _run(["-c", "-f", "--ingest-only", "-1", str(bad), "-o", str(tmp_path / "bad")], tmp_path)
+    assert r.returncode != 0
+    with capsys.disabled():
+        print("\n[ingest] " + ", ".join(f"{k} {v[3]:.0f} MB/s" for k, v in got.items()))
