@@ -89,6 +89,8 @@ def parse_args(argv=None):
                     help="the end-to-end files hold the e2e batches this many times over (a longer stream, so "
                          "pipeline fill and drain weigh less; 0: 3 at one rank, 2 x N with N ranks)")
     ap.add_argument("--e2e-batch", type=int, default=0, help="blocks per CLI batch in the e2e run (0: the bench's)")
+    ap.add_argument("--e2e-gz-blocks", type=int, default=20,
+                    help="the gzip end-to-end legs (BGZF, member-serial gzip) on this many blocks of batch 0 (0: skip)")
     ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--e2e-log", default=None, help="write the CLI's stderr (-v stage lines, SA_TRACE) here")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
@@ -209,6 +211,42 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
             "parse": "none (--ingest-only)" if ingest_only else "device (sa_stage_text from page-locked text windows)",
             "leading_blocks_identical_to_bench": same,
             "command": " ".join(os.path.basename(c) if i == 0 else c for i, c in enumerate(cmd))}
+
+
+def write_gz(src: str, dst: str, nbytes: int, kind: str, threads: int):
+    """The first nbytes of src as gzip: kind "bgzf" (bgzip's <= 64 KiB members with
+    the 'BC' size field, inflated in parallel by the reader) or "gzip" (one member
+    per 16 MiB, inflated member after member).  Compressed on host threads (zlib
+    releases the GIL)."""
+    import struct
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+
+    def bgzf(part: bytes) -> bytes:
+        out = bytearray()
+        for i in range(0, len(part), 65280):
+            chunk = part[i:i + 65280]
+            c = zlib.compressobj(1, zlib.DEFLATED, -15)
+            cd = c.compress(chunk) + c.flush()
+            out += b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00"
+            out += struct.pack("<H", 25 + len(cd)) + cd + struct.pack("<II", zlib.crc32(chunk), len(chunk))
+        return bytes(out)
+
+    def member(part: bytes) -> bytes:
+        c = zlib.compressobj(1, zlib.DEFLATED, 31)
+        return c.compress(part) + c.flush()
+
+    with open(src, "rb") as f:
+        data = f.read(nbytes)
+    step = 16 << 20 if kind == "gzip" else 65280 * 256
+    parts = [data[i:i + step] for i in range(0, len(data), step)]
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        comp = list(ex.map(bgzf if kind == "bgzf" else member, parts))
+    with open(dst, "wb") as f:
+        for c in comp:
+            f.write(c)
+        if kind == "bgzf":
+            f.write(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
 
 
 def replicate(files, times: int):
@@ -596,6 +634,32 @@ def main():
     # (the whole node in one process, the reference's one reader feeding every
     # encoder); the other ranks wait
     barrier()
+    if e2e_files and world == 1 and args.e2e_gz_blocks > 0:
+        # gzip inputs (the usual .fq.gz): the first blocks of batch 0 as BGZF and as
+        # member-serial gzip, through the inflate-ahead reader; the archive's blocks
+        # must be the bench's
+        nb = min(args.e2e_gz_blocks, len(keep["verify"]))
+        vb = keep["verify"][:nb]
+        sizes = [sum(b.text1 or b.text_bytes for b in vb)] + ([sum(b.text2 for b in vb)] if len(e2e_files) > 1 else [])
+        gz = {}
+        for kind in ("bgzf", "gzip"):
+            gzf = [f + "." + kind + ".gz" for f in e2e_files]
+            t0 = time.perf_counter()
+            for f, g, n in zip(e2e_files, gzf, sizes):
+                write_gz(f, g, n, kind, share["usable"])
+            gzb = sum(os.path.getsize(g) for g in gzf)
+            log(f"[rank 0] {kind} input: {gzb / 1e6:.0f} MB ({time.perf_counter() - t0:.1f}s)")
+            try:
+                r = end_to_end(args, gzf, args.contexts, b"".join(outs[:nb]), args.e2e_batch or len(vb),
+                               share["usable"])
+            finally:
+                for g in gzf:
+                    os.remove(g)
+            r["fastq_bytes"] = sum(sizes)
+            r["value"] = round(sum(sizes) / r["wall_s"] / 1e6, 1)
+            r["gz_bytes"] = gzb
+            gz[kind] = r
+        res["end_to_end_gz"] = gz
     if e2e_files:
         expect = b"".join(outs if args.e2e_batches == 1 else outs[:-1])
         replicate(e2e_files, args.e2e_repeat or (3 if world == 1 else 2 * world))
