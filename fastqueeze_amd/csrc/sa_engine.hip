@@ -27,6 +27,10 @@ namespace {
 
 std::atomic<uint32_t> g_grows{0};   // buffer re-allocations (each hipFree synchronises the device)
 std::atomic<uint64_t> g_alloc_ns{0};  // host time in hipMalloc / hipFree (SA_TRACE)
+// (sa_set_reserve) a context whose batches grow -- the command line's ramp of
+// first batches -- allocates for its full batch from the first one: a
+// re-allocation's hipFree would synchronise the device under the other contexts
+thread_local double g_reserve_scale = 1.0;
 
 struct DBuf {
     void* p = nullptr;
@@ -43,6 +47,7 @@ struct DBuf {
         // slack for the next, slightly larger batch: a re-allocation's hipFree
         // synchronises the whole device, stalling every other context on it
         size_t want = std::max(bytes + bytes / 16, cap + cap / 16);
+        if (g_reserve_scale > 1.0) want = std::max(want, (size_t)((double)bytes * g_reserve_scale));
         want = std::max<size_t>(want, 256);
         hipError_t e = hipMalloc(&p, want);
         cap = e == hipSuccess ? want : 0;
@@ -57,6 +62,14 @@ struct DBuf {
         p = nullptr;
         cap = 0;
     }
+};
+
+struct ReserveScope {   // g_reserve_scale for one call on a batch of nbk blocks
+    explicit ReserveScope(uint32_t reserve_blocks, uint32_t nbk)
+    {
+        g_reserve_scale = reserve_blocks > nbk && nbk ? (double)reserve_blocks / nbk : 1.0;
+    }
+    ~ReserveScope() { g_reserve_scale = 1.0; }
 };
 
 // Device time of each phase of the last sa_run, from HIP events on the stream
@@ -170,7 +183,8 @@ struct sa_ctx {
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
-    bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;   // k_emit_sq's SEQ / QUAL instead of k_emit_sq16
+    bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
+    uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for   // k_emit_sq's SEQ / QUAL instead of k_emit_sq16
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -925,8 +939,14 @@ int input_upload(sa_input* I, const sa_block* in, int n, hipStream_t st, std::st
 
 extern "C" {
 
+void sa_set_reserve(sa_ctx* c, uint32_t blocks)
+{
+    if (c) c->reserve_blocks = blocks;
+}
+
 int sa_stage(sa_ctx* c, const sa_block* in, int n)
 {
+    const ReserveScope reserve(c ? c->reserve_blocks : 0, n > 0 ? (uint32_t)n : 0);
     if (!c) return -1;
     SA_CHECK(c, hipSetDevice(c->device));
     c->have_output = false;
@@ -997,6 +1017,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         c->err = "sa_run_input: no input, no config, or an input of another device";
         return -1;
     }
+    const ReserveScope reserve(c->reserve_blocks, I->nblocks);
     SA_CHECK(c, hipSetDevice(c->device));
     c->have_output = false;
     if (mail_reset(c)) return -1;

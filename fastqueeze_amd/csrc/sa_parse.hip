@@ -252,6 +252,7 @@ void sa_host_free(void* p)
 
 int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
 {
+    const ReserveScope reserve(c ? c->reserve_blocks : 0, n > 0 ? (uint32_t)n : 0);
     if (!c) return -1;
     if (n < 0 || (n > 0 && !in)) {
         c->err = "sa_stage_text: invalid block list";

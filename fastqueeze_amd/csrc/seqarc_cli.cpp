@@ -719,7 +719,7 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_tex
 struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
-         verbose = false, host_only = false, host_parse = false, ingest_only = false;
+         verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = true;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -876,6 +876,20 @@ int compress(const Options& o)
     }
     const int64_t B = std::max(1, o.batch);
     const size_t max_inflight = (size_t)B * (ctxs.size() + 2);   // blocks read but not yet written
+    // batch k = blocks [bstart(k), bstart(k + 1)).  The first batch of each
+    // context ramps up (B (k+1) / (C+1) blocks: the first encode starts after a
+    // fraction of a batch is read, and the contexts' first tails are staggered);
+    // the contexts allocate for B from the start (sa_set_reserve).  --no-ramp: all B.
+    const int64_t C = (int64_t)ctxs.size();
+    std::vector<int64_t> ramp_start{0};
+    for (int64_t k = 0; o.ramp && k < C; k++) ramp_start.push_back(ramp_start.back() + std::max<int64_t>(1, B * (k + 1) / (C + 1)));
+    auto bstart = [&](int64_t k) -> int64_t {
+        const int64_t r = (int64_t)ramp_start.size() - 1;
+        return k <= r ? ramp_start[(size_t)k] : ramp_start.back() + (k - r) * B;
+    };
+    if (o.ramp)
+        for (sa_ctx* c : ctxs)
+            if (c) sa_set_reserve(c, (uint32_t)B);
 
     std::mutex mu;
     std::condition_variable cv;
@@ -1032,8 +1046,8 @@ int compress(const Options& o)
     // encoders: one host thread per context, batches of B blocks in order
     auto batch_ready = [&](int64_t k) {   // under mu
         if (!tmpl_ready) return false;
-        const int64_t b0 = k * B;
-        const int64_t b1 = nblocks >= 0 ? std::min(nblocks, b0 + B) : b0 + B;
+        const int64_t b0 = bstart(k);
+        const int64_t b1 = nblocks >= 0 ? std::min(nblocks, bstart(k + 1)) : bstart(k + 1);
         if (nblocks < 0 && nread < b1) return false;
         for (int64_t i = b0; i < b1; i++)
             if (jobs.count(i) == 0 || jobs[i]->state < 1) return false;
@@ -1050,10 +1064,10 @@ int compress(const Options& o)
                     std::unique_lock<std::mutex> lk(mu);
                     if (failed) return;
                     k = next_batch++;
-                    cv.wait(lk, [&] { return failed || (nblocks >= 0 && k * B >= nblocks) || batch_ready(k); });
-                    if (failed || (nblocks >= 0 && k * B >= nblocks)) return;
-                    b0 = k * B;
-                    b1 = nblocks >= 0 ? std::min(nblocks, b0 + B) : b0 + B;
+                    cv.wait(lk, [&] { return failed || (nblocks >= 0 && bstart(k) >= nblocks) || batch_ready(k); });
+                    if (failed || (nblocks >= 0 && bstart(k) >= nblocks)) return;
+                    b0 = bstart(k);
+                    b1 = nblocks >= 0 ? std::min(nblocks, bstart(k + 1)) : bstart(k + 1);
                     for (int64_t i = b0; i < b1; i++) js.push_back(jobs[i].get());
                 }
                 std::vector<sa_out> outs(js.size());
@@ -1201,14 +1215,21 @@ int compress(const Options& o)
     for (auto& t : parsers) t.join();
     for (auto& t : encoders) t.join();
     const double t_joined = now_s();
-    // (releasing five contexts' ~200 GB of buffers takes ~1.4 s; leaving them to
-    // the process exit moves the same time there, r3k)
-    for (sa_hash_index* ix : indexes) sa_hash_destroy(ix);
-    if (chain) sa_align_chain_destroy(chain);
-    for (sa_ctx* c : ctxs)
-        if (c) sa_destroy(c);
-    if (o.verbose) fprintf(stderr, "seqarc_amd: encoders done %.3f s, contexts released %.3f s\n", t_joined, now_s());
+    // the archive is finished (trailer, header, closed) before the contexts'
+    // device buffers are released (~1.4 s for five contexts' ~200 GB)
+    auto release = [&]() {
+        for (sa_hash_index* ix : indexes) sa_hash_destroy(ix);
+        indexes.clear();
+        if (chain) sa_align_chain_destroy(chain);
+        chain = nullptr;
+        for (sa_ctx*& c : ctxs)
+            if (c) {
+                sa_destroy(c);
+                c = nullptr;
+            }
+    };
     if (failed) {
+        release();
         fprintf(stderr, "seqarc_amd: %s\n", err.c_str());
         if (fo) fclose(fo);
         return 1;
@@ -1225,7 +1246,15 @@ int compress(const Options& o)
         sa_arc_header(total, hdr);
         fseek(fo, 0, SEEK_SET);
         fwrite(hdr, 1, 16, fo);
-        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    if (fclose(fo) != 0) rc = 1;
+    const double t_closed = now_s();
+    release();
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    if (o.verbose)
+        fprintf(stderr, "seqarc_amd: encoders done %.3f s, archive closed %.3f s, contexts released %.3f s\n", t_joined,
+                t_closed, secs);
+    if (tl >= 0) {
         if (o.verbose)
             fprintf(stderr,
                     "seqarc_amd: contexts ready %.3f s, input read %.3f s, first encode %.3f s, last encode "
@@ -1239,7 +1268,6 @@ int compress(const Options& o)
                 (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
                 (double)total_in / (double)(16 + total + tl), secs, (double)total_in / secs / 1e6);
     }
-    if (fclose(fo) != 0) rc = 1;
     return rc;
 }
 
@@ -1533,6 +1561,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--share-device")) o.share_device = true;
         else if (!strcmp(a, "--host-only")) o.host_only = true;
         else if (!strcmp(a, "--ingest-only")) o.ingest_only = true;
+        else if (!strcmp(a, "--no-ramp")) o.ramp = false;
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (!strcmp(a, "-i")) { o.index = true; if (!(o.ref = val())) return usage(); }

@@ -79,6 +79,10 @@ int sa_host_unregister(void *p);
 int sa_encode_blocks(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, sa_out *out);
 
 /* ---- staged API (inputs resident in HBM; used by bench.py) ------------ */
+/* the batch size (blocks) the context's buffers are sized for from its first
+ * batch on, when its first batches are smaller (a re-allocation synchronises
+ * the device); 0: as each batch needs */
+void sa_set_reserve(sa_ctx *ctx, uint32_t blocks);
 int sa_stage(sa_ctx *ctx, const sa_block *in, int n);     /* H2D copy of a batch   */
 /* FASTQ text of one block as the reader cut it (doReadPEJob@0x432d10 /
  * cultPEbuf@0x432180 hand these to getBlockRead[PE]): file 1 and, for PE,
