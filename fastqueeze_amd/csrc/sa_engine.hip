@@ -184,7 +184,8 @@ struct sa_ctx {
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
     bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
-    uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for   // k_emit_sq's SEQ / QUAL instead of k_emit_sq16
+    uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for
+    int rv_variant = std::getenv("SA_RV_V2") ? std::atoi(std::getenv("SA_RV_V2")) != 0 : 0;   // pass-R step (A/B)   // k_emit_sq's SEQ / QUAL instead of k_emit_sq16
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -543,7 +544,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderVi
 {
     if (!tl.count) return;
     if (ph >= 0) ev_begin(c, ph, st);
-    hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
+    hipLaunchKernelGGL(c->rv_variant ? k_coder_rv<1> : k_coder_rv<0>, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
                        c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio);
     if (ph >= 0) ev_finish(c, ph, st);
@@ -706,8 +707,10 @@ sa_ctx* sa_create(int device)
     }
     if (const char* e = std::getenv("SA_CODER_LDS")) c->coder_lds = (uint32_t)std::min(std::max(std::atoi(e), 0), 160 * 1024);
     if (c->coder_lds > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)c->coder_lds) != hipSuccess) {
+        (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess ||
+         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess)) {
         std::fprintf(stderr, "seqarc_amd: cannot reserve %u B of LDS for pass R\n", c->coder_lds);
         delete c;
         return nullptr;

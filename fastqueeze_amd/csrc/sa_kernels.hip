@@ -2218,30 +2218,147 @@ constexpr uint32_t CODER_LA = 6;
         "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
         ""
 
-template <int J>
+// SA_RV_STEP8B (SA_RV_V2=1): the same step with the q.f product taken from the
+// uncorrected quotient and the correction folded into a select, so two of the
+// three multiplies are off the dependent path: rr = (r < q0 t) ? q0 f - f : q0 f
+#define SA_RV_STEP8B                                                                             \
+        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l0]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l1]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l2]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l3]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l4]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l5]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t"                    \
+        "v_readlane_b32 %[tb], %[ctf], %[l6]\n\t"                   \
+        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t"                    \
+        "v_readlane_b32 %[ta], %[ctf], %[l7]\n\t"                   \
+        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
+        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
+        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
+        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
+        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
+        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
+        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
+        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
+        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+        ""
+
+template <int J, int V>
 __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& mb, uint32_t& tb,
                                          uint32_t cm, uint32_t ctf, uint32_t tmask)
 {
     uint32_t t, f, q, p;
-    asm volatile(SA_RV_STEP8
-                 : [r] "+s"(r), [ma] "+s"(ma), [ta] "+s"(ta), [mb] "+s"(mb), [tb] "+s"(tb), [t] "=&s"(t),
-                   [f] "=&s"(f), [q] "=&s"(q), [p] "=&s"(p)
-                 : [tmask] "s"(tmask), [cm] "v"(cm), [ctf] "v"(ctf), [l0] "i"((J + 1) & 63), [l1] "i"((J + 2) & 63),
-                   [l2] "i"((J + 3) & 63), [l3] "i"((J + 4) & 63), [l4] "i"((J + 5) & 63), [l5] "i"((J + 6) & 63),
-                   [l6] "i"((J + 7) & 63), [l7] "i"((J + 8) & 63)
-                 : "scc");
+#define SA_RV_OPERANDS                                                                                            \
+    : [r] "+s"(r), [ma] "+s"(ma), [ta] "+s"(ta), [mb] "+s"(mb), [tb] "+s"(tb), [t] "=&s"(t), [f] "=&s"(f),       \
+      [q] "=&s"(q), [p] "=&s"(p)                                                                                  \
+    : [tmask] "s"(tmask), [cm] "v"(cm), [ctf] "v"(ctf), [l0] "i"((J + 1) & 63), [l1] "i"((J + 2) & 63),          \
+      [l2] "i"((J + 3) & 63), [l3] "i"((J + 4) & 63), [l4] "i"((J + 5) & 63), [l5] "i"((J + 6) & 63),             \
+      [l6] "i"((J + 7) & 63), [l7] "i"((J + 8) & 63)                                                             \
+    : "scc"
+    if constexpr (V == 0)
+        asm volatile(SA_RV_STEP8 SA_RV_OPERANDS);
+    else
+        asm volatile(SA_RV_STEP8B SA_RV_OPERANDS);
+#undef SA_RV_OPERANDS
 }
 #undef SA_RV_STEP8
+#undef SA_RV_STEP8B
 
 // the 64 steps of one segment (records in lanes 0..63 of cm / ctf)
-template <int... P>
+template <int V, int... P>
 __device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t ctf, uint32_t tmask,
                                            std::integer_sequence<int, P...>)
 {
     uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(ctf, 0), mb = 0, tb = 0;
-    (rv_step8<8 * P>(r, ma, ta, mb, tb, cm, ctf, tmask), ...);
+    (rv_step8<8 * P, V>(r, ma, ta, mb, tb, cm, ctf, tmask), ...);
 }
 
+template <int V>
 __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
                                                const TaskList& tl, const PRec* __restrict__ prs0,
                                                const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
@@ -2281,7 +2398,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                 }
                 const uint32_t r_seg = r;
                 const uint32_t cm = recip32z(ctf & tmask);
-                rv_segment(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
+                rv_segment<V>(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
                 if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
                 g++;
             }
@@ -2293,6 +2410,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
     if (s >= first && s <= g) ck[s] = kv;
 }
 
+template <int V>
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
     const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio)
@@ -2300,7 +2418,7 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const uint32_t wpg = blockDim.x >> 6;
     const uint32_t li = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (li >= tl.count) return;
-    coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+    coder_rv_chain<V>(li, tasks, tl, prs0, prs1, ck_r, err, prio);
 }
 
 // Locate list entry and segment of global coder-lane gi (gbase ascending).
