@@ -93,6 +93,7 @@ def parse_args(argv=None):
                     help="the gzip end-to-end legs (BGZF, member-serial gzip) on this many blocks of batch 0 (0: skip)")
     ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--e2e-log", default=None, help="write the CLI's stderr (-v stage lines, SA_TRACE) here")
+    ap.add_argument("--e2e-args", default="", help="extra seqarc_amd arguments for the end-to-end runs (A/B)")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
@@ -184,15 +185,16 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
     cmd = [build.CLI, "-c", "-f", "-v", "-t", str(threads), "-1", files[0]] + (["-2", files[1]] if len(files) > 1 else []) \
         + ["-o", out, "--contexts", str(contexts), "--batch", str(batch), "--slevel", str(args.slevel),
            "--qlevel", str(args.qlevel), "--block-size", str(max(1, args.block_size >> 20))] \
-        + (["--devices", str(devices)] if devices > 1 else []) + (["--ingest-only"] if ingest_only else [])
+        + (["--devices", str(devices)] if devices > 1 else []) + (["--ingest-only"] if ingest_only else []) \
+        + args.e2e_args.split()
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     wall = time.perf_counter() - t0
     if r.returncode != 0:
         raise SystemExit(f"end-to-end run failed: {r.stderr[-2000:]}")
     if args.e2e_log:
-        with open(args.e2e_log, "w") as f:
-            f.write(r.stderr)
+        with open(args.e2e_log, "a") as f:
+            f.write(f"== {' '.join(os.path.basename(c) for c in cmd)}\n" + r.stderr)
     in_bytes = sum(os.path.getsize(f) for f in files)
     with open(out + ".arc", "rb") as f:
         arc = f.read()
@@ -662,6 +664,22 @@ def main():
         res["end_to_end_gz"] = gz
     if e2e_files:
         expect = b"".join(outs if args.e2e_batches == 1 else outs[:-1])
+        if world == 1 and args.e2e_batches != 1:
+            # a short stream at configs[2]'s per-GPU share (143 GB / 8 GPUs ~ 18 GB, five
+            # batches: the written batches plus batch 0 once more), where pipeline fill
+            # and drain weigh most; the files are cut back to the written batches after it
+            base = [os.path.getsize(f) for f in e2e_files]
+            sizes = [sum(b.text1 or b.text_bytes for b in keep["verify"])] + \
+                ([sum(b.text2 for b in keep["verify"])] if len(e2e_files) > 1 else [])
+            for f, n in zip(e2e_files, sizes):
+                with open(f, "rb") as src, open(f, "ab") as dst:
+                    dst.write(src.read(n))
+            try:
+                res["end_to_end_short"] = end_to_end(args, e2e_files, args.contexts, expect,
+                                                     args.e2e_batch or len(keep["verify"]), share["usable"])
+            finally:
+                for f, n in zip(e2e_files, base):
+                    os.truncate(f, n)
         replicate(e2e_files, args.e2e_repeat or (3 if world == 1 else 2 * world))
         try:
             # batches of the bench's size (69 blocks): pass R of a batch takes as long for 28 blocks as

@@ -46,8 +46,12 @@ struct DBuf {
         p = nullptr;
         // slack for the next, slightly larger batch: a re-allocation's hipFree
         // synchronises the whole device, stalling every other context on it
-        size_t want = std::max(bytes + bytes / 16, cap + cap / 16);
-        if (g_reserve_scale > 1.0) want = std::max(want, (size_t)((double)bytes * g_reserve_scale));
+        // (the reserve scale gets the same slack on top: a full batch of the
+        // command line's ramp can need a little more than scale x a ramp batch,
+        // e.g. the exact payload arena, and a grow then stalled every context
+        // for 1.5 s, round 3 g3m)
+        const size_t scaled = g_reserve_scale > 1.0 ? (size_t)((double)bytes * g_reserve_scale) : bytes;
+        size_t want = std::max(scaled + scaled / 16, cap + cap / 16);
         want = std::max<size_t>(want, 256);
         hipError_t e = hipMalloc(&p, want);
         cap = e == hipSuccess ? want : 0;
@@ -941,6 +945,12 @@ int input_upload(sa_input* I, const sa_block* in, int n, hipStream_t st, std::st
 }  // namespace
 
 extern "C" {
+
+void sa_alloc_stats(uint32_t* grows, double* alloc_ms)
+{
+    if (grows) *grows = g_grows.load();
+    if (alloc_ms) *alloc_ms = g_alloc_ns.load() / 1e6;
+}
 
 void sa_set_reserve(sa_ctx* c, uint32_t blocks)
 {

@@ -1133,10 +1133,14 @@ int compress(const Options& o)
                             snprintf(pb, sizeof pb, " %s %.0f", pn[x], pm[x]);
                             ph += pb;
                         }
+                        uint32_t grows = 0;
+                        double alloc_ms = 0;
+                        sa_alloc_stats(&grows, &alloc_ms);
                         fprintf(stderr,
                                 "seqarc_amd: batch %lld (%zu blocks) context %p: asked %.3f s, ready %.3f s, stage %.3f s, "
-                                "run %.3f s, fetch %.3f s; device ms:%s\n",
-                                (long long)k, js.size(), (void*)ctx, tw, te, tr - te, tf - tr, now_s() - tf, ph.c_str());
+                                "run %.3f s, fetch %.3f s; grows %u, alloc %.0f ms; device ms:%s\n",
+                                (long long)k, js.size(), (void*)ctx, tw, te, tr - te, tf - tr, now_s() - tf, grows, alloc_ms,
+                                ph.c_str());
                     }
                 } else {
                     std::vector<sa_block> in(js.size());

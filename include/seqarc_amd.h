@@ -83,6 +83,9 @@ int sa_encode_blocks(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, 
  * batch on, when its first batches are smaller (a re-allocation synchronises
  * the device); 0: as each batch needs */
 void sa_set_reserve(sa_ctx *ctx, uint32_t blocks);
+/* device buffer re-allocations in this process so far (each one's hipFree
+ * synchronises the device) and the host time spent allocating, in ms */
+void sa_alloc_stats(uint32_t *grows, double *alloc_ms);
 int sa_stage(sa_ctx *ctx, const sa_block *in, int n);     /* H2D copy of a batch   */
 /* FASTQ text of one block as the reader cut it (doReadPEJob@0x432d10 /
  * cultPEbuf@0x432180 hand these to getBlockRead[PE]): file 1 and, for PE,
