@@ -93,6 +93,9 @@ def parse_args(argv=None):
                     help="the gzip end-to-end legs (BGZF, member-serial gzip) on this many blocks of batch 0 (0: skip)")
     ap.add_argument("--e2e-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--e2e-log", default=None, help="write the CLI's stderr (-v stage lines, SA_TRACE) here")
+    ap.add_argument("--e2e-settle", type=float, default=8.0,
+                    help="seconds the device is left idle before each end-to-end run: the driver reclaims the "
+                         "~200 GB the previous run released in the background, and allocations wait for it")
     ap.add_argument("--e2e-args", default="", help="extra seqarc_amd arguments for the end-to-end runs (A/B)")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -187,6 +190,8 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
            "--qlevel", str(args.qlevel), "--block-size", str(max(1, args.block_size >> 20))] \
         + (["--devices", str(devices)] if devices > 1 else []) + (["--ingest-only"] if ingest_only else []) \
         + args.e2e_args.split()
+    if not ingest_only and args.e2e_settle > 0:
+        time.sleep(args.e2e_settle)   # (outside the timed run: a fresh job starts on a settled device)
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     wall = time.perf_counter() - t0
@@ -209,7 +214,7 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
     os.remove(out + ".arc")
     return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
             "cli_clock_mb_s": clock, "cli_stages": stages, "fastq_bytes": in_bytes, "devices": devices,
-            "contexts": contexts, "batch_blocks": batch,
+            "contexts": contexts, "batch_blocks": batch, "device_settle_s": 0 if ingest_only else args.e2e_settle,
             "parse": "none (--ingest-only)" if ingest_only else "device (sa_stage_text from page-locked text windows)",
             "leading_blocks_identical_to_bench": same,
             "command": " ".join(os.path.basename(c) if i == 0 else c for i, c in enumerate(cmd))}

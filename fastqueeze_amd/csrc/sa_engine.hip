@@ -186,6 +186,7 @@ struct sa_ctx {
     bool serial_seq = false;
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
+    bool prep_split = std::getenv("SA_PREP_SPLIT") != nullptr;   // k_prep beside k_prep_sq16 (A/B)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
     bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
     uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for
@@ -909,7 +910,7 @@ int input_upload(sa_input* I, const sa_block* in, int n, hipStream_t st, std::st
             so += (uint32_t)in[b].seq_lens[r];
         }
     }
-    IN_CHECK(I->d_names.ensure(nb + 16));
+    IN_CHECK(I->d_names.ensure(nb + 64));   // (k_prep_sq16 reads whole dwords past a name)
     IN_CHECK(I->d_seq.ensure(sb + 64));   // (k_prep_sq16 reads whole dwords past a read)
     IN_CHECK(I->d_qual.ensure(sb + 64));
     const size_t nr4 = (size_t)std::max<uint32_t>(nr, 1) * 4;
@@ -1142,14 +1143,25 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // 8 workgroups per CU measured slower: k_prep 1.2 -> 1.7 ms, k_emit 6.8 -> 9.4)
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
-        hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                           c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
-        if (c->prep_wave)   // (SA_PREP_WAVE=1: the wave-per-read variant, for A/B)
+        // k_prep_sq16 also takes k_prep's name / length columns (a row per read:
+        // k_prep's lane-per-read byte loops took 1.2 ms alone but 15 ms beside
+        // other batches' tails, round 3 g3n); SA_PREP_WAVE=1: round 2's k_prep +
+        // wave-per-read k_prep_sq, for A/B
+        if (c->prep_split) {   // (SA_PREP_SPLIT=1: k_prep's lane per read beside k_prep_sq16, for A/B)
+            hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
+            hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
+                               c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr);
+        } else if (c->prep_wave) {
+            hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
             hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                c->d_counts.as<uint32_t>(), d_err);
-        else
+        } else {
             hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                               c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>());
+                               c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(),
+                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>());
+        }
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
                        c->d_totals.as<uint32_t>(), c->d_maxlen.as<uint16_t>());

@@ -279,8 +279,83 @@ __device__ __forceinline__ uint32_t row_min(uint32_t v)
 
 constexpr uint32_t PREP_ROW = 16;
 
+// k_prep's name columns, row-parallel (name_prefix_suffix of sa_common.h,
+// encode_name@0x421070's prefix / suffix against the previous name of the
+// block): each lane compares 16 bytes per step, from the front for the common
+// prefix and from the back for the common suffix; the row minimum of the first
+// mismatches.  Loop bounds are wave-uniform (every row of the wave steps).
+__device__ __forceinline__ uint32_t first_diff16(const uint32_t a[4], const uint32_t b[4], uint32_t cnt)
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t nb = cnt > 4u * k ? (cnt - 4u * k < 4 ? cnt - 4u * k : 4) : 0;
+        const uint32_t inm = nb >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * nb)) - 1u));
+        const uint32_t d = bytes_nonzero(a[k] ^ b[k]) & inm;
+        if (d) return 4u * k + (uint32_t)(__ffs(d) - 1) / 8;
+        if (nb < 4) break;
+    }
+    return 0xffffffffu;
+}
+
+__device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint32_t r, uint32_t rl, int& p, int& sfx)
+{
+    const uint8_t *nm = nullptr, *pv = nullptr;
+    uint32_t nl = 0, pl = 0;
+    if (live) {
+        const DevBlock& blk = bv.blocks[bv.read_block[r]];
+        nm = bv.names + blk.name_base + bv.name_off[r];
+        nl = bv.name_len[r];
+        if (r > blk.read0) {
+            pv = bv.names + blk.name_base + bv.name_off[r - 1];
+            pl = bv.name_len[r - 1];
+        }
+    }
+    const uint32_t lim = nl < pl ? nl : pl;   // (0 for a block's first read: p = s = 0)
+    const uint32_t wlim = (uint32_t)wave_max_i32((int)lim);
+    uint32_t lcp = lim, lcs = lim;
+    bool pdone = false, sdone = false;
+    for (uint32_t i0 = 0; i0 < wlim; i0 += 16 * PREP_ROW) {
+        const uint32_t t0 = i0 + 16 * rl;
+        uint32_t dp = 0xffffffffu, ds = 0xffffffffu;
+        if (t0 < lim) {
+            const uint32_t cnt = lim - t0 < 16 ? lim - t0 : 16;
+            if (!pdone) {   // from the front: bytes t0 .. t0 + cnt of both names
+                uint32_t a[4], b[4];
+                load16(nm + t0, a);
+                load16(pv + t0, b);
+                const uint32_t f = first_diff16(a, b, cnt);
+                if (f != 0xffffffffu) dp = t0 + f;
+            }
+            if (!sdone) {   // from the back: byte t of the window is name[len - 1 - t]
+                for (uint32_t j = 0; j < cnt; j++) {
+                    const uint32_t t = t0 + j;
+                    if (nm[nl - 1 - t] != pv[pl - 1 - t]) {
+                        ds = t;
+                        break;
+                    }
+                }
+            }
+        }
+        dp = row_min<PREP_ROW>(dp);
+        ds = row_min<PREP_ROW>(ds);
+        if (!pdone && dp != 0xffffffffu) {
+            lcp = dp;
+            pdone = true;
+        }
+        if (!sdone && ds != 0xffffffffu) {
+            lcs = ds;
+            sdone = true;
+        }
+        if (__ballot(live && !(pdone && sdone)) == 0) break;
+    }
+    p = (int)lcp;
+    sfx = (int)lcs;
+    if ((int)nl - sfx - p < 0) sfx = (int)nl - p;
+}
+
 __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t* __restrict__ counts,
-                                                   uint32_t* __restrict__ err, uint8_t* __restrict__ dege_maxq)
+                                                   uint32_t* __restrict__ err, uint8_t* __restrict__ dege_maxq,
+                                                   int16_t* __restrict__ name_p, int16_t* __restrict__ name_s)
 {
     const uint32_t rl = threadIdx.x & (PREP_ROW - 1);
     const uint32_t rows = gridDim.x * (blockDim.x / PREP_ROW);
@@ -408,13 +483,30 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
             exc = row_sum<PREP_ROW>(exc);
             nsym = row_sum<PREP_ROW>(nsym);
         }
+        // k_prep's columns (name_p == nullptr: k_prep runs, SA_PREP_WAVE)
+        int np = 0, ns = 0;
+        if (name_p && !bv.bin_mode) name_cols16(bv, live, r, rl, np, ns);
         if (live && rl == 0) {
             SeqStat st{valid, len - valid, maxq & 0xffu, hasn ? exc : 0u, hasn ? nsym : 0u,
                        nonascii ? (uint32_t)E_NONASCII : 0u};
-            const uint32_t e = prep_sq_cols(counts + (size_t)r * NCOL, len, lastnz, st, firstbad < lastnz,
-                                            bv.seq_skip && bv.seq_skip[r]);
-            if (e) atomicOr(err, e);
+            uint32_t* c = counts + (size_t)r * NCOL;
+            uint32_t e = prep_sq_cols(c, len, lastnz, st, firstbad < lastnz, bv.seq_skip && bv.seq_skip[r]);
             dege_maxq[r] = (uint8_t)st.maxq;   // (k_emit / k_emit_sq: the side streams)
+            if (name_p) {   // (prep_read with bulk = false)
+                c[C_LEN] = len == 0 ? 1 : (bv.blocks[bv.read_block[r]].len_long ? 5 : 3);
+                c[C_TIP] = 1;
+                if (bv.bin_mode) {
+                    c[C_NAME] = 0;
+                } else {
+                    const int nl = bv.name_len[r];
+                    if (nl > 255) e |= E_NAME;
+                    name_p[r] = (int16_t)np;
+                    name_s[r] = (int16_t)ns;
+                    const int mid = nl - ns - np;
+                    c[C_NAME] = 3 + (mid > 0 ? (uint32_t)mid : 0);
+                }
+            }
+            if (e) atomicOr(err, e);
         }
     }
 }

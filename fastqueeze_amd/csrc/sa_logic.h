@@ -748,19 +748,48 @@ SA_HD bool rb_extend(RbRun& s, uint32_t c, double R)
 constexpr uint32_t RB_CHUNK = 8192;
 constexpr uint32_t RB_WORDS = RB_CHUNK / 32;
 
+// The bytes [from, len) of the chunk starting at q + base, in order, to
+// f(i, c) until it returns false.  16 bytes per load (a lane walks its own
+// chunk: byte loads left it at one load latency per byte, 39 / 64 ms for
+// k_rb_spec / k_rb_apply per ONT batch, r3t); chunk bases are 16-byte aligned
+// (blocks start on 16 bytes, chunks every RB_CHUNK bytes of a block).
+template <class F>
+SA_HD void rb_for_bytes(const uint8_t* q, uint64_t base, uint32_t from, uint32_t len, F f)
+{
+    for (uint32_t i0 = from & ~15u; i0 < len; i0 += 16) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        const uint8_t* p = q + base + i0;
+        if (i0 + 16 <= len && ((base + i0) & 15) == 0) {
+            __builtin_memcpy(w, __builtin_assume_aligned(p, 16), 16);
+        } else {
+            for (uint32_t j = 0; j < 16 && i0 + j < len; j++) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            uint32_t x = w[k];
+            for (uint32_t j = 0; j < 4; j++, x >>= 8) {
+                const uint32_t i = i0 + 4 * k + j;
+                if (i < from) continue;
+                if (i >= len) return;
+                if (!f(i, x & 0xffu)) return;
+            }
+        }
+    }
+}
+
 // Speculative pass over one chunk: bit i of opens = a run opens at byte i.
 SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, double R, uint32_t* opens)
 {
     RbRun s{ck.base, q[ck.base], q[ck.base]};
     uint32_t w = 1u;   // a run opens at the chunk's first byte
-    for (uint32_t i = 1; i < ck.len; i++) {
-        const uint32_t c = q[ck.base + i];
+    rb_for_bytes(q, ck.base, 1, ck.len, [&](uint32_t i, uint32_t c) {
         if (!rb_extend(s, c, R)) {
             s = RbRun{ck.base + i, c, c};
             w |= 1u << (i & 31);
         }
         if ((i & 31) == 31) { opens[i >> 5] = w; w = 0; }
-    }
+        return true;
+    });
     if ((ck.len & 31) != 0) opens[(ck.len - 1) >> 5] = w;
     for (uint32_t k = (ck.len + 31) >> 5; k < RB_WORDS; k++) opens[k] = 0;
     return s;
@@ -769,33 +798,37 @@ SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, double R, uint32_t* ope
 // The true open run after chunk ck, given the true run open before it.
 SA_HD RbRun rb_carry(const uint8_t* q, const RbChunk& ck, RbRun s, double R, const uint32_t* opens, const RbRun& spec_exit)
 {
-    for (uint32_t i = 0; i < ck.len; i++) {
-        const uint32_t c = q[ck.base + i];
+    bool conv = false;
+    rb_for_bytes(q, ck.base, 0, ck.len, [&](uint32_t i, uint32_t c) {
         if (!rb_extend(s, c, R)) {
-            if ((opens[i >> 5] >> (i & 31)) & 1u) return spec_exit;   // converged
+            if ((opens[i >> 5] >> (i & 31)) & 1u) {   // converged
+                conv = true;
+                return false;
+            }
             s = RbRun{ck.base + i, c, c};
         }
-    }
-    return s;
+        return true;
+    });
+    return conv ? spec_exit : s;
 }
 
 // Writes every run that closes inside chunk ck (and, in the block's last
 // chunk, the final run); entry = the true run open before the chunk.
 SA_HD void rb_apply(const uint8_t* q, uint8_t* out, const RbChunk& ck, RbRun s, double R)
 {
-    uint32_t i = 0;
+    uint32_t from = 0;
     if (ck.flags & RB_FIRST) {
         s = RbRun{ck.base, q[ck.base], q[ck.base]};
-        i = 1;
+        from = 1;
     }
-    for (; i < ck.len; i++) {
-        const uint32_t c = q[ck.base + i];
+    rb_for_bytes(q, ck.base, from, ck.len, [&](uint32_t i, uint32_t c) {
         if (!rb_extend(s, c, R)) {
             const uint8_t g = (uint8_t)rb_round_sqrt(s.mn * s.mx);
             for (uint64_t j = s.start; j < ck.base + i; j++) out[j] = g;
             s = RbRun{ck.base + i, c, c};
         }
-    }
+        return true;
+    });
     if (ck.flags & RB_LAST) {
         const uint8_t g = (uint8_t)rb_round_sqrt(s.mn * s.mx);
         for (uint64_t j = s.start; j < ck.base + ck.len; j++) out[j] = g;

@@ -451,7 +451,7 @@ int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
     I->names_bytes = nb;
     I->seq_bytes = sb;
     I->text_bytes = tb;
-    SA_CHECK(c, I->d_names.ensure(nb + 16));
+    SA_CHECK(c, I->d_names.ensure(nb + 64));   // (k_prep_sq16 reads whole dwords past a name)
     SA_CHECK(c, I->d_seq.ensure(sb + 64));
     SA_CHECK(c, I->d_qual.ensure(sb + 64));
     SA_CHECK(c, h2d(c, I->d_pblocks.p, pb.data(), sizeof(ParseBlock) * (size_t)n, st));
