@@ -64,7 +64,9 @@ def parse_args(argv=None):
                     help="timed batch encodes (the pipeline drain, ~1 batch latency, is amortised over them)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--contexts", type=int, default=5, help="encoder contexts (pipeline lanes) per GPU")
-    ap.add_argument("--batches", type=int, default=4, help="distinct resident batches per GPU")
+    ap.add_argument("--batches", type=int, default=0,
+                    help="distinct resident batches per GPU (0: 4 at one rank, 2 with more ranks, whose generators "
+                         "share the host's cores)")
     ap.add_argument("--no-share", action="store_true", help="contexts with their own front scratch (A/B)")
     ap.add_argument("--pairs", type=int, default=5_000_000, help="mate pairs per batch (reads with --se)")
     ap.add_argument("--se", action="store_true", help="single-end reads (configs[1] shape) instead of PE")
@@ -106,6 +108,8 @@ def parse_args(argv=None):
         a.se = True
         if a.pairs == 5_000_000:
             a.pairs = 60_000
+    if a.batches <= 0:
+        a.batches = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 2
     if a.e2e_batches < 0:   # (N ranks: rank 0's first batch, N x 2 times over, one seqarc_amd --devices N run)
         a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 1
     if a.dry_run:

@@ -186,11 +186,19 @@ struct sa_ctx {
     bool serial_seq = false;
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
     uint32_t md5_prio = 1;     // ... and in k_md5 (SA_MD5_PRIO; off the critical path)
-    bool prep_split = std::getenv("SA_PREP_SPLIT") != nullptr;   // k_prep beside k_prep_sq16 (A/B)
+    bool prep_fused = std::getenv("SA_PREP_FUSED") != nullptr;   // name columns in k_prep_sq16 (A/B)
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
     bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
     uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for
-    int rv_variant = std::getenv("SA_RV_V2") ? std::atoi(std::getenv("SA_RV_V2")) != 0 : 0;   // pass-R step (A/B)   // k_emit_sq's SEQ / QUAL instead of k_emit_sq16
+    // SA_RV_PART=1: pass R of each context of a device on its own share of the
+    // coder CUs (st5, CU-masked: context k of C takes every C-th of them), so no
+    // two batches' chains meet on a SIMD and no LDS needs reserving (coder_lds 0)
+    bool rv_part = std::getenv("SA_RV_PART") && std::atoi(std::getenv("SA_RV_PART")) != 0;
+    int share_index = 0;             // this context's index among the contexts sharing the front
+    hipStream_t st5 = nullptr;       // (rv_part) pass R
+    hipEvent_t ev_r5a = nullptr, ev_r5b = nullptr;
+    int st5_parts = 0;               // the partition count st5 was made for
+    std::vector<uint32_t> m_coder;   // CU mask of the coder CUs (st3's)
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -303,6 +311,9 @@ struct sa_ctx {
         if (st2) (void)hipStreamDestroy(st2);
         if (st3) (void)hipStreamDestroy(st3);
         if (st4) (void)hipStreamDestroy(st4);
+        if (st5) (void)hipStreamDestroy(st5);
+        if (ev_r5a) (void)hipEventDestroy(ev_r5a);
+        if (ev_r5b) (void)hipEventDestroy(ev_r5b);
     }
 };
 
@@ -548,11 +559,51 @@ int coder_list(sa_ctx* c, hipStream_t st, int slot, const std::vector<CoderTask>
 void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv, int ph)
 {
     if (!tl.count) return;
-    if (ph >= 0) ev_begin(c, ph, st);
-    hipLaunchKernelGGL(c->rv_variant ? k_coder_rv<1> : k_coder_rv<0>, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
-                       c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
+    hipStream_t sr = st;
+    if (c->st5) {   // (rv_part) on the context's own coder CUs, in order with st
+        (void)hipEventRecord(c->ev_r5a, st);
+        (void)hipStreamWaitEvent(c->st5, c->ev_r5a, 0);
+        sr = c->st5;
+    }
+    if (ph >= 0) ev_begin(c, ph, sr);
+    hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
+                       c->coder_lds, sr, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio);
-    if (ph >= 0) ev_finish(c, ph, st);
+    if (ph >= 0) ev_finish(c, ph, sr);
+    if (c->st5) {
+        (void)hipEventRecord(c->ev_r5b, c->st5);
+        (void)hipStreamWaitEvent(st, c->ev_r5b, 0);
+    }
+}
+
+// (rv_part) st5 over this context's share of the coder CUs: the coder CUs in
+// order, every C-th from the context's index (C = the contexts sharing the
+// front when the batch starts)
+int rv_part_stream(sa_ctx* c)
+{
+    const int parts = std::max(1, c->fs->refs);
+    if (c->st5 && c->st5_parts == parts) return 0;
+    if (c->st5) {
+        SA_CHECK(c, hipStreamSynchronize(c->st5));
+        (void)hipStreamDestroy(c->st5);
+        c->st5 = nullptr;
+    }
+    std::vector<uint32_t> m(c->m_coder.size(), 0u);
+    int j = 0, got = 0;
+    for (uint32_t cu = 0; cu < 32u * (uint32_t)m.size(); cu++)
+        if ((c->m_coder[cu / 32] >> (cu % 32)) & 1u) {
+            if (j % parts == c->share_index % parts) {
+                m[cu / 32] |= 1u << (cu % 32);
+                got++;
+            }
+            j++;
+        }
+    if (!got) m = c->m_coder;
+    SA_CHECK(c, hipExtStreamCreateWithCUMask(&c->st5, (uint32_t)m.size(), m.data()));
+    if (!c->ev_r5a) SA_CHECK(c, hipEventCreateWithFlags(&c->ev_r5a, hipEventDisableTiming));
+    if (!c->ev_r5b) SA_CHECK(c, hipEventCreateWithFlags(&c->ev_r5b, hipEventDisableTiming));
+    c->st5_parts = parts;
+    return 0;
 }
 
 void coder_launch_l12(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv)
@@ -710,12 +761,11 @@ sa_ctx* sa_create(int device)
         const int w = std::atoi(e);
         c->coder_waves = (w == 1 || w == 2) ? (uint32_t)w : 4u;
     }
+    if (c->rv_part) c->coder_lds = 0;
     if (const char* e = std::getenv("SA_CODER_LDS")) c->coder_lds = (uint32_t)std::min(std::max(std::atoi(e), 0), 160 * 1024);
     if (c->coder_lds > 64 * 1024 &&
-        (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)c->coder_lds) != hipSuccess ||
-         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)c->coder_lds) != hipSuccess)) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)c->coder_lds) != hipSuccess) {
         std::fprintf(stderr, "seqarc_amd: cannot reserve %u B of LDS for pass R\n", c->coder_lds);
         delete c;
         return nullptr;
@@ -741,10 +791,16 @@ sa_ctx* sa_create(int device)
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
     if (every == 1) m_seq = m_long;   // (st3: the coder chains; st4: the long model runs)
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)prop.multiProcessorCount, m_long.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)prop.multiProcessorCount, m_seq.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)prop.multiProcessorCount, m_long.data()) != hipSuccess ||
+    c->m_coder = m_seq;
+    // SA_FRONT_PRIO=1: the front's stream at the device's highest stream
+    // priority (its workgroups dispatched ahead of the tails' when CUs free up)
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const bool front_prio = std::getenv("SA_FRONT_PRIO") && std::atoi(std::getenv("SA_FRONT_PRIO")) != 0;
+    if (hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, front_prio ? prio_hi : prio_lo) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)m_seq.size(), m_seq.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_seq_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_long_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -778,6 +834,7 @@ sa_ctx* sa_create_shared(int device, sa_ctx* peer)
     std::lock_guard<std::mutex> g(g_share_mu);
     FrontShare* own = c->fs;
     c->fs = peer->fs;
+    c->share_index = c->fs->refs;
     c->fs->refs++;
     for (DBuf* b : own->buffers()) b->release();
     if (own->ev_free) (void)hipEventDestroy(own->ev_free);
@@ -1143,24 +1200,25 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // 8 workgroups per CU measured slower: k_prep 1.2 -> 1.7 ms, k_emit 6.8 -> 9.4)
     const uint32_t rgrid = (nr + 255) / 256;
     if (nr) {
-        // k_prep_sq16 also takes k_prep's name / length columns (a row per read:
-        // k_prep's lane-per-read byte loops took 1.2 ms alone but 15 ms beside
-        // other batches' tails, round 3 g3n); SA_PREP_WAVE=1: round 2's k_prep +
-        // wave-per-read k_prep_sq, for A/B
-        if (c->prep_split) {   // (SA_PREP_SPLIT=1: k_prep's lane per read beside k_prep_sq16, for A/B)
-            hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
-            hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                               c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr);
-        } else if (c->prep_wave) {
-            hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
-            hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
-                               c->d_counts.as<uint32_t>(), d_err);
-        } else {
+        // k_prep (names, lengths: lane per read) and k_prep_sq16 (SEQ / QUAL /
+        // N-IUPAC columns: a row per read).  SA_PREP_FUSED=1: k_prep_sq16 takes
+        // the name columns too (row-parallel prefix / suffix) -- measured no
+        // faster under load (prep 38 vs 32 ms, same GB/s, round 3 g3r / g3s);
+        // SA_PREP_WAVE=1: round 2's wave-per-read k_prep_sq
+        if (c->prep_fused) {
             hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
                                c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(),
                                c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>());
+        } else {
+            hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
+            if (c->prep_wave)
+                hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
+                                   c->d_counts.as<uint32_t>(), d_err);
+            else
+                hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
+                                   c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(), nullptr,
+                                   nullptr);
         }
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
@@ -1380,6 +1438,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     //      (concurrent latency-bound launches land on shared SIMDs); the L passes
     //      after the long runs are done ----
     SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
+    if (c->rv_part && rv_part_stream(c)) return -1;
     std::vector<uint32_t> out_len;
     {
         const int rc = coder_run(c, tasks, cv, st3, PH_CODER_R, PH_CODER_L, c->ev_long_done, exact, out_len, payload);

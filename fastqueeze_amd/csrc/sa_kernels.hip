@@ -326,12 +326,30 @@ __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint
                 const uint32_t f = first_diff16(a, b, cnt);
                 if (f != 0xffffffffu) dp = t0 + f;
             }
-            if (!sdone) {   // from the back: byte t of the window is name[len - 1 - t]
-                for (uint32_t j = 0; j < cnt; j++) {
-                    const uint32_t t = t0 + j;
-                    if (nm[nl - 1 - t] != pv[pl - 1 - t]) {
-                        ds = t;
-                        break;
+            if (!sdone) {   // from the back: the 16 bytes ending at name[len - t0] of both names
+                if (nl - t0 >= 16 && pl - t0 >= 16) {
+                    uint32_t a[4], b[4];
+                    load16(nm + nl - t0 - 16, a);
+                    load16(pv + pl - t0 - 16, b);
+                    // window byte i is t = t0 + 15 - i; valid for i >= 16 - cnt; the first
+                    // mismatch from the back is the highest mismatching byte of the window
+                    const uint32_t first_ok = 16u - cnt;
+#pragma unroll
+                    for (int w = 3; w >= 0; w--) {
+                        uint32_t inm = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (4u * (uint32_t)w + (uint32_t)j >= first_ok) inm |= 0x80u << (8 * j);
+                        const uint32_t d = bytes_nonzero(a[w] ^ b[w]) & inm;
+                        if (d && ds == 0xffffffffu) ds = t0 + 15u - (4u * (uint32_t)w + (uint32_t)(31 - __clz(d)) / 8);
+                    }
+                } else {   // (a window reaching the front of a name: byte by byte)
+                    for (uint32_t j = 0; j < cnt; j++) {
+                        const uint32_t t = t0 + j;
+                        if (nm[nl - 1 - t] != pv[pl - 1 - t]) {
+                            ds = t;
+                            break;
+                        }
                     }
                 }
             }
@@ -1279,7 +1297,9 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
                                                                uint32_t* __restrict__ vout, uint32_t shift)
 {
     constexpr uint32_t ND = 1u << DB, NW = SORT_THREADS / 64, C = ND >= SORT_THREADS ? ND / SORT_THREADS : 1;
-    __shared__ uint32_t wc[NW][ND];   // per wave and digit: count, then the wave's slot base in the tile
+    // per wave and digit: count, then the wave's slot base in the tile (<= 4096:
+    // 16 bits, so the 9-bit pass fits twice beside pass R's 82 KB of LDS)
+    __shared__ uint16_t wc[NW][ND];
     __shared__ uint32_t gstart[ND], dsum[NW];
     __shared__ uint32_t sk[SORT_TILE], svl[SORT_TILE];
     const uint32_t t = blockIdx.x;
@@ -1310,7 +1330,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         }
         const uint32_t before = wc[w][d];
         rk[r] = before + (uint32_t)__popcll(peers & lt_mask);
-        if ((peers & lt_mask) == 0) wc[w][d] = before + (uint32_t)__popcll(peers);
+        if ((peers & lt_mask) == 0) wc[w][d] = (uint16_t)(before + (uint32_t)__popcll(peers));
     }
     __syncthreads();
     {
@@ -1327,7 +1347,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 #pragma unroll
                 for (uint32_t ww = 0; ww < NW; ww++) {
                     const uint32_t tcount = wc[ww][d];
-                    wc[ww][d] = acc;
+                    wc[ww][d] = (uint16_t)acc;
                     acc += tcount;
                 }
             }
@@ -1341,7 +1361,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
             const uint32_t d = threadIdx.x * C + c;
             if (d < ND) {
 #pragma unroll
-                for (uint32_t ww = 0; ww < NW; ww++) wc[ww][d] += ex;
+                for (uint32_t ww = 0; ww < NW; ww++) wc[ww][d] = (uint16_t)(wc[ww][d] + ex);
                 gstart[d] = sv.hist[(size_t)t * ND + d] - ex;
             }
             ex += cnt[c];
@@ -2310,117 +2330,7 @@ constexpr uint32_t CODER_LA = 6;
         "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
         ""
 
-// SA_RV_STEP8B (SA_RV_V2=1): the same step with the q.f product taken from the
-// uncorrected quotient and the correction folded into a select, so two of the
-// three multiplies are off the dependent path: rr = (r < q0 t) ? q0 f - f : q0 f
-#define SA_RV_STEP8B                                                                             \
-        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l0]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l1]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l2]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l3]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l4]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l5]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l6]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l7]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_sub_u32 %[t], %[q], %[f]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_cselect_b32 %[q], %[t], %[q]\n\t"                                                     \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        ""
-
-template <int J, int V>
+template <int J>
 __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& mb, uint32_t& tb,
                                          uint32_t cm, uint32_t ctf, uint32_t tmask)
 {
@@ -2432,25 +2342,20 @@ __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta
       [l2] "i"((J + 3) & 63), [l3] "i"((J + 4) & 63), [l4] "i"((J + 5) & 63), [l5] "i"((J + 6) & 63),             \
       [l6] "i"((J + 7) & 63), [l7] "i"((J + 8) & 63)                                                             \
     : "scc"
-    if constexpr (V == 0)
-        asm volatile(SA_RV_STEP8 SA_RV_OPERANDS);
-    else
-        asm volatile(SA_RV_STEP8B SA_RV_OPERANDS);
+    asm volatile(SA_RV_STEP8 SA_RV_OPERANDS);
 #undef SA_RV_OPERANDS
 }
 #undef SA_RV_STEP8
-#undef SA_RV_STEP8B
 
 // the 64 steps of one segment (records in lanes 0..63 of cm / ctf)
-template <int V, int... P>
+template <int... P>
 __device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t ctf, uint32_t tmask,
                                            std::integer_sequence<int, P...>)
 {
     uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(ctf, 0), mb = 0, tb = 0;
-    (rv_step8<8 * P, V>(r, ma, ta, mb, tb, cm, ctf, tmask), ...);
+    (rv_step8<8 * P>(r, ma, ta, mb, tb, cm, ctf, tmask), ...);
 }
 
-template <int V>
 __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
                                                const TaskList& tl, const PRec* __restrict__ prs0,
                                                const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
@@ -2490,7 +2395,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                 }
                 const uint32_t r_seg = r;
                 const uint32_t cm = recip32z(ctf & tmask);
-                rv_segment<V>(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
+                rv_segment(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
                 if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
                 g++;
             }
@@ -2502,7 +2407,6 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
     if (s >= first && s <= g) ck[s] = kv;
 }
 
-template <int V>
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
     const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio)
@@ -2510,7 +2414,7 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const uint32_t wpg = blockDim.x >> 6;
     const uint32_t li = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (li >= tl.count) return;
-    coder_rv_chain<V>(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+    coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
 }
 
 // Locate list entry and segment of global coder-lane gi (gbase ascending).

@@ -17,7 +17,7 @@ def name(r):
 ks = sorted(({"n": name(r), "s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"]), "q": r.get("Queue_Id", "")}
              for r in rows), key=lambda k: k["s"])
 t0 = ks[0]["s"]
-passr = [k for k in ks if k["n"] == "k_coder_rv"]
+passr = [k for k in ks if k["n"].startswith("k_coder_rv")]
 print("pass R launches: %d" % len(passr))
 for p in passr:
     inside = [k for k in ks if k["q"] != p["q"] and k["n"].startswith(FRONT) and k["s"] < p["e"] and k["e"] > p["s"]]

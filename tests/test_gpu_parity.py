@@ -65,6 +65,49 @@ def test_golden_cases(enc, name):
     assert [len(o) for o in out] == g["blocks"]
 
 
+def test_name_prefix_suffix_lengths(enc):
+    """k_prep_sq16's row-parallel name columns (name_prefix_suffix): consecutive
+    names sharing prefixes and suffixes of 0..250 bytes, names that are prefixes
+    or suffixes of their neighbour, equal names, 1-byte names; tokenizer mode."""
+    rng = np.random.default_rng(7)
+    alpha = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789:_-./", dtype=np.uint8)
+
+    def word(n):
+        return bytes(alpha[rng.integers(0, len(alpha), n)])
+
+    names, prev = [], word(40)
+    for i in range(3000):
+        kind = i % 6
+        if kind == 0:
+            p, s, m = int(rng.integers(0, 120)), int(rng.integers(0, 120)), int(rng.integers(0, 16))
+            nm = prev[:p] + word(m) + prev[len(prev) - min(s, len(prev)):]
+        elif kind == 1:
+            nm = prev
+        elif kind == 2:
+            nm = prev[:int(rng.integers(1, len(prev) + 1))]
+        elif kind == 3:
+            nm = prev[int(rng.integers(0, len(prev))):]
+        elif kind == 4:
+            nm = word(int(rng.integers(1, 250)))
+        else:
+            nm = word(1) if rng.integers(0, 2) else prev + word(int(rng.integers(0, 60)))
+        nm = (nm or b"X")[:245]
+        names.append(nm)
+        prev = nm
+    # every header starts with the first one's first bytes (the block cut looks for
+    # "\n@" + more than five bytes of the file's first line, end_pos)
+    names = [b"SIMRD" + nm for nm in names]
+    recs = []
+    for nm in names:
+        L = int(rng.integers(20, 120))
+        seq = bytes(np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, L)])
+        qual = bytes(rng.integers(35, 64, L).astype(np.uint8))   # (no '@' in the qualities)
+        recs.append(b"@" + nm + b"\n" + seq + b"\n+\n" + qual + b"\n")
+    blocks = fq.blocks_from_fastq(b"".join(recs), None, 100_000)
+    assert len(blocks) > 2
+    _check(enc, blocks, fq.Config(bin_mode=0))
+
+
 def test_md5_off_and_empty_reads(enc):
     blocks = fq.blocks_from_fastq(synth.edge_cases())
     _check(enc, blocks, fq.Config(md5=False))
