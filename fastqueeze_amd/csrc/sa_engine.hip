@@ -190,15 +190,6 @@ struct sa_ctx {
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
     bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
     uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for
-    // SA_RV_PART=1: pass R of each context of a device on its own share of the
-    // coder CUs (st5, CU-masked: context k of C takes every C-th of them), so no
-    // two batches' chains meet on a SIMD and no LDS needs reserving (coder_lds 0)
-    bool rv_part = std::getenv("SA_RV_PART") && std::atoi(std::getenv("SA_RV_PART")) != 0;
-    int share_index = 0;             // this context's index among the contexts sharing the front
-    hipStream_t st5 = nullptr;       // (rv_part) pass R
-    hipEvent_t ev_r5a = nullptr, ev_r5b = nullptr;
-    int st5_parts = 0;               // the partition count st5 was made for
-    std::vector<uint32_t> m_coder;   // CU mask of the coder CUs (st3's)
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -311,9 +302,6 @@ struct sa_ctx {
         if (st2) (void)hipStreamDestroy(st2);
         if (st3) (void)hipStreamDestroy(st3);
         if (st4) (void)hipStreamDestroy(st4);
-        if (st5) (void)hipStreamDestroy(st5);
-        if (ev_r5a) (void)hipEventDestroy(ev_r5a);
-        if (ev_r5b) (void)hipEventDestroy(ev_r5b);
     }
 };
 
@@ -559,51 +547,11 @@ int coder_list(sa_ctx* c, hipStream_t st, int slot, const std::vector<CoderTask>
 void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv, int ph)
 {
     if (!tl.count) return;
-    hipStream_t sr = st;
-    if (c->st5) {   // (rv_part) on the context's own coder CUs, in order with st
-        (void)hipEventRecord(c->ev_r5a, st);
-        (void)hipStreamWaitEvent(c->st5, c->ev_r5a, 0);
-        sr = c->st5;
-    }
-    if (ph >= 0) ev_begin(c, ph, sr);
+    if (ph >= 0) ev_begin(c, ph, st);
     hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
-                       c->coder_lds, sr, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
+                       c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio);
-    if (ph >= 0) ev_finish(c, ph, sr);
-    if (c->st5) {
-        (void)hipEventRecord(c->ev_r5b, c->st5);
-        (void)hipStreamWaitEvent(st, c->ev_r5b, 0);
-    }
-}
-
-// (rv_part) st5 over this context's share of the coder CUs: the coder CUs in
-// order, every C-th from the context's index (C = the contexts sharing the
-// front when the batch starts)
-int rv_part_stream(sa_ctx* c)
-{
-    const int parts = std::max(1, c->fs->refs);
-    if (c->st5 && c->st5_parts == parts) return 0;
-    if (c->st5) {
-        SA_CHECK(c, hipStreamSynchronize(c->st5));
-        (void)hipStreamDestroy(c->st5);
-        c->st5 = nullptr;
-    }
-    std::vector<uint32_t> m(c->m_coder.size(), 0u);
-    int j = 0, got = 0;
-    for (uint32_t cu = 0; cu < 32u * (uint32_t)m.size(); cu++)
-        if ((c->m_coder[cu / 32] >> (cu % 32)) & 1u) {
-            if (j % parts == c->share_index % parts) {
-                m[cu / 32] |= 1u << (cu % 32);
-                got++;
-            }
-            j++;
-        }
-    if (!got) m = c->m_coder;
-    SA_CHECK(c, hipExtStreamCreateWithCUMask(&c->st5, (uint32_t)m.size(), m.data()));
-    if (!c->ev_r5a) SA_CHECK(c, hipEventCreateWithFlags(&c->ev_r5a, hipEventDisableTiming));
-    if (!c->ev_r5b) SA_CHECK(c, hipEventCreateWithFlags(&c->ev_r5b, hipEventDisableTiming));
-    c->st5_parts = parts;
-    return 0;
+    if (ph >= 0) ev_finish(c, ph, st);
 }
 
 void coder_launch_l12(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv)
@@ -761,7 +709,6 @@ sa_ctx* sa_create(int device)
         const int w = std::atoi(e);
         c->coder_waves = (w == 1 || w == 2) ? (uint32_t)w : 4u;
     }
-    if (c->rv_part) c->coder_lds = 0;
     if (const char* e = std::getenv("SA_CODER_LDS")) c->coder_lds = (uint32_t)std::min(std::max(std::atoi(e), 0), 160 * 1024);
     if (c->coder_lds > 64 * 1024 &&
         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -791,13 +738,7 @@ sa_ctx* sa_create(int device)
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
     if (every == 1) m_seq = m_long;   // (st3: the coder chains; st4: the long model runs)
-    c->m_coder = m_seq;
-    // SA_FRONT_PRIO=1: the front's stream at the device's highest stream
-    // priority (its workgroups dispatched ahead of the tails' when CUs free up)
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const bool front_prio = std::getenv("SA_FRONT_PRIO") && std::atoi(std::getenv("SA_FRONT_PRIO")) != 0;
-    if (hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, front_prio ? prio_hi : prio_lo) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)m_seq.size(), m_seq.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
@@ -834,7 +775,6 @@ sa_ctx* sa_create_shared(int device, sa_ctx* peer)
     std::lock_guard<std::mutex> g(g_share_mu);
     FrontShare* own = c->fs;
     c->fs = peer->fs;
-    c->share_index = c->fs->refs;
     c->fs->refs++;
     for (DBuf* b : own->buffers()) b->release();
     if (own->ev_free) (void)hipEventDestroy(own->ev_free);
@@ -1438,7 +1378,6 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     //      (concurrent latency-bound launches land on shared SIMDs); the L passes
     //      after the long runs are done ----
     SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
-    if (c->rv_part && rv_part_stream(c)) return -1;
     std::vector<uint32_t> out_len;
     {
         const int rc = coder_run(c, tasks, cv, st3, PH_CODER_R, PH_CODER_L, c->ev_long_done, exact, out_len, payload);
