@@ -330,8 +330,7 @@ int mail_reset(sa_ctx* c)
         if (c->mail) c->mail_retired.push_back(c->mail);
         c->mail = nullptr;
         c->mail_cap = 0;
-        // (mapped: k_mail_copy reads and writes it from the device)
-        if (hipHostMalloc(reinterpret_cast<void**>(&c->mail), want, hipHostMallocMapped) != hipSuccess) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->mail), want, hipHostMallocDefault) != hipSuccess) {
             c->mail = nullptr;
             return 0;   // (copies fall back to pageable memory)
         }
@@ -349,35 +348,6 @@ uint8_t* mail_take(sa_ctx* c, size_t n)
     return c->mail + at;
 }
 
-// The mailbox's copies run as a kernel on the stream (reading or writing the
-// pinned, device-mapped mailbox over PCIe): as hipMemcpyAsync they went to the
-// copy engines, where in the command line they queued behind the other
-// contexts' multi-GB text uploads (sa_stage_text) -- a front waited tens of ms
-// for a 1 MB plan (round 3 g3u: prep+scan / emit phases of 100-150 ms against
-// 30-45 in the bench).  SA_MAIL_DMA=1: hipMemcpyAsync, for A/B.
-__global__ void k_mail_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, size_t n)
-{
-    const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, step = (size_t)gridDim.x * blockDim.x;
-    if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
-        const size_t n16 = n / 16;
-        for (size_t i = i0; i < n16; i += step)
-            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-        for (size_t i = n16 * 16 + i0; i < n; i += step) dst[i] = src[i];
-    } else {
-        for (size_t i = i0; i < n; i += step) dst[i] = src[i];
-    }
-}
-
-hipError_t mail_copy(void* dst, const void* src, size_t n, hipStream_t st)
-{
-    const uint32_t grid = (uint32_t)std::min<size_t>((n + 4095) / 4096, 1024);
-    hipLaunchKernelGGL(k_mail_copy, dim3(std::max(1u, grid)), dim3(256), 0, st, reinterpret_cast<uint8_t*>(dst),
-                       reinterpret_cast<const uint8_t*>(src), n);
-    return hipGetLastError();
-}
-
-const bool g_mail_dma = std::getenv("SA_MAIL_DMA") && std::atoi(std::getenv("SA_MAIL_DMA")) != 0;
-
 // host -> device through the mailbox (the source may be reused at once)
 hipError_t h2d(sa_ctx* c, void* dst, const void* src, size_t n, hipStream_t st)
 {
@@ -385,8 +355,7 @@ hipError_t h2d(sa_ctx* c, void* dst, const void* src, size_t n, hipStream_t st)
     uint8_t* m = mail_take(c, n);
     if (!m) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
     std::memcpy(m, src, n);
-    if (g_mail_dma) return hipMemcpyAsync(dst, m, n, hipMemcpyHostToDevice, st);
-    return mail_copy(dst, m, n, st);
+    return hipMemcpyAsync(dst, m, n, hipMemcpyHostToDevice, st);
 }
 
 // device -> host through the mailbox: `dst` holds the bytes after sync_d2h
@@ -396,8 +365,7 @@ hipError_t d2h(sa_ctx* c, void* dst, const void* src, size_t n, hipStream_t st)
     uint8_t* m = mail_take(c, n);
     if (!m) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st);
     c->pending.push_back(sa_ctx::Pending{dst, m, n});
-    if (g_mail_dma) return hipMemcpyAsync(m, src, n, hipMemcpyDeviceToHost, st);
-    return mail_copy(m, src, n, st);
+    return hipMemcpyAsync(m, src, n, hipMemcpyDeviceToHost, st);
 }
 
 hipError_t sync_d2h(sa_ctx* c, hipStream_t st)
