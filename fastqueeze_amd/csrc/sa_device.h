@@ -144,7 +144,7 @@ struct TaskList {
     const uint64_t* gbase;   // count + 1 entries
     const CoderRun* run;
     uint32_t count;
-    uint32_t pad_;
+    uint32_t nlong;          // pass R: entries [0, nlong) get a wave each, the rest are shared (k_coder_rv)
     uint64_t total_segs;
 };
 

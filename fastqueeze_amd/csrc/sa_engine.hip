@@ -201,6 +201,10 @@ struct sa_ctx {
     // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
     // SA_CODER_LDS)
     uint32_t coder_waves = 4;
+    uint32_t rv_short_waves = std::getenv("SA_RV_SHORT_WAVES") ? (uint32_t)std::atoi(std::getenv("SA_RV_SHORT_WAVES")) : 32u;
+    // k_replay_aux_long workgroups: what the long-run CUs hold at once (6 per CU;
+    // SA_LONG_GRID overrides, round 2 used 2048)
+    uint32_t long_grid = 0;
     uint32_t coder_lds = 82 * 1024;
     std::string err;
     bool timing = false;
@@ -544,11 +548,21 @@ int coder_list(sa_ctx* c, hipStream_t st, int slot, const std::vector<CoderTask>
     return 0;
 }
 
-void coder_launch_r(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv, int ph)
+// pass R: chains of at least RV_LONG_SYMS symbols get a wave each; the others
+// share rv_short_waves waves (k_coder_rv; SA_RV_SHORT_WAVES=0: a wave per chain)
+constexpr uint32_t RV_LONG_SYMS = 1u << 21;
+
+void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv, int ph, uint32_t nlong)
 {
     if (!tl.count) return;
+    uint32_t waves = tl.count;
+    tl.nlong = tl.count;
+    if (c->rv_short_waves && nlong + c->rv_short_waves < tl.count) {
+        tl.nlong = nlong;
+        waves = nlong + c->rv_short_waves;
+    }
     if (ph >= 0) ev_begin(c, ph, st);
-    hipLaunchKernelGGL(k_coder_rv, dim3((tl.count + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
+    hipLaunchKernelGGL(k_coder_rv, dim3((waves + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
                        c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio);
     if (ph >= 0) ev_finish(c, ph, st);
@@ -587,6 +601,7 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
     c->coder_restarts = 0;
     std::vector<uint64_t> gb;
     TaskList tl;
+    uint32_t nlong = 0;
     {
         std::vector<uint32_t> ids;
         for (uint32_t t = 0; t < (uint32_t)tasks.size(); t++) ids.push_back(t);
@@ -594,8 +609,9 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         std::stable_sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t b) { return tasks[a].n > tasks[b].n; });
         std::vector<CoderRun> runs(ids.size(), CoderRun{0ull, 0xffffffffu, 0u, 0u, 0u});
         if (coder_list(c, st, 0, tasks, ids, runs, gb, tl)) return -1;
+        for (const uint32_t t : ids) nlong += tasks[t].n >= RV_LONG_SYMS ? 1u : 0u;
     }
-    coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1);
+    coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1, nlong);
     if (before_l) SA_CHECK(c, hipStreamWaitEvent(st, before_l, 0));
     if (c->timing && ph_l >= 0) ev_begin(c, ph_l, st);
     coder_launch_l12(c, st, tl, cv);
@@ -654,7 +670,7 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         }
         c->coder_restarts += (uint32_t)ids.size();
         if (coder_list(c, st, 0, tasks, ids, runs, gb, tl)) return -1;
-        coder_launch_r(c, st, tl, cv, -1);
+        coder_launch_r(c, st, tl, cv, -1, 0);
         coder_launch_l12(c, st, tl, cv);
         coder_launch_l3(c, st, tl, cv);
         SA_CHECK(c, hipGetLastError());
@@ -738,6 +754,12 @@ sa_ctx* sa_create(int device)
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
     if (every == 1) m_seq = m_long;   // (st3: the coder chains; st4: the long model runs)
+    {
+        uint32_t ncu_long = 0;
+        for (uint32_t w : m_long) ncu_long += (uint32_t)__builtin_popcount(w);
+        c->long_grid = std::max(1u, 6u * ncu_long);
+        if (const char* lg = std::getenv("SA_LONG_GRID")) c->long_grid = (uint32_t)std::max(1, std::atoi(lg));
+    }
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)m_seq.size(), m_seq.data()) != hipSuccess ||
@@ -1368,7 +1390,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     hipStream_t st3 = c->st3, st4 = c->st4;
     SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
     if (pa.total)
-        hipLaunchKernelGGL(k_replay_aux_long, dim3(LONG_GRID), dim3(128), c->long_lds, st4, rl, ak, av, sink_aux,
+        hipLaunchKernelGGL(k_replay_aux_long, dim3(c->long_grid), dim3(128), c->long_lds, st4, rl, ak, av, sink_aux,
                            d_err, c->chain_prio);
     SA_CHECK(c, hipGetLastError());
     SA_CHECK(c, hipEventRecord(c->ev_long_done, st4));

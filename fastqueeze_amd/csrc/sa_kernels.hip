@@ -2031,7 +2031,10 @@ __device__ __forceinline__ void replay_long_run(const LongRun& lr, const SymSink
 
 // Workgroups of two waves (wave 0 replays, wave 1 loads) take long runs from
 // a work queue, the runs of >= HUGE_RUN symbols first.
-constexpr uint32_t LONG_GRID = 2048;
+// (k_replay_aux_long's grid is sized to what its CUs hold at once -- sa_engine
+// long_grid: it is a work queue, and workgroups beyond that waited for slots
+// until the queue was empty, holding up the kernels queued behind the launch
+// on its hardware queue: 100-200 ms stalls of single front kernels, round 3)
 
 __global__ __launch_bounds__(128) void k_replay_aux_long(const RunLists rl, const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, const SymSink rec_all,
@@ -2393,6 +2396,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                     const uint32_t s = g - 63 + lane;
                     if (s >= first) ck[s] = kv;
                 }
+                r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);   // (scalar for the asm: see k_coder_rv)
                 const uint32_t r_seg = r;
                 const uint32_t cm = recip32z(ctf & tmask);
                 rv_segment(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
@@ -2407,14 +2411,27 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
     if (s >= first && s <= g) ck[s] = kv;
 }
 
+// Waves [0, nlong) take one (long) chain each; the waves after them share the
+// remaining (short) chains round robin, longest first.  A launch then asks for
+// one pass-R workgroup slot (one per CU) per four long chains plus a few,
+// instead of one per four chains: with three or four batches' pass R in flight
+// the excess waited for slots, and a launch that cannot place all its
+// workgroups holds up the kernels queued behind it on its hardware queue.
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
     const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio)
 {
     const uint32_t wpg = blockDim.x >> 6;
-    const uint32_t li = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (li >= tl.count) return;
-    coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+    const uint32_t wi = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t nl = tl.nlong < tl.count ? tl.nlong : tl.count;
+    // (one call site: two inlined copies of the chain's asm made the compiler
+    // move its scalar operands through VGPRs)
+    const uint32_t step = wi < nl ? 0u : gridDim.x * wpg - nl;
+    for (uint32_t li = wi; li < tl.count;) {
+        coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+        if (!step) break;
+        li += step;
+    }
 }
 
 // Locate list entry and segment of global coder-lane gi (gbase ascending).

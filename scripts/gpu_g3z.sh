@@ -1,0 +1,30 @@
+#!/bin/bash
+# round 3, call g3z: k_replay_aux_long's grid sized to its resident capacity + pass R's short chains on shared
+# waves: parity, bench and CLI A/B against round 2's grids (SA_LONG_GRID=2048 SA_RV_SHORT_WAVES=0)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/g3z
+mkdir -p $O
+cd $R
+export TMPDIR=/tmp SA_NO_BUILD=1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_align.py tests/test_gpu_hash.py -x -q --timeout 120 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+B="python -u bench.py --steps 16 --e2e-batches 0 --cpu-seconds 0 --no-verify"
+OLD="SA_LONG_GRID=2048 SA_RV_SHORT_WAVES=0"
+timeout -k 10 300 $B > $O/new.json 2> $O/new.err || exit 2
+env $OLD timeout -k 10 300 $B > $O/old.json 2> $O/old.err || exit 3
+D=/dev/shm/sa_e2e_$$
+trap 'rm -rf $D' EXIT
+timeout -k 10 300 python -u scripts/make_e2e_files.py $D 4 3 > $O/make.log 2>&1 || exit 4
+CLI="./fastqueeze_amd/bin/seqarc_amd -c -f -v -t 16 -1 $D/r1.fq -2 $D/r2.fq -o $D/e2e --batch 69 --contexts 5"
+run() {
+    local n=$1; shift
+    sleep 8
+    local t0=$(date +%s.%N)
+    env "$@" > $O/$n.log 2>&1 || return 1
+    local t1=$(date +%s.%N)
+    echo "$n wall $(python3 -c "print(round($t1 - $t0, 3))") s" >> $O/walls.txt
+}
+run cli_new timeout -k 10 120 $CLI || exit 5
+run cli_old $OLD timeout -k 10 120 $CLI || exit 6
+run cli_new2 timeout -k 10 120 $CLI || exit 7
+run cli_old2 $OLD timeout -k 10 120 $CLI || exit 8
