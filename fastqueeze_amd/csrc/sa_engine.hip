@@ -200,6 +200,13 @@ struct sa_ctx {
     // pass-R placement (k_coder_rv): four chains per workgroup, one per SIMD, and
     // enough unused LDS that a CU holds one pass-R workgroup (SA_CODER_WAVES /
     // SA_CODER_LDS)
+    // The waits between this context's streams happen on the host thread (which
+    // has nothing else to do then) instead of as barrier packets: the boxes run
+    // with four hardware queues per process (GPU_MAX_HW_QUEUES=4), so the
+    // contexts' streams share queues, and a barrier waiting for this batch's
+    // front or long runs held up every other context's work queued behind it
+    // (pass R, L passes).  SA_HOST_WAITS=0: device-side waits, for A/B.
+    bool host_waits = !(std::getenv("SA_HOST_WAITS") && std::atoi(std::getenv("SA_HOST_WAITS")) == 0);
     uint32_t coder_waves = 4;
     uint32_t rv_short_waves = std::getenv("SA_RV_SHORT_WAVES") ? (uint32_t)std::atoi(std::getenv("SA_RV_SHORT_WAVES")) : 32u;
     // k_replay_aux_long workgroups: what the long-run CUs hold at once (6 per CU;
@@ -612,7 +619,10 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         for (const uint32_t t : ids) nlong += tasks[t].n >= RV_LONG_SYMS ? 1u : 0u;
     }
     coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1, nlong);
-    if (before_l) SA_CHECK(c, hipStreamWaitEvent(st, before_l, 0));
+    if (before_l) {
+        if (c->host_waits) SA_CHECK(c, hipEventSynchronize(before_l));   // (see host_waits)
+        else SA_CHECK(c, hipStreamWaitEvent(st, before_l, 0));
+    }
     if (c->timing && ph_l >= 0) ev_begin(c, ph_l, st);
     coder_launch_l12(c, st, tl, cv);
     SA_CHECK(c, hipGetLastError());
@@ -1388,7 +1398,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     front_lock.freed = true;
     front_lock.unlock();
     hipStream_t st3 = c->st3, st4 = c->st4;
-    SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
+    if (c->host_waits) SA_CHECK(c, hipEventSynchronize(c->ev_fork_seq));
+    else SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
     if (pa.total)
         hipLaunchKernelGGL(k_replay_aux_long, dim3(c->long_grid), dim3(128), c->long_lds, st4, rl, ak, av, sink_aux,
                            d_err, c->chain_prio);
@@ -1399,7 +1410,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // ---- range coders: every chain in one launch on st3, longest first
     //      (concurrent latency-bound launches land on shared SIMDs); the L passes
     //      after the long runs are done ----
-    SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
+    if (!c->host_waits) SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
     std::vector<uint32_t> out_len;
     {
         const int rc = coder_run(c, tasks, cv, st3, PH_CODER_R, PH_CODER_L, c->ev_long_done, exact, out_len, payload);

@@ -1614,12 +1614,13 @@ int main(int argc, char** argv)
     }
     if (!o.f1 || !o.out) return usage();
     // one hardware queue per stream (four per context): with the runtime's
-    // default of four queues, the contexts' streams share queues and a front
-    // waits behind another context's range coder (set before the device is used)
+    // default of four queues (which the GPU boxes preset), the contexts' streams
+    // share queues and one context's packets wait behind another's (DESIGN.md
+    // 5); set before the device is used, overriding a preset value
     {
         char q[16];
-        snprintf(q, sizeof q, "%d", std::min(32, 4 * o.contexts * o.devices + 4));
-        setenv("GPU_MAX_HW_QUEUES", q, 0);
+        snprintf(q, sizeof q, "%d", std::min(32, 4 * o.contexts + 4));   // (per device)
+        setenv("GPU_MAX_HW_QUEUES", q, 1);
     }
     const int rc = compress(o);
     if (g_fast_exit) {   // (every thread joined, the archive closed): no runtime teardown
