@@ -250,7 +250,13 @@ void sa_host_free(void* p)
     if (p) (void)hipHostFree(p);
 }
 
-int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
+}  // extern "C"
+
+namespace {
+
+// Stages the texts into input I with context c's stream and mailbox
+// (sa_stage_text: c's own input; sa_stage_text_input: any input of the device)
+int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_info* info)
 {
     const ReserveScope reserve(c ? c->reserve_blocks : 0, n > 0 ? (uint32_t)n : 0);
     if (!c) return -1;
@@ -258,9 +264,11 @@ int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
         c->err = "sa_stage_text: invalid block list";
         return -1;
     }
+    if (!I || I->device != c->device) {
+        c->err = "sa_stage_text_input: no input, or an input of another device";
+        return -1;
+    }
     SA_CHECK(c, hipSetDevice(c->device));
-    c->have_output = false;
-    sa_input* I = &c->own;
     hipStream_t st = c->st;
     if (mail_reset(c)) return -1;
     // (the input is empty until the whole batch is staged: a failed staging
@@ -469,6 +477,31 @@ int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
     I->blocks = std::move(dblocks);
     I->nblocks = (uint32_t)n;
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sa_stage_text(sa_ctx* c, const sa_text_block* in, int n, sa_text_info* info)
+{
+    if (!c) return -1;
+    c->have_output = false;
+    return stage_text(c, &c->own, in, n, info);
+}
+
+sa_input* sa_input_empty(int device)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    sa_input* I = new sa_input();
+    I->device = device;
+    return I;
+}
+
+int sa_stage_text_input(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_info* info)
+{
+    return stage_text(c, I, in, n, info);
 }
 
 }  // extern "C"

@@ -65,6 +65,7 @@ int usage()
             "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
             "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
             "                  [--block-size MiB] [--device D] [--share-device] [--no-ramp] [--release]\n"
+            "                  [--no-stage-ahead]\n"
             "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
             "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
             "       (-c / -d with ref.fa: the reference path; -I N insert size, --maxmis M)\n");
@@ -720,7 +721,7 @@ struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
          verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = true,
-         release = false;
+         release = false, stage_ahead = true;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -826,6 +827,7 @@ int compress(const Options& o)
                                        : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // contexts: K per device; every device's contexts share one front scratch
     std::vector<sa_ctx*> ctxs;
+    std::vector<int> ctx_dev;   // (the device of each context)
     // --ingest-only: the reader and the block cut alone, feeding devices x
     // contexts consumers that take batches as the device parse would (no device)
     if (o.host_only || o.ingest_only) ctxs.assign((size_t)o.contexts * (o.ingest_only ? o.devices : 1), nullptr);
@@ -837,6 +839,7 @@ int compress(const Options& o)
             if (!c) break;
             if (!first) first = c;
             ctxs.push_back(c);
+            ctx_dev.push_back(dev);
         }
         if (!first) break;
     }
@@ -1057,8 +1060,149 @@ int compress(const Options& o)
         return true;
     };
     std::vector<std::thread> encoders;
-    for (sa_ctx* ctx : ctxs)
-        encoders.emplace_back([&, ctx]() {
+    // Stage ahead (device parse, default): each context stages its next batch
+    // into a second device input -- with a staging context of its own (stream,
+    // mailbox) on a helper thread -- while it encodes the current one, so the
+    // H2D copy and the parse leave the context's cycle.  --no-stage-ahead: the
+    // stage is part of the cycle (sa_stage_text into the context's own input).
+    const bool stage_ahead = dev_parse && !o.ingest_only && o.stage_ahead && !ctxs.empty() && ctxs[0];
+    std::vector<sa_ctx*> stagers;
+    std::vector<sa_input*> sinputs;   // two per context
+    if (stage_ahead) {
+        for (size_t i = 0; i < ctxs.size(); i++) {
+            sa_ctx* s = sa_create(ctx_dev[i]);
+            sa_input* a = sa_input_empty(ctx_dev[i]);
+            sa_input* b = sa_input_empty(ctx_dev[i]);
+            if (!s || !a || !b) {
+                fprintf(stderr, "seqarc_amd: cannot create the staging contexts\n");
+                return 1;
+            }
+            if (o.ramp) sa_set_reserve(s, (uint32_t)B);
+            stagers.push_back(s);
+            sinputs.push_back(a);
+            sinputs.push_back(b);
+        }
+    }
+    // takes batch k (in order) once the reader has cut it: false when the input
+    // is exhausted or the run failed
+    auto claim = [&](int64_t& k, std::vector<Job*>& js) -> bool {
+        std::unique_lock<std::mutex> lk(mu);
+        if (failed) return false;
+        k = next_batch++;
+        cv.wait(lk, [&] { return failed || (nblocks >= 0 && bstart(k) >= nblocks) || batch_ready(k); });
+        if (failed || (nblocks >= 0 && bstart(k) >= nblocks)) return false;
+        const int64_t b0 = bstart(k), b1 = nblocks >= 0 ? std::min(nblocks, bstart(k + 1)) : bstart(k + 1);
+        js.clear();
+        for (int64_t i = b0; i < b1; i++) js.push_back(jobs[i].get());
+        return true;
+    };
+    // stages the batch's texts into input I with staging context s (the text
+    // windows go back to the reader at once)
+    auto stage_into = [&](sa_ctx* s, sa_input* I, std::vector<Job*>& js) -> bool {
+        const double t0 = now_s();
+        std::vector<sa_text_block> tin(js.size());
+        std::vector<sa_text_info> ti(js.size());
+        for (size_t i = 0; i < js.size(); i++)
+            tin[i] = sa_text_block{js[i]->t1.data(), js[i]->t1.size(), pe ? js[i]->t2.data() : nullptr,
+                                   pe ? js[i]->t2.size() : 0};
+        if (sa_stage_text_input(s, I, tin.data(), (int)tin.size(), ti.data()) != 0) {
+            fail(std::string("staging failed: ") + sa_last_error(s));
+            return false;
+        }
+        {
+            double cur = stage_busy.load();
+            while (!stage_busy.compare_exchange_weak(cur, cur + now_s() - t0)) {}
+        }
+        {
+            std::lock_guard<std::mutex> g(mu);
+            staged += (int64_t)js.size();
+            for (size_t i = 0; i < js.size(); i++) {
+                texts.put(js[i]->t1);   // (the device holds the text now)
+                texts.put(js[i]->t2);
+                js[i]->nreads = ti[i].nreads;
+                js[i]->len_long = ti[i].len_long;
+                js[i]->out.resize(ti[i].out_bound);
+            }
+        }
+        cv.notify_all();
+        return true;
+    };
+    for (size_t ci = 0; stage_ahead && ci < ctxs.size(); ci++)
+        encoders.emplace_back([&, ci]() {
+            sa_ctx* ctx = ctxs[ci];
+            sa_ctx* stg = stagers[ci];
+            sa_input* in2[2] = {sinputs[2 * ci], sinputs[2 * ci + 1]};
+            int64_t k = 0;
+            std::vector<Job*> js;
+            double tw = now_s();
+            if (!claim(k, js)) return;
+            double te = now_s();
+            if (!stage_into(stg, in2[0], js)) return;
+            for (int cur = 0;; cur ^= 1) {
+                // the next batch is claimed and staged while this one encodes
+                int64_t k2 = -1;
+                std::vector<Job*> js2;
+                double tw2 = 0, te2 = 0;
+                std::future<int> next = std::async(std::launch::async, [&]() -> int {
+                    tw2 = now_s();
+                    if (!claim(k2, js2)) return 0;
+                    te2 = now_s();
+                    return stage_into(stg, in2[cur ^ 1], js2) ? 1 : -1;
+                });
+                {
+                    double c0 = t_first_enc.load();
+                    while (te < c0 && !t_first_enc.compare_exchange_weak(c0, te)) {}
+                }
+                std::vector<sa_out> outs(js.size());
+                for (size_t i = 0; i < js.size(); i++) outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                const sa_cfg c = cfg;
+                const double tr = now_s();
+                if ((chain ? sa_run_input_aligned(ctx, in2[cur], &c, &acfg[ctx], chain, (uint64_t)k)
+                           : sa_run_input(ctx, in2[cur], &c)) != 0)
+                    return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                const double tf = now_s();
+                if (sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
+                    return fail(std::string("fetch failed: ") + sa_last_error(ctx));
+                if (o.verbose) {
+                    const char* pn[16];
+                    float pm[16];
+                    const int np = sa_phase_times(ctx, pn, pm, 16);
+                    std::string ph;
+                    for (int x = 0; x < np; x++) {
+                        char pb[48];
+                        snprintf(pb, sizeof pb, " %s %.0f", pn[x], pm[x]);
+                        ph += pb;
+                    }
+                    fprintf(stderr,
+                            "seqarc_amd: batch %lld (%zu blocks) context %p: asked %.3f s, ready %.3f s, staged ahead, "
+                            "run from %.3f s for %.3f s, fetch %.3f s; device ms:%s\n",
+                            (long long)k, js.size(), (void*)ctx, tw, te, tr, tf - tr, now_s() - tf, ph.c_str());
+                }
+                {
+                    const double t1 = now_s();
+                    double c0 = enc_busy.load();
+                    while (!enc_busy.compare_exchange_weak(c0, c0 + t1 - tr)) {}
+                    c0 = t_last_enc.load();
+                    while (t1 > c0 && !t_last_enc.compare_exchange_weak(c0, t1)) {}
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    for (size_t i = 0; i < js.size(); i++) {
+                        js[i]->out.n = outs[i].size;
+                        js[i]->state = 2;
+                    }
+                }
+                cv.notify_all();
+                const int r = next.get();
+                if (r <= 0) return;   // (no more batches, or the staging failed: fail() was called)
+                k = k2;
+                js = std::move(js2);
+                tw = tw2;
+                te = te2;
+            }
+        });
+    for (size_t ci = 0; !stage_ahead && ci < ctxs.size(); ci++)
+        encoders.emplace_back([&, ctx = ctxs[ci]]() {
             for (;;) {
                 int64_t k, b0, b1;
                 std::vector<Job*> js;
@@ -1229,6 +1373,14 @@ int compress(const Options& o)
         indexes.clear();
         if (chain) sa_align_chain_destroy(chain);
         chain = nullptr;
+        for (sa_input*& I : sinputs) {
+            sa_input_destroy(I);
+            I = nullptr;
+        }
+        for (sa_ctx*& s : stagers) {
+            sa_destroy(s);
+            s = nullptr;
+        }
         for (sa_ctx*& c : ctxs)
             if (c) {
                 sa_destroy(c);
@@ -1575,6 +1727,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--ingest-only")) o.ingest_only = true;
         else if (!strcmp(a, "--no-ramp")) o.ramp = false;
         else if (!strcmp(a, "--release")) o.release = true;
+        else if (!strcmp(a, "--no-stage-ahead")) o.stage_ahead = false;
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (!strcmp(a, "-i")) { o.index = true; if (!(o.ref = val())) return usage(); }

@@ -134,6 +134,12 @@ typedef struct sa_input sa_input;
 sa_input *sa_input_create(int device, const sa_block *in, int n);   /* NULL on error */
 void sa_input_destroy(sa_input *in);
 int sa_run_input(sa_ctx *ctx, const sa_input *in, const sa_cfg *cfg);   /* then sa_fetch */
+/* an empty input of a device, filled by sa_stage_text_input: FASTQ text staged
+ * and parsed on the device with ctx's stream (ctx may be another context than
+ * the one that later runs the input: the command line stages a context's next
+ * batch while the context encodes the current one) */
+sa_input *sa_input_empty(int device);
+int sa_stage_text_input(sa_ctx *ctx, sa_input *in, const sa_text_block *blocks, int n, sa_text_info *info);
 
 /* ---- range coder over pre-modelled symbols ---------------------------- */
 /* The carry-less range coder inlined in every EncapFqzComp::encode_* (e.g.
