@@ -65,7 +65,7 @@ int usage()
             "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
             "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
             "                  [--block-size MiB] [--device D] [--share-device] [--no-ramp] [--release]\n"
-            "                  [--no-stage-ahead]\n"
+            "                  [--stage-ahead]\n"
             "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
             "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
             "       (-c / -d with ref.fa: the reference path; -I N insert size, --maxmis M)\n");
@@ -721,7 +721,7 @@ struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
          verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = true,
-         release = false, stage_ahead = true;
+         release = false, stage_ahead = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -1060,11 +1060,14 @@ int compress(const Options& o)
         return true;
     };
     std::vector<std::thread> encoders;
-    // Stage ahead (device parse, default): each context stages its next batch
-    // into a second device input -- with a staging context of its own (stream,
+    // --stage-ahead (device parse): each context stages its next batch into a
+    // second device input -- with a staging context of its own (stream,
     // mailbox) on a helper thread -- while it encodes the current one, so the
-    // H2D copy and the parse leave the context's cycle.  --no-stage-ahead: the
-    // stage is part of the cycle (sa_stage_text into the context's own input).
+    // H2D copy and the parse leave the context's cycle.  Measured slower (4.7-5.0
+    // against 6.6-6.7 GB/s on 42.8 GB, round 3 g4d: the staging contexts' streams
+    // outnumber the hardware queues, and the tails slowed under the concurrent
+    // parse), so by default the stage is part of the cycle (sa_stage_text into
+    // the context's own input).
     const bool stage_ahead = dev_parse && !o.ingest_only && o.stage_ahead && !ctxs.empty() && ctxs[0];
     std::vector<sa_ctx*> stagers;
     std::vector<sa_input*> sinputs;   // two per context
@@ -1727,7 +1730,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--ingest-only")) o.ingest_only = true;
         else if (!strcmp(a, "--no-ramp")) o.ramp = false;
         else if (!strcmp(a, "--release")) o.release = true;
-        else if (!strcmp(a, "--no-stage-ahead")) o.stage_ahead = false;
+        else if (!strcmp(a, "--stage-ahead")) o.stage_ahead = true;
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (!strcmp(a, "-i")) { o.index = true; if (!(o.ref = val())) return usage(); }
