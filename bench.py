@@ -196,14 +196,14 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
         + args.e2e_args.split()
     if not ingest_only and args.e2e_settle > 0:
         time.sleep(args.e2e_settle)   # (outside the timed run: a fresh job starts on a settled device)
-    t0 = time.perf_counter()
+    t0, m0 = time.perf_counter(), time.monotonic()
     cmdline = " ".join(os.path.basename(c) if i == 0 else c for i, c in enumerate(cmd))
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     except subprocess.TimeoutExpired:
         log(f"end-to-end run timed out: {cmdline}")
         return {"value": None, "unit": "MB/s", "error": "timed out after 900 s", "command": cmdline}
-    wall = time.perf_counter() - t0
+    wall, m1 = time.perf_counter() - t0, time.monotonic()
     if r.returncode != 0:   # (recorded, not fatal: the in-HBM line above is the bench's measurement)
         log(f"end-to-end run failed ({r.returncode}): {r.stderr[-2000:]}")
         return {"value": None, "unit": "MB/s", "error": f"exit {r.returncode}: {r.stderr[-500:]}", "command": cmdline}
@@ -215,15 +215,18 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
         arc = f.read()
     same = None if ingest_only else arc[16:16 + len(expect)] == expect   # (a batch's last, short block merges
     #                                                                          with the next batch's text)
-    clock, stages = None, None
+    clock, stages, proc = None, None, None
     for ln in r.stderr.splitlines():
         if "MB/s" in ln:
             clock = float(ln.rsplit(",", 1)[1].split()[0])
         if "contexts ready" in ln:
             stages = ln.split(": ", 1)[1]
+        if "monotonic clock: main" in ln:   # process start -> main, and exit -> reaped (dynamic loading; the
+            mm, me = (float(x.split()[-1]) for x in ln.split(": ", 2)[2].split(", "))   # driver's teardown)
+            proc = {"start_to_main_s": round(mm - m0, 3), "exit_to_reaped_s": round(m1 - me, 3)}
     os.remove(out + ".arc")
     return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
-            "cli_clock_mb_s": clock, "cli_stages": stages, "fastq_bytes": in_bytes, "devices": devices,
+            "cli_clock_mb_s": clock, "cli_stages": stages, "process": proc, "fastq_bytes": in_bytes, "devices": devices,
             "contexts": contexts, "batch_blocks": batch, "device_settle_s": 0 if ingest_only else args.e2e_settle,
             "parse": "none (--ingest-only)" if ingest_only else "device (sa_stage_text from page-locked text windows)",
             "leading_blocks_identical_to_bench": same,

@@ -39,6 +39,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 #include <zlib.h>
 
@@ -797,6 +798,14 @@ bool load_ref(const char* ref, bool need_fasta, RefFiles& rf)
 
 // ---- compression: the streaming pipeline ------------------------------------
 bool g_fast_exit = false;   // compress() left the device buffers to the process exit
+
+double mono_s()   // CLOCK_MONOTONIC (the clock of Python's time.monotonic: bench.py splits its wall clock)
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+double g_main_s = 0.0;
 
 int compress(const Options& o)
 {
@@ -1695,6 +1704,7 @@ int decompress(const Options& o)
 
 int main(int argc, char** argv)
 {
+    g_main_s = mono_s();
     setenv("SA_SYNC", "block", 0);   // encoder threads sleep on their streams (sa_create)
     Options o;
     std::vector<const char*> pos;
@@ -1779,6 +1789,8 @@ int main(int argc, char** argv)
         setenv("GPU_MAX_HW_QUEUES", q, 1);
     }
     const int rc = compress(o);
+    if (o.verbose && !o.decompress)   // (process start -> main and exit -> reaped are the caller's to see)
+        fprintf(stderr, "seqarc_amd: monotonic clock: main %.6f, exit %.6f\n", g_main_s, mono_s());
     if (g_fast_exit) {   // (every thread joined, the archive closed): no runtime teardown
         fflush(stdout);
         fflush(stderr);
