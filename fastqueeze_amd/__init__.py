@@ -87,6 +87,8 @@ def load_library(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
+    if path is None and os.environ.get("SA_LIB"):   # (A/B runs: another build of the library)
+        path = os.environ["SA_LIB"]
     if path is None:
         path = _build.LIB
         if _build.needs_build():
