@@ -2230,118 +2230,112 @@ constexpr uint32_t CODER_MAX_WAVES = 4;
 constexpr uint32_t CODER_LA = 6;
 
 // Eight steps of the chain per asm block.  Each step reads the record of the
-// step after it out of its lane first (readlane -> SGPR; used one step later,
-// so the SALU never waits on it); two register pairs alternate, so there are
-// no copies.  (One block per step made the compiler put an s_nop between the
+// step after it out of its lanes first (readlane -> SGPR; used one step later,
+// so the SALU never waits on it): reciprocal, total and frequency, split per
+// segment in the VALU (11 instructions a step; with the record read whole and
+// split in the SALU, 12); two register triples alternate, so there are no
+// copies.  (One block per step made the compiler put an s_nop between the
 // blocks: a ninth of the issue slots.)
-#define SA_RV_STEP8                                                                              \
-        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l0]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l1]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l2]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l3]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l4]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l5]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t"                    \
-        "v_readlane_b32 %[tb], %[ctf], %[l6]\n\t"                   \
-        "s_and_b32 %[t], %[ta], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[ta], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
-        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t"                    \
-        "v_readlane_b32 %[ta], %[ctf], %[l7]\n\t"                   \
-        "s_and_b32 %[t], %[tb], %[tmask]\n\t"                                                   \
-        "s_lshr_b32 %[f], %[tb], 16\n\t"                                                        \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t"                                                     \
-        "s_mul_i32 %[p], %[q], %[t]\n\t"                                                         \
-        "s_cmp_lt_u32 %[r], %[p]\n\t"                                                            \
-        "s_subb_u32 %[q], %[q], 0\n\t"                                                           \
-        "s_mul_i32 %[q], %[q], %[f]\n\t"                                                         \
-        "s_flbit_i32_b32 %[p], %[q]\n\t"                                                         \
-        "s_and_b32 %[p], %[p], 24\n\t"                                                           \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t"                                                        \
+#define SA_RV_STEP8 \
+        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t" \
+        "v_readlane_b32 %[tb], %[vt], %[l0]\n\t" \
+        "v_readlane_b32 %[fb], %[vf], %[l0]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
+        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fa]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t" \
+        "v_readlane_b32 %[ta], %[vt], %[l1]\n\t" \
+        "v_readlane_b32 %[fa], %[vf], %[l1]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
+        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fb]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t" \
+        "v_readlane_b32 %[tb], %[vt], %[l2]\n\t" \
+        "v_readlane_b32 %[fb], %[vf], %[l2]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
+        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fa]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t" \
+        "v_readlane_b32 %[ta], %[vt], %[l3]\n\t" \
+        "v_readlane_b32 %[fa], %[vf], %[l3]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
+        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fb]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t" \
+        "v_readlane_b32 %[tb], %[vt], %[l4]\n\t" \
+        "v_readlane_b32 %[fb], %[vf], %[l4]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
+        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fa]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t" \
+        "v_readlane_b32 %[ta], %[vt], %[l5]\n\t" \
+        "v_readlane_b32 %[fa], %[vf], %[l5]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
+        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fb]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t" \
+        "v_readlane_b32 %[tb], %[vt], %[l6]\n\t" \
+        "v_readlane_b32 %[fb], %[vf], %[l6]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
+        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fa]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
+        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t" \
+        "v_readlane_b32 %[ta], %[vt], %[l7]\n\t" \
+        "v_readlane_b32 %[fa], %[vf], %[l7]\n\t" \
+        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
+        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
+        "s_cmp_lt_u32 %[r], %[p]\n\t" \
+        "s_subb_u32 %[q], %[q], 0\n\t" \
+        "s_mul_i32 %[q], %[q], %[fb]\n\t" \
+        "s_flbit_i32_b32 %[p], %[q]\n\t" \
+        "s_and_b32 %[p], %[p], 24\n\t" \
+        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
         ""
 
 template <int J>
-__device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& mb, uint32_t& tb,
-                                         uint32_t cm, uint32_t ctf, uint32_t tmask)
+__device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& fa, uint32_t& mb,
+                                         uint32_t& tb, uint32_t& fb, uint32_t cm, uint32_t vt, uint32_t vf)
 {
-    uint32_t t, f, q, p;
+    uint32_t q, p;
 #define SA_RV_OPERANDS                                                                                            \
-    : [r] "+s"(r), [ma] "+s"(ma), [ta] "+s"(ta), [mb] "+s"(mb), [tb] "+s"(tb), [t] "=&s"(t), [f] "=&s"(f),       \
+    : [r] "+s"(r), [ma] "+s"(ma), [ta] "+s"(ta), [fa] "+s"(fa), [mb] "+s"(mb), [tb] "+s"(tb), [fb] "+s"(fb),     \
       [q] "=&s"(q), [p] "=&s"(p)                                                                                  \
-    : [tmask] "s"(tmask), [cm] "v"(cm), [ctf] "v"(ctf), [l0] "i"((J + 1) & 63), [l1] "i"((J + 2) & 63),          \
+    : [cm] "v"(cm), [vt] "v"(vt), [vf] "v"(vf), [l0] "i"((J + 1) & 63), [l1] "i"((J + 2) & 63),                  \
       [l2] "i"((J + 3) & 63), [l3] "i"((J + 4) & 63), [l4] "i"((J + 5) & 63), [l5] "i"((J + 6) & 63),             \
       [l6] "i"((J + 7) & 63), [l7] "i"((J + 8) & 63)                                                             \
     : "scc"
@@ -2352,11 +2346,12 @@ __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta
 
 // the 64 steps of one segment (records in lanes 0..63 of cm / ctf)
 template <int... P>
-__device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t ctf, uint32_t tmask,
+__device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t vt, uint32_t vf,
                                            std::integer_sequence<int, P...>)
 {
-    uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(ctf, 0), mb = 0, tb = 0;
-    (rv_step8<8 * P>(r, ma, ta, mb, tb, cm, ctf, tmask), ...);
+    uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(vt, 0),
+             fa = __builtin_amdgcn_readlane(vf, 0), mb = 0, tb = 0, fb = 0;
+    (rv_step8<8 * P>(r, ma, ta, fa, mb, tb, fb, cm, vt, vf), ...);
 }
 
 __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
@@ -2398,8 +2393,8 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                 }
                 r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);   // (scalar for the asm: see k_coder_rv)
                 const uint32_t r_seg = r;
-                const uint32_t cm = recip32z(ctf & tmask);
-                rv_segment(r, cm, ctf, tmask, std::make_integer_sequence<int, 8>{});
+                const uint32_t vt = ctf & tmask, cm = recip32z(vt);
+                rv_segment(r, cm, vt, ctf >> 16, std::make_integer_sequence<int, 8>{});
                 if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
                 g++;
             }
