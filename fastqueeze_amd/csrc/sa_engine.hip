@@ -13,6 +13,7 @@
 #include <cstring>
 #include <condition_variable>
 #include <mutex>
+#include <sys/mman.h>
 #include <string>
 #include <vector>
 

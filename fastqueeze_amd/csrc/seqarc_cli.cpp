@@ -610,7 +610,7 @@ struct ParsedPool {
 // mapped anew and faults in every page on the first read into it.
 //
 // Device parse: the windows are page-locked, carved from arena chunks of
-// kChunk windows each -- one hipHostMalloc per chunk, not per window (the
+// kChunk windows each -- one sa_host_alloc per chunk, not per window (the
 // runtime serialises host allocations against the encoder threads' calls).
 struct TextPool {
     static constexpr size_t kChunk = 16;
@@ -624,23 +624,34 @@ struct TextPool {
         free.clear();
         for (void* c : chunks) sa_host_free(c);
     }
+    void add_locked(uint8_t* c)
+    {
+        chunks.push_back(c);
+        for (size_t k = 0; k < kChunk; k++) {
+            Buf<uint8_t> b;
+            b.pinned = true;
+            b.external = true;
+            b.d = c + k * win;
+            b.cap = win;
+            free.push_back(std::move(b));
+        }
+    }
+    // one more chunk of windows, pinned outside the lock (the prefill thread:
+    // pinning runs beside the contexts' creation and the reader's first reads)
+    bool grow()
+    {
+        if (!pinned || !win) return false;
+        uint8_t* c = static_cast<uint8_t*>(sa_host_alloc(kChunk * win));
+        if (!c) return false;
+        std::lock_guard<std::mutex> g(mu);
+        add_locked(c);
+        return true;
+    }
     Buf<uint8_t> get()
     {
         std::lock_guard<std::mutex> g(mu);
-        if (free.empty() && pinned && win) {
-            uint8_t* c = static_cast<uint8_t*>(sa_host_alloc(kChunk * win));
-            if (c) {
-                chunks.push_back(c);
-                for (size_t k = 0; k < kChunk; k++) {
-                    Buf<uint8_t> b;
-                    b.pinned = true;
-                    b.external = true;
-                    b.d = c + k * win;
-                    b.cap = win;
-                    free.push_back(std::move(b));
-                }
-            }
-        }
+        if (free.empty() && pinned && win)
+            if (uint8_t* c = static_cast<uint8_t*>(sa_host_alloc(kChunk * win))) add_locked(c);
         if (free.empty()) {
             Buf<uint8_t> b;
             b.pinned = pinned;
@@ -847,6 +858,39 @@ int compress(const Options& o)
     const int nparse = !o.host_parse && !o.host_only ? 1   // (device parse: block 0 only, for the ID template)
                        : o.threads > 0 ? o.threads
                                        : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // Device parse (default): the reader's text windows are page-locked, the
+    // encoder threads stage them with sa_stage_text (H2D DMA + parse in HBM)
+    // and recycle them at once; only block 0 is parsed here, for the ID
+    // template.  --host-parse / --host-only: -t parser threads build the SoA.
+    const bool dev_parse = !o.host_parse && !o.host_only;
+    ParsedPool pool;   // (declared before the jobs: outlive them)
+    TextPool texts;
+    texts.pinned = dev_parse && !o.ingest_only;
+    texts.win = (pe ? (size_t)((uint32_t)bs >> 1) : (size_t)bs) + (64u << 10);   // a window + slack for the carry
+    // the windows the reader will hold (two batches ahead of the staging, both
+    // mates), pinned by a thread of their own beside the reader (an input that
+    // is smaller needs fewer)
+    struct Joiner {
+        std::thread t;
+        ~Joiner()
+        {
+            if (t.joinable()) t.join();
+        }
+    } prefill;
+    size_t prefill_chunks = 0;
+    if (texts.pinned) {
+        size_t wins = (size_t)(pe ? 2 : 1) * (2 * (size_t)std::max(1, o.batch) + 4);
+        uint64_t tot = 0;
+        bool known = true;
+        struct stat st;
+        for (const char* f : {o.f1, pe ? o.f2 : nullptr})
+            if (f) {
+                if (stat(f, &st) == 0 && S_ISREG(st.st_mode) && !in1.is_gz && !in2.is_gz) tot = std::max<uint64_t>(tot, (uint64_t)st.st_size);
+                else known = false;
+            }
+        if (known) wins = std::min(wins, (size_t)(pe ? 2 : 1) * (size_t)(tot / (texts.win - (64u << 10)) + 3));
+        prefill_chunks = (wins + TextPool::kChunk - 1) / TextPool::kChunk;
+    }
     // contexts: K per device; every device's contexts share one front scratch
     std::vector<sa_ctx*> ctxs;
     std::vector<int> ctx_dev;   // (the device of each context)
@@ -865,6 +909,13 @@ int compress(const Options& o)
         }
         if (!first) break;
     }
+    // (started once the contexts exist: pinning beside their creation held
+    // it up, 0.25 -> 0.83 s, round 3 g4j)
+    if (prefill_chunks && !ctxs.empty() && ctxs[0])
+        prefill.t = std::thread([&texts, prefill_chunks]() {
+            for (size_t i = 0; i < prefill_chunks; i++)
+                if (!texts.grow()) break;
+        });
     if (o.verbose)
         for (sa_ctx* c : ctxs)
             if (c) sa_set_timing(c, 1);
@@ -902,34 +953,42 @@ int compress(const Options& o)
                     rf.hash.empty() ? "built" : "loaded",
                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() - ti);
     }
-    const int64_t B = std::max(1, o.batch);
-    const size_t max_inflight = (size_t)B * (ctxs.size() + 2);   // blocks read but not yet written
+    int64_t B = std::max(1, o.batch);
+    const int64_t C = (int64_t)ctxs.size();
     // batch k = blocks [bstart(k), bstart(k + 1)).  The first batch of each
     // context ramps up (B (k+1) / (C+1) blocks: the first encode starts after a
     // fraction of a batch is read, and the contexts' first tails are staggered);
     // the contexts allocate for B from the start (sa_set_reserve).  --no-ramp: all B.
-    const int64_t C = (int64_t)ctxs.size();
+    // A plain-file input that fits one round (C batches of B blocks, by its
+    // size) is dealt as C equal batches instead: with the ramp its last blocks
+    // waited for a second round of batch latencies (round 3 g4g: 17.8 GB, five
+    // ramp batches, then three more).
+    bool ramp = o.ramp;
+    if (ramp && !o.host_only && !o.ingest_only && !in1.is_gz && (!pe || !in2.is_gz)) {
+        uint64_t tot = 0;
+        struct stat st;
+        for (const char* f : {o.f1, pe ? o.f2 : nullptr})
+            if (f && stat(f, &st) == 0 && S_ISREG(st.st_mode)) tot += (uint64_t)st.st_size;
+            else tot = ~0ull >> 1;   // (a pipe: size unknown)
+        const int64_t est = (int64_t)((tot + bs - 1) / bs) + 1;   // blocks (cut at record ends: <= bs each)
+        if (tot < (~0ull >> 2) && est <= C * B) {
+            ramp = false;
+            B = (est + C - 1) / C;
+        }
+    }
+    const size_t max_inflight = (size_t)B * (ctxs.size() + 2);   // blocks read but not yet written
     std::vector<int64_t> ramp_start{0};
-    for (int64_t k = 0; o.ramp && k < C; k++) ramp_start.push_back(ramp_start.back() + std::max<int64_t>(1, B * (k + 1) / (C + 1)));
+    for (int64_t k = 0; ramp && k < C; k++) ramp_start.push_back(ramp_start.back() + std::max<int64_t>(1, B * (k + 1) / (C + 1)));
     auto bstart = [&](int64_t k) -> int64_t {
         const int64_t r = (int64_t)ramp_start.size() - 1;
         return k <= r ? ramp_start[(size_t)k] : ramp_start.back() + (k - r) * B;
     };
-    if (o.ramp)
+    if (ramp)
         for (sa_ctx* c : ctxs)
             if (c) sa_set_reserve(c, (uint32_t)B);
 
     std::mutex mu;
     std::condition_variable cv;
-    ParsedPool pool;   // (declared before the jobs: outlive them)
-    TextPool texts;
-    // Device parse (default): the reader's text windows are page-locked, the
-    // encoder threads stage them with sa_stage_text (H2D DMA + parse in HBM)
-    // and recycle them at once; only block 0 is parsed here, for the ID
-    // template.  --host-parse / --host-only: -t parser threads build the SoA.
-    const bool dev_parse = !o.host_parse && !o.host_only;
-    texts.pinned = dev_parse && !o.ingest_only;
-    texts.win = (pe ? (size_t)((uint32_t)bs >> 1) : (size_t)bs) + (64u << 10);   // a window + slack for the carry
     std::atomic<double> stage_busy{0};
     std::map<int64_t, std::unique_ptr<Job>> jobs;
     // -v: when the stages first / last did something (seconds from the start)
@@ -1102,7 +1161,7 @@ int compress(const Options& o)
                 fprintf(stderr, "seqarc_amd: cannot create the staging contexts\n");
                 return 1;
             }
-            if (o.ramp) sa_set_reserve(s, (uint32_t)B);
+            if (ramp) sa_set_reserve(s, (uint32_t)B);
             stagers.push_back(s);
             sinputs.push_back(a);
             sinputs.push_back(b);

@@ -110,7 +110,8 @@ typedef struct sa_text_info {   /* per block, written by sa_stage_text */
  * entries) gets each block's counts.  Then sa_run / sa_fetch.  -1 and
  * sa_last_error where sa_parse_* fail.  The texts may be reused on return. */
 int sa_stage_text(sa_ctx *ctx, const sa_text_block *in, int n, sa_text_info *info);
-/* page-locked host memory (hipHostMalloc) for the reader's text windows */
+/* page-locked host memory for the reader's text windows (2 MiB-aligned, huge pages
+ * asked for, registered portable with the runtime); free with sa_host_free */
 void *sa_host_alloc(uint64_t bytes);
 void sa_host_free(void *p);
 int sa_run(sa_ctx *ctx, const sa_cfg *cfg);                /* encode the staged batch */
