@@ -1298,10 +1298,12 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
 {
     constexpr uint32_t ND = 1u << DB, NW = SORT_THREADS / 64, C = ND >= SORT_THREADS ? ND / SORT_THREADS : 1;
     // per wave and digit: count, then the wave's slot base in the tile (<= 4096:
-    // 16 bits, so the 9-bit pass fits twice beside pass R's 82 KB of LDS)
+    // 16 bits); one tile buffer, keys then values: 22 KB for the 9-bit pass, so
+    // three workgroups fit beside pass R's 82 KB of LDS (two with a key and a
+    // value buffer)
     __shared__ uint16_t wc[NW][ND];
     __shared__ uint32_t gstart[ND], dsum[NW];
-    __shared__ uint32_t sk[SORT_TILE], svl[SORT_TILE];
+    __shared__ uint32_t sb[SORT_TILE];
     const uint32_t t = blockIdx.x;
     const SortSeg& sg = sv.segs[sv.tile_seg[t]];
     const uint32_t lt = t - sg.tile0;
@@ -1369,23 +1371,35 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     }
     __syncthreads();
     // stage the tile in digit order in LDS, then write it out: consecutive
-    // threads write consecutive slots of one digit's run (coalesced)
+    // threads write consecutive slots of one digit's run (coalesced); the keys
+    // first (each thread keeps the output slots of its tile slots), then the
+    // values through the same buffer
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
         const uint32_t d = (k[r] >> shift) & (ND - 1);
-        const uint32_t at = wc[w][d] + rk[r];
-        sk[at] = k[r];
-        svl[at] = v[r];
+        rk[r] += wc[w][d];   // (the key's slot in the tile)
+        sb[rk[r]] = k[r];
     }
     __syncthreads();
+    // (byte offsets in the segment, 32-bit: a segment is one block's symbols,
+    // < 2^28 keys, so the stores take a scalar base and a 32-bit lane offset)
+    char* const ko = reinterpret_cast<char*>(kout + sg.base);
+    char* const vo = reinterpret_cast<char*>(vout + sg.base);
+    uint32_t ro[SORT_ITEMS];
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
         const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
-        const uint32_t kk = sk[i];
-        const size_t dst = sg.base + gstart[(kk >> shift) & (ND - 1)] + i;
-        kout[dst] = kk;
-        vout[dst] = svl[i];
+        const uint32_t kk = sb[i];
+        ro[r] = (gstart[(kk >> shift) & (ND - 1)] + i) << 2;
+        *reinterpret_cast<uint32_t*>(ko + ro[r]) = kk;
     }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++)
+        *reinterpret_cast<uint32_t*>(vo + ro[r]) = sb[threadIdx.x + (uint32_t)r * SORT_THREADS];
 }
 
 // ---------------------------------------------------------------------------
