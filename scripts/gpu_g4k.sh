@@ -14,12 +14,3 @@ cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u $R/bench.py --steps 8 --e2e-batches 0 --cpu-seconds 0 --no-verify > $O/prof_bench.json 2> $O/prof_bench.err || exit 5
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 -u $R/bench.py --steps 2 --warmup 1 --e2e-batches 0 --cpu-seconds 0 --no-verify > $O/pmc_fetch.json 2> $O/pmc_fetch.err || exit 6
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 -u $R/bench.py --steps 2 --warmup 1 --e2e-batches 0 --cpu-seconds 0 --no-verify > $O/pmc_write.json 2> $O/pmc_write.err || exit 7
-# then (not part of the final set): pass R with the readlanes interleaved into its SALU chain
-# (libseqarc_amd_il.so through SA_LIB): its GPU parity, and an A/B against the default, alternating
-IL=$R/fastqueeze_amd/lib/libseqarc_amd_il.so
-SA_LIB=$IL timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/il_tests.log 2>&1 || exit 8
-B="python -u bench.py --steps 16 --e2e-batches 0 --cpu-seconds 0 --no-verify"
-for i in 1 2; do
-    SA_LIB=$IL timeout -k 10 300 $B > $O/il_$i.json 2> $O/il_$i.err || exit 9
-    timeout -k 10 300 $B > $O/rf_$i.json 2> $O/rf_$i.err || exit 10
-done
