@@ -104,6 +104,11 @@ def parse_args(argv=None):
                          "~200 GB the previous run released in the background, and allocations wait for it")
     ap.add_argument("--e2e-args", default="", help="extra seqarc_amd arguments for the end-to-end runs (A/B)")
     ap.add_argument("--dry-run", action="store_true", help="no GPU: CPU restatement, tiny batches (plumbing test)")
+    ap.add_argument("--write-inputs", default=None, metavar="DIR",
+                    help="generate this rank's batches as FASTQ files in DIR and exit (no GPU call): run it before a "
+                         "profiled bench, whose process must not start generator processes under the profiler")
+    ap.add_argument("--inputs", default=None, metavar="DIR",
+                    help="read the batches from FASTQ files written by --write-inputs (no generator processes)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
                          "(scripts/pmc_traffic.py), committed under profiles/")
@@ -160,21 +165,44 @@ def launch_ranks(argv: list[str], n: int) -> int:
     return rc
 
 
-def make_batch(gid: int, args, workers: int, files=None):
-    """Global batch `gid`: its FASTQ (seed 1000 + gid), cut and parsed as the
-    reference's reader does.  Returns the parsed blocks; `files` (paths) get the
-    FASTQ text appended (the end-to-end run's input)."""
+INPUT_KEYS = ("pairs", "se", "ont", "read_len", "x_span")
+
+
+def input_paths(d: str, gid: int, se: bool) -> list[str]:
+    return [os.path.join(d, f"b{gid}_r1.fq")] + ([] if se else [os.path.join(d, f"b{gid}_r2.fq")])
+
+
+def batch_text(gid: int, args, workers: int):
+    """Global batch `gid`'s FASTQ text (seed 1000 + gid): (r1, r2 or None).
+    With --inputs, the files --write-inputs made (their shape must match)."""
+    if args.inputs:
+        with open(os.path.join(args.inputs, "meta.json")) as f:
+            meta = json.load(f)
+        want = {k: getattr(args, k) for k in INPUT_KEYS}
+        if {k: meta.get(k) for k in INPUT_KEYS} != want:
+            raise SystemExit(f"--inputs {args.inputs}: written for {meta}, this run asks for {want}")
+        texts = []
+        for p in input_paths(args.inputs, gid, args.se):
+            with open(p, "rb") as f:
+                texts.append(f.read())
+        return texts[0], (texts[1] if len(texts) > 1 else None)
     import synth
-    import fastqueeze_amd as fq
     paired = not args.se
     if args.ont:   # five read lengths, a fifth of the reads each, chunks small enough for the generator's arrays
         parts = [synth.generate(args.pairs // 5, read_len=L, seed=1000 + 10 * gid + k, workers=workers,
                                 chunk=1000, x_span=args.x_span)[0]
                  for k, L in enumerate((10_000, 20_000, 30_000, 40_000, 50_000))]
-        t1, t2 = b"".join(parts), None
-    else:
-        t1, t2 = synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers,
-                                x_span=args.x_span)
+        return b"".join(parts), None
+    return synth.generate(args.pairs, read_len=args.read_len, paired=paired, seed=1000 + gid, workers=workers,
+                          x_span=args.x_span)
+
+
+def make_batch(gid: int, args, workers: int, files=None):
+    """Global batch `gid`, cut and parsed as the reference's reader does.
+    Returns the parsed blocks; `files` (paths) get the FASTQ text appended (the
+    end-to-end run's input)."""
+    import fastqueeze_amd as fq
+    t1, t2 = batch_text(gid, args, workers)
     if files:
         for path, t in zip(files, (t1, t2)):
             if t is not None:
@@ -449,6 +477,16 @@ def main():
     # ---- this rank's batches (global ids dealt round robin) ----
     gids = shard_indices(world * args.batches, rank, world)
     t0 = time.time()
+    if args.write_inputs:   # (no GPU call in this mode)
+        os.makedirs(args.write_inputs, exist_ok=True)
+        for g in gids:
+            for p, t in zip(input_paths(args.write_inputs, g, args.se), batch_text(g, args, workers)):
+                with open(p, "wb") as f:
+                    f.write(t)
+            log(f"[rank {rank}] batch {g} written to {args.write_inputs} ({time.time() - t0:.1f}s)")
+        with open(os.path.join(args.write_inputs, "meta.json"), "w") as f:
+            json.dump({k: getattr(args, k) for k in INPUT_KEYS}, f)
+        return
     batches = []
     e2e_files = None
     if args.e2e_batches > 0 and rank == 0:

@@ -50,7 +50,7 @@ class _SaArcBlock(C.Structure):
 class _SaArcInfo(C.Structure):
     _fields_ = [("file1", C.c_char_p), ("file2", C.c_char_p), ("paired", C.c_int32), ("gz1", C.c_int32),
                 ("bare_plus", C.c_int32), ("md5", C.c_int32), ("lossy", C.c_int32), ("id_template", C.c_void_p),
-                ("ref_md5", C.c_void_p), ("insert_size", C.c_uint32)]
+                ("ref_md5", C.c_void_p), ("insert_size", C.c_uint32), ("maxmis", C.c_int32)]
 
 
 class _SaDecoded(C.Structure):
@@ -469,7 +469,7 @@ def bare_plus(text) -> int:
 
 def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str | None = None,
                 template: np.ndarray | None = None, cfg: Config | None = None, gz1: bool = False,
-                plus_bare: int = 1, ref_md5: bytes | None = None, insert_size: int = 0) -> bytes:
+                plus_bare: int = 1, ref_md5: bytes | None = None, insert_size: int = 0, maxmis: int = 7) -> bytes:
     """The .arc file around encoded blocks (header, blocks in input order, trailer):
     SeqArcFile::writeFileInfo@0x4171b0 / writeParam@0x416450 / writeBlockLenArry (arc_file.cpp)."""
     lib = load_library()
@@ -482,7 +482,7 @@ def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str
     rm = None if ref_md5 is None else np.frombuffer(ref_md5, np.uint8)
     info = _SaArcInfo(file1.encode(), (file2 or "").encode(), 1 if file2 else 0, 1 if gz1 else 0, int(plus_bare),
                       1 if cfg.md5 else 0, 1 if cfg.lossy > 0 else 0, _ptr(tmpl), None if rm is None else _ptr(rm),
-                      int(insert_size))
+                      int(insert_size), int(maxmis))
     cap = 4096 + 40 * len(encaps)
     tr = np.empty(cap, np.uint8)
     n = lib.sa_arc_trailer(C.byref(info), recs, len(encaps), _ptr(tr), cap)
@@ -571,7 +571,10 @@ class HashIndex:
             if not self._h:
                 enc._err("sa_hash_load")
             return
-        self._h = self._lib.sa_hash_build(enc._ctx, fasta, len(fasta), k, step, maxcount)
+        if isinstance(fasta, np.ndarray):   # (a genome-scale FASTA as a uint8 array: no bytes copy)
+            self._h = self._lib.sa_hash_build(enc._ctx, _ptr(fasta), fasta.size, k, step, maxcount)
+        else:
+            self._h = self._lib.sa_hash_build(enc._ctx, fasta, len(fasta), k, step, maxcount)
         if not self._h:
             enc._err("sa_hash_build")
 
@@ -589,11 +592,15 @@ class HashIndex:
 
     def file_bytes(self) -> bytes:
         """The `<ref.fa>.hash` file (HashRefIndex32::writeIndexFile@0x41ed00)."""
+        return self.file_array().tobytes()
+
+    def file_array(self) -> np.ndarray:
+        """file_bytes() as a uint8 array."""
         n = int(self._lib.sa_hash_file_bytes(self._h))
         out = np.empty(n, dtype=np.uint8)
         if self._lib.sa_hash_serialize(self._enc._ctx, self._h, _ptr(out), n) != 0:
             self._enc._err("sa_hash_serialize")
-        return out.tobytes()
+        return out
 
     def align(self, reads: list[bytes], maxmis: int = MAXMIS, good: int = GOOD, ai_nmis: int = 0):
         """The reads in order, one align_info state carried across them

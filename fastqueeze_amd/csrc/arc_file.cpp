@@ -149,6 +149,8 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     field_bool(o, 16, in->lossy);               // param+0x1870
     field_bool(o, 17, in->md5);                 // param+0x1880
     field_bool(o, 18, 0);                       // param+0xd: file list (-m)
+    if (in->ref_md5 && in->maxmis != 7)         // (ours: a non-default maxmis, see sa_arc_info)
+        field_uint(o, 19, 1, (uint32_t)in->maxmis);
     if (!o.ok) return -1;
     put_size((uint64_t)(o.p - pbeg), 2, ph + 1);
     if (in->ref_md5) {   // writeMd5@0x416b10: setID(8), 1-byte size 0x10, the 16 bytes

@@ -901,6 +901,20 @@ void align_chain_fail(sa_align_chain* ch)
     ch->cv.notify_all();
 }
 
+// a batch without blocks passes the chain unchanged (its turn still comes:
+// later batches wait for it)
+static int align_chain_pass_empty(sa_align_chain* ch, uint64_t batch)
+{
+    std::unique_lock<std::mutex> lk(ch->mu);
+    const uint64_t me = batch == UINT64_MAX ? ch->next : batch;
+    ch->cv.wait(lk, [&] { return ch->failed || ch->next == me; });
+    if (ch->failed) return -1;
+    ch->next = me + 1;
+    lk.unlock();
+    ch->cv.notify_all();
+    return 0;
+}
+
 int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq, std::vector<uint32_t>& atot,
                 AlignView& av)
 {
@@ -911,8 +925,8 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
         c->err = "sa_run_input_aligned: no index / chain, or an index of another device";
         return -1;
     }
-    if (a.maxmis < 0 || a.maxmis > 63 || ix->total < 4) {
-        c->err = "sa_run_input_aligned: maxmis must be 0..63 and the genome at least 4 bases";
+    if (a.maxmis < 0 || a.maxmis > 8 || ix->total < 4) {   // (the Mis model exists for maxmis 1..8)
+        c->err = "sa_run_input_aligned: maxmis must be 0..8 and the genome at least 4 bases";
         return -1;
     }
     if (a.paired)
@@ -1063,6 +1077,8 @@ sa_align_chain* sa_align_chain_create(int32_t nmis_mate1, int32_t nmis_mate2)
 
 void sa_align_chain_destroy(sa_align_chain* ch) { delete ch; }
 
+void sa_align_chain_fail(sa_align_chain* ch) { align_chain_fail(ch); }
+
 int sa_run_input_aligned(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, const sa_align_cfg* acfg,
                          sa_align_chain* chain, uint64_t batch)
 {
@@ -1071,14 +1087,26 @@ int sa_run_input_aligned(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, const 
         c->err = "sa_run_input_aligned: no alignment config or chain";
         return -1;
     }
+    if (acfg->maxmis < 0 || acfg->maxmis > 8) {   // (before anything waits on the chain)
+        c->err = "sa_run_input_aligned: maxmis must be 0..8";
+        align_chain_fail(chain);
+        return -1;
+    }
     const AlignReq rq{acfg->index, *acfg, chain, batch};
     c->al_input = nullptr;   // (a new batch: pass the chain)
     int rc = run_input(c, I, cfg, true, &rq);
     if (rc == 2) {   // exact payload outgrown: drain, re-run with the bound (same alignment plan)
-        for (hipStream_t s : {c->st, c->st2, c->st3, c->st4}) SA_CHECK(c, hipStreamSynchronize(s));
+        for (hipStream_t s : {c->st, c->st2, c->st3, c->st4}) (void)hipStreamSynchronize(s);
         const AlignReq rq2{acfg->index, *acfg, chain, c->al_batch};
         rc = run_input(c, I, cfg, false, &rq2);
     }
+    if (rc == 0 && I && I->nblocks == 0 && align_chain_pass_empty(chain, batch)) {
+        c->err = "sa_run_input_aligned: an earlier batch of the chain failed";
+        rc = -1;
+    }
+    // any failure ends the chain: the contexts waiting on later batches return
+    // an error instead of waiting for this batch forever
+    if (rc) align_chain_fail(chain);
     return rc ? -1 : 0;
 }
 

@@ -1382,7 +1382,8 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     }
     __syncthreads();
     // (byte offsets in the segment, 32-bit: a segment is one block's symbols,
-    // < 2^28 keys, so the stores take a scalar base and a 32-bit lane offset)
+    // < 2^30 keys (plan_batch refuses larger blocks), so the stores take a
+    // scalar base and a 32-bit lane offset)
     char* const ko = reinterpret_cast<char*>(kout + sg.base);
     char* const vo = reinterpret_cast<char*>(vout + sg.base);
     uint32_t ro[SORT_ITEMS];

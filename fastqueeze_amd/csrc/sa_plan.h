@@ -81,7 +81,8 @@ inline bool plan_batch(std::vector<DevBlock>& blocks, const std::vector<uint32_t
             }
             d.align_count = at[A_REV];
         }
-        if (a >= (1ull << 31) || t[C_SEQ] >= (1u << 30)) return false;
+        // (< 2^30 keys per space: the sort scatter's 32-bit byte offsets in a segment)
+        if (a >= (1ull << 30) || t[C_SEQ] >= (1u << 30)) return false;
         d.n_aux = (uint32_t)a;
         d.n_seq = t[C_SEQ];
         for (int s = 0; s < NSTREAM; s++) d.vcount[s] = 0;

@@ -1005,10 +1005,15 @@ int compress(const Options& o)
     int plus_bare = 1;
     uint64_t total_in = 0;
     auto fail = [&](const std::string& m) {
-        std::lock_guard<std::mutex> g(mu);
-        if (!failed) err = m;
-        failed = true;
-        cv.notify_all();
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!failed) err = m;
+            failed = true;
+            cv.notify_all();
+        }
+        // contexts waiting on the alignment chain for a batch that will never
+        // reach it return instead of waiting forever
+        if (chain) sa_align_chain_fail(chain);
     };
 
     // reader: cuts blocks as the input arrives
@@ -1478,7 +1483,7 @@ int compress(const Options& o)
         return 1;
     }
     sa_arc_info ai{o.f1, pe ? o.f2 : nullptr, pe ? 1 : 0, in1.is_gz ? 1 : 0, plus_bare, cfg.md5,
-                   cfg.lossy > 0.0 ? 1 : 0, tmpl, o.ref ? rf.md5 : nullptr, (uint32_t)o.insert};
+                   cfg.lossy > 0.0 ? 1 : 0, tmpl, o.ref ? rf.md5 : nullptr, (uint32_t)o.insert, o.maxmis};
     std::vector<uint8_t> tr(4096 + 40 * info.size());
     const int64_t tl = sa_arc_trailer(&ai, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
     if (tl < 0) {
@@ -1606,6 +1611,7 @@ int decompress(const Options& o)
     uint8_t tmpl[512] = {0};
     int bare = 1, paired = 0, lossy = 0, md5 = 1, gz1 = 0, noref = 1;
     uint32_t nblocks = 0, insert = 0;
+    int maxmis = 7;   // SeqArc's default (param+0x1b60); field 19 when the archive was made with another
     std::string name1, name2;
     while (t < pend) {
         const uint64_t id = vint(t, pend, w);
@@ -1625,6 +1631,7 @@ int decompress(const Options& o)
         else if (id == 15 && ln == 512) memcpy(tmpl, t, 512);
         else if (id == 16) lossy = t[0];
         else if (id == 17) md5 = t[0];
+        else if (id == 19 && ln >= 1) maxmis = t[0];   // (ours: a non-default --maxmis)
         t += ln;
     }
     // writeMd5@0x416b10: the reference FASTA's MD5 (ID 8), archives made with one
@@ -1668,7 +1675,11 @@ int decompress(const Options& o)
             return 1;
         }
     }
-    const sa_ref gref{gwords.data(), gbases, paired, o.maxmis, insert};
+    if (maxmis < 0 || maxmis > 8) {
+        fprintf(stderr, "seqarc_amd: maxmis %d in the archive trailer (0..8 expected)\n", maxmis);
+        return 1;
+    }
+    const sa_ref gref{gwords.data(), gbases, paired, maxmis, insert};
     if (vint(t, end, w) != 7 || !w) return 1;
     t += w;
     const uint64_t bt = be(t, 4) & 0x0fffffff;
@@ -1822,7 +1833,12 @@ int main(int argc, char** argv)
             return 2;
         }
         else if (!strcmp(a, "-I")) { if (!ival(o.insert, 0)) return usage(); o.insert = std::min(o.insert, 65535); }
-        else if (!strcmp(a, "--maxmis")) { if (!ival(o.maxmis, 0)) return usage(); o.maxmis = std::min(o.maxmis, 63); }
+        else if (!strcmp(a, "--maxmis")) {   // the Mis model (compressAlignInfo_Mis@0x425ff0) exists for 1..8
+            if (!ival(o.maxmis, 0) || o.maxmis > 8) {
+                fprintf(stderr, "seqarc_amd: --maxmis takes 0..8\n");
+                return usage();
+            }
+        }
         else if (a[0] != '-') pos.push_back(a);
         else return usage();
     }

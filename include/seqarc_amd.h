@@ -212,6 +212,10 @@ typedef struct {
      * the MD5 of the FASTA file, getMd5@0x416810) */
     const uint8_t *ref_md5;        /* NULL: no reference                                 */
     uint32_t insert_size;          /* param+0x28 (-I)                                    */
+    int32_t maxmis;                /* reference path: param+0x1b60 (0..8).  SeqArc reads it
+                                    * from ./seqarc.config and stores none; a value other
+                                    * than its default 7 is written as params field 19 so
+                                    * that -d rebuilds the same Mis model                   */
 } sa_arc_info;
 
 /* ---- block decoder (SeqArc -d; host) ------------------------------------ */
@@ -297,7 +301,7 @@ int sa_hash_align(sa_ctx *ctx, const sa_hash_index *ix, const char *seq, const u
 typedef struct {
     const sa_hash_index *index;   /* on the encoding context's device              */
     int32_t paired;               /* PE, reads interleaved r1, r2 (-2 given)       */
-    int32_t maxmis;               /* param+0x1b60 (7), 0..63                       */
+    int32_t maxmis;               /* param+0x1b60 (7), 0..8 (the Mis model's range) */
     int32_t good;                 /* param+0x1b74 (1)                              */
     uint32_t insert_size;         /* -I (param+0x28); 0: estimated per block       */
 } sa_align_cfg;
@@ -306,6 +310,10 @@ typedef struct sa_align_chain sa_align_chain;
  * 0 for a fresh encode thread) */
 sa_align_chain *sa_align_chain_create(int32_t nmis_mate1, int32_t nmis_mate2);
 void sa_align_chain_destroy(sa_align_chain *ch);
+/* marks the chain failed: every call waiting on it (and every later one)
+ * returns an error.  For a caller whose batch cannot reach the chain (e.g. its
+ * staging failed), so that the batches after it do not wait forever. */
+void sa_align_chain_fail(sa_align_chain *ch);
 /* encodes the resident batch in the doAlignEncode layout; batch = its place in
  * the chain (0, 1, 2, ...: a call waits until the previous batch has passed
  * its alignment), or UINT64_MAX for the chain's next.  Then sa_fetch. */

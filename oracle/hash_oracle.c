@@ -15,10 +15,14 @@
  * rejected: the reference counts them in one pass but not the other and
  * writes past its position table (buildRefIndex@0x410190).
  */
+#define _DEFAULT_SOURCE   /* madvise, posix_memalign */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include "hash_oracle.h"
 
@@ -70,11 +74,104 @@ static uint64_t ho_mask(uint32_t k) { return k >= 32 ? ~0ull : (1ull << (2 * k))
 /* ---- index ------------------------------------------------------------- */
 void ho_index_free(ho_index* ix)
 {
-    free(ix->seq);
+    free(ix->seq);   /* (ho_alloc: posix_memalign, freed with free) */
     free(ix->num);
     free(ix->ind);
     free(ix->pos);
     memset(ix, 0, sizeof *ix);
+}
+
+/* Large tables: 2 MiB-aligned and backed by transparent huge pages where the
+ * kernel allows (a genome-scale index does hundreds of millions of random
+ * accesses into GB-sized tables; 4 KiB pages make each a TLB miss). */
+static void* ho_alloc(uint64_t bytes)
+{
+    const uint64_t al = 2ull << 20, sz = (bytes + al - 1) / al * al;
+    void* p = NULL;
+    if (posix_memalign(&p, al, sz ? sz : al)) return NULL;
+    if (sz >= al) (void)madvise(p, sz, MADV_HUGEPAGE);
+    memset(p, 0, sz ? sz : al);
+    return p;
+}
+static void ho_free(void* p, uint64_t bytes) { (void)bytes; free(p); }
+
+#define HO_SEEDBUF (1u << 24)
+#define HO_AHEAD 16
+/* The random-access phases run on several threads, each owning a range of
+ * K-mers and walking the collected seeds in order: every K-mer's counter and
+ * list see exactly the sequential order of updates. */
+typedef struct {
+    uint32_t *num, *pos, *cur;
+    const uint32_t *sk, *sp;
+    uint32_t ns, maxcount;
+    uint64_t lo, hi;   /* K-mers [lo, hi) */
+} ho_job;
+
+/* setSeednum: count the collected seeds in order (saturating at maxcount) */
+static void* ho_count_job(void* arg)
+{
+    const ho_job* j = (const ho_job*)arg;
+    for (uint32_t i = 0; i < j->ns; i++) {
+        const uint32_t k = j->sk[i];
+        if (k < j->lo || k >= j->hi) continue;
+        if (j->num[k] < j->maxcount) j->num[k]++;
+    }
+    return NULL;
+}
+/* setSeedpos: the collected seeds' positions into their K-mers' lists, in order */
+static void* ho_place_job(void* arg)
+{
+    const ho_job* j = (const ho_job*)arg;
+    for (uint32_t i = 0; i < j->ns; i++) {
+        const uint32_t k = j->sk[i];
+        if (k < j->lo || k >= j->hi) continue;
+        const uint32_t c = j->cur[k];
+        if (c != UINT32_MAX) {
+            j->pos[c] = j->sp[i];
+            j->cur[k] = c + 1;
+        }
+    }
+    return NULL;
+}
+
+static int ho_threads(void)
+{
+    long n = sysconf(_SC_NPROCESSORS_ONLN);
+    const char* e = getenv("OMP_NUM_THREADS");
+    if (e && atoi(e) > 0) n = atoi(e);
+    return n < 1 ? 1 : n > 16 ? 16 : (int)n;
+}
+
+static uint32_t ho_run_jobs(void* (*fn)(void*), ho_job proto, uint64_t nkmers)
+{
+    enum { MAXT = 16 };
+    const int T = proto.ns < 65536 ? 1 : ho_threads();
+    ho_job jobs[MAXT];
+    pthread_t th[MAXT];
+    int started[MAXT] = {0};
+    for (int t = 0; t < T; t++) {
+        jobs[t] = proto;
+        jobs[t].lo = nkmers * (uint64_t)t / (uint64_t)T;
+        jobs[t].hi = nkmers * (uint64_t)(t + 1) / (uint64_t)T;
+        if (t > 0) started[t] = pthread_create(&th[t], NULL, fn, &jobs[t]) == 0;
+    }
+    fn(&jobs[0]);
+    for (int t = 1; t < T; t++) {
+        if (started[t]) pthread_join(th[t], NULL);
+        else fn(&jobs[t]);
+    }
+    return 0;
+}
+static uint32_t ho_count_seeds(uint32_t* num, const uint32_t* sk, uint32_t ns, uint32_t maxcount, uint64_t nk)
+{
+    const ho_job p = {num, NULL, NULL, sk, NULL, ns, maxcount, 0, 0};
+    return ho_run_jobs(ho_count_job, p, nk);
+}
+static uint32_t ho_place_seeds(uint32_t* pos, uint32_t* cur, const uint32_t* sk, const uint32_t* sp, uint32_t ns,
+                               uint64_t nk)
+{
+    const ho_job p = {NULL, pos, cur, sk, sp, ns, 0, 0, 0};
+    return ho_run_jobs(ho_place_job, p, nk);
 }
 
 /* getdelim('\n') over a buffer: the next line [*at, end) including its '\n' */
@@ -113,10 +210,22 @@ int ho_index_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32
     ix->maxcount = maxcount;
     ix->nkmers = ho_mask(K) + 1;
     const uint64_t mask = ho_mask(K);
-    ix->seq = (uint32_t*)calloc(n / 16 + 1, 4);   /* initMemory@0x41e7e0: file size / 16 + 1 */
-    ix->num = (uint32_t*)calloc(ix->nkmers, 4);
+    uint8_t code[256], isn[256];   /* ho_code & 3 and the (c & 0xdf) == 'N' test per character */
+    for (int c = 0; c < 256; c++) {
+        code[c] = ho_code((char)c) & 3;
+        isn[c] = (c & 0xdf) == 'N';
+    }
+    ix->seq = (uint32_t*)ho_alloc((n / 16 + 1) * 4);   /* initMemory@0x41e7e0: file size / 16 + 1 */
+    ix->num = (uint32_t*)ho_alloc(ix->nkmers * 4);
     if (!ix->seq || !ix->num) return -1;
-    /* pass 1: pack, count sampled seeds */
+    /* pass 1: pack, count sampled seeds.  The seeds of a stretch of input are
+     * collected first and counted in order after it (the same increments in
+     * the same order), prefetching the counters ahead: genome-scale tables are
+     * GBs and each seed is a random access. */
+    uint32_t* sk = (uint32_t*)malloc(HO_SEEDBUF * 4);
+    uint32_t* sp = (uint32_t*)malloc(HO_SEEDBUF * 4);
+    if (!sk || !sp) { free(sk); free(sp); return -1; }
+    uint32_t ns = 0;
     uint64_t at = 0, ll, pos = 0, lastword = 0;
     const char* line;
     uint32_t headers = 0, run = 0, kmer = 0;
@@ -127,29 +236,32 @@ int ho_index_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32
         }
         const uint64_t nb = line_bases(line, ll);
         if (!headers) {
-            if (nb) return -1;   /* (see the header comment) */
+            if (nb) { free(sk); free(sp); return -1; }   /* (see the header comment) */
             continue;
         }
         for (uint64_t j = 0; j < nb; j++) {
-            const uint8_t c = ho_code(line[j]) & 3;
+            const uint8_t ch = (uint8_t)line[j], c = code[ch];
             lastword = pos / 16;
             ix->seq[lastword] = (ix->seq[lastword] << 2) | c;
             kmer = (uint32_t)(((uint64_t)kmer << 2 | c) & mask);
             pos++;
-            if ((line[j] & 0xdf) == 'N') run = 0;
+            if (isn[ch]) run = 0;
             else if (run + 1 == K) {
-                if (pos % step == 0 && ix->num[kmer] < maxcount) ix->num[kmer]++;
+                if (pos % step == 0) sk[ns++] = kmer;
             } else run++;
         }
+        if (ns > HO_SEEDBUF - 65536) ns = ho_count_seeds(ix->num, sk, ns, maxcount, ix->nkmers);
     }
-    if (!headers) return -1;
+    ns = ho_count_seeds(ix->num, sk, ns, maxcount, ix->nkmers);
+    if (!headers) { free(sk); free(sp); return -1; }
     if (pos % 16) ix->seq[lastword] <<= 2 * (16 - pos % 16);
     ix->total = (uint32_t)pos;
     ix->nwords = (uint32_t)lastword + 1;
     /* setSeedind: drop seeds at the cap, exclusive scan */
-    ix->ind = (uint32_t*)calloc(ix->nkmers, 4);
-    if (!ix->ind) return -1;
+    ix->ind = (uint32_t*)ho_alloc(ix->nkmers * 4);
+    if (!ix->ind) { free(sk); free(sp); return -1; }
     uint32_t npos = 0;
+    ix->ind[0] = 0;
     for (uint64_t c = 0; c < mask; c++) {
         if (ix->num[c] >= maxcount) ix->num[c] = 0;
         ix->ind[c + 1] = ix->ind[c] + ix->num[c];
@@ -158,9 +270,12 @@ int ho_index_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32
     if (ix->num[mask] >= maxcount) ix->num[mask] = 0;
     npos += ix->num[mask];
     ix->npos = npos;
-    ix->pos = (uint32_t*)calloc(npos ? npos : 1, 4);
-    uint32_t* cur = (uint32_t*)calloc(ix->nkmers, 4);
-    if (!ix->pos || !cur) return -1;
+    ix->pos = (uint32_t*)ho_alloc((uint64_t)(npos ? npos : 1) * 4);
+    /* the write cursor of each K-mer's list (the reference's ind + running
+     * count); dropped K-mers get none */
+    uint32_t* cur = (uint32_t*)ho_alloc(ix->nkmers * 4);
+    if (!ix->pos || !cur) { free(sk); free(sp); return -1; }
+    for (uint64_t c = 0; c <= mask; c++) cur[c] = ix->num[c] ? ix->ind[c] : UINT32_MAX;
     /* pass 2: positions (1-based seed starts), in order */
     at = 0;
     pos = 0;
@@ -170,16 +285,23 @@ int ho_index_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32
         if (line[0] == '>') continue;
         const uint64_t nb = line_bases(line, ll);
         for (uint64_t j = 0; j < nb; j++) {
-            const uint8_t c = ho_code(line[j]) & 3;
-            kmer = (uint32_t)(((uint64_t)kmer << 2 | c) & mask);
+            const uint8_t ch = (uint8_t)line[j];
+            kmer = (uint32_t)(((uint64_t)kmer << 2 | code[ch]) & mask);
             pos++;
-            if ((line[j] & 0xdf) == 'N') run = 0;
+            if (isn[ch]) run = 0;
             else if (run + 1 == K) {
-                if (pos % step == 0 && ix->num[kmer]) ix->pos[ix->ind[kmer] + cur[kmer]++] = (uint32_t)(pos - (K - 1));
+                if (pos % step == 0) {
+                    sk[ns] = kmer;
+                    sp[ns++] = (uint32_t)(pos - (K - 1));
+                }
             } else run++;
         }
+        if (ns > HO_SEEDBUF - 65536) ns = ho_place_seeds(ix->pos, cur, sk, sp, ns, ix->nkmers);
     }
-    free(cur);
+    ho_place_seeds(ix->pos, cur, sk, sp, ns, ix->nkmers);
+    ho_free(cur, ix->nkmers * 4);
+    free(sk);
+    free(sp);
     return 0;
 }
 

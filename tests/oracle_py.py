@@ -175,14 +175,24 @@ HASH_K, HASH_STEP, HASH_MAXCOUNT, HASH_MAXMIS, HASH_GOOD = 14, 2, 1 << 16, 7, 1 
 def hash_index(fasta: bytes, k: int = HASH_K, step: int = HASH_STEP, maxcount: int = HASH_MAXCOUNT) -> bytes:
     """The `.hash` file buildRefIndex@0x410190 writes for this FASTA (the
     oracle keeps the index for hash_align)."""
+    out = hash_index_array(fasta, k, step, maxcount)
+    return out.tobytes()
+
+
+def hash_index_array(fasta, k: int = HASH_K, step: int = HASH_STEP, maxcount: int = HASH_MAXCOUNT) -> np.ndarray:
+    """hash_index() as a uint8 array; fasta may be bytes or a uint8 array
+    (genome-scale FASTA without a bytes copy)."""
     l = lib()
-    n = l.ho_build(fasta, len(fasta), k, step, maxcount)
+    if isinstance(fasta, np.ndarray):
+        n = l.ho_build(_p(fasta), fasta.size, k, step, maxcount)
+    else:
+        n = l.ho_build(fasta, len(fasta), k, step, maxcount)
     if n < 0:
         raise ValueError("hash index build failed")
     out = np.empty(n, dtype=np.uint8)
     if l.ho_serialize(_p(out), n):
         raise ValueError("hash index serialize failed")
-    return out.tobytes()
+    return out
 
 
 def hash_align(reads: list[bytes], maxmis: int = HASH_MAXMIS, good: int = HASH_GOOD, ai_nmis: int = 0):

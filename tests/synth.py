@@ -183,12 +183,47 @@ def reference(genome_len: int, seed: int, chroms: int = 3, width: int = 60) -> t
     return b"".join(out), g
 
 
+def big_reference(genome_len: int, seed: int, chroms: int = 3, width: int = 60) -> tuple[np.ndarray, np.ndarray]:
+    """reference() at genome scale (numpy throughout, no per-line Python):
+    FASTA as a uint8 array and the bases (ACGTN).  Random bases, N runs of
+    1-39 every ~200 kb, the second record in lower case, `chroms` records of
+    `width`-base lines."""
+    rng = np.random.default_rng([seed, 8])
+    g = _BASES[rng.integers(0, 4, size=genome_len, dtype=np.uint8)]
+    at = rng.integers(0, max(genome_len - 64, 1), size=max(genome_len // 200000, 1))
+    ln = rng.integers(1, 40, size=at.size)
+    for a, l in zip(at.tolist(), ln.tolist()):
+        g[a:a + l] = ord("N")
+    cuts = sorted(set(int(x) for x in rng.integers(1, genome_len, size=chroms - 1))) if chroms > 1 else []
+    bounds = [0] + cuts + [genome_len]
+    parts = []
+    for i in range(len(bounds) - 1):
+        c = g[bounds[i]:bounds[i + 1]]
+        n = c.size
+        rows = (n + width - 1) // width
+        body = np.full((rows, width + 1), ord("\n"), dtype=np.uint8)
+        pad = np.zeros(rows * width, dtype=np.uint8)
+        pad[:n] = c
+        if i == 1:
+            pad[:n] |= 0x20   # lower case (N -> n)
+        body[:, :width] = pad.reshape(rows, width)
+        del pad
+        body = body.reshape(-1)
+        if n % width:   # the last line holds n % width bases, then its newline
+            body = body[: (rows - 1) * (width + 1) + n % width + 1]
+            body[-1] = ord("\n")
+        parts += [np.frombuffer(b">chr%d synthetic\n" % (i + 1), dtype=np.uint8), body]
+    return np.concatenate(parts), g
+
+
 def aligned_reads(genome: np.ndarray, n: int, seed: int, paired: bool = False, read_len: int = 150,
-                  random_frac: float = 0.05, far_frac: float = 0.05, short_frac: float = 0.0) -> tuple[bytes, bytes | None]:
+                  random_frac: float = 0.05, far_frac: float = 0.05, short_frac: float = 0.0,
+                  lo: int = 0) -> tuple[bytes, bytes | None]:
     """Reads for the reference path: drawn from `genome` (either strand) with
     0-10 substitutions, some N runs (more than maxmis in some reads), a fraction
     of random (unalignable) reads; PE mates mostly 250-449 apart, a fraction
-    far apart or on another chromosome region (the relation's other cases)."""
+    far apart or on another chromosome region (the relation's other cases).
+    Fragments start at or after genome position `lo` (0-based)."""
     rng = np.random.default_rng([seed, 11])
     G = genome.size
     comp = bytes.maketrans(b"ACGTN", b"TGCAN")
@@ -214,12 +249,12 @@ def aligned_reads(genome: np.ndarray, n: int, seed: int, paired: bool = False, r
 
     r1, r2 = [], []
     for i in range(n):
-        st = int(rng.integers(0, G - 1000 - read_len))
+        st = int(rng.integers(lo, G - 1000 - read_len))
         rv = bool(rng.random() < 0.5)
         r1.append(one(st, rv))
         if paired:
             if rng.random() < far_frac:
-                st2 = int(rng.integers(0, G - read_len))
+                st2 = int(rng.integers(lo, G - read_len))
             else:
                 st2 = min(st + int(rng.integers(250, 450)) - read_len, G - read_len)
             r2.append(one(max(st2, 0), not rv))

@@ -104,6 +104,31 @@ def test_compress_usage_errors(tmp_path):
     assert r.returncode == 2
     r = _run(["-i", str(tmp_path / "missing.fa")], tmp_path)
     assert r.returncode == 1 and b"may be not exist" in r.stderr
+    r = _run(["-c", "--maxmis", "9", "-1", str(tmp_path / "e.fq"), "x"], tmp_path)   # (no Mis model beyond 8)
+    assert r.returncode == 2 and b"0..8" in r.stderr
+
+
+@pytest.mark.parametrize("maxmis", [0, 3, 8])
+def test_decode_reference_maxmis_from_archive(tmp_path, maxmis):
+    """An archive of the reference path made with a non-default maxmis carries it
+    (params field 19, ours; SeqArc keeps maxmis in ./seqarc.config and stores
+    none): -d rebuilds the Mis model without being told."""
+    fa, g = synth.reference(600_000, 73, chroms=2)
+    fa = fa.upper()
+    (tmp_path / "ref.fa").write_bytes(fa)
+    (tmp_path / "ref.fa.hash").write_bytes(oracle_py.hash_index(fa))
+    r1, _ = synth.aligned_reads(g, 2000, 74, short_frac=0.2)
+    blocks = fq.blocks_from_fastq(r1, None, block_size=120_000)
+    tmpl = fq.analyze_ids(blocks[0], True)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    carry = [0, 0]
+    enc = [oracle_py.encode_block_hash(b, False, carry, bin_mode=cfg.bin_mode, maxmis=maxmis) for b in blocks]
+    data = fq.arc_archive(enc, blocks, "s.fq", None, tmpl, cfg, plus_bare=fq.bare_plus(r1),
+                          ref_md5=hashlib.md5(fa).digest(), maxmis=maxmis)
+    (tmp_path / "a.arc").write_bytes(data)
+    r = _run(["-d", "-t", "2", "ref.fa", "a.arc", "back"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "back.fastq").read_bytes() == r1
 
 
 @pytest.mark.parametrize("paired,with_hash", [(False, True), (True, False), (True, True)])

@@ -212,3 +212,62 @@ def test_cli_reference_path(tmp_path):
     r = run(["-d", "ref.fa", "pi.arc", "bi"])
     assert r.returncode == 0, r.stderr
     same([(tmp_path / "bi_1.fastq").read_bytes()], [r1])
+
+
+def test_cli_reference_maxmis_bailout_chain(tmp_path):
+    """a non-default --maxmis is recorded in the archive (params field
+    19) so -d rebuilds the same Mis model without the flag; blocks that bail out
+    and -I across several batches per chain on two contexts; --maxmis 9 (no Mis
+    model) is refused."""
+    import hashlib
+    import subprocess
+    from fastqueeze_amd import build
+    fa, g = synth.reference(1_200_000, 61, chroms=2)
+    fa = fa.upper()
+    (tmp_path / "ref.fa").write_bytes(fa)
+    run = lambda args: subprocess.run([build.CLI] + args, capture_output=True, cwd=tmp_path, timeout=300)
+    # first half aligns, second half mostly random reads (later blocks bail out)
+    a1, a2 = synth.aligned_reads(g, 6000, 62, paired=True, short_frac=0.2)
+    b1, b2 = synth.aligned_reads(g, 6000, 63, paired=True, random_frac=0.8, far_frac=0.3)
+    r1, r2 = a1 + b1, a2 + b2
+    (tmp_path / "a_1.fq").write_bytes(r1)
+    (tmp_path / "a_2.fq").write_bytes(r2)
+    for maxmis, ins in ((3, 300), (0, 0), (8, 0)):
+        blocks = fq.blocks_from_fastq(r1, r2, 1 << 20)
+        assert len(blocks) >= 4
+        tmpl = fq.analyze_ids(blocks[0], False)
+        cfg = fq.Config(bin_mode=int(tmpl[0]))
+        carry = [0, 0]
+        enc = [orc.encode_block_hash(b, True, carry, bin_mode=cfg.bin_mode, insert_size=ins, maxmis=maxmis)
+               for b in blocks]
+        want = fq.arc_archive(enc, blocks, "a_1.fq", "a_2.fq", tmpl, cfg, plus_bare=fq.bare_plus(r1),
+                              ref_md5=hashlib.md5(fa).digest(), insert_size=ins, maxmis=maxmis)
+        args = ["-c", "-f", "--block-size", "1", "--batch", "1", "--contexts", "2", "--maxmis", str(maxmis)]
+        args += (["-I", str(ins)] if ins else []) + ["ref.fa", "-1", "a_1.fq", "-2", "a_2.fq", f"m{maxmis}"]
+        r = run(args)
+        assert r.returncode == 0, r.stderr
+        same([(tmp_path / f"m{maxmis}.arc").read_bytes()], [want])
+        r = run(["-d", "ref.fa", f"m{maxmis}.arc", f"d{maxmis}"])   # (no --maxmis: from the archive)
+        assert r.returncode == 0, r.stderr
+        same([(tmp_path / f"d{maxmis}_1.fastq").read_bytes(), (tmp_path / f"d{maxmis}_2.fastq").read_bytes()],
+             [r1, r2])
+    r = run(["-c", "-f", "--maxmis", "9", "ref.fa", "-1", "a_1.fq", "-2", "a_2.fq", "bad"])
+    assert r.returncode != 0 and b"0..8" in r.stderr
+
+
+def test_aligned_maxmis_out_of_range_fails_chain(enc, index, ref):
+    """maxmis 9 is refused by sa_run_input_aligned, and the chain is failed so a
+    later batch waiting on it returns an error instead of hanging."""
+    _, g = ref
+    r1, _ = synth.aligned_reads(g, 2000, 64)
+    blocks = fq.blocks_from_fastq(r1, None, block_size=200_000)
+    chain = fq.AlignChain()
+    try:
+        enc.stage(blocks[:1])
+        with pytest.raises(fq.SeqArcError):
+            enc.run_aligned(fq.Config(), index, False, chain, batch=0, maxmis=9)
+        enc.stage(blocks[1:2])
+        with pytest.raises(fq.SeqArcError):   # batch 1 would wait for batch 0 forever
+            enc.run_aligned(fq.Config(), index, False, chain, batch=1)
+    finally:
+        chain.close()
