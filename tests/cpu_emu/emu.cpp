@@ -140,11 +140,13 @@ int main(int argc, char** argv)
     double lossy = 0.0;
     const char* ref = nullptr;
     uint32_t insert_size = 0;
-    const int maxmis = 7, good = 1;
+    int maxmis = 7;
+    const int good = 1;
     std::vector<const char*> in;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "-r") && i + 1 < argc) { ref = argv[++i]; continue; }
         if (!std::strcmp(argv[i], "-I") && i + 1 < argc) { insert_size = (uint32_t)std::atoi(argv[++i]); continue; }
+        if (!std::strcmp(argv[i], "-m") && i + 1 < argc) { maxmis = std::atoi(argv[++i]); continue; }
         if (!std::strcmp(argv[i], "-b") && i + 1 < argc) bs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "-s") && i + 1 < argc) slevel = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "-q") && i + 1 < argc) qlevel = std::atoi(argv[++i]);

@@ -225,6 +225,7 @@ def test_cli_reference_maxmis_bailout_chain(tmp_path):
     fa, g = synth.reference(1_200_000, 61, chroms=2)
     fa = fa.upper()
     (tmp_path / "ref.fa").write_bytes(fa)
+    orc.hash_index(fa)   # (the oracle aligns against its last built index)
     run = lambda args: subprocess.run([build.CLI] + args, capture_output=True, cwd=tmp_path, timeout=300)
     # first half aligns, second half mostly random reads (later blocks bail out)
     a1, a2 = synth.aligned_reads(g, 6000, 62, paired=True, short_frac=0.2)
