@@ -109,6 +109,20 @@ def parse_args(argv=None):
                          "profiled bench, whose process must not start generator processes under the profiler")
     ap.add_argument("--inputs", default=None, metavar="DIR",
                     help="read the batches from FASTQ files written by --write-inputs (no generator processes)")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="only the in-HBM line (no e2e / gzip / ingest / ONT / HASH legs, no CPU baselines)")
+    ap.add_argument("--ont-leg", type=int, default=1, help="configs[4] leg: ONT-shape SE long reads, -l 1.15 (0: skip)")
+    ap.add_argument("--ont-reads", type=int, default=60_000, help="reads of the ONT leg's batch (10-50 kbp)")
+    ap.add_argument("--hash-leg", type=int, default=1, help="configs[3] leg: the HASH reference path (0: skip)")
+    ap.add_argument("--hash-genome-mb", type=float, default=3100.0, help="synthetic genome of the HASH leg (GRCh38: 3100)")
+    ap.add_argument("--hash-pairs", type=int, default=1_200_000, help="PE pairs of the HASH leg's batch (16 blocks)")
+    ap.add_argument("--hash-align-reads", type=int, default=4_000_000, help="single reads of the aligner leg")
+    ap.add_argument("--leg-steps", type=int, default=10, help="timed steps of the ONT and HASH legs")
+    ap.add_argument("--decode-check", type=int, default=1,
+                    help="decode the short e2e leg's archive with seqarc_amd -d and compare MD5s with the input")
+    ap.add_argument("--ingest-devices", type=int, default=8,
+                    help="the whole-node ingest leg: seqarc_amd --ingest-only --devices N over the long e2e files "
+                         "(0: skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
                          "(scripts/pmc_traffic.py), committed under profiles/")
@@ -121,6 +135,8 @@ def parse_args(argv=None):
         a.batches = 4 if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 2
     if a.e2e_batches < 0:   # (N ranks: rank 0's first batch, N x 2 times over, one seqarc_amd --devices N run)
         a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 1
+    if a.no_legs:
+        a.e2e_batches, a.cpu_seconds, a.ont_leg, a.hash_leg, a.ingest_devices = 0, 0.0, 0, 0, 0
     if a.dry_run:
         a.pairs = min(a.pairs, 3000)
         a.block_size = min(a.block_size, 300_000)
@@ -212,7 +228,7 @@ def make_batch(gid: int, args, workers: int, files=None):
 
 
 def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, devices: int = 1,
-               ingest_only: bool = False):
+               ingest_only: bool = False, keep_arc: bool = False):
     """`seqarc_amd -c` (the streaming reader / parser / encoder / writer
     pipeline) on the FASTQ files on disk: wall time of the whole process, and
     its own clock (device init to the closed .arc).  The archive's blocks must
@@ -256,13 +272,221 @@ def end_to_end(args, files, contexts, expect: bytes, batch: int, threads: int, d
         if "monotonic clock: main" in ln:   # process start -> main, and exit -> reaped (dynamic loading; the
             mm, me = (float(x.split()[-1]) for x in ln.split(": ", 2)[2].split(", "))   # driver's teardown)
             proc = {"start_to_main_s": round(mm - m0, 3), "exit_to_reaped_s": round(m1 - me, 3)}
-    os.remove(out + ".arc")
+    if not keep_arc:
+        os.remove(out + ".arc")
     return {"value": round(in_bytes / wall / 1e6, 1), "unit": "MB/s", "wall_s": round(wall, 3),
             "cli_clock_mb_s": clock, "cli_stages": stages, "process": proc, "fastq_bytes": in_bytes, "devices": devices,
             "contexts": contexts, "batch_blocks": batch, "device_settle_s": 0 if ingest_only else args.e2e_settle,
             "parse": "none (--ingest-only)" if ingest_only else "device (sa_stage_text from page-locked text windows)",
             "leading_blocks_identical_to_bench": same,
-            "command": " ".join(os.path.basename(c) if i == 0 else c for i, c in enumerate(cmd))}
+            "command": " ".join(os.path.basename(c) if i == 0 else c for i, c in enumerate(cmd)),
+            **({"archive": out + ".arc", "archive_bytes": len(arc)} if keep_arc else {})}
+
+
+def md5_files(paths, threads: int) -> list[str]:
+    """MD5 of each file (hashlib releases the GIL: one thread per file, 64 MiB reads)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(p):
+        h = hashlib.md5()
+        with open(p, "rb") as f:
+            while True:
+                b = f.read(64 << 20)
+                if not b:
+                    return h.hexdigest()
+                h.update(b)
+    with ThreadPoolExecutor(max(1, min(threads, len(paths)))) as ex:
+        return list(ex.map(one, paths))
+
+
+def decode_roundtrip(arc: str, inputs: list[str], threads: int) -> dict:
+    """f1/f2: `seqarc_amd -d` of an e2e archive (host decoder, -t threads), and
+    the decoded FASTQ's MD5 against the input files': the whole archive (every
+    block, the block table, the trailer) comes back to the input."""
+    from fastqueeze_amd import build
+    prefix = os.path.join(os.path.dirname(arc), "rt")
+    cmd = [build.CLI, "-d", "-f", "-t", str(threads), arc, prefix]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    wall = time.perf_counter() - t0
+    outs = [prefix + "_1.fastq", prefix + "_2.fastq"] if len(inputs) > 1 else [prefix + ".fastq"]
+    try:
+        if r.returncode != 0:
+            return {"e2e_roundtrip_md5_ok": False, "error": f"exit {r.returncode}: {r.stderr[-500:]}"}
+        t1 = time.perf_counter()
+        got = md5_files(outs + list(inputs), 2 * len(inputs))
+        md5_s = time.perf_counter() - t1
+        n = len(inputs)
+        in_bytes = sum(os.path.getsize(f) for f in inputs)
+        return {"e2e_roundtrip_md5_ok": got[:n] == got[n:], "decoded_md5": got[:n], "input_md5": got[n:],
+                "decode_wall_s": round(wall, 3), "decode_mb_s": round(in_bytes / wall / 1e6, 1),
+                "decode_threads": threads, "md5_s": round(md5_s, 2), "fastq_bytes": in_bytes,
+                "command": " ".join(["seqarc_amd"] + cmd[1:])}
+    finally:
+        for f in outs:
+            if os.path.exists(f):
+                os.remove(f)
+
+
+def pipeline(encs, inputs, cfg, steps: int, warmup: int, local: int, runner=None):
+    """The contexts' pipeline over resident inputs: warm (every context every
+    input), W untimed steps, then K timed steps between device synchronisations.
+    Returns (seconds, Workers)."""
+    import torch
+    W = Workers(encs, inputs, cfg, runner)
+    W.warm_all()
+    W.run(warmup, record=False)
+    torch.cuda.synchronize(local)
+    t0 = time.perf_counter()
+    W.run(steps, record=True)
+    torch.cuda.synchronize(local)
+    return time.perf_counter() - t0, W
+
+
+def phase_medians(W) -> dict:
+    import numpy as np
+    return {k: round(float(np.median([p[k] for p in W.phases])), 2) for k in W.phases[0]}
+
+
+def make_contexts(local: int, n: int, share: bool = True):
+    import fastqueeze_amd as fq
+    encs = [fq.Encoder(local)]
+    for _ in range(n - 1):
+        encs.append(fq.Encoder(local, share_with=encs[0] if share else None))
+    for e in encs:
+        e.set_timing(True)
+    return encs
+
+
+def ont_leg(args, workers: int, local: int) -> dict:
+    """configs[4]: ONT-shape SE long reads (10/20/30/40/50 kbp, 0.05 % N), -l
+    1.15 R-Block lossy qualities (rblock@0x426c10), one batch resident in HBM,
+    the contexts' pipeline as in the headline; first and last block checked
+    against the CPU restatement (same -l)."""
+    import copy
+    import fastqueeze_amd as fq
+    import oracle_py
+    a = copy.copy(args)
+    a.ont, a.se, a.pairs, a.lossy, a.inputs = True, True, args.ont_reads, 1.15, None
+    t0 = time.perf_counter()
+    blocks = make_batch(0, a, workers)
+    gen_s = time.perf_counter() - t0
+    tmpl = fq.analyze_ids(blocks[0], True)
+    cfg = fq.Config(slevel=args.slevel, qlevel=args.qlevel, bin_mode=int(tmpl[0]), lossy=a.lossy)
+    inp = fq.Input(blocks, local)
+    encs = make_contexts(local, args.contexts)
+    try:
+        el, W = pipeline(encs, [inp], cfg, args.leg_steps, 2, local)
+        encs[0].run_input(inp, cfg)
+        outs = encs[0].fetch()
+    finally:
+        for e in encs:
+            e.close()
+        inp.close()
+    for i in sorted({0, len(blocks) - 1}):
+        b = blocks[i]
+        if outs[i] != oracle_py.encode_block(b, cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode, cfg.lossy):
+            raise SystemExit(f"ONT leg: block {i} differs from the CPU restatement")
+    tb = inp.text_bytes
+    return {"metric": "MB/s FASTQ compressed, ONT-shape SE long reads, -l 1.15 (configs[4], 1 MI355X)",
+            "value": round(tb * args.leg_steps / el / 1e6, 1), "unit": "MB/s", "steps": args.leg_steps,
+            "ms_per_step": round(el / args.leg_steps * 1e3, 2), "fastq_bytes_per_batch": tb, "blocks": len(blocks),
+            "reads": a.pairs, "ratio": round(tb / sum(map(len, outs)), 3), "contexts": args.contexts,
+            "phase_ms": phase_medians(W), "generate_s": round(gen_s, 1),
+            "check": "first and last block bit-identical to oracle/fqz_oracle.c with -l 1.15",
+            "data": "synthetic (tests/synth.py, 10/20/30/40/50 kbp SE, seed 1000 + k), inputs resident in HBM"}
+
+
+def hash_leg(args, local: int) -> dict:
+    """configs[3]: the HASH reference path at GRCh38 size.  A synthetic genome
+    of --hash-genome-mb Mb (3 records, N runs, one in lower case) indexed on the
+    device (buildRefIndex@0x410190), single reads aligned
+    (getHashAlignInfo@0x4113c0), and a batch of 16 x 50 MiB PE blocks encoded
+    through the aligned path (doAlign + doAlignEncode@0x42d4c0) by the contexts'
+    pipeline, each step with its own align_info chain.  Checked by decoding the
+    first and last blocks with the host decoder against the genome: the reads
+    come back.  (The oracle's index of a 3 Gb genome takes minutes on the host:
+    parity at this scale is tests/test_gpu_genome_scale.py's.)"""
+    import numpy as np
+    import torch
+    import fastqueeze_amd as fq
+    import synth
+    t0 = time.perf_counter()
+    glen = int(args.hash_genome_mb * 1e6)
+    fa, g = synth.big_reference(glen, 2024)
+    gen_s = time.perf_counter() - t0
+    encs = make_contexts(local, args.contexts)
+    ix = inp = None
+    try:
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        ix = fq.HashIndex(encs[0], fa)
+        torch.cuda.synchronize(local)
+        build_s = time.perf_counter() - t0
+        fa_bytes = fa.size
+        del fa
+        # single reads: 150 bp, 0.2 % substitutions, either strand
+        rng = np.random.default_rng(77)
+        n = args.hash_align_reads
+        starts = rng.integers(0, glen - 200, n)
+        rv = np.arange(n) % 2 == 1
+        raw = synth.draw_reads(rng, g, starts, rv, 150, sub=0.002, random_frac=0.0).reshape(-1)
+        off = np.arange(n, dtype=np.uint64) * 150
+        lens = np.full(n, 150, np.int32)
+        ix.align_arrays(raw, off, lens, 20_000)
+        t0 = time.perf_counter()
+        ret, rev, pos, _, _ = ix.align_arrays(raw, off, lens, n)
+        align_s = time.perf_counter() - t0
+        del raw, off, lens
+        good = int(((ret >= 0) & (pos == starts + 1) & (rev == rv)).sum())
+        # the aligned encode of a 16-block PE batch
+        t1, t2 = synth.pe_reads_fast(g, args.hash_pairs, 78)
+        del g
+        blocks = fq.blocks_from_fastq(t1, t2)
+        del t1, t2
+        tmpl = fq.analyze_ids(blocks[0], False)
+        cfg = fq.Config(slevel=args.slevel, qlevel=args.qlevel, bin_mode=int(tmpl[0]))
+        inp = fq.Input(blocks, local)
+
+        def aligned(enc, i, c):
+            ch = fq.AlignChain()
+            try:
+                enc.run_aligned(c, ix, True, ch, inp=i)
+            finally:
+                ch.close()
+        el, W = pipeline(encs, [inp], cfg, args.leg_steps, 2, local, aligned)
+        aligned(encs[0], inp, cfg)
+        outs = encs[0].fetch()
+        encs[0].run_input(inp, cfg)
+        noref = sum(map(len, encs[0].fetch()))
+        words, bases = ix.packed()
+        for i in sorted({0, len(blocks) - 1}):
+            b = blocks[i]
+            d, ok = fq.decode_block(outs[i], b.text_bytes, cfg, tmpl, ref=(words, bases, True, 7))
+            if not (ok and np.array_equal(d.seq, b.seq) and np.array_equal(d.qual, b.qual)
+                    and np.array_equal(d.names, b.names)):
+                raise SystemExit(f"HASH leg: aligned block {i} does not decode back to its reads")
+    finally:
+        if ix is not None:
+            ix.close()
+        if inp is not None:
+            inp.close()
+        for e in encs:
+            e.close()
+    tb = sum(b.text_bytes for b in blocks)
+    return {"metric": "MB/s FASTQ compressed, HASH reference path, 150 bp PE (configs[3] shape, 1 MI355X)",
+            "value": round(tb * args.leg_steps / el / 1e6, 1), "unit": "MB/s", "steps": args.leg_steps,
+            "ms_per_step": round(el / args.leg_steps * 1e3, 2), "fastq_bytes_per_batch": tb, "blocks": len(blocks),
+            "ratio": round(tb / sum(map(len, outs)), 3), "ratio_noref_same_batch": round(tb / noref, 3),
+            "contexts": args.contexts, "phase_ms": phase_medians(W),
+            "genome_bases": glen, "fasta_bytes": fa_bytes, "genome_generate_s": round(gen_s, 1),
+            "index_build_s": round(build_s, 3),
+            "align": {"reads": n, "read_len": 150, "s": round(align_s, 3), "reads_per_s": round(n / align_s, 1),
+                      "aligned_at_true_position": round(good / n, 5)},
+            "check": "first and last aligned blocks decode back to their reads (sa_decode_block_ref, genome words)",
+            "parity": "GPU == oracle/ restatement (tests/test_gpu_align.py, tests/test_gpu_genome_scale.py); "
+                      "unpinned against SeqArc itself",
+            "data": "synthetic genome (tests/synth.py big_reference, seed 2024) and reads (pe_reads_fast, seed 78)"}
 
 
 def write_gz(src: str, dst: str, nbytes: int, kind: str, threads: int):
@@ -342,8 +566,10 @@ class Workers:
     """C encoder contexts on one GPU, each driven by its own host thread, taking
     steps (batch encodes) from a shared counter."""
 
-    def __init__(self, encoders, inputs, cfg):
+    def __init__(self, encoders, inputs, cfg, runner=None):
+        """runner(enc, inp, cfg): one step (default: the no-reference encode)."""
         self.encs, self.inputs, self.cfg = encoders, inputs, cfg
+        self.step = runner or (lambda enc, inp, c: enc.run_input(inp, c))
         self.phases, self.restarts, self.stats = [], 0, (0, 0)
 
     def warm_all(self):
@@ -354,7 +580,7 @@ class Workers:
         def worker(enc):
             try:
                 for inp in self.inputs:
-                    enc.run_input(inp, self.cfg)
+                    self.step(enc, inp, self.cfg)
             except Exception as e:
                 errs.append(e)
 
@@ -379,7 +605,7 @@ class Workers:
                         if s >= nsteps:
                             return
                         nxt[0] += 1
-                    enc.run_input(self.inputs[s % len(self.inputs)], self.cfg)
+                    self.step(enc, self.inputs[s % len(self.inputs)], self.cfg)
                     if record:
                         ph = enc.phase_times()
                         with lock:
@@ -652,6 +878,9 @@ def main():
         "metric": "MB/s FASTQ compressed (whole node) + ratio, 150 bp PE, 1/2/4/8 MI355X",
         "value": round(value, 1),
         "unit": "MB/s",
+        "value_kind": "device_encode: inputs parsed and resident in HBM before the timed region (FASTQ parse, "
+                      "H2D and the .arc write are outside it; end_to_end_short / metric_end_to_end is the "
+                      "metric-faithful seqarc_amd -c number)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -700,60 +929,91 @@ def main():
     # (the whole node in one process, the reference's one reader feeding every
     # encoder); the other ranks wait
     barrier()
-    if e2e_files and world == 1 and args.e2e_gz_blocks > 0:
-        # gzip inputs (the usual .fq.gz): the first blocks of batch 0 as BGZF and as
-        # member-serial gzip, through the inflate-ahead reader; the archive's blocks
-        # must be the bench's
-        nb = min(args.e2e_gz_blocks, len(keep["verify"]))
-        vb = keep["verify"][:nb]
-        sizes = [sum(b.text1 or b.text_bytes for b in vb)] + ([sum(b.text2 for b in vb)] if len(e2e_files) > 1 else [])
-        gz = {}
-        for kind in ("bgzf", "gzip"):
-            gzf = [f + "." + kind + ".gz" for f in e2e_files]
-            t0 = time.perf_counter()
-            for f, g, n in zip(e2e_files, gzf, sizes):
-                write_gz(f, g, n, kind, share["usable"])
-            gzb = sum(os.path.getsize(g) for g in gzf)
-            log(f"[rank 0] {kind} input: {gzb / 1e6:.0f} MB ({time.perf_counter() - t0:.1f}s)")
-            try:
-                r = end_to_end(args, gzf, args.contexts, b"".join(outs[:nb]), args.e2e_batch or len(vb),
-                               share["usable"])
-            finally:
-                for g in gzf:
-                    os.remove(g)
-            r["fastq_bytes"] = sum(sizes)
-            if r.get("wall_s"):
-                r["value"] = round(sum(sizes) / r["wall_s"] / 1e6, 1)
-            r["gz_bytes"] = gzb
-            gz[kind] = r
-        res["end_to_end_gz"] = gz
     if e2e_files:
         expect = b"".join(outs if args.e2e_batches == 1 else outs[:-1])
-        if world == 1 and args.e2e_batches != 1:
-            # a short stream at configs[2]'s per-GPU share (143 GB / 8 GPUs ~ 18 GB, five
-            # batches: the written batches plus batch 0 once more), where pipeline fill
-            # and drain weigh most; the files are cut back to the written batches after it
-            base = [os.path.getsize(f) for f in e2e_files]
-            sizes = [sum(b.text1 or b.text_bytes for b in keep["verify"])] + \
-                ([sum(b.text2 for b in keep["verify"])] if len(e2e_files) > 1 else [])
-            for f, n in zip(e2e_files, sizes):
-                with open(f, "rb") as src, open(f, "ab") as dst:
-                    dst.write(src.read(n))
-            try:
-                res["end_to_end_short"] = end_to_end(args, e2e_files, args.contexts, expect,
-                                                     args.e2e_batch or len(keep["verify"]), share["usable"])
-            finally:
+        blk = args.e2e_batch or len(keep["verify"])
+        try:
+            if world == 1 and args.e2e_batches != 1:
+                # a short stream at configs[2]'s per-GPU share (143 GB / 8 GPUs ~ 18 GB, five
+                # batches: the written batches plus batch 0 once more), where pipeline fill
+                # and drain weigh most; the files are cut back to the written batches after it
+                base = [os.path.getsize(f) for f in e2e_files]
+                sizes = [sum(b.text1 or b.text_bytes for b in keep["verify"])] + \
+                    ([sum(b.text2 for b in keep["verify"])] if len(e2e_files) > 1 else [])
+                for f, n in zip(e2e_files, sizes):
+                    with open(f, "rb") as src, open(f, "ab") as dst:
+                        dst.write(src.read(n))
+                short = end_to_end(args, e2e_files, args.contexts, expect, blk, share["usable"],
+                                   keep_arc=args.decode_check > 0)
+                arc = short.pop("archive", None)
+                if arc:   # the whole archive back through seqarc_amd -d (f1 / f2), MD5 against the input
+                    try:
+                        short["roundtrip"] = decode_roundtrip(arc, e2e_files, share["usable"])
+                        short["e2e_roundtrip_md5_ok"] = short["roundtrip"]["e2e_roundtrip_md5_ok"]
+                    finally:
+                        os.remove(arc)
+                res["end_to_end_short"] = short
+                if args.e2e_gz_blocks > 0:
+                    # gzip inputs (the usual .fq.gz) at the short leg's size: BGZF (members
+                    # inflated in parallel) and member-serial gzip (one inflate thread per
+                    # file), through the inflate-ahead reader; the archive's leading blocks
+                    # must be the bench's
+                    gz = {}
+                    sizes = [os.path.getsize(f) for f in e2e_files]
+                    for kind in ("bgzf", "gzip"):
+                        gzf = [f + "." + kind + ".gz" for f in e2e_files]
+                        t0 = time.perf_counter()
+                        for f, g, n in zip(e2e_files, gzf, sizes):
+                            write_gz(f, g, n, kind, share["usable"])
+                        gzb = sum(os.path.getsize(g) for g in gzf)
+                        log(f"[rank 0] {kind} input: {gzb / 1e6:.0f} MB ({time.perf_counter() - t0:.1f}s)")
+                        try:
+                            r = end_to_end(args, gzf, args.contexts, expect, blk, share["usable"])
+                        finally:
+                            for g in gzf:
+                                os.remove(g)
+                        r["fastq_bytes"] = sum(sizes)
+                        if r.get("wall_s"):
+                            r["value"] = round(sum(sizes) / r["wall_s"] / 1e6, 1)
+                        r["gz_bytes"] = gzb
+                        if r.get("value") and short.get("value"):
+                            r["vs_plain_short"] = round(r["value"] / short["value"], 3)
+                        gz[kind] = r
+                    res["end_to_end_gz"] = gz
                 for f, n in zip(e2e_files, base):
                     os.truncate(f, n)
-        replicate(e2e_files, args.e2e_repeat or (3 if world == 1 else 2 * world))
-        try:
+            replicate(e2e_files, args.e2e_repeat or (3 if world == 1 else 2 * world))
             # batches of the bench's size (69 blocks): pass R of a batch takes as long for 28 blocks as
             # for 69, so smaller batches lose the coder's parallelism
-            e2e = end_to_end(args, e2e_files, args.contexts, expect, args.e2e_batch or len(keep["verify"]),
-                             share["usable"], devices=world)
+            res["end_to_end"] = end_to_end(args, e2e_files, args.contexts, expect, blk, share["usable"],
+                                           devices=world)
+            if args.ingest_devices > 0 and world == 1:
+                # the whole node's ingest: the reader and the block cut dealt to N devices x C
+                # contexts (no device work): the host ceiling an 8-GPU node meets
+                ing = end_to_end(args, e2e_files, args.contexts, b"", blk, share["usable"],
+                                 devices=args.ingest_devices, ingest_only=True)
+                res["ingest_8way"] = ing
+                res["ingest_8way_mb_s"] = ing.get("value")
         finally:
             shutil.rmtree(os.path.dirname(e2e_files[0]), True)
-        res["end_to_end"] = e2e
+    if rank == 0 and world == 1:
+        for name, leg, on in (("ont_lossy", ont_leg, args.ont_leg), ("hash_path", hash_leg, args.hash_leg)):
+            if not on:
+                continue
+            t0 = time.perf_counter()
+            try:
+                res[name] = ont_leg(args, workers, local) if leg is ont_leg else hash_leg(args, local)
+            except SystemExit:
+                raise
+            except Exception as e:   # (recorded: the headline line stands on its own)
+                log(f"[rank 0] {name} leg failed: {e!r}")
+                res[name] = {"value": None, "error": repr(e)[:500]}
+            res[name]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+            log(f"[rank 0] {name}: {res[name].get('value')} MB/s ({res[name]['leg_wall_s']} s)")
+    if "end_to_end_short" in res:   # the metric-faithful number (parse, H2D, .arc write included)
+        res["metric_end_to_end"] = {k: res["end_to_end_short"].get(k) for k in ("value", "unit", "wall_s",
+                                                                                  "fastq_bytes",
+                                                                                  "e2e_roundtrip_md5_ok")}
     barrier()
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -602,6 +602,15 @@ class HashIndex:
             self._enc._err("sa_hash_serialize")
         return out
 
+    def packed(self) -> tuple[np.ndarray, int]:
+        """(the genome's packed words, bases): what the aligned-read decoder
+        reads (sa_hash_packed; HashAlignment::doGetSeq@0x40ff90)."""
+        n = self.genome_length
+        words = np.empty(max(1, (n + 15) // 16), np.uint32)
+        if self._lib.sa_hash_packed(self._enc._ctx, self._h, _ptr(words), words.size) != 0:
+            self._enc._err("sa_hash_packed")
+        return words, n
+
     def align(self, reads: list[bytes], maxmis: int = MAXMIS, good: int = GOOD, ai_nmis: int = 0):
         """The reads in order, one align_info state carried across them
         (ai_nmis: before the first read; 0 = a zero-filled AlignParam).  Per
@@ -613,6 +622,15 @@ class HashIndex:
         off = np.zeros(max(n, 1), dtype=np.uint64)
         if n > 1:
             off[1:n] = np.cumsum(lens[:n - 1])
+        return self.align_arrays(seq, off, lens, n, maxmis, good, ai_nmis)
+
+    def align_arrays(self, seq: np.ndarray, off: np.ndarray, lens: np.ndarray, n: int, maxmis: int = MAXMIS,
+                     good: int = GOOD, ai_nmis: int = 0):
+        """align() over reads given as one uint8 array with uint64 offsets and
+        int32 lengths (no per-read Python objects)."""
+        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
         ret = np.zeros(max(n, 1), dtype=np.int32)
         rev = np.zeros(max(n, 1), dtype=np.uint8)
         pos = np.zeros(max(n, 1), dtype=np.uint64)

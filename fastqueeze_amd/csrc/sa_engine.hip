@@ -424,13 +424,17 @@ uint64_t sort_hist_per_tile(int lo, int hi)
 
 template <int DB>
 void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-               uint32_t* vout, uint32_t shift)
+               uint32_t* vout, uint32_t shift, bool wide)
 {
     hipLaunchKernelGGL(k_sort_hist<DB>, dim3((sv.ntiles + HIST_TILES - 1) / HIST_TILES), dim3(SORT_THREADS), 0, st,
                        sv, kin, shift);
     hipLaunchKernelGGL(k_sort_scan<DB>, dim3(sv.nsegs), dim3(1024), 0, st, sv);
-    hipLaunchKernelGGL(k_sort_scatter<DB>, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout, vout,
-                       shift);
+    if (wide)
+        hipLaunchKernelGGL((k_sort_scatter<DB, true>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout,
+                           vout, shift);
+    else
+        hipLaunchKernelGGL((k_sort_scatter<DB, false>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout,
+                           vout, shift);
 }
 
 // sorts keys by bits [lo, hi) (bits below lo ride along); the result is in
@@ -453,15 +457,23 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     sv.total = plan.total;
     sv.ntiles = (uint32_t)plan.tile_seg.size();
     sv.nsegs = (uint32_t)plan.segs.size();
+    // a segment of >= 2^30 keys needs 64-bit offsets in the scatter (the HASH
+    // index of a genome > 2^31 bases: one segment of all its seeds)
+    bool wide = false;
+    for (const SortSeg& g : plan.segs) wide |= (uint64_t)g.ntiles * SORT_TILE >= (1ull << 30);
+    if (plan.segs.size() && (uint64_t)plan.segs.back().ntiles * SORT_TILE >= (1ull << 32)) {
+        c->err = "sort segment of 2^32 keys or more";
+        return -1;
+    }
     int cur = 0, shift = lo;
     for (const int db : sort_digits(lo, hi)) {
         const uint32_t* kin = keys[cur]->as<uint32_t>();
         const uint32_t* vin = index_vals && shift == lo ? nullptr : vals[cur]->as<uint32_t>();
         uint32_t* kout = keys[cur ^ 1]->as<uint32_t>();
         uint32_t* vout = vals[cur ^ 1]->as<uint32_t>();
-        if (db == 7) sort_pass<7>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
-        else if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
-        else sort_pass<9>(st, sv, kin, vin, kout, vout, (uint32_t)shift);
+        if (db == 7) sort_pass<7>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide);
+        else if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide);
+        else sort_pass<9>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide);
         shift += db;
         cur ^= 1;
     }

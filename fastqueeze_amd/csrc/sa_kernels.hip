@@ -1289,7 +1289,9 @@ __global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
     }
 }
 
-template <int DB>
+// WIDE: a segment of >= 2^30 keys (the HASH index of a genome of > 2^31
+// bases sorts all its seeds as one segment): 64-bit element offsets
+template <int DB, bool WIDE>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv,
                                                                const uint32_t* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin,
@@ -1381,26 +1383,45 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         sb[rk[r]] = k[r];
     }
     __syncthreads();
-    // (byte offsets in the segment, 32-bit: a segment is one block's symbols,
-    // < 2^30 keys (plan_batch refuses larger blocks), so the stores take a
-    // scalar base and a 32-bit lane offset)
-    char* const ko = reinterpret_cast<char*>(kout + sg.base);
-    char* const vo = reinterpret_cast<char*>(vout + sg.base);
-    uint32_t ro[SORT_ITEMS];
+    if constexpr (WIDE) {
+        uint32_t* const ko = kout + sg.base;
+        uint32_t* const vo = vout + sg.base;
+        uint32_t ro[SORT_ITEMS];   // element offsets in the segment (< 2^32)
 #pragma unroll
-    for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
-        const uint32_t kk = sb[i];
-        ro[r] = (gstart[(kk >> shift) & (ND - 1)] + i) << 2;
-        *reinterpret_cast<uint32_t*>(ko + ro[r]) = kk;
+        for (int r = 0; r < SORT_ITEMS; r++) {
+            const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
+            const uint32_t kk = sb[i];
+            ro[r] = gstart[(kk >> shift) & (ND - 1)] + i;
+            ko[(uint64_t)ro[r]] = kk;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < SORT_ITEMS; r++) vo[(uint64_t)ro[r]] = sb[threadIdx.x + (uint32_t)r * SORT_THREADS];
+    } else {
+        // (byte offsets in the segment, 32-bit: a segment of a block's symbols
+        // holds < 2^30 keys (plan_batch refuses larger blocks), so the stores take
+        // a scalar base and a 32-bit lane offset)
+        char* const ko = reinterpret_cast<char*>(kout + sg.base);
+        char* const vo = reinterpret_cast<char*>(vout + sg.base);
+        uint32_t ro[SORT_ITEMS];
+#pragma unroll
+        for (int r = 0; r < SORT_ITEMS; r++) {
+            const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
+            const uint32_t kk = sb[i];
+            ro[r] = (gstart[(kk >> shift) & (ND - 1)] + i) << 2;
+            *reinterpret_cast<uint32_t*>(ko + ro[r]) = kk;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < SORT_ITEMS; r++)
+            *reinterpret_cast<uint32_t*>(vo + ro[r]) = sb[threadIdx.x + (uint32_t)r * SORT_THREADS];
     }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = v[r];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < SORT_ITEMS; r++)
-        *reinterpret_cast<uint32_t*>(vo + ro[r]) = sb[threadIdx.x + (uint32_t)r * SORT_THREADS];
 }
 
 // ---------------------------------------------------------------------------

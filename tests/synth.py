@@ -266,3 +266,63 @@ def aligned_reads(genome: np.ndarray, n: int, seed: int, paired: bool = False, r
         names = _headers(0, x, mate)
         return b"".join(b"%s\n%s\n+\n%s\n" % (names[i], s, q[i, :len(s)].tobytes()) for i, s in enumerate(reads))
     return fq(r1, 1), (fq(r2, 2) if paired else None)
+
+
+_COMP256 = np.zeros(256, np.uint8)
+_COMP256[list(b"ACGTN")] = list(b"TGCAN")
+
+
+def fixed_fastq(seq: np.ndarray, mate: int, first: int, qual_seed: int) -> bytes:
+    """Fixed-width FASTQ records (Illumina-style headers `@SYN:7:HXX3:1:<10-digit
+    index> <mate>:N:0:1`, qualities from F : ,) for an n x L base array: numpy
+    throughout, for genome-scale read sets."""
+    n, L = seq.shape
+    pre, suf, digits = b"@SYN:7:HXX3:1:", b" %d:N:0:1" % mate, 10
+    rec = len(pre) + digits + len(suf) + 1 + L + 1 + 2 + L + 1
+    a = np.empty((n, rec), np.uint8)
+    o = 0
+    a[:, o:o + len(pre)] = np.frombuffer(pre, np.uint8)
+    o += len(pre)
+    idx = np.arange(first, first + n, dtype=np.int64)
+    for k in range(digits):
+        a[:, o + digits - 1 - k] = 48 + (idx // 10 ** k) % 10
+    o += digits
+    a[:, o:o + len(suf)] = np.frombuffer(suf, np.uint8)
+    o += len(suf)
+    a[:, o] = 10
+    a[:, o + 1:o + 1 + L] = seq
+    o += 1 + L
+    a[:, o:o + 3] = np.frombuffer(b"\n+\n", np.uint8)
+    o += 3
+    rng = np.random.default_rng([qual_seed, mate])
+    a[:, o:o + L] = np.frombuffer(b"F:,F", np.uint8)[rng.integers(0, 4, (n, L), dtype=np.uint8)]
+    a[:, o + L] = 10
+    return a.tobytes()
+
+
+def draw_reads(rng: np.random.Generator, g: np.ndarray, starts: np.ndarray, rev: np.ndarray, L: int,
+               sub: float = 0.004, random_frac: float = 0.02) -> np.ndarray:
+    """n x L reads from genome g (ACGTN) at `starts`, substitutions at rate
+    `sub`, a fraction of random reads, reverse complement where `rev`."""
+    seq = g[starts[:, None] + np.arange(L)]
+    m = rng.random(seq.shape) < sub
+    seq[m] = _BASES[rng.integers(0, 4, int(m.sum()), dtype=np.uint8)]
+    rnd = rng.random(len(starts)) < random_frac
+    seq[rnd] = _BASES[rng.integers(0, 4, (int(rnd.sum()), L), dtype=np.uint8)]
+    seq[rev] = _COMP256[seq[rev][:, ::-1]]
+    return seq
+
+
+def pe_reads_fast(g: np.ndarray, pairs: int, seed: int, L: int = 150, first: int = 0) -> tuple[bytes, bytes]:
+    """Genome-scale PE reads (configs[3] shape): fragments of 250-449 bp at
+    uniform starts, either strand, 2 % of mates far away, 0.4 % substitutions,
+    2 % random reads."""
+    rng = np.random.default_rng([seed, 12])
+    glen = g.size
+    s1 = rng.integers(0, glen - 1000 - L, pairs)
+    rv = rng.random(pairs) < 0.5
+    s2 = np.minimum(s1 + rng.integers(250, 450, pairs) - L, glen - L)
+    far = rng.random(pairs) < 0.02
+    s2[far] = rng.integers(0, glen - L, int(far.sum()))
+    return (fixed_fastq(draw_reads(rng, g, s1, rv, L), 1, first, seed),
+            fixed_fastq(draw_reads(rng, g, s2, ~rv, L), 2, first, seed))
