@@ -437,6 +437,7 @@ def hash_leg(args, local: int) -> dict:
         t0 = time.perf_counter()
         ret, rev, pos, _, _ = ix.align_arrays(raw, off, lens, n)
         align_s = time.perf_counter() - t0
+        align_kernel_ms = ix.last_kernel_ms
         del raw, off, lens
         good = int(((ret >= 0) & (pos == starts + 1) & (rev == rv)).sum())
         # the aligned encode of a 16-block PE batch
@@ -482,6 +483,8 @@ def hash_leg(args, local: int) -> dict:
             "genome_bases": glen, "fasta_bytes": fa_bytes, "genome_generate_s": round(gen_s, 1),
             "index_build_s": round(build_s, 3),
             "align": {"reads": n, "read_len": 150, "s": round(align_s, 3), "reads_per_s": round(n / align_s, 1),
+                      "kernel_ms": round(align_kernel_ms, 3),
+                      "kernel_reads_per_s": round(n / max(align_kernel_ms, 1e-6) * 1e3, 1),
                       "aligned_at_true_position": round(good / n, 5)},
             "check": "first and last aligned blocks decode back to their reads (sa_decode_block_ref, genome words)",
             "parity": "GPU == oracle/ restatement (tests/test_gpu_align.py, tests/test_gpu_genome_scale.py); "

@@ -124,6 +124,7 @@ def load_library(path: str | None = None):
         "sa_run_input_aligned": ([P, P, P, P, P, U64], I32), "sa_run_aligned": ([P, P, P, P, U64], I32),
         "sa_encode_blocks_aligned": ([P, P, I32, P, P, P, P], I32),
         "sa_hash_load": ([P, P, U64], P), "sa_hash_packed": ([P, P, P, U64], I32),
+        "sa_hash_align_kernel_ms": ([P], C.c_float),
         "sa_decode_block_ref": ([P, U64, P, P, I32, P, P], I64),
     }
     for name, (args, res) in sigs.items():
@@ -640,4 +641,5 @@ class HashIndex:
         if self._lib.sa_hash_align(self._enc._ctx, self._h, _ptr(seq), _ptr(off), _ptr(lens), n, maxmis, good,
                                    _ptr(st), _ptr(ret), _ptr(rev), _ptr(pos), _ptr(mp), _ptr(mt)) != 0:
             self._enc._err("sa_hash_align")
+        self.last_kernel_ms = float(self._lib.sa_hash_align_kernel_ms(self._enc._ctx))
         return ret[:n], rev[:n], pos[:n], mp[:n], mt[:n]

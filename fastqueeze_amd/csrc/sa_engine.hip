@@ -237,6 +237,7 @@ struct sa_ctx {
     uint64_t max_stream_syms = 0, total_stream_syms = 0;
     hipEvent_t ev_beg[PH_N] = {}, ev_end[PH_N] = {};
     float ph_ms[PH_N];
+    float align_kernel_ms = 0.f;   // sa_hash_align: the aligner kernel of the last call (variant 0)
 
     // the batch sa_stage uploads (sa_run encodes it); blocks = the working copy
     // of the batch being encoded (its symbol spaces filled by plan_batch)

@@ -402,29 +402,349 @@ __device__ void aligner_parts_d(const HashRead& h, const HashView& ix, const Has
 // carried state was consulted (the host then re-runs those reads with the
 // other state and picks per read in order, sa_hash_align).  `sel`: the reads
 // to do (NULL: all n), outputs at the read's index.
-__global__ __launch_bounds__(256) void k_hash_align(const HashView ix, const HashArgs a, const uint8_t* __restrict__ seq,
-                                                    const uint64_t* __restrict__ off, const int32_t* __restrict__ lens,
-                                                    const uint64_t* __restrict__ woff, uint32_t* __restrict__ scratch,
-                                                    const uint32_t* __restrict__ sel, uint64_t n, int stale,
-                                                    int32_t* __restrict__ ret, uint8_t* __restrict__ rev,
-                                                    uint64_t* __restrict__ pos, int32_t* __restrict__ mispos,
-                                                    int32_t* __restrict__ mistype, uint8_t* __restrict__ consulted)
+// (k_hash_align, sa_hash_align's kernel, is defined after the row functions)
+
+// ---------------------------------------------------------------------------
+// Row-cooperative alignment: one 16-lane row per read (four reads per wave).
+// The control flow of getHashAlignInfo@0x4113c0 and its callees is the serial
+// one above, row-uniform; the data-parallel steps are spread over the row:
+//   * the read is staged in LDS (16-byte loads), both strands packed there, a
+//     word per lane, with a mask of its N / IUPAC bases;
+//   * findHashSeeds@0x4108d0: the row's lanes look up their seeds' counts
+//     together (all loads in flight), then a row minimum of (count, offset):
+//     the serial scan's "first strictly smaller" is the smallest count at the
+//     smallest offset (stop_first: the smallest qualifying offset);
+//   * gaplessSEHashAlign@0x410d80: the next 16 candidate positions are loaded
+//     at once, then verified in order;
+//   * gaplessHashAlignPositions@0x410990: a word per lane -- the 2-bit XOR
+//     count (a row sum: the serial early exit past maxmis changes only the
+//     partial count, never the verdict, see align_at_row) and the mismatch
+//     list, placed by a row scan of the lanes' mismatch counts.
+// Reads longer than AR_MAXW * 16 bases take the serial path on the row's first
+// lane (global scratch).
+// ---------------------------------------------------------------------------
+constexpr int AR = 16;                     // lanes per read
+constexpr int AR_MAXW = 32;                // packed words per strand in LDS (reads <= 512 bases)
+constexpr int AR_ROWS = 256 / AR;          // rows per 256-thread workgroup
+constexpr int AR_BYTES = 16 * AR_MAXW + 32;   // staged read bytes per row (+ the 16-byte loads' slack)
+
+struct RowStrand {
+    const uint32_t* pk;   // packed 2-bit codes, 16 bases a word, first base in the top bits (LDS)
+    const uint32_t* nm;   // per word: bit j set when base 16 w + j is N / IUPAC (code > 3)
+    int len;
+    bool rc;
+};
+
+__device__ __forceinline__ uint64_t row_min64(uint64_t v)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint64_t i = sel ? sel[t] : t;
-    const int len = lens[i];
-    const int stride = a.maxmis + 1;
-    int* mp = mispos + i * stride;
-    int* mt = mistype + i * stride;
-    HashRead fw{seq + off[i], len, false, scratch + 2 * woff[i]};
-    HashRead rc{seq + off[i], len, true, scratch + 2 * woff[i] + ((len - 1) >> 4) + 1};
-    HashAlign ai{stale ? 0 : -1, 0, 0, false, false};
+#pragma unroll
+    for (int d = AR / 2; d >= 1; d >>= 1) {
+        const uint64_t o = __shfl_xor(v, d, AR);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t row_excl_scan(uint32_t v, uint32_t rl)
+{
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < AR; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, AR);
+        if (rl >= (uint32_t)d) x += y;
+    }
+    return x - v;
+}
+
+// the K-mer ending at offset i + K - 1 (seed i) from the packed words
+__device__ __forceinline__ uint32_t seed_at_row(const RowStrand& h, int i, uint32_t K)
+{
+    const int e = i + (int)K - 1;
+    const int w = e >> 4, sh = 2 * (15 - (e & 15));
+    uint64_t v = (uint64_t)h.pk[w] >> sh;
+    if (w > 0) v |= (uint64_t)h.pk[w - 1] << (32 - sh);
+    return (uint32_t)(v & mask2(K));
+}
+
+// the row's read (len bytes at rd) into LDS, then both strands packed:
+// getHashSeeds@0x4107f0's words (codes & 3) and the N / IUPAC masks.
+// Returns the N / IUPAC count (row-uniform).
+__device__ int row_stage_pack(const uint8_t* rd, int len, uint8_t* sb, uint32_t* pk, uint32_t* nm, uint32_t* pkr,
+                              uint32_t* nmr, const uint8_t* tab, uint32_t rl)
+{
+    // 16-byte chunks, a lane each (dword loads, funnel-shifted: any start byte);
+    // a chunk may read up to 19 bytes past the read, as k_emit_sq16 does
+    for (int c = (int)rl; 16 * c < len; c += AR) {
+        uint32_t w[4];
+        load16(rd + 16 * c, w);
+        *reinterpret_cast<uint4*>(sb + 16 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nw = (len + 15) >> 4;
+    int nn = 0;
+    for (int wd = (int)rl; wd < nw; wd += AR) {
+        uint32_t v = 0, m = 0, vr = 0, mr = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int i = 16 * wd + j;
+            uint32_t c = 0, cr = 0;
+            if (i < len) {
+                c = tab[sb[i]];
+                cr = tab[comp_base(sb[len - 1 - i])];   // rev@0x40d9a0 then the code
+                if (c > 3) m |= 1u << j;
+                if (cr > 3) mr |= 1u << j;
+            }
+            v = (v << 2) | (c & 3u);
+            vr = (vr << 2) | (cr & 3u);
+        }
+        pk[wd] = v;
+        nm[wd] = m;
+        pkr[wd] = vr;
+        nmr[wd] = mr;
+        nn += __popc(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return (int)row_sum<AR>((uint32_t)nn);
+}
+
+__device__ __forceinline__ bool find_seed_row(const HashView& ix, const RowStrand& h, int from, int to,
+                                              uint32_t maxcnt, bool stop_first, int& out, uint32_t rl)
+{
+    uint64_t key = ~0ull;
+    // every lane's seeds first (loads in flight together), then the reduction
+    for (int k0 = from; k0 <= to; k0 += 2 * AR * 4) {
+        uint32_t c[4];
+        int at[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            at[u] = k0 + 2 * ((int)rl + AR * u);
+            c[u] = at[u] <= to ? ix.num[seed_at_row(h, at[u], ix.K)] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (c[u] && c[u] < maxcnt && c[u] < 100000u) {
+                const uint64_t kk = stop_first ? (uint64_t)(uint32_t)at[u] : ((uint64_t)c[u] << 32 | (uint32_t)at[u]);
+                key = kk < key ? kk : key;
+            }
+    }
+    key = row_min64(key);
+    if (key == ~0ull) return false;
+    out = (int)(uint32_t)key;
+    return true;
+}
+
+// gaplessHashAlignPositions@0x410990 for the row.  The serial word loop stops
+// once its running count passes maxmis; its verdict depends on the count only
+// through "count > maxmis" (then: fail, whether partial or full) or, within
+// maxmis, the full count -- so the full count (a row sum) decides identically.
+// The base-wise pass: the mismatches are the 2-bit groups that differ plus the
+// N / IUPAC bases; it fails (maxmis + 1) past the genome end or past maxmis
+// mismatches; a passing candidate lists its mismatches in order.
+__device__ void align_at_row(uint64_t pos, const RowStrand& h, const HashView& ix, const HashArgs& a,
+                             HashAlign& ai, int* mp, int* mt, int& best, uint32_t rl)
+{
+    const uint64_t p0 = pos - 1;
+    const uint32_t off = (uint32_t)(p0 & 15);
+    const int len = h.len, lw = (len - 1) >> 4, nfull = len >> 4;
+    ai.fresh = true;
+    uint32_t xw[AR_MAXW / AR], rw[AR_MAXW / AR];
+    int mis = 0;
+#pragma unroll
+    for (int k = 0; k < AR_MAXW / AR; k++) {
+        const int j = (int)rl + AR * k;
+        xw[k] = rw[k] = 0;
+        if (j <= lw) {
+            const uint64_t w = (p0 >> 4) + (uint64_t)j;
+            uint32_t ref = ix.seq[w];
+            if (off) {
+                const uint32_t nxt = ix.seq[w + 1];
+                ref = (uint32_t)(((nxt >> (32 - 2 * off)) & mask2(off)) | (((uint64_t)ref << (2 * off)) & ~mask2(off)));
+            }
+            uint64_t x = ref ^ h.pk[j];
+            if (j >= nfull) x &= ~mask2(16 - (len & 15));
+            mis += (int)mis2_d((uint32_t)x);
+            xw[k] = (uint32_t)x;
+            rw[k] = ref;
+        }
+    }
+    mis = (int)row_sum<AR>((uint32_t)mis);
+    int limit;
+    if (best > mis) limit = best;
+    else if (a.maxmis >= mis) limit = a.maxmis + 1;
+    else {
+        ai.nmis = -1;
+        return;
+    }
+    int n;
+    if (p0 >= ix.glen || (len >= 2 && p0 + (uint64_t)len - 1 >= ix.glen)) {
+        n = a.maxmis + 1;
+    } else {
+        uint32_t mm[AR_MAXW / AR], cnt = 0;
+#pragma unroll
+        for (int k = 0; k < AR_MAXW / AR; k++) {
+            const int j = (int)rl + AR * k;
+            mm[k] = 0;
+            if (j <= lw) {
+                const uint32_t y = (xw[k] | (xw[k] >> 1)) & 0x55555555u;   // a bit per differing 2-bit group
+                uint32_t g = 0;   // bit jj = base 16 j + jj (group 15 - jj)
+#pragma unroll
+                for (int jj = 0; jj < 16; jj++) g |= ((y >> (30 - 2 * jj)) & 1u) << jj;
+                g |= h.nm[j];
+                const int nb = len - 16 * j;
+                if (nb < 16) g &= (1u << nb) - 1u;
+                mm[k] = g;
+                cnt += (uint32_t)__popc(g);
+            }
+        }
+        const int total = (int)row_sum<AR>(cnt);
+        n = total > a.maxmis ? a.maxmis + 1 : total;
+        if (n < limit) {   // the candidate passes: its mismatch list, in order
+            uint32_t before = 0;
+#pragma unroll
+            for (int k = 0; k < AR_MAXW / AR; k++) {
+                const int j = (int)rl + AR * k;
+                if (AR * k > lw) break;   // (row-uniform)
+                const uint32_t c = (uint32_t)__popc(mm[k]);
+                uint32_t idx = before + row_excl_scan(c, rl);
+                for (uint32_t g = mm[k]; g; g &= g - 1) {
+                    const int jj = __builtin_ctz(g);
+                    if ((int)idx < n) {
+                        const uint32_t rb = (rw[k] >> (30 - 2 * jj)) & 3u;
+                        const bool isn = (h.nm[j] >> jj) & 1u;
+                        const uint32_t code = (h.pk[j] >> (30 - 2 * jj)) & 3u;
+                        mp[idx] = 16 * j + jj;
+                        mt[idx] = isn ? 3 : (int)mistype_d(code, rb);
+                    }
+                    idx++;
+                }
+                before += row_sum<AR>(c);
+            }
+        }
+    }
+    if (limit <= n) {
+        ai.nmis = -1;
+        return;
+    }
+    ai.pos = pos;
+    ai.rev = h.rc ? 1 : 0;
+    ai.nmis = n;
+    if (n < best) best = n;
+}
+
+__device__ void try_seed_row(int so, const RowStrand& h, const HashView& ix, const HashArgs& a, uint32_t kmer,
+                             HashAlign& ai, int* mp, int* mt, uint32_t& cnt, int& best, int thr, uint32_t rl)
+{
+    const uint32_t n = ix.num[kmer], base = ix.ind[kmer];
+    for (uint32_t j0 = 0; j0 < n; j0 += AR) {
+        const uint32_t mine = j0 + rl < n ? ix.pos[base + j0 + rl] : 0u;   // the next 16 candidates at once
+        const uint32_t m = n - j0 < (uint32_t)AR ? n - j0 : (uint32_t)AR;
+        for (uint32_t jj = 0; jj < m; jj++) {
+            const uint64_t p = __shfl(mine, (int)jj, AR);
+            if (p <= (uint64_t)(int64_t)so) continue;
+            if (p >= (uint64_t)(int64_t)so + ix.glen - (uint64_t)(int64_t)h.len) continue;
+            cnt++;
+            align_at_row(p - (uint64_t)(int64_t)so, h, ix, a, ai, mp, mt, best, rl);
+            if (thr >= best) return;
+            if (ai.nmis >= 0 && ai.nmis <= a.maxmis) return;
+            if (cnt > 300) return;
+        }
+    }
+}
+
+__device__ void aligner_row(const RowStrand& h, const HashView& ix, const HashArgs& a, int* sidx, HashAlign& ai,
+                            int* mp, int* mt, uint32_t& cnt, int& best, int thr, uint32_t rl)
+{
+    for (int par = 0; par < 2; par++) {
+        if (find_seed_row(ix, h, par, h.len - (int)ix.K, 100000u, false, sidx[par], rl))
+            try_seed_row(sidx[par], h, ix, a, seed_at_row(h, sidx[par], ix.K), ai, mp, mt, cnt, best, thr, rl);
+        if (hash_done(ai, a, cnt, best, thr)) return;
+    }
+}
+
+__device__ void aligner_parts_row(const RowStrand& h, const HashView& ix, const HashArgs& a, int* sidx, HashAlign& ai,
+                                  int* mp, int* mt, uint32_t& cnt, int& best, int thr, uint32_t rl)
+{
+    const int len = h.len, K = (int)ix.K;
+    const int np = len > 75 ? 4 : len >= 45 ? 3 : 2;
+    const int ovl = len > np * K ? len / np - K : 0;
+    bool found = false;
+    int b = 0;
+    for (int p = 0; p < np; p++) {
+        const int e = (len + b) / np, s = b / np;
+        b += len;
+        for (int par = 0; par < 2; par++) {
+            found = find_seed_row(ix, h, s + par, e - K, 620u, false, sidx[par + 2], rl);
+            if (found && sidx[par + 2] != sidx[par]) {
+                try_seed_row(sidx[par + 2], h, ix, a, seed_at_row(h, sidx[par + 2], ix.K), ai, mp, mt, cnt, best, thr,
+                             rl);
+                if (hash_done(ai, a, cnt, best, thr)) return;
+            }
+        }
+    }
+    if (found) return;
+    b = 0;
+    for (int p = 0; p < np; p++) {
+        const int e8 = (len + b) / np - 8, s = b / np + ovl;
+        b += len;
+        for (int par = 0; par < 2; par++) {
+            const int to = e8 < len - K ? e8 : len - K;
+            if (find_seed_row(ix, h, s + par, to, 620u, true, sidx[par + 2], rl) && sidx[par + 2] != sidx[par]) {
+                try_seed_row(sidx[par + 2], h, ix, a, seed_at_row(h, sidx[par + 2], ix.K), ai, mp, mt, cnt, best, thr,
+                             rl);
+                if (hash_done(ai, a, cnt, best, thr)) return;
+            }
+        }
+    }
+}
+
+// getHashAlignInfo@0x4113c0 for one read on a row (len <= 16 AR_MAXW); the
+// results on every lane.  Returns ret (mismatches, -1 unaligned); nn: the N /
+// IUPAC count.
+__device__ int align_read_row(const uint8_t* rd, int len, const HashView& ix, const HashArgs& a, int stale,
+                              HashAlign& ai, int* mp, int* mt, int& nn, uint8_t* sb, uint32_t* lw4, const uint8_t* tab,
+                              uint32_t rl)
+{
+    ai = HashAlign{stale ? 0 : -1, 0, 0, false, false};
+    int sidx[4] = {-1, -1, -1, -1};
+    int best = -1, r = -1;
+    uint32_t cnt = 0;
+    nn = 0;
+    const int thr = a.good < a.maxmis ? a.good : a.maxmis;
+    if (len <= 0) return -1;
+    nn = row_stage_pack(rd, len, sb, lw4, lw4 + AR_MAXW, lw4 + 2 * AR_MAXW, lw4 + 3 * AR_MAXW, tab, rl);
+    if (nn <= a.maxmis) {
+        const RowStrand fw{lw4, lw4 + AR_MAXW, len, false};
+        const RowStrand rc{lw4 + 2 * AR_MAXW, lw4 + 3 * AR_MAXW, len, true};
+        best = a.maxmis + 1;
+        aligner_row(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr, rl);
+        if (!(a.maxmis >= best) && cnt <= 299) {
+            aligner_row(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr, rl);
+            if (!(a.maxmis >= best) && cnt <= 299) {
+                aligner_parts_row(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr, rl);
+                if (!(a.maxmis >= best) && cnt <= 299) aligner_parts_row(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr, rl);
+            }
+        }
+        if (best <= a.maxmis) r = best;
+    }
+    return r;
+}
+
+// the serial path for one read (the row's first lane): reads longer than the
+// rows' LDS staging
+__device__ int align_read_serial(const uint8_t* rd, int len, const HashView& ix, const HashArgs& a, int stale,
+                                 HashAlign& ai, int* mp, int* mt, int& nn, uint32_t* scr)
+{
+    const HashRead fw{rd, len, false, scr};
+    const HashRead rc{rd, len, true, scr + ((len - 1) >> 4) + 1};
+    ai = HashAlign{stale ? 0 : -1, 0, 0, false, false};
     int sidx[4] = {-1, -1, -1, -1};
     int best = -1, r = -1;
     uint32_t cnt = 0;
     const int thr = a.good < a.maxmis ? a.good : a.maxmis;
-    if (len > 0 && hash_pack_read(fw) <= a.maxmis) {
+    nn = 0;
+    if (len > 0 && (nn = hash_pack_read(fw)) <= a.maxmis) {
         best = a.maxmis + 1;
         aligner_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
         if (!(a.maxmis >= best) && cnt <= 299) {
@@ -437,15 +757,74 @@ __global__ __launch_bounds__(256) void k_hash_align(const HashView ix, const Has
         }
         if (best <= a.maxmis) r = best;
     }
-    ret[i] = r;
-    rev[i] = r >= 0 ? ai.rev : 0;
-    pos[i] = r >= 0 ? ai.pos : 0;
-    if (consulted) consulted[i] = ai.consulted ? 1 : 0;
-    for (int k = 0; k < stride; k++)
-        if (r < 0 || k >= ai.nmis) {
-            mp[k] = -1;
-            mt[k] = -1;
+    return r;
+}
+
+// per workgroup: the base-code table (seq_val_table@0x44b800 / hash_code) and
+// each row's staging
+struct AlignRowsLds {
+    alignas(16) uint8_t bytes[AR_ROWS][AR_BYTES];
+    uint32_t words[AR_ROWS][4 * AR_MAXW];
+    uint8_t tab[256];
+};
+
+__device__ __forceinline__ void align_rows_init(AlignRowsLds& L)
+{
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) L.tab[c] = (uint8_t)hash_code((uint8_t)c);
+    __syncthreads();
+}
+
+// getHashAlignInfo@0x4113c0 over reads given by offset / length (sa_hash_align),
+// with the carried align_info state taken as `stale` (0: not aligned, 1:
+// aligned).  Outputs per read: ret (mismatches, -1 unaligned), strand, 1-based
+// position, maxmis + 1 slots of mismatch offsets / types (-1 past the read's
+// mismatches) and whether the carried state was consulted (the host then
+// re-runs those reads with the other state and picks per read in order).
+// `sel`: the reads to do (NULL: all n), outputs at the read's index.  A row
+// per read, grid-stride.
+__global__ __launch_bounds__(256) void k_hash_align(const HashView ix, const HashArgs a, const uint8_t* __restrict__ seq,
+                                                    const uint64_t* __restrict__ off, const int32_t* __restrict__ lens,
+                                                    const uint64_t* __restrict__ woff, uint32_t* __restrict__ scratch,
+                                                    const uint32_t* __restrict__ sel, uint64_t n, int stale,
+                                                    int32_t* __restrict__ ret, uint8_t* __restrict__ rev,
+                                                    uint64_t* __restrict__ pos, int32_t* __restrict__ mispos,
+                                                    int32_t* __restrict__ mistype, uint8_t* __restrict__ consulted)
+{
+    __shared__ AlignRowsLds L;
+    align_rows_init(L);
+    const uint32_t rl = threadIdx.x % AR, row = threadIdx.x / AR;
+    for (uint64_t t = (uint64_t)blockIdx.x * AR_ROWS + row; t < n; t += (uint64_t)gridDim.x * AR_ROWS) {
+        const uint64_t i = sel ? sel[t] : t;
+        const int len = lens[i];
+        const int stride = a.maxmis + 1;
+        int* mp = mispos + i * stride;
+        int* mt = mistype + i * stride;
+        HashAlign ai{-1, 0, 0, false, false};
+        int nn = 0, r = -1;
+        if (len <= 16 * AR_MAXW) {
+            r = align_read_row(seq + off[i], len, ix, a, stale, ai, mp, mt, nn, L.bytes[row], L.words[row], L.tab, rl);
+        } else {
+            if (rl == 0) r = align_read_serial(seq + off[i], len, ix, a, stale, ai, mp, mt, nn, scratch + 2 * woff[i]);
+            __builtin_amdgcn_wave_barrier();
+            r = __shfl(rl == 0 ? r : 0, 0, AR);
+            ai.nmis = __shfl(rl == 0 ? ai.nmis : 0, 0, AR);
+            const uint32_t bits = __shfl(rl == 0 ? (uint32_t)ai.rev | (ai.consulted ? 2u : 0u) : 0u, 0, AR);
+            ai.rev = (uint8_t)(bits & 1u);
+            ai.consulted = (bits & 2u) != 0;
+            ai.pos = __shfl(rl == 0 ? ai.pos : 0ull, 0, AR);
         }
+        if (rl == 0) {
+            ret[i] = r;
+            rev[i] = r >= 0 ? ai.rev : 0;
+            pos[i] = r >= 0 ? ai.pos : 0;
+            if (consulted) consulted[i] = ai.consulted ? 1 : 0;
+        }
+        for (int k = (int)rl; k < stride; k += AR)
+            if (r < 0 || k >= ai.nmis) {
+                mp[k] = -1;
+                mt[k] = -1;
+            }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -472,43 +851,55 @@ __global__ __launch_bounds__(256) void k_hash_align_batch(const HashView ix, con
                                                           int32_t* __restrict__ mispos, int32_t* __restrict__ mistype,
                                                           uint8_t* __restrict__ status)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint32_t i = sel ? sel[t] : t;
-    const DevBlock& blk = bv.blocks[bv.read_block[i]];
-    const uint8_t* rd = bv.seq + blk.seq_base + bv.seq_off[i];
-    const int len = (int)bv.seq_len[i];
-    const int stride = a.maxmis + 1;
-    int* mp = mispos + (size_t)i * stride;
-    int* mt = mistype + (size_t)i * stride;
-    uint32_t* scr = scratch + align_scratch_word(bv, i);
-    HashRead fw{rd, len, false, scr};
-    HashRead rc{rd, len, true, scr + ((len - 1) >> 4) + 1};
-    HashAlign ai{stale ? 0 : -1, 0, 0, false, false};
-    int sidx[4] = {-1, -1, -1, -1};
-    int best = -1, r = -1, nn = 0;
-    uint32_t cnt = 0;
-    const int thr = a.good < a.maxmis ? a.good : a.maxmis;
-    if (len > 0 && (nn = hash_pack_read(fw)) <= a.maxmis) {
-        best = a.maxmis + 1;
-        aligner_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
-        if (!(a.maxmis >= best) && cnt <= 299) {
-            hash_pack_read(rc);
-            aligner_d(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr);
-            if (!(a.maxmis >= best) && cnt <= 299) {
-                aligner_parts_d(fw, ix, a, sidx, ai, mp, mt, cnt, best, thr);
-                if (!(a.maxmis >= best) && cnt <= 299) aligner_parts_d(rc, ix, a, sidx, ai, mp, mt, cnt, best, thr);
-            }
+    __shared__ AlignRowsLds L;
+    align_rows_init(L);
+    const uint32_t rl = threadIdx.x % AR, row = threadIdx.x / AR;
+    for (uint32_t t = blockIdx.x * AR_ROWS + row; t < n; t += gridDim.x * AR_ROWS) {
+        const uint32_t i = sel ? sel[t] : t;
+        const DevBlock& blk = bv.blocks[bv.read_block[i]];
+        const uint8_t* rd = bv.seq + blk.seq_base + bv.seq_off[i];
+        const int len = (int)bv.seq_len[i];
+        const int stride = a.maxmis + 1;
+        int* mp = mispos + (size_t)i * stride;
+        int* mt = mistype + (size_t)i * stride;
+        HashAlign ai{-1, 0, 0, false, false};
+        int nn = 0, r = -1;
+        if (len <= 16 * AR_MAXW) {
+            r = align_read_row(rd, len, ix, a, stale, ai, mp, mt, nn, L.bytes[row], L.words[row], L.tab, rl);
+        } else {   // (long reads: the serial path on the row's first lane)
+            if (rl == 0) r = align_read_serial(rd, len, ix, a, stale, ai, mp, mt, nn, scratch + align_scratch_word(bv, i));
+            __builtin_amdgcn_wave_barrier();
+            r = __shfl(rl == 0 ? r : 0, 0, AR);
+            nn = __shfl(rl == 0 ? nn : 0, 0, AR);
+            ai.nmis = __shfl(rl == 0 ? ai.nmis : 0, 0, AR);
+            const uint32_t bits = __shfl(rl == 0 ? (uint32_t)ai.rev | (ai.consulted ? 2u : 0u) : 0u, 0, AR);
+            ai.rev = (uint8_t)(bits & 1u);
+            ai.consulted = (bits & 2u) != 0;
+            ai.pos = __shfl(rl == 0 ? ai.pos : 0ull, 0, AR);
         }
-        if (best <= a.maxmis) r = best;
+        if (rl == 0) {
+            ret[i] = r;
+            rev[i] = r >= 0 ? ai.rev : 0;
+            pos[i] = r >= 0 ? (uint32_t)ai.pos : 0u;
+            if (!stale)
+                status[i] = (uint8_t)((r >= 0 ? AL_OK0 : 0) | (ai.consulted ? AL_CONS : 0) |
+                                      (se && nn > a.maxmis ? AL_NSKIP : 0));
+            else if (r >= 0)
+                status[i] |= AL_OK1;
+        }
+        for (int k = (int)rl; k < stride; k += AR)
+            if (r < 0 || k >= ai.nmis) {
+                mp[k] = -1;
+                mt[k] = -1;
+            }
     }
-    ret[i] = r;
-    rev[i] = r >= 0 ? ai.rev : 0;
-    pos[i] = r >= 0 ? (uint32_t)ai.pos : 0u;
-    if (!stale)
-        status[i] = (uint8_t)((r >= 0 ? AL_OK0 : 0) | (ai.consulted ? AL_CONS : 0) | (se && nn > a.maxmis ? AL_NSKIP : 0));
-    else if (r >= 0)
-        status[i] |= AL_OK1;
+}
+
+// workgroups of the row kernels: a row per read, grid-stride beyond 8192 workgroups
+inline uint32_t align_rows_grid(uint64_t reads)
+{
+    const uint64_t g = (reads + AR_ROWS - 1) / AR_ROWS;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, 8192));
 }
 
 // the reads whose carried state was "aligned": variant 1 over variant 0
@@ -784,7 +1175,7 @@ int sa_hash_align(sa_ctx* c, const sa_hash_index* ix, const char* seq, const uin
     }
     const uint64_t N = (uint64_t)n, stride = (uint64_t)maxmis + 1;
     DTmp d_seq, d_off, d_len, d_woff, d_scr, d_sel, d_ret[2], d_rev[2], d_pos[2], d_mp[2], d_mt[2], d_con;
-    SA_CHECK(c, d_seq.ensure(bytes + 16));
+    SA_CHECK(c, d_seq.ensure(bytes + 64));   // (the rows' 16-byte loads read up to 19 bytes past a read)
     SA_CHECK(c, d_off.ensure(8 * N));
     SA_CHECK(c, d_len.ensure(4 * N));
     SA_CHECK(c, d_woff.ensure(8 * N));
@@ -806,21 +1197,30 @@ int sa_hash_align(sa_ctx* c, const sa_hash_index* ix, const char* seq, const uin
     const HashArgs a{maxmis, good};
     // every read with the carried state "not aligned"; then the reads that
     // consulted it again with "aligned"; then the choice, read by read, in order
-    hipLaunchKernelGGL(k_hash_align, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, st, v, a, d_seq.as<uint8_t>(),
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    SA_CHECK(c, hipEventCreate(&e0));
+    SA_CHECK(c, hipEventCreate(&e1));
+    SA_CHECK(c, hipEventRecord(e0, st));
+    hipLaunchKernelGGL(k_hash_align, dim3(align_rows_grid(N)), dim3(256), 0, st, v, a, d_seq.as<uint8_t>(),
                        d_off.as<uint64_t>(), d_len.as<int32_t>(), d_woff.as<uint64_t>(), d_scr.as<uint32_t>(),
                        nullptr, N, 0, d_ret[0].as<int32_t>(), d_rev[0].as<uint8_t>(), d_pos[0].as<uint64_t>(),
                        d_mp[0].as<int32_t>(), d_mt[0].as<int32_t>(), d_con.as<uint8_t>());
     SA_CHECK(c, hipGetLastError());
+    SA_CHECK(c, hipEventRecord(e1, st));
     std::vector<uint8_t> con(N);
     SA_CHECK(c, hipMemcpyAsync(con.data(), d_con.p, N, hipMemcpyDeviceToHost, st));
     SA_CHECK(c, hipStreamSynchronize(st));
+    c->align_kernel_ms = 0.f;
+    (void)hipEventElapsedTime(&c->align_kernel_ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     std::vector<uint32_t> sel;
     for (uint64_t i = 0; i < N; i++)
         if (con[i]) sel.push_back((uint32_t)i);
     if (!sel.empty()) {
         SA_CHECK(c, d_sel.ensure(4 * sel.size()));
         SA_CHECK(c, hipMemcpyAsync(d_sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_hash_align, dim3((uint32_t)((sel.size() + 255) / 256)), dim3(256), 0, st, v, a,
+        hipLaunchKernelGGL(k_hash_align, dim3(align_rows_grid(sel.size())), dim3(256), 0, st, v, a,
                            d_seq.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<int32_t>(), d_woff.as<uint64_t>(),
                            d_scr.as<uint32_t>(), d_sel.as<uint32_t>(), (uint64_t)sel.size(), 1,
                            d_ret[1].as<int32_t>(), d_rev[1].as<uint8_t>(), d_pos[1].as<uint64_t>(),
@@ -959,7 +1359,7 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
     if (!rerun) {
         // ---- every read with the carried state "not aligned" ----
         if (nr)
-            hipLaunchKernelGGL(k_hash_align_batch, dim3((nr + 255) / 256), dim3(256), 0, st, hv, ha, bv,
+            hipLaunchKernelGGL(k_hash_align_batch, dim3(align_rows_grid(nr)), dim3(256), 0, st, hv, ha, bv,
                                c->d_al_scr.as<uint32_t>(), nullptr, nr, 0, a.paired ? 0 : 1, c->d_al_ret[0].as<int32_t>(),
                                c->d_al_rev[0].as<uint8_t>(), c->d_al_pos[0].as<uint32_t>(), c->d_al_mp[0].as<int32_t>(),
                                c->d_al_mt[0].as<int32_t>(), c->d_al_st.as<uint8_t>());
@@ -977,7 +1377,7 @@ int align_front(sa_ctx* c, const sa_input* I, BatchView& bv, const AlignReq& rq,
         if (!cons.empty()) {
             SA_CHECK(c, c->d_al_sel.ensure(4 * cons.size()));
             SA_CHECK(c, h2d(c, c->d_al_sel.p, cons.data(), 4 * cons.size(), st));
-            hipLaunchKernelGGL(k_hash_align_batch, dim3((uint32_t)((cons.size() + 255) / 256)), dim3(256), 0, st, hv, ha, bv,
+            hipLaunchKernelGGL(k_hash_align_batch, dim3(align_rows_grid(cons.size())), dim3(256), 0, st, hv, ha, bv,
                                c->d_al_scr.as<uint32_t>(), c->d_al_sel.as<uint32_t>(), (uint32_t)cons.size(), 1,
                                a.paired ? 0 : 1, c->d_al_ret[1].as<int32_t>(), c->d_al_rev[1].as<uint8_t>(),
                                c->d_al_pos[1].as<uint32_t>(), c->d_al_mp[1].as<int32_t>(), c->d_al_mt[1].as<int32_t>(),
@@ -1078,6 +1478,8 @@ sa_align_chain* sa_align_chain_create(int32_t nmis_mate1, int32_t nmis_mate2)
 void sa_align_chain_destroy(sa_align_chain* ch) { delete ch; }
 
 void sa_align_chain_fail(sa_align_chain* ch) { align_chain_fail(ch); }
+
+float sa_hash_align_kernel_ms(const sa_ctx* c) { return c ? c->align_kernel_ms : 0.f; }
 
 int sa_run_input_aligned(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, const sa_align_cfg* acfg,
                          sa_align_chain* chain, uint64_t batch)

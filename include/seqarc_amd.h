@@ -323,6 +323,9 @@ int sa_run_aligned(sa_ctx *ctx, const sa_cfg *cfg, const sa_align_cfg *acfg, sa_
 /* one-shot form of the above (sub-batches in order through the chain) */
 int sa_encode_blocks_aligned(sa_ctx *ctx, const sa_block *in, int n, const sa_cfg *cfg, const sa_align_cfg *acfg,
                              sa_align_chain *chain, sa_out *out);
+/* device time (ms, HIP events) of sa_hash_align's aligner kernel over all the
+ * reads of the last call (the first pass: the carried state "not aligned") */
+float sa_hash_align_kernel_ms(const sa_ctx *ctx);
 /* the ".hash" file back onto ctx's device (HashRefIndex32::readIndexFile) */
 sa_hash_index *sa_hash_load(sa_ctx *ctx, const uint8_t *file, uint64_t bytes);
 /* the genome's packed bases (16 a word, 2 bits, first base in the top bits,
