@@ -238,6 +238,11 @@ struct sa_ctx {
     hipEvent_t ev_beg[PH_N] = {}, ev_end[PH_N] = {};
     float ph_ms[PH_N];
     float align_kernel_ms = 0.f;   // sa_hash_align: the aligner kernel of the last call (variant 0)
+    // SA_RV_PROBE=file: per pass-R wave its timing and placement, appended to
+    // the file per batch (diagnostics, k_coder_rv)
+    const char* rv_probe = std::getenv("SA_RV_PROBE");
+    DBuf d_probe;
+    uint32_t probe_waves = 0;
 
     // the batch sa_stage uploads (sa_run encodes it); blocks = the working copy
     // of the batch being encoded (its symbol spaces filled by plan_batch)
@@ -281,7 +286,7 @@ struct sa_ctx {
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
-                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq};
+                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe};
     }
     uint64_t held_bytes()
     {
@@ -583,10 +588,41 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
         waves = nlong + c->rv_short_waves;
     }
     if (ph >= 0) ev_begin(c, ph, st);
-    hipLaunchKernelGGL(k_coder_rv, dim3((waves + c->coder_waves - 1) / c->coder_waves), dim3(64 * c->coder_waves),
+    const uint32_t grid = (waves + c->coder_waves - 1) / c->coder_waves;
+    uint64_t* probe = nullptr;
+    if (c->rv_probe && ph >= 0 && c->d_probe.ensure(32ull * grid * c->coder_waves) == hipSuccess) {
+        probe = c->d_probe.as<uint64_t>();
+        c->probe_waves = grid * c->coder_waves;
+        (void)hipMemsetAsync(probe, 0, 32ull * c->probe_waves, st);
+    }
+    hipLaunchKernelGGL(k_coder_rv, dim3(grid), dim3(64 * c->coder_waves),
                        c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
-                       c->chain_prio);
+                       c->chain_prio, probe);
     if (ph >= 0) ev_finish(c, ph, st);
+}
+
+// SA_RV_PROBE: one line per pass-R wave of this batch: context, batch, wave,
+// start / end (us on the 100 MHz clock, absolute), shader MHz over the wave,
+// XCC, SE, CU, SIMD, wave slot, chains
+void write_rv_probe(sa_ctx* c, const std::vector<uint64_t>& p)
+{
+    static std::mutex mu;
+    static uint64_t batch = 0;
+    std::lock_guard<std::mutex> g(mu);
+    FILE* f = std::fopen(c->rv_probe, "a");
+    if (!f) return;
+    const uint64_t b = batch++;
+    for (size_t w = 0; w + 3 < p.size(); w += 4) {
+        const uint64_t t0 = p[w], t1 = p[w + 1], cyc = p[w + 2], id = p[w + 3];
+        if (!t1) continue;
+        const uint32_t hw = (uint32_t)id;
+        const double us = (double)(t1 - t0) / 100.0;
+        std::fprintf(f, "%p %llu %zu %.1f %.1f %.0f xcc %u se %u cu %u simd %u slot %u chains %u\n", (void*)c,
+                     (unsigned long long)b, w / 4, (double)t0 / 100.0, (double)t1 / 100.0,
+                     us > 0 ? (double)cyc / us : 0.0, (unsigned)((id >> 32) & 0xff), (hw >> 13) & 7u,
+                     (hw >> 8) & 15u, (hw >> 4) & 3u, hw & 15u, (unsigned)(id >> 40));
+    }
+    std::fclose(f);
 }
 
 void coder_launch_l12(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderView& cv)
@@ -646,7 +682,13 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
                            c->d_task_ends.as<uint32_t>());
         std::vector<uint32_t> ends(tasks.size());
         SA_CHECK(c, d2h(c, ends.data(), c->d_task_ends.p, 4 * tasks.size(), st));
+        std::vector<uint64_t> probe;
+        if (c->rv_probe && c->probe_waves) {
+            probe.resize(4ull * c->probe_waves);
+            SA_CHECK(c, d2h(c, probe.data(), c->d_probe.p, 32ull * c->probe_waves, st));
+        }
         SA_CHECK(c, sync_d2h(c, st));
+        if (!probe.empty()) write_rv_probe(c, probe);
         uint64_t payload = 0, slack = 4096;
         if (const char* e = std::getenv("SA_PAYLOAD_SLACK")) slack = std::strtoull(e, nullptr, 10);   // (tests)
         for (size_t t = 0; t < tasks.size(); t++) {

@@ -2448,20 +2448,44 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
 // instead of one per four chains: with three or four batches' pass R in flight
 // the excess waited for slots, and a launch that cannot place all its
 // workgroups holds up the kernels queued behind it on its hardware queue.
+// probe (SA_RV_PROBE, diagnostics): per wave its start / end on the constant
+// 100 MHz clock (s_memrealtime), the shader-clock cycles between them
+// (s_memtime), and where it ran (HW_ID: wave slot, SIMD, CU, SE; XCC_ID) with
+// the number of chains it coded
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
-    const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio)
+    const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio,
+    uint64_t* __restrict__ probe)
 {
     const uint32_t wpg = blockDim.x >> 6;
     const uint32_t wi = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t nl = tl.nlong < tl.count ? tl.nlong : tl.count;
+    uint64_t t0 = 0, c0 = 0;
+    if (probe) {
+        t0 = __builtin_amdgcn_s_memrealtime();
+        c0 = __builtin_amdgcn_s_memtime();
+    }
     // (one call site: two inlined copies of the chain's asm made the compiler
     // move its scalar operands through VGPRs)
     const uint32_t step = wi < nl ? 0u : gridDim.x * wpg - nl;
+    uint32_t chains = 0;
     for (uint32_t li = wi; li < tl.count;) {
         coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+        chains++;
         if (!step) break;
         li += step;
+    }
+    if (probe) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if ((threadIdx.x & 63) == 0) {
+            probe[4 * wi + 0] = t0;
+            probe[4 * wi + 1] = t1;
+            probe[4 * wi + 2] = c1 - c0;
+            probe[4 * wi + 3] = hw | (uint64_t)(xcc & 0xffu) << 32 | (uint64_t)chains << 40;
+        }
     }
 }
 

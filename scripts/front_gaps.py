@@ -22,7 +22,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 ks = sorted(({"n": name(r), "s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"])} for r in rows),
             key=lambda k: k["s"])
 fr = [k for k in ks if k["n"].startswith(FRONT)]
-preps = [i for i, k in enumerate(fr) if k["n"].startswith("k_prep")]
+preps = [i for i, k in enumerate(fr) if k["n"] in ("k_prep", "k_prep_sq16") and (i == 0 or not fr[i - 1]["n"].startswith("k_prep"))]
 if len(preps) < 4:
     sys.exit("too few fronts in the trace")
 # fronts: from one k_prep to the kernel before the next k_prep (fronts run one at a time)

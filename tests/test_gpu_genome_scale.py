@@ -65,8 +65,8 @@ def test_hash_path_beyond_2_31():
         oa = orc.hash_align(sample)
         for name, x, y in zip(("ret", "rev", "pos", "mispos", "mistype"), ga, oa):
             assert np.array_equal(x, y), f"aligner {name} differs"
-        ok = ga[0] >= 0
-        assert ok.mean() > 0.8 and (ga[2][ok] > (1 << 31)).all()
+        ok = ga[0] >= 0   # (synth.aligned_reads: 0-10 substitutions, a fifth beyond maxmis 7, 2 % random)
+        assert ok.mean() > 0.7 and (ga[2][ok] > (1 << 31)).all()
 
         cfg = fq.Config()
         got_blk = enc.encode_aligned(blocks[:1], cfg, ix, True)
