@@ -115,7 +115,8 @@ def parse_args(argv=None):
     ap.add_argument("--ont-reads", type=int, default=60_000, help="reads of the ONT leg's batch (10-50 kbp)")
     ap.add_argument("--hash-leg", type=int, default=1, help="configs[3] leg: the HASH reference path (0: skip)")
     ap.add_argument("--hash-genome-mb", type=float, default=3100.0, help="synthetic genome of the HASH leg (GRCh38: 3100)")
-    ap.add_argument("--hash-pairs", type=int, default=1_200_000, help="PE pairs of the HASH leg's batch (16 blocks)")
+    ap.add_argument("--hash-pairs", type=int, default=5_000_000,
+                    help="PE pairs of the HASH leg's batch (5 M: 69 blocks, the headline's batch)")
     ap.add_argument("--hash-align-reads", type=int, default=4_000_000, help="single reads of the aligner leg")
     ap.add_argument("--leg-steps", type=int, default=10, help="timed steps of the ONT and HASH legs")
     ap.add_argument("--decode-check", type=int, default=1,
@@ -401,7 +402,7 @@ def hash_leg(args, local: int) -> dict:
     """configs[3]: the HASH reference path at GRCh38 size.  A synthetic genome
     of --hash-genome-mb Mb (3 records, N runs, one in lower case) indexed on the
     device (buildRefIndex@0x410190), single reads aligned
-    (getHashAlignInfo@0x4113c0), and a batch of 16 x 50 MiB PE blocks encoded
+    (getHashAlignInfo@0x4113c0), and a batch of --hash-pairs PE pairs (69 x 50 MiB blocks) encoded
     through the aligned path (doAlign + doAlignEncode@0x42d4c0) by the contexts'
     pipeline, each step with its own align_info chain.  Checked by decoding the
     first and last blocks with the host decoder against the genome: the reads
@@ -440,7 +441,7 @@ def hash_leg(args, local: int) -> dict:
         align_kernel_ms = ix.last_kernel_ms
         del raw, off, lens
         good = int(((ret >= 0) & (pos == starts + 1) & (rev == rv)).sum())
-        # the aligned encode of a 16-block PE batch
+        # the aligned encode of a PE batch (69 blocks by default)
         t1, t2 = synth.pe_reads_fast(g, args.hash_pairs, 78)
         del g
         blocks = fq.blocks_from_fastq(t1, t2)
