@@ -140,26 +140,19 @@ enum Err : uint32_t {
     E_CODER = 32u,       // cum + freq > tot (reference: abort())
 };
 
-// seq_val_table@0x44b800
+// seq_val_table@0x44b800: A/a C/c G/g T/t -> 0..3, the IUPAC letters M R Y K
+// S W H B V D (either case) -> 5..14, every other byte -> 4.  Branch-free (a
+// switch became a compare-and-branch tree per byte in the per-read kernels):
+// only bytes 0x40..0x7f can be letters; `(c | 0x20) - 0x60` indexes a table
+// of 32 nibbles held in two 64-bit constants.
 SA_HD uint32_t base_code(uint8_t c)
 {
-    switch (c | 0x20) {
-    case 'a': return 0;
-    case 'c': return 1;
-    case 'g': return 2;
-    case 't': return 3;
-    case 'm': return 5;
-    case 'r': return 6;
-    case 'y': return 7;
-    case 'k': return 8;
-    case 's': return 9;
-    case 'w': return 10;
-    case 'h': return 11;
-    case 'b': return 12;
-    case 'v': return 13;
-    case 'd': return 14;
-    default: return 4;
-    }
+    constexpr uint64_t LO = 0x4454844b244e1c04ull;   // nibbles of '`' a b c ... o
+    constexpr uint64_t HI = 0x44444474ad439644ull;   // p q r s ... z { | } ~ DEL
+    const uint32_t idx = ((uint32_t)c | 0x20u) - 0x60u;
+    const uint64_t v = (idx & 16u) ? HI : LO;
+    const uint32_t code = (uint32_t)(v >> (4u * (idx & 15u))) & 15u;
+    return ((uint32_t)c & 0xc0u) == 0x40u ? code : 4u;
 }
 // `c | 0x20` folds case but also maps some non-letters onto letters
 // (e.g. 'A'-0x20 = '!' stays '!'); only letters can reach the cases above

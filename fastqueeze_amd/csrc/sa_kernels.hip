@@ -881,8 +881,10 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
                                                    uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
                                                    uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val)
 {
-    __shared__ uint32_t stk[256 / ER][ER_STEP];
-    __shared__ uint32_t stv[SH ? 1 : 256 / ER][SH ? 1 : ER_STEP];
+    // (one slot past each row's ER_STEP: the stores of the branch-free loops
+    // below that carry no symbol land there)
+    __shared__ uint32_t stk[256 / ER][ER_STEP + 1];
+    __shared__ uint32_t stv[SH ? 1 : 256 / ER][SH ? 1 : ER_STEP + 1];
     const uint32_t rl = threadIdx.x & (ER - 1), rw = threadIdx.x / ER;
     const uint32_t rows = gridDim.x * (blockDim.x / ER);
     const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / ER;
@@ -932,14 +934,14 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
             if (cnt) load16(s + pos, sw);
             uint32_t P = 0, nv = 0, vmask = 0, codes = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 16; j++) {
+            for (uint32_t j = 0; j < 16; j++) {   // (branch-free: selects, no per-lane branches)
                 const uint32_t c = j < cnt ? base_code((uint8_t)byte_at(sw, j)) : 4u;
-                if (c <= 3) {
-                    P = (P << 2) | c;
-                    nv++;
-                    vmask |= 1u << j;
-                    codes |= c << (2 * j);
-                }
+                const bool ok = c <= 3;
+                const uint32_t cc = c & 3u;
+                P = ok ? (P << 2) | cc : P;
+                nv += ok ? 1u : 0u;
+                vmask |= (ok ? 1u : 0u) << j;
+                codes |= (ok ? cc : 0u) << (2 * j);
             }
             uint32_t ip = P, in = nv;   // inclusive row scan of (codes, count): concatenation
 #pragma unroll
@@ -955,19 +957,19 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
             uint32_t ctx = cat_codes(carry, ep, en);
             uint32_t k = en;
 #pragma unroll
-            for (uint32_t j = 0; j < 16; j++) {
-                if (vmask & (1u << j)) {
-                    const uint32_t c = (codes >> (2 * j)) & 3u;
-                    const uint32_t cm = ctx & mask;
-                    if constexpr (SH != 0) {
-                        sk[k] = (cm << 2) | c;
-                    } else {
-                        sk[k] = cm;
-                        sv[k] = ((dseq + k) << 2) | c;
-                    }
-                    ctx = (ctx << 2) | c;
-                    k++;
+            for (uint32_t j = 0; j < 16; j++) {   // (branch-free: a base that is not coded stores to the dummy slot)
+                const bool ok = (vmask >> j) & 1u;
+                const uint32_t c = (codes >> (2 * j)) & 3u;
+                const uint32_t cm = ctx & mask;
+                const uint32_t at = ok ? k : ER_STEP;
+                if constexpr (SH != 0) {
+                    sk[at] = (cm << 2) | c;
+                } else {
+                    sk[at] = cm;
+                    sv[at] = ((dseq + k) << 2) | c;
                 }
+                ctx = ok ? (ctx << 2) | c : ctx;
+                k += ok ? 1u : 0u;
             }
             const uint32_t tp = __shfl(ip, ER - 1, ER), tn = __shfl(in, ER - 1, ER);
             carry = cat_codes(carry, tp, tn);
@@ -988,8 +990,7 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
             if (cnt) load16(q + pos, qw);
             uint32_t last = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 16; j++)
-                if (j < cnt && byte_at(qw, j) != '#') last = pos + j + 1;
+            for (uint32_t j = 0; j < 16; j++) last = (j < cnt && byte_at(qw, j) != '#') ? pos + j + 1 : last;
             last = row_max<ER>(last);
             n = last > n ? last : n;
         }
@@ -1009,12 +1010,12 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
             {
                 uint32_t a1 = q1;
 #pragma unroll
-                for (uint32_t j = 0; j < 16; j++)
-                    if (j < cnt) {
-                        const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
-                        dsum += a1 > sym ? a1 - sym : 0u;
-                        a1 = sym;
-                    }
+                for (uint32_t j = 0; j < 16; j++) {   // (branch-free)
+                    const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
+                    const bool in = j < cnt;
+                    dsum += in && a1 > sym ? a1 - sym : 0u;
+                    a1 = in ? sym : a1;
+                }
             }
             uint32_t id = dsum;   // inclusive row scan of the drop sums
 #pragma unroll
@@ -1026,32 +1027,30 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
             uint32_t ctxs[16];
             uint32_t cl = 0;   // the context after the lane's last symbol
 #pragma unroll
-            for (uint32_t j = 0; j < 16; j++) {
-                if (j < cnt) {
-                    const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
-                    const uint32_t i = pos + j;
-                    delta += (int)(q1 > sym ? q1 - sym : 0u);
-                    uint32_t cx = (((q1 > q2 ? q1 : q2) << 6) + sym) & 0xfffu;
-                    if (ql > 1) {
-                        cx += q1 == q2 ? 0x1000u : 0u;
-                        cx += (uint32_t)(((delta <= 56 ? delta : 56) & 0xf8) << 10);
-                        if (ql > 2) cx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
-                    }
-                    ctxs[j] = cx;
-                    cl = cx;
-                    q2 = q1;
-                    q1 = sym;
+            for (uint32_t j = 0; j < 16; j++) {   // (branch-free: past cnt the state holds)
+                const bool in = j < cnt;
+                const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
+                const uint32_t i = pos + j;
+                delta += in ? (int)(q1 > sym ? q1 - sym : 0u) : 0;
+                uint32_t cx = (((q1 > q2 ? q1 : q2) << 6) + sym) & 0xfffu;
+                if (ql > 1) {
+                    cx += q1 == q2 ? 0x1000u : 0u;
+                    cx += (uint32_t)(((delta <= 56 ? delta : 56) & 0xf8) << 10);
+                    if (ql > 2) cx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
                 }
+                ctxs[j] = cx;
+                cl = in ? cx : cl;
+                q2 = in ? q1 : q2;
+                q1 = in ? sym : q1;
             }
             uint32_t prev = __shfl_up(cl, 1, ER);
             if (rl == 0) prev = ctx_c;
 #pragma unroll
-            for (uint32_t j = 0; j < 16; j++)
-                if (j < cnt) {
-                    const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
-                    sk[16 * rl + j] = ((M_QUAL + prev) << AUX_SYM_BITS) | sym;
-                    prev = ctxs[j];
-                }
+            for (uint32_t j = 0; j < 16; j++) {
+                const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
+                sk[j < cnt ? 16 * rl + j : ER_STEP] = ((M_QUAL + prev) << AUX_SYM_BITS) | sym;
+                prev = ctxs[j];
+            }
             // the step's last symbol: its lane carries the state on
             const uint32_t tot = n > i0 ? (n - i0 < ER_STEP ? n - i0 : ER_STEP) : 0u;
             const uint32_t src = tot ? (tot - 1) / 16 : 0u;
