@@ -124,6 +124,9 @@ def parse_args(argv=None):
     ap.add_argument("--ingest-devices", type=int, default=8,
                     help="the whole-node ingest leg: seqarc_amd --ingest-only --devices N over the long e2e files "
                          "(0: skip)")
+    ap.add_argument("--step-gap-ms", type=float, default=0.0,
+                    help="each context idles this long after each timed step (diagnostics: a bursty load like the "
+                         "CLI's, whose contexts wait for the reader)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes per kernel from rocprofv3 --pmc passes of this bench "
                          "(scripts/pmc_traffic.py), committed under profiles/")
@@ -570,9 +573,10 @@ class Workers:
     """C encoder contexts on one GPU, each driven by its own host thread, taking
     steps (batch encodes) from a shared counter."""
 
-    def __init__(self, encoders, inputs, cfg, runner=None):
-        """runner(enc, inp, cfg): one step (default: the no-reference encode)."""
-        self.encs, self.inputs, self.cfg = encoders, inputs, cfg
+    def __init__(self, encoders, inputs, cfg, runner=None, gap_s: float = 0.0):
+        """runner(enc, inp, cfg): one step (default: the no-reference encode);
+        gap_s: a pause after each recorded step (diagnostics)."""
+        self.encs, self.inputs, self.cfg, self.gap_s = encoders, inputs, cfg, gap_s
         self.step = runner or (lambda enc, inp, c: enc.run_input(inp, c))
         self.phases, self.restarts, self.stats = [], 0, (0, 0)
 
@@ -610,6 +614,8 @@ class Workers:
                             return
                         nxt[0] += 1
                     self.step(enc, self.inputs[s % len(self.inputs)], self.cfg)
+                    if record and self.gap_s > 0:
+                        time.sleep(self.gap_s)
                     if record:
                         ph = enc.phase_times()
                         with lock:
@@ -767,7 +773,7 @@ def main():
         encs.append(fq.Encoder(local, share_with=None if args.no_share else encs[0]))
     for e in encs:
         e.set_timing(True)
-    W = Workers(encs, inputs, cfg)
+    W = Workers(encs, inputs, cfg, gap_s=args.step_gap_ms / 1e3)
     W.warm_all()
     W.run(args.warmup, record=False)
     barrier()

@@ -1024,32 +1024,33 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
                 if (rl >= d) id += pd;
             }
             int delta = delta_c + (int)(id - dsum);
-            uint32_t ctxs[16];
+            // the context before the lane's first symbol: after the previous
+            // lane's last symbol, i.e. from its last three symbols and the delta
+            // entering this lane (every earlier lane of a step holds 16 symbols)
+            const auto qctx = [&](uint32_t a1, uint32_t a2, uint32_t sym, int d, uint32_t i) {
+                uint32_t cx = (((a1 > a2 ? a1 : a2) << 6) + sym) & 0xfffu;
+                if (ql > 1) {
+                    cx += a1 == a2 ? 0x1000u : 0u;
+                    cx += (uint32_t)(((d <= 56 ? d : 56) & 0xf8) << 10);
+                    if (ql > 2) cx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
+                }
+                return cx;
+            };
+            const uint32_t l3 = (byte_at(qw, 13) - 33u) & 0xffu;
+            const uint32_t s3 = __shfl_up(l3, 1, ER);
+            uint32_t prev = rl ? qctx(q2, s3, q1, delta, pos - 1) : ctx_c;
             uint32_t cl = 0;   // the context after the lane's last symbol
 #pragma unroll
             for (uint32_t j = 0; j < 16; j++) {   // (branch-free: past cnt the state holds)
                 const bool in = j < cnt;
                 const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
-                const uint32_t i = pos + j;
                 delta += in ? (int)(q1 > sym ? q1 - sym : 0u) : 0;
-                uint32_t cx = (((q1 > q2 ? q1 : q2) << 6) + sym) & 0xfffu;
-                if (ql > 1) {
-                    cx += q1 == q2 ? 0x1000u : 0u;
-                    cx += (uint32_t)(((delta <= 56 ? delta : 56) & 0xf8) << 10);
-                    if (ql > 2) cx += i <= 0x6f ? (uint32_t)(((i + 15) & 0x78) << 13) : 0xf0000u;
-                }
-                ctxs[j] = cx;
+                const uint32_t cx = qctx(q1, q2, sym, delta, pos + j);
+                sk[in ? 16 * rl + j : ER_STEP] = ((M_QUAL + prev) << AUX_SYM_BITS) | sym;
+                prev = in ? cx : prev;
                 cl = in ? cx : cl;
                 q2 = in ? q1 : q2;
                 q1 = in ? sym : q1;
-            }
-            uint32_t prev = __shfl_up(cl, 1, ER);
-            if (rl == 0) prev = ctx_c;
-#pragma unroll
-            for (uint32_t j = 0; j < 16; j++) {
-                const uint32_t sym = (byte_at(qw, j) - 33u) & 0xffu;
-                sk[j < cnt ? 16 * rl + j : ER_STEP] = ((M_QUAL + prev) << AUX_SYM_BITS) | sym;
-                prev = ctxs[j];
             }
             // the step's last symbol: its lane carries the state on
             const uint32_t tot = n > i0 ? (n - i0 < ER_STEP ? n - i0 : ER_STEP) : 0u;
