@@ -107,6 +107,10 @@ struct SortView {
     uint64_t total;             // padded elements over all segments
     uint32_t ntiles;
     uint32_t nsegs;
+    // AUX space, dense model ids (k_aux_dense): per segment AUX_DENSE_WORDS
+    // entries {models present in the 32 ids, bits; models below them, << 32};
+    // the digits of a DENSE sort pass are digits of the dense id
+    const uint64_t* dense = nullptr;
 };
 
 // A model run long enough for its own wave (k_replay_aux_long).

@@ -181,6 +181,14 @@ struct sa_ctx {
     int device = 0;
     // main/AUX, MD5, SEQ path (CU-masked), long AUX runs (CU-masked, disjoint)
     hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr, st4 = nullptr;
+    // SA_L_CU_EVERY=N (N >= 2): the L passes of the coder (L1 / L2 / L3) on a
+    // stream of their own, masked to every N-th CU, after the host has seen
+    // pass R end (the L passes are throughput kernels: on pass R's CUs they
+    // take the whole GPU for ~40 ms per batch and the other batches' front
+    // kernels beside them run ~3x slower, round 4 r4c trace).  0: after pass R
+    // on its stream (st3).
+    hipStream_t st5 = nullptr;
+    hipEvent_t ev_r_done = nullptr;
     hipEvent_t ev_fork = nullptr, ev_fork_seq = nullptr, ev_md5_done = nullptr, ev_r[2] = {nullptr, nullptr};
     hipEvent_t ev_seq_done = nullptr, ev_long_done = nullptr;
     uint32_t long_lds = 0;
@@ -320,6 +328,8 @@ struct sa_ctx {
         if (st2) (void)hipStreamDestroy(st2);
         if (st3) (void)hipStreamDestroy(st3);
         if (st4) (void)hipStreamDestroy(st4);
+        if (st5) (void)hipStreamDestroy(st5);
+        if (ev_r_done) (void)hipEventDestroy(ev_r_done);
     }
 };
 
@@ -432,23 +442,32 @@ template <int DB>
 void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
                uint32_t* vout, uint32_t shift, bool wide)
 {
-    hipLaunchKernelGGL(k_sort_hist<DB>, dim3((sv.ntiles + HIST_TILES - 1) / HIST_TILES), dim3(SORT_THREADS), 0, st,
-                       sv, kin, shift);
+    const dim3 hgrid((sv.ntiles + HIST_TILES - 1) / HIST_TILES);
+    if (sv.dense)
+        hipLaunchKernelGGL((k_sort_hist<DB, true>), hgrid, dim3(SORT_THREADS), 0, st, sv, kin, shift);
+    else
+        hipLaunchKernelGGL((k_sort_hist<DB, false>), hgrid, dim3(SORT_THREADS), 0, st, sv, kin, shift);
     hipLaunchKernelGGL(k_sort_scan<DB>, dim3(sv.nsegs), dim3(1024), 0, st, sv);
     if (wide)
-        hipLaunchKernelGGL((k_sort_scatter<DB, true>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout,
-                           vout, shift);
+        hipLaunchKernelGGL((k_sort_scatter<DB, true, false>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin,
+                           kout, vout, shift);
+    else if (sv.dense)
+        hipLaunchKernelGGL((k_sort_scatter<DB, false, true>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin,
+                           kout, vout, shift);
     else
-        hipLaunchKernelGGL((k_sort_scatter<DB, false>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout,
-                           vout, shift);
+        hipLaunchKernelGGL((k_sort_scatter<DB, false, false>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin,
+                           kout, vout, shift);
 }
 
 // sorts keys by bits [lo, hi) (bits below lo ride along); the result is in
 // keys[result_buf] / vals[result_buf]
 // index_vals: the input values are each element's index in its segment and are
 // not read (the first pass computes them)
+// dense: the AUX space by dense model ids (k_aux_dense's tables; bits
+// [lo, hi) of the dense id)
 int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
-             DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf, bool index_vals = false)
+             DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf, bool index_vals = false,
+             const uint64_t* dense = nullptr)
 {
     result_buf = 0;
     if (plan.total && hi <= lo && index_vals) {
@@ -463,12 +482,19 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
     sv.total = plan.total;
     sv.ntiles = (uint32_t)plan.tile_seg.size();
     sv.nsegs = (uint32_t)plan.segs.size();
+    sv.dense = dense;
     // a segment of >= 2^30 keys needs 64-bit offsets in the scatter (the HASH
     // index of a genome > 2^31 bases: one segment of all its seeds)
     bool wide = false;
-    for (const SortSeg& g : plan.segs) wide |= (uint64_t)g.ntiles * SORT_TILE >= (1ull << 30);
-    if (plan.segs.size() && (uint64_t)plan.segs.back().ntiles * SORT_TILE >= (1ull << 32)) {
-        c->err = "sort segment of 2^32 keys or more";
+    for (const SortSeg& g : plan.segs) {
+        wide |= (uint64_t)g.ntiles * SORT_TILE >= (1ull << 30);
+        if ((uint64_t)g.ntiles * SORT_TILE >= (1ull << 32)) {
+            c->err = "sort segment of 2^32 keys or more";
+            return -1;
+        }
+    }
+    if (wide && dense) {
+        c->err = "internal: a dense sort of a segment of 2^30 keys or more";
         return -1;
     }
     int cur = 0, shift = lo;
@@ -617,10 +643,10 @@ void write_rv_probe(sa_ctx* c, const std::vector<uint64_t>& p)
         if (!t1) continue;
         const uint32_t hw = (uint32_t)id;
         const double us = (double)(t1 - t0) / 100.0;
-        std::fprintf(f, "%p %llu %zu %.1f %.1f %.0f xcc %u se %u cu %u simd %u slot %u chains %u\n", (void*)c,
-                     (unsigned long long)b, w / 4, (double)t0 / 100.0, (double)t1 / 100.0,
+        std::fprintf(f, "%p %llu %zu %.1f %.1f %.0f xcc %u se %u cu %u simd %u slot %u chains %u sh %u hwid %08x\n",
+                     (void*)c, (unsigned long long)b, w / 4, (double)t0 / 100.0, (double)t1 / 100.0,
                      us > 0 ? (double)cyc / us : 0.0, (unsigned)((id >> 32) & 0xff), (hw >> 13) & 7u,
-                     (hw >> 8) & 15u, (hw >> 4) & 3u, hw & 15u, (unsigned)(id >> 40));
+                     (hw >> 8) & 15u, (hw >> 4) & 3u, hw & 15u, (unsigned)(id >> 40), (hw >> 12) & 1u, hw);
     }
     std::fclose(f);
 }
@@ -669,6 +695,11 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         for (const uint32_t t : ids) nlong += tasks[t].n >= RV_LONG_SYMS ? 1u : 0u;
     }
     coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1, nlong);
+    if (c->st5) {   // (SA_L_CU_EVERY) the L passes on their own CUs once pass R is done
+        SA_CHECK(c, hipEventRecord(c->ev_r_done, st));
+        SA_CHECK(c, hipEventSynchronize(c->ev_r_done));
+        st = c->st5;
+    }
     if (before_l) {
         if (c->host_waits) SA_CHECK(c, hipEventSynchronize(before_l));   // (see host_waits)
         else SA_CHECK(c, hipStreamWaitEvent(st, before_l, 0));
@@ -839,6 +870,19 @@ sa_ctx* sa_create(int device)
         hipEventCreateWithFlags(&c->ev_r[1], hipEventDisableTiming) != hipSuccess) {
         delete c;
         return nullptr;
+    }
+    if (const char* le = std::getenv("SA_L_CU_EVERY")) {
+        const int n = std::atoi(le);
+        if (n >= 2) {
+            std::vector<uint32_t> m_l(m_long.size(), 0u);
+            for (int cu = 0; cu < prop.multiProcessorCount; cu++)
+                if (cu % n == n / 2) m_l[cu / 32] |= 1u << (cu % 32);   // (offset: not the long runs' CUs when n = 4)
+            if (hipExtStreamCreateWithCUMask(&c->st5, (uint32_t)m_l.size(), m_l.data()) != hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_r_done, hipEventDisableTiming) != hipSuccess) {
+                delete c;
+                return nullptr;
+            }
+        }
     }
     for (int i = 0; i < PH_N; i++) {
         if (hipEventCreate(&c->ev_beg[i]) != hipSuccess || hipEventCreate(&c->ev_end[i]) != hipSuccess) {

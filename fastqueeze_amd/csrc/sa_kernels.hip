@@ -1163,7 +1163,83 @@ constexpr uint32_t HIST_TILES = 2;
 // digit run, too short for coalesced writes)
 constexpr int SORT_MIN_DB = 7, SORT_MAX_DB = 9;   // (SA_SORT_MIN_DB=8: round 1's floor, for A/B)
 
-template <int DB>
+// ---------------------------------------------------------------------------
+// Dense AUX model ids.  A block's AUX symbols use a few hundred of the 2^17
+// model ids (Qlevel <= 2: 16384 + 65536 quality contexts and the other
+// streams' models), so the AUX sort can order them by their rank among the
+// block's present models -- the same order as by model id -- in one 9-bit pass
+// instead of two passes over the 17-bit id.  k_aux_presence marks the models of
+// each tile in an LDS bitmap and ORs its non-zero words into the block's
+// bitmap; k_aux_dense turns each block's bitmap into the rank table.
+// ---------------------------------------------------------------------------
+constexpr uint32_t AUX_DENSE_BITS = 17;                             // model ids < 2^17
+constexpr uint32_t AUX_DENSE_WORDS = 1u << (AUX_DENSE_BITS - 5);    // 4096 bitmap words per block
+
+__global__ __launch_bounds__(SORT_THREADS) void k_aux_presence(const SortView sv, const uint32_t* __restrict__ keys,
+                                                               uint32_t* __restrict__ bm)
+{
+    __shared__ uint32_t lb[AUX_DENSE_WORDS];
+    for (uint32_t i = threadIdx.x; i < AUX_DENSE_WORDS; i += SORT_THREADS) lb[i] = 0;
+    __syncthreads();
+    const uint32_t t = blockIdx.x, seg = sv.tile_seg[t];
+    const SortSeg& sg = sv.segs[seg];
+    const uint32_t* K = keys + sg.base + (size_t)(t - sg.tile0) * SORT_TILE;
+    uint32_t k[SORT_ITEMS];
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) k[r] = K[threadIdx.x + r * SORT_THREADS];
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) {
+        const uint32_t m = k[r] >> AUX_SYM_BITS;
+        if (k[r] != SORT_PAD && m < (1u << AUX_DENSE_BITS)) atomicOr(&lb[m >> 5], 1u << (m & 31));
+    }
+    __syncthreads();
+    uint32_t* B = bm + (size_t)seg * AUX_DENSE_WORDS;
+    for (uint32_t i = threadIdx.x; i < AUX_DENSE_WORDS; i += SORT_THREADS)
+        if (lb[i]) atomicOr(&B[i], lb[i]);
+}
+
+// per block (one workgroup): the rank table and the number of models
+__global__ __launch_bounds__(256) void k_aux_dense(const uint32_t* __restrict__ bm, uint64_t* __restrict__ tab,
+                                                   uint32_t* __restrict__ nmodels)
+{
+    __shared__ uint32_t sh[4];
+    constexpr uint32_t PER = AUX_DENSE_WORDS / 256;
+    const uint32_t* B = bm + (size_t)blockIdx.x * AUX_DENSE_WORDS;
+    uint64_t* T = tab + (size_t)blockIdx.x * AUX_DENSE_WORDS;
+    uint32_t w[PER], s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+        w[j] = B[threadIdx.x * PER + j];
+        s += (uint32_t)__popc(w[j]);
+    }
+    uint32_t ex;
+    wg256_excl_scan(s, ex, sh);
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+        T[threadIdx.x * PER + j] = (uint64_t)ex << 32 | w[j];
+        ex += (uint32_t)__popc(w[j]);
+    }
+    if (threadIdx.x == 255) nmodels[blockIdx.x] = ex;
+}
+
+// the digit of a key in a sort pass: bits [shift, shift + DB) of the key, or
+// (DENSE) of the dense id of its model; pad keys take the last digit
+template <int DB, bool DENSE>
+__device__ __forceinline__ uint32_t sort_digit(uint32_t k, uint32_t shift, const uint64_t* __restrict__ T)
+{
+    constexpr uint32_t ND = 1u << DB;
+    if constexpr (!DENSE) {
+        return (k >> shift) & (ND - 1);
+    } else {
+        if (k == SORT_PAD) return ND - 1;
+        const uint32_t m = (k >> AUX_SYM_BITS) & ((1u << AUX_DENSE_BITS) - 1u);
+        const uint64_t e = T[m >> 5];
+        const uint32_t d = (uint32_t)(e >> 32) + (uint32_t)__popc((uint32_t)e & ((1u << (m & 31)) - 1u));
+        return (d >> shift) & (ND - 1);
+    }
+}
+
+template <int DB, bool DENSE>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, const uint32_t* __restrict__ keys,
                                                             uint32_t shift)
 {
@@ -1191,8 +1267,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_hist(const SortView sv, c
 #pragma unroll
     for (int j = 0; j < HIST_TILES; j++) {
         if (!sgp[j]) continue;
+        const uint64_t* T = DENSE ? sv.dense + (size_t)sv.tile_seg[blockIdx.x * HIST_TILES + j] * AUX_DENSE_WORDS
+                                  : nullptr;
 #pragma unroll
-        for (int i = 0; i < SORT_ITEMS; i++) atomicAdd(&h[j][(k[j][i] >> shift) & (ND - 1)], 1u);
+        for (int i = 0; i < SORT_ITEMS; i++) atomicAdd(&h[j][sort_digit<DB, DENSE>(k[j][i], shift, T)], 1u);
     }
     __syncthreads();
 #pragma unroll
@@ -1291,7 +1369,7 @@ __global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
 
 // WIDE: a segment of >= 2^30 keys (the HASH index of a genome of > 2^31
 // bases sorts all its seeds as one segment): 64-bit element offsets
-template <int DB, bool WIDE>
+template <int DB, bool WIDE, bool DENSE>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv,
                                                                const uint32_t* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin,
@@ -1323,9 +1401,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
                    : lt * SORT_TILE + w * (64 * SORT_ITEMS) + (uint32_t)r * 64 + lane;
     }
     const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint64_t* T = DENSE ? sv.dense + (size_t)sv.tile_seg[t] * AUX_DENSE_WORDS : nullptr;
+    uint32_t dg[SORT_ITEMS];   // (the keys' digits: DENSE ones cost a table read)
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; r++) dg[r] = sort_digit<DB, DENSE>(k[r], shift, T);
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t d = (k[r] >> shift) & (ND - 1);
+        const uint32_t d = dg[r];
         uint64_t peers = ~0ull;
 #pragma unroll
         for (int bit = 0; bit < DB; bit++) {
@@ -1376,11 +1458,14 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     // threads write consecutive slots of one digit's run (coalesced); the keys
     // first (each thread keeps the output slots of its tile slots), then the
     // values through the same buffer
+    // the keys' digits in tile order, for the output offsets
+    __shared__ uint16_t sd[DENSE ? SORT_TILE : 1];
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t d = (k[r] >> shift) & (ND - 1);
+        const uint32_t d = dg[r];
         rk[r] += wc[w][d];   // (the key's slot in the tile)
         sb[rk[r]] = k[r];
+        if constexpr (DENSE) sd[rk[r]] = (uint16_t)d;
     }
     __syncthreads();
     if constexpr (WIDE) {
@@ -1391,7 +1476,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         for (int r = 0; r < SORT_ITEMS; r++) {
             const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
             const uint32_t kk = sb[i];
-            ro[r] = gstart[(kk >> shift) & (ND - 1)] + i;
+            ro[r] = gstart[DENSE ? (uint32_t)sd[i] : (kk >> shift) & (ND - 1)] + i;
             ko[(uint64_t)ro[r]] = kk;
         }
         __syncthreads();
@@ -1411,7 +1496,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         for (int r = 0; r < SORT_ITEMS; r++) {
             const uint32_t i = threadIdx.x + (uint32_t)r * SORT_THREADS;
             const uint32_t kk = sb[i];
-            ro[r] = (gstart[(kk >> shift) & (ND - 1)] + i) << 2;
+            ro[r] = (gstart[DENSE ? (uint32_t)sd[i] : (kk >> shift) & (ND - 1)] + i) << 2;
             *reinterpret_cast<uint32_t*>(ko + ro[r]) = kk;
         }
         __syncthreads();

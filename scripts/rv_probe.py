@@ -16,7 +16,7 @@ def load(path):
             continue
         waves.append({"ctx": f[0], "batch": int(f[1]), "wave": int(f[2]), "t0": float(f[3]), "t1": float(f[4]),
                       "mhz": float(f[5]), "xcc": int(f[7]), "se": int(f[9]), "cu": int(f[11]), "simd": int(f[13]),
-                      "slot": int(f[15]), "chains": int(f[17])})
+                      "slot": int(f[15]), "chains": int(f[17]), "sh": int(f[19]) if len(f) > 19 else 0})
     return waves
 
 
@@ -33,8 +33,8 @@ def report(path):
     by_simd = collections.defaultdict(list)
     by_cu = collections.defaultdict(list)
     for w in ws:
-        by_simd[(w["xcc"], w["se"], w["cu"], w["simd"])].append(w)
-        by_cu[(w["xcc"], w["se"], w["cu"])].append(w)
+        by_simd[(w["xcc"], w["se"], w["sh"], w["cu"], w["simd"])].append(w)
+        by_cu[(w["xcc"], w["se"], w["sh"], w["cu"])].append(w)
 
     def shared_frac(w, group):
         ov = 0.0
@@ -55,8 +55,8 @@ def report(path):
         longs = [w for w in bw if w["chains"] == 1]
         d = [(w["t1"] - w["t0"]) / 1e3 for w in longs] or [0.0]
         mhz = [w["mhz"] for w in bw if w["mhz"] > 0] or [0.0]
-        sh = [shared_frac(w, by_simd[(w["xcc"], w["se"], w["cu"], w["simd"])]) for w in longs] or [0.0]
-        cuw = [len([o for o in by_cu[(w["xcc"], w["se"], w["cu"])] if o["t0"] < w["t1"] and o["t1"] > w["t0"]])
+        sh = [shared_frac(w, by_simd[(w["xcc"], w["se"], w["sh"], w["cu"], w["simd"])]) for w in longs] or [0.0]
+        cuw = [len([o for o in by_cu[(w["xcc"], w["se"], w["sh"], w["cu"])] if o["t0"] < w["t1"] and o["t1"] > w["t0"]])
                for w in longs] or [0]
         print(f"{b:5d} {(t1 - t0) / 1e3:8.1f} {len(bw):6d}   {statistics.median(d):7.1f} / {max(d):7.1f}"
               f"   {statistics.median(mhz):6.0f} / {min(mhz):6.0f}   {statistics.mean(sh):8.3f}   "
