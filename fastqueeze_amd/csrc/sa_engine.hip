@@ -189,6 +189,16 @@ struct sa_ctx {
     // on its stream (st3).
     hipStream_t st5 = nullptr;
     hipEvent_t ev_r_done = nullptr;
+    // the dense AUX sort (k_aux_presence / k_aux_dense: one 9-bit pass over the
+    // blocks' dense model ids instead of two over the 17-bit ids).  The emit's
+    // target buffer depends on the number of passes, so the batch follows this
+    // context's previous one: a batch with more than 512 models in a block sorts
+    // in two dense passes and a copy, and turns it off.  SA_AUX_DENSE=0: off.
+    bool aux_dense = !(std::getenv("SA_AUX_DENSE") && std::atoi(std::getenv("SA_AUX_DENSE")) == 0);
+    DBuf d_aux_bm, d_aux_tab, d_aux_nmod;
+    uint32_t* h_aux_nmod = nullptr;   // (pinned)
+    size_t h_aux_nmod_cap = 0;
+    hipEvent_t ev_dense = nullptr;
     hipEvent_t ev_fork = nullptr, ev_fork_seq = nullptr, ev_md5_done = nullptr, ev_r[2] = {nullptr, nullptr};
     hipEvent_t ev_seq_done = nullptr, ev_long_done = nullptr;
     uint32_t long_lds = 0;
@@ -294,7 +304,8 @@ struct sa_ctx {
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
-                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe};
+                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe, &d_aux_bm,
+                &d_aux_tab, &d_aux_nmod};
     }
     uint64_t held_bytes()
     {
@@ -330,6 +341,8 @@ struct sa_ctx {
         if (st4) (void)hipStreamDestroy(st4);
         if (st5) (void)hipStreamDestroy(st5);
         if (ev_r_done) (void)hipEventDestroy(ev_r_done);
+        if (ev_dense) (void)hipEventDestroy(ev_dense);
+        if (h_aux_nmod) (void)hipHostFree(h_aux_nmod);
     }
 };
 
@@ -867,7 +880,8 @@ sa_ctx* sa_create(int device)
         hipEventCreateWithFlags(&c->ev_fork_seq, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_md5_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_r[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_r[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_dense, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -1342,7 +1356,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, c->d_auxp_v.ensure(atot * 4));
     // AUX sort ping-pong: the sorted keys/values must land in this context's
     // buffers (the long model runs read them after the front scratch is released)
-    const int aux_passes = (int)sort_digits(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits).size();
+    const bool dense = c->aux_dense && aux_bits == (int)AUX_DENSE_BITS && pa.total;
+    const int aux_passes = dense ? 1 : (int)sort_digits(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits).size();
     DBuf* akb[2] = {aux_passes % 2 ? &F->d_auxs_k : &c->d_auxp_k, aux_passes % 2 ? &c->d_auxp_k : &F->d_auxs_k};
     DBuf* avb[2] = {aux_passes % 2 ? &F->d_auxs_v : &c->d_auxp_v, aux_passes % 2 ? &c->d_auxp_v : &F->d_auxs_v};
     DBuf* skb[2] = {&F->d_seq_k[0], &F->d_seq_k[1]};
@@ -1442,6 +1457,26 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                  pa.total, (uint32_t)pa.tile_seg.size(), nbk};
     const SymSink sink_seq{c->d_prs_seq.as<PRec>(), nullptr};   // packed
     const SymSink sink_aux{c->d_prs_aux.as<PRec>(), c->d_cum_aux.as<uint16_t>()};
+    if (dense) {   // the blocks' model bitmaps and rank tables; the model counts to the host
+        SA_CHECK(c, c->d_aux_bm.ensure(4ull * AUX_DENSE_WORDS * nbk));
+        SA_CHECK(c, c->d_aux_tab.ensure(8ull * AUX_DENSE_WORDS * nbk));
+        SA_CHECK(c, c->d_aux_nmod.ensure(4ull * nbk));
+        if (c->h_aux_nmod_cap < nbk) {
+            if (c->h_aux_nmod) SA_CHECK(c, hipHostFree(c->h_aux_nmod));
+            c->h_aux_nmod = nullptr;
+            c->h_aux_nmod_cap = 0;
+            SA_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_aux_nmod), 4ull * nbk * 2, 0));
+            c->h_aux_nmod_cap = 2ull * nbk;
+        }
+        SA_CHECK(c, hipMemsetAsync(c->d_aux_bm.p, 0, 4ull * AUX_DENSE_WORDS * nbk, st));
+        hipLaunchKernelGGL(k_aux_presence, dim3((uint32_t)pa.tile_seg.size()), dim3(SORT_THREADS), 0, st, sva,
+                           akb[0]->as<uint32_t>(), c->d_aux_bm.as<uint32_t>());
+        hipLaunchKernelGGL(k_aux_dense, dim3(nbk), dim3(256), 0, st, c->d_aux_bm.as<uint32_t>(),
+                           c->d_aux_tab.as<uint64_t>(), c->d_aux_nmod.as<uint32_t>());
+        SA_CHECK(c, hipGetLastError());
+        SA_CHECK(c, hipMemcpyAsync(c->h_aux_nmod, c->d_aux_nmod.p, 4ull * nbk, hipMemcpyDeviceToHost, st));
+        SA_CHECK(c, hipEventRecord(c->ev_dense, st));
+    }
 
     // ---- throughput phases on st (each fills the GPU): SEQ sort and BASE_MODEL
     //      replay, AUX sort and short SIMPLE_MODEL runs.  Then the long SIMPLE_MODEL
@@ -1468,9 +1503,26 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_SORT_AUX, st);
-    if (run_sort(c, st, pa, F->d_segs_aux, F->d_tile_aux, F->d_hist_aux, akb, avb, AUX_SYM_BITS,
-                 AUX_SYM_BITS + aux_bits, aux_sorted_buf, true))
+    if (dense) {
+        // (the counts were read back right after the emit: the SEQ sort and
+        // replay queued above keep the device busy while the host waits here)
+        SA_CHECK(c, hipEventSynchronize(c->ev_dense));
+        uint32_t dmax = 0;
+        for (uint32_t b = 0; b < nbk; b++) dmax = std::max(dmax, c->h_aux_nmod[b]);
+        const int dbits = dmax > 512 ? (int)AUX_DENSE_BITS : 9;
+        if (run_sort(c, st, pa, F->d_segs_aux, F->d_tile_aux, F->d_hist_aux, akb, avb, 0, dbits, aux_sorted_buf, true,
+                     c->d_aux_tab.as<uint64_t>()))
+            return -1;
+        if (aux_sorted_buf != 1) {   // (two dense passes: the result is in the front scratch)
+            SA_CHECK(c, hipMemcpyAsync(c->d_auxp_k.p, F->d_auxs_k.p, atot * 4, hipMemcpyDeviceToDevice, st));
+            SA_CHECK(c, hipMemcpyAsync(c->d_auxp_v.p, F->d_auxs_v.p, atot * 4, hipMemcpyDeviceToDevice, st));
+            aux_sorted_buf = 1;
+            c->aux_dense = false;   // (this input has too many models per block for one pass)
+        }
+    } else if (run_sort(c, st, pa, F->d_segs_aux, F->d_tile_aux, F->d_hist_aux, akb, avb, AUX_SYM_BITS,
+                        AUX_SYM_BITS + aux_bits, aux_sorted_buf, true)) {
         return -1;
+    }
     ev_finish(c, PH_SORT_AUX, st);
     ev_begin(c, PH_REPLAY_AUX, st);
     if (pa.total && akb[aux_sorted_buf] != &c->d_auxp_k) {
