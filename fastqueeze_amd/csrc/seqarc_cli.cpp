@@ -241,6 +241,29 @@ struct Buf {
     bool empty() const { return n == 0; }
 };
 
+// byte buffers that resize without zero-filling (filled right after)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept
+    {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a)
+    {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
+
 // ---- gzip input -------------------------------------------------------------
 // The reference inflates with gzread on its reader thread.  Here a producer
 // thread per input inflates ahead of the block cut into a bounded queue of
@@ -256,10 +279,10 @@ struct GzStream {
     std::thread prod;
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<std::vector<uint8_t>> q;
+    std::deque<Bytes> q;
     size_t q_bytes = 0;
     bool done = false, failed = false, stop = false;
-    std::vector<uint8_t> cur;
+    Bytes cur;
     size_t cur_at = 0;
     static constexpr size_t kMaxQueued = 512u << 20;
 
@@ -280,7 +303,7 @@ struct GzStream {
         });
         return true;
     }
-    bool push(std::vector<uint8_t>&& v)   // false: the reader went away
+    bool push(Bytes&& v)   // false: the reader went away
     {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return stop || q_bytes < kMaxQueued; });
@@ -311,7 +334,7 @@ struct GzStream {
         std::vector<uint8_t> in(4u << 20);
         uint64_t at = 0;
         bool eof = false, member_end = false;
-        std::vector<uint8_t> out(8u << 20);
+        Bytes out(8u << 20);
         size_t have = 0;
         for (;;) {
             if (z.avail_in == 0 && !eof) {
@@ -346,7 +369,8 @@ struct GzStream {
             if (have == out.size() || (member_end && have > (6u << 20))) {
                 out.resize(have);
                 if (!push(std::move(out))) { inflateEnd(&z); return true; }
-                out.assign(8u << 20, 0);
+                out = Bytes();
+                out.resize(8u << 20);
                 have = 0;
             }
         }
@@ -356,89 +380,153 @@ struct GzStream {
         if (have && !push(std::move(out))) return true;
         return true;
     }
-    // BGZF: slabs of whole members, inflated in parallel; the next slab is read
-    // while the workers inflate this one
+    // BGZF: slabs of whole members; a pool of `workers` threads inflates the
+    // members of up to kInFlight slabs (each member into its place, by its
+    // ISIZE; CRC checked), while this thread reads and parses the next slab;
+    // finished slabs leave in order.  (Round 3 started the workers per slab
+    // and joined them before the next one: every slab waited for its slowest
+    // member and the threads' start-up; the outputs were zero-filled first.)
     bool run_bgzf()
     {
         const size_t kSlab = 32u << 20;
-        std::vector<uint8_t> slabs[2] = {std::vector<uint8_t>(kSlab), std::vector<uint8_t>(kSlab)};
-        int cs = 0;
-        size_t carry = 0;
-        uint64_t at = 0;
-        bool eof = false;
+        const size_t kInFlight = 4;
         struct Mem { size_t off, len; uint64_t out; uint32_t crc, isize; };
-        auto fill_slab = [&](std::vector<uint8_t>& sl) -> bool {   // after the carry
-            const long r = readn(sl.data() + carry, kSlab - carry, at);
-            if (r < 0) return false;
-            if ((size_t)r < kSlab - carry) eof = true;
-            carry += (size_t)r;
+        struct Slab {
+            std::vector<uint8_t> in;
+            std::vector<Mem> ms;
+            Bytes out;
+            size_t next = 0, done = 0;
+            bool bad = false;
+        };
+        std::mutex pm;
+        std::condition_variable pcv;
+        std::deque<std::unique_ptr<Slab>> jobs;   // in file order
+        bool quit = false;
+        auto work = [&]() {
+            z_stream z{};
+            const bool ok = inflateInit2(&z, -15) == Z_OK;
+            std::unique_lock<std::mutex> lk(pm);
+            for (;;) {
+                Slab* s = nullptr;
+                pcv.wait(lk, [&] {
+                    if (quit) return true;
+                    for (auto& j : jobs)
+                        if (j->next < j->ms.size()) return true;
+                    return false;
+                });
+                if (quit) break;
+                for (auto& j : jobs)
+                    if (j->next < j->ms.size()) { s = j.get(); break; }
+                const size_t i = s->next++;
+                lk.unlock();
+                const Mem& m = s->ms[i];
+                bool bad = !ok;
+                if (ok && m.isize == 0) {   // (the BGZF end-of-file marker: an empty member)
+                    bad = m.crc != 0;
+                } else if (ok) {
+                    inflateReset(&z);
+                    z.next_in = s->in.data() + m.off;
+                    z.avail_in = (uInt)m.len;
+                    z.next_out = s->out.data() + m.out;
+                    z.avail_out = (uInt)m.isize;
+                    const int rc = inflate(&z, Z_FINISH);
+                    bad = rc != Z_STREAM_END || z.avail_out != 0 ||
+                          crc32(0L, s->out.data() + m.out, (uInt)m.isize) != m.crc;
+                }
+                lk.lock();
+                s->bad |= bad;
+                if (++s->done == s->ms.size()) pcv.notify_all();
+            }
+            if (ok) inflateEnd(&z);
+        };
+        std::vector<std::thread> pool;
+        for (int k = 0; k < workers; k++) pool.emplace_back(work);
+        auto finish = [&](bool rc) {
+            {
+                std::lock_guard<std::mutex> g(pm);
+                quit = true;
+            }
+            pcv.notify_all();
+            for (auto& t : pool) t.join();
+            return rc;
+        };
+        // the oldest slab, once inflated, to the reader (false: failed or the reader went away)
+        auto retire = [&](bool& stopped) -> bool {
+            std::unique_ptr<Slab> s;
+            {
+                std::unique_lock<std::mutex> lk(pm);
+                pcv.wait(lk, [&] { return jobs.front()->done == jobs.front()->ms.size(); });
+                s = std::move(jobs.front());
+                jobs.pop_front();
+            }
+            if (s->bad) return false;
+            if (!s->out.empty() && !push(std::move(s->out))) stopped = true;
             return true;
         };
-        if (!fill_slab(slabs[0])) return false;
-        while (carry) {
-            std::vector<uint8_t>& slab = slabs[cs];
-            std::vector<Mem> ms;
+        std::vector<uint8_t> carry_buf;   // a member cut by the end of the previous slab
+        uint64_t at = 0;
+        bool eof = false, stopped = false;
+        while (!eof || !carry_buf.empty()) {
+            std::unique_ptr<Slab> s(new Slab());
+            s->in.resize(kSlab);
+            const size_t c0 = carry_buf.size();
+            if (c0) memcpy(s->in.data(), carry_buf.data(), c0);
+            carry_buf.clear();
+            const long r = eof ? 0 : readn(s->in.data() + c0, kSlab - c0, at);
+            if (r < 0) return finish(false);
+            if ((size_t)r < kSlab - c0) eof = true;
+            const size_t have = c0 + (size_t)r;
             size_t p = 0;
             uint64_t total = 0;
-            while (p + 18 <= carry) {
-                const uint8_t* h = slab.data() + p;
-                if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return false;
+            while (p + 18 <= have) {
+                const uint8_t* h = s->in.data() + p;
+                if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return finish(false);
                 const size_t xlen = h[10] | (size_t)h[11] << 8;
                 size_t bsize = 0;
-                for (size_t x = 12; x + 4 <= 12 + xlen && p + x + 4 <= carry;) {   // the 'BC' subfield
+                for (size_t x = 12; x + 4 <= 12 + xlen && p + x + 4 <= have;) {   // the 'BC' subfield
                     const size_t sl = h[x + 2] | (size_t)h[x + 3] << 8;
                     if (h[x] == 'B' && h[x + 1] == 'C' && sl == 2) bsize = (h[x + 4] | (size_t)h[x + 5] << 8) + 1;
                     x += 4 + sl;
                 }
-                if (!bsize || bsize < 12 + xlen + 8) return false;   // not BGZF after all
-                if (p + bsize > carry) break;                      // the member continues in the next slab
+                if (!bsize || bsize < 12 + xlen + 8) return finish(false);   // not BGZF after all
+                if (p + bsize > have) break;                                // the member continues in the next slab
                 const uint8_t* t = h + bsize - 8;
-                Mem m{p + 12 + xlen, bsize - 12 - xlen - 8, total,
-                      (uint32_t)(t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24),
-                      (uint32_t)(t[4] | t[5] << 8 | t[6] << 16 | (uint32_t)t[7] << 24)};
+                const Mem m{p + 12 + xlen, bsize - 12 - xlen - 8, total,
+                            (uint32_t)(t[0] | t[1] << 8 | t[2] << 16 | (uint32_t)t[3] << 24),
+                            (uint32_t)(t[4] | t[5] << 8 | t[6] << 16 | (uint32_t)t[7] << 24)};
                 total += m.isize;
-                ms.push_back(m);
+                s->ms.push_back(m);
                 p += bsize;
             }
-            if (ms.empty()) return false;   // a truncated or oversized member
-            std::vector<uint8_t> out(total);
-            std::atomic<size_t> next{0};
-            std::atomic<bool> bad{false};
-            auto work = [&]() {
-                z_stream z{};
-                if (inflateInit2(&z, -15) != Z_OK) { bad = true; return; }
-                for (size_t i; (i = next.fetch_add(1)) < ms.size();) {
-                    const Mem& m = ms[i];
-                    if (m.isize == 0) {   // (the BGZF end-of-file marker: an empty member)
-                        if (m.crc != 0) bad = true;
-                        continue;
-                    }
-                    inflateReset(&z);
-                    z.next_in = slab.data() + m.off;
-                    z.avail_in = (uInt)m.len;
-                    z.next_out = out.data() + m.out;
-                    z.avail_out = (uInt)m.isize;
-                    const int rc = inflate(&z, Z_FINISH);
-                    if (rc != Z_STREAM_END || z.avail_out != 0 || crc32(0L, out.data() + m.out, (uInt)m.isize) != m.crc)
-                        bad = true;
-                }
-                inflateEnd(&z);
-            };
-            std::vector<std::thread> th;
-            for (int k = 0; k < workers; k++) th.emplace_back(work);
-            // the next slab: this one's partial last member, then fresh bytes
-            std::vector<uint8_t>& nx = slabs[cs ^ 1];
-            const size_t rest = carry - p;
-            memcpy(nx.data(), slab.data() + p, rest);
-            carry = rest;
-            const bool rd = eof || fill_slab(nx);
-            for (auto& x : th) x.join();
-            if (bad || !rd) return false;
-            if (!out.empty() && !push(std::move(out))) return true;
-            cs ^= 1;
-            if (eof && carry && carry == rest && rest < 18) return false;   // trailing bytes that are no member
+            if (s->ms.empty()) {
+                if (eof && have == 0) break;
+                return finish(false);   // a truncated or oversized member, or trailing bytes that are no member
+            }
+            carry_buf.assign(s->in.begin() + (std::ptrdiff_t)p, s->in.begin() + (std::ptrdiff_t)have);
+            if (eof && !carry_buf.empty() && carry_buf.size() < 18) return finish(false);
+            s->out.resize(total);   // (default-initialised: no zero fill)
+            {
+                std::lock_guard<std::mutex> g(pm);
+                jobs.push_back(std::move(s));
+            }
+            pcv.notify_all();
+            size_t n;
+            {
+                std::lock_guard<std::mutex> g(pm);
+                n = jobs.size();
+            }
+            if (n >= kInFlight && !retire(stopped)) return finish(false);
+            if (stopped) return finish(true);
         }
-        return true;
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> g(pm);
+                if (jobs.empty()) break;
+            }
+            if (!retire(stopped)) return finish(false);
+            if (stopped) return finish(true);
+        }
+        return finish(true);
     }
     // up to n bytes into dst; 0 at the end; -1 on a gzip error
     long read(uint8_t* dst, size_t n)
