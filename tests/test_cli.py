@@ -310,5 +310,12 @@ def test_gzip_ingest_plain_multimember_bgzf(tmp_path, capsys):
     bad.write_bytes(files["gz"][0][: len(files["gz"][0]) // 2])
     r = _run(["-c", "-f", "--ingest-only", "-1", str(bad), "-o", str(tmp_path / "bad")], tmp_path)
     assert r.returncode != 0
+    # BGZF cut inside a member, and with bytes that are no member after the last
+    for k, data in (("bgzf_cut", files["bgzf"][0][: len(files["bgzf"][0]) * 2 // 3]),
+                    ("bgzf_tail", files["bgzf"][0] + b"\x1f\x8bjunk")):
+        bad = tmp_path / f"{k}_1.fq"
+        bad.write_bytes(data)
+        r = _run(["-c", "-f", "--ingest-only", "-t", "4", "-1", str(bad), "-o", str(tmp_path / k)], tmp_path)
+        assert r.returncode != 0, k
     with capsys.disabled():
         print("\n[ingest] " + ", ".join(f"{k} {v[3]:.0f} MB/s" for k, v in got.items()))
