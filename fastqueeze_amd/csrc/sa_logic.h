@@ -586,30 +586,29 @@ SA_HD LowMap lowmap_compose(const LowMap& a, const LowMap& b)
 // The records of a segment, RC_CHUNK at a time: a chunk's loads are issued
 // back to back before it is coded (on the GPU one lane walks one segment, so
 // its cache lines must not be evicted between dependent steps).  The last
-// chunk re-reads record n - 1 instead of reading past the segment.
-constexpr uint32_t RC_CHUNK = 16;
-
-// The reciprocals of a chunk are computed after its loads, independently of
-// the chain.
+// chunk re-reads record n - 1 instead of reading past the segment.  32
+// records are one 128-byte line: with 16, a lane's second half-line was often
+// evicted before it came back for it (L1 / L3 read 1.5 / 2.1 x the records' bytes,
+// round 4 r4c PMC); the reciprocals are derived as the records are coded (off
+// the chain), so the 32 records cost no more registers than 16 with their
+// reciprocals did (88 VGPRs).
+constexpr uint32_t RC_CHUNK = 32;
 template <bool PACKED, class Fn>
 SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
 {
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
     for (uint32_t b = 0; b < n; b += RC_CHUNK) {
         PRec p[RC_CHUNK];
-        uint32_t c[RC_CHUNK], m[RC_CHUNK];
+        uint32_t c[PACKED ? 1 : RC_CHUNK];
 #pragma unroll
         for (uint32_t k = 0; k < RC_CHUNK; k++) {
             const uint32_t i = b + k < n ? b + k : n - 1;
             p[k] = P[i];
-            if constexpr (PACKED) c[k] = (p[k].tf >> 8) & 0xffu;
-            else c[k] = cum[i];
+            if constexpr (!PACKED) c[k] = cum[i];
         }
 #pragma unroll
-        for (uint32_t k = 0; k < RC_CHUNK; k++) m[k] = recip32z(p[k].tf & tmask);
-#pragma unroll
         for (uint32_t k = 0; k < RC_CHUNK; k++)
-            if (b + k < n) fn(p[k], m[k], c[k]);
+            if (b + k < n) fn(p[k], recip32z(p[k].tf & tmask), PACKED ? (p[k].tf >> 8) & 0xffu : c[PACKED ? 0 : k]);
     }
 }
 

@@ -1,0 +1,49 @@
+"""Front duty cycle from a rocprofv3 kernel trace of bench.py: per batch the
+front's span (its k_prep start to its k_replay_aux_short end) and the idle
+stretch before the next front starts, and per context (host thread) the cycle
+front -> pass R -> L passes -> assembly -> next front, so it shows whether the
+next front waited for a free front turn or for a context to come back from its
+tail.  usage: python scripts/front_cycle.py run_kernel_trace.csv"""
+import csv
+import statistics
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+
+
+def nm(r):
+    return r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sa::", "")
+
+
+ks = sorted(({"n": nm(r), "s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"]), "th": r["Thread_Id"]}
+             for r in rows), key=lambda k: k["s"])
+fronts = []
+cur = None
+for k in ks:
+    if k["n"] == "k_prep" or (k["n"] == "k_prep_sq16" and (cur is None or cur.get("done"))):
+        if cur is None or cur.get("done"):
+            cur = {"s": k["s"], "th": k["th"]}
+            fronts.append(cur)
+    if cur is not None and k["n"] == "k_replay_aux_short" and k["th"] == cur["th"]:
+        cur["e"] = k["e"]
+        cur["done"] = True
+fronts = [f for f in fronts if "e" in f]
+# per host thread: the end of its previous batch's assembly before each front
+asm_end = {}
+for k in ks:
+    if k["n"].startswith("k_assemble_copy"):
+        asm_end.setdefault(k["th"], []).append(k["e"])
+sel = fronts[2:-1]
+span = [(f["e"] - f["s"]) / 1e6 for f in sel]
+gap = [(b["s"] - a["e"]) / 1e6 for a, b in zip(sel, sel[1:])]
+wait_tail = []
+for a, b in zip(sel, sel[1:]):
+    prev = [t for t in asm_end.get(b["th"], []) if t < b["s"]]
+    wait_tail.append((b["s"] - max(prev)) / 1e6 if prev else float("nan"))
+print(f"fronts {len(sel)}: span median {statistics.median(span):.1f} ms (min {min(span):.1f}, max {max(span):.1f})")
+print(f"idle between fronts: median {statistics.median(gap):.1f} ms, mean {statistics.mean(gap):.1f}, "
+      f"max {max(gap):.1f}; share of time {100 * sum(gap) / ((sel[-1]['e'] - sel[0]['s']) / 1e6):.1f} %")
+print(f"next front start - that context's previous assembly end: median {statistics.median(wait_tail):.2f} ms")
+print("batch  th     span   idle_after  ctx_back(ms before start)")
+for f, g, w in zip(sel, gap + [0], wait_tail + [0]):
+    print(f"  {f['th']:>6} {(f['e'] - f['s']) / 1e6:7.1f} {g:8.1f}   {w:8.2f}")
