@@ -119,6 +119,10 @@ def parse_args(argv=None):
                     help="PE pairs of the HASH leg's batch (5 M: 69 blocks, the headline's batch)")
     ap.add_argument("--hash-align-reads", type=int, default=4_000_000, help="single reads of the aligner leg")
     ap.add_argument("--leg-steps", type=int, default=10, help="timed steps of the ONT and HASH legs")
+    ap.add_argument("--text-leg", type=int, default=1,
+                    help="staged-text leg: each step hands its batch over as FASTQ text in page-locked host "
+                         "memory (sa_stage_text: H2D + device parse), encodes and fetches (0: skip)")
+    ap.add_argument("--text-steps", type=int, default=15, help="timed steps of the staged-text leg")
     ap.add_argument("--decode-check", type=int, default=1,
                     help="decode the short e2e leg's archive with seqarc_amd -d and compare MD5s with the input")
     ap.add_argument("--ingest-devices", type=int, default=8,
@@ -217,12 +221,14 @@ def batch_text(gid: int, args, workers: int):
                           x_span=args.x_span)
 
 
-def make_batch(gid: int, args, workers: int, files=None):
+def make_batch(gid: int, args, workers: int, files=None, texts=None):
     """Global batch `gid`, cut and parsed as the reference's reader does.
     Returns the parsed blocks; `files` (paths) get the FASTQ text appended (the
-    end-to-end run's input)."""
+    end-to-end run's input), `texts` (a list) the text itself."""
     import fastqueeze_amd as fq
     t1, t2 = batch_text(gid, args, workers)
+    if texts is not None:
+        texts.append((t1, t2))
     if files:
         for path, t in zip(files, (t1, t2)):
             if t is not None:
@@ -569,6 +575,98 @@ def stream_sizes(block: bytes) -> dict:
     return out
 
 
+def text_leg(args, encs, texts, cfg, want_digest: bytes, device_value: float) -> dict:
+    """The bench's batches handed over as the reader cuts them: each block's
+    FASTQ text in page-locked host memory (sa_host_alloc).  A step is one
+    context's cycle in seqarc_amd -c without its file reader and writer:
+    sa_stage_text (the text DMA'd to HBM and parsed there), sa_run, sa_fetch
+    (the encoded blocks back to host memory).  Its MB/s is the PCIe-inclusive
+    device rate; batch 0's blocks must equal the resident run's."""
+    import numpy as np
+    import fastqueeze_amd as fq
+    t0 = time.perf_counter()
+    bufs, batches = [], []
+    for t1, t2 in texts:
+        hb = []
+        for t in (t1, t2):
+            if t is not None:
+                b = fq.HostBuffer(len(t))
+                b.array[:] = np.frombuffer(t, np.uint8)
+                hb.append(b)
+        bufs += hb
+        a = hb[0].array
+        if len(hb) == 1:
+            batches.append([(a[s:e], None) for s, e in fq.cut_se(a, args.block_size)])
+        else:
+            b2 = hb[1].array
+            batches.append([(a[s1:e1], b2[s2:e2]) for (s1, e1), (s2, e2) in fq.cut_pe(a, b2, args.block_size)])
+    pin_s = time.perf_counter() - t0
+    nbytes = [sum(x.size + (0 if y is None else y.size) for x, y in bl) for bl in batches]
+    lock = threading.Lock()
+    phases, errs, stage_ms = [], [], []
+
+    def one(enc, s, record):
+        t = time.perf_counter()
+        enc.stage_text(batches[s % len(batches)])
+        st = time.perf_counter() - t
+        enc.run(cfg)
+        outs = enc.fetch()
+        if record:
+            ph = enc.phase_times()
+            with lock:
+                phases.append(ph)
+                stage_ms.append(st * 1e3)
+        return outs
+
+    def drive(nsteps, record, per_enc=None):
+        nxt = [0]
+
+        def worker(enc):
+            try:
+                if per_enc is not None:
+                    for s in range(per_enc):
+                        one(enc, s, False)
+                    return
+                while True:
+                    with lock:
+                        s = nxt[0]
+                        if s >= nsteps:
+                            return
+                        nxt[0] += 1
+                    one(enc, s, record)
+            except Exception as e:
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(e,)) for e in encs]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            raise errs[0]
+
+    drive(0, False, per_enc=len(batches))   # every context every batch once: buffers at size
+    outs = one(encs[0], 0, False)
+    got = hashlib.sha256(b"".join(hashlib.sha256(o).digest() for o in outs)).digest()
+    if got != want_digest:
+        raise SystemExit("staged-text leg: batch 0 encoded from its text differs from the resident run")
+    ts = time.perf_counter()
+    drive(args.text_steps, True)
+    el = time.perf_counter() - ts
+    total = sum(nbytes[s % len(nbytes)] for s in range(args.text_steps))
+    for b in bufs:
+        b.close()
+    med = {k: round(float(np.median([p[k] for p in phases])), 2) for k in phases[0]}
+    v = total / el / 1e6
+    return {"value": round(v, 1), "unit": "MB/s", "steps": args.text_steps, "ms_per_step": round(el / args.text_steps * 1e3, 2),
+            "vs_device_encode": round(v / device_value, 3) if device_value else None,
+            "stage_ms_median": round(float(np.median(stage_ms)), 1), "phase_ms": med,
+            "pin_and_cut_s": round(pin_s, 1), "contexts": len(encs),
+            "check": "batch 0's blocks from sa_stage_text identical to the resident run's",
+            "what": "per step: sa_stage_text (FASTQ text in page-locked host memory -> HBM, device parse), "
+                    "sa_run, sa_fetch (encoded blocks -> host); no file reader, no .arc writer"}
+
+
 class Workers:
     """C encoder contexts on one GPU, each driven by its own host thread, taking
     steps (batch encodes) from a shared counter."""
@@ -734,8 +832,10 @@ def main():
         atexit.register(shutil.rmtree, d, True)   # /dev/shm is memory: never leave the files behind
         for f in e2e_files:
             open(f, "wb").close()
+    texts = [] if args.text_leg and rank == 0 and world == 1 else None
     for k, g in enumerate(gids):
-        batches.append(make_batch(g, args, workers, e2e_files if e2e_files and k < args.e2e_batches else None))
+        batches.append(make_batch(g, args, workers, e2e_files if e2e_files and k < args.e2e_batches else None,
+                                  texts))
         log(f"[rank {rank}] batch {g}: {len(batches[-1])} blocks, "
             f"{sum(b.text_bytes for b in batches[-1]) / 1e9:.2f} GB ({time.time() - t0:.1f}s)")
     tmpl = fq.analyze_ids(batches[0][0], args.se)
@@ -929,10 +1029,22 @@ def main():
         "cpu_baseline": cpu,
         "cpu_baseline_threads": cpu_mt,
     }
-    for e in encs:
-        e.close()
     for i in inputs:
         i.close()
+    if texts:
+        t0 = time.perf_counter()
+        try:
+            res["staged_text"] = text_leg(args, encs, texts, cfg, digest, value)
+        except SystemExit:
+            raise
+        except Exception as e:   # (recorded: the headline line stands on its own)
+            log(f"[rank 0] staged-text leg failed: {e!r}")
+            res["staged_text"] = {"value": None, "error": repr(e)[:500]}
+        res["staged_text"]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+        log(f"[rank 0] staged_text: {res['staged_text'].get('value')} MB/s ({res['staged_text']['leg_wall_s']} s)")
+        del texts
+    for e in encs:
+        e.close()
     # the whole host path: the CLI reads the FASTQ from disk (HBM of every rank's
     # contexts released above).  One rank: its batches, 3 times over.  N ranks:
     # rank 0's first batch 2 N times over through one seqarc_amd --devices N

@@ -434,6 +434,31 @@ class Encoder:
         return {names[i].decode(): float(ms[i]) for i in range(n)}
 
 
+class HostBuffer:
+    """Page-locked host memory (sa_host_alloc: portable across devices, so a copy
+    from it is a DMA) seen as a numpy uint8 array: where sa_stage_text wants the
+    reader's text windows."""
+
+    def __init__(self, nbytes: int):
+        self._lib = load_library()
+        self._p = self._lib.sa_host_alloc(max(1, nbytes))
+        if not self._p:
+            raise SeqArcError(f"sa_host_alloc({nbytes}) failed")
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(1, nbytes)).from_address(self._p))[:nbytes]
+
+    def close(self):
+        if self._p:
+            self.array = None
+            self._lib.sa_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Input:
     """A batch of blocks resident in HBM (sa_input_create): uploaded once, encoded
     by any Encoder of the same device, concurrently from several host threads."""

@@ -13,8 +13,9 @@ export TMPDIR=/tmp SA_NO_BUILD=1
 trap 'rm -rf $IN' EXIT
 step() {
     local name=$1; shift
+    local t0=$SECONDS
     "$@"; local rc=$?
-    echo "$name rc=$rc" >> $O/steps.txt
+    echo "$name rc=$rc $((SECONDS - t0))s" >> $O/steps.txt
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
 step tests timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 120 --timeout-method thread -o cache_dir=/tmp/pyc > $O/tests.log 2>&1
