@@ -47,3 +47,28 @@ print(f"next front start - that context's previous assembly end: median {statist
 print("batch  th     span   idle_after  ctx_back(ms before start)")
 for f, g, w in zip(sel, gap + [0], wait_tail + [0]):
     print(f"  {f['th']:>6} {(f['e'] - f['s']) / 1e6:7.1f} {g:8.1f}   {w:8.2f}")
+
+# per context (host thread), batch by batch: front -> pass R -> L passes ->
+# assembly -> the same context's next front
+by = {}
+for k in ks:
+    by.setdefault(k["th"], []).append(k)
+acc = {}
+for th, L in by.items():
+    idx = [i for i, k in enumerate(L) if k["n"] == "k_prep"]
+    for a, b in zip(idx, idx[1:]):
+        d = {k["n"]: k for k in L[a:b]}
+        try:
+            fs, fe = L[a]["s"], d["k_replay_aux_short"]["e"]
+            rs, re_ = d["k_coder_rv"]["s"], d["k_coder_rv"]["e"]
+            l1, l3, ae = d["k_coder_l1"]["s"], d["k_coder_l3"]["e"], d["k_assemble_copy"]["e"]
+        except KeyError:
+            continue
+        for name, v in (("front", fe - fs), ("front end -> pass R start", rs - fe), ("pass R", re_ - rs),
+                        ("pass R end -> L1", l1 - re_), ("L1 .. L3", l3 - l1), ("L3 -> assembly end", ae - l3),
+                        ("assembly end -> next front", L[b]["s"] - ae), ("cycle", L[b]["s"] - fs)):
+            acc.setdefault(name, []).append(v / 1e6)
+print("\nper context (host thread), batch by batch: the cycle front -> pass R -> L passes -> assembly -> next front (ms)")
+for name, v in acc.items():
+    print(f"  {name:28s} n {len(v):3d}  median {statistics.median(v):8.1f}  mean {statistics.mean(v):8.1f}  "
+          f"min {min(v):8.1f}  max {max(v):8.1f}")

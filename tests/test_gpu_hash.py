@@ -93,3 +93,20 @@ def test_empty_and_short_inputs(enc):
     for a, b in zip(got, want):
         assert np.array_equal(a, b)
     ix.close()
+
+
+def test_long_reads_identical(enc):
+    """Reads beyond the row kernel's 512 bp (one lane of their row walks them,
+    sa_hash.hip align_read_serial) mixed with short ones in one launch."""
+    g = genome(1_000_000, 17)
+    fa = fasta([g])
+    orc.hash_index(fa)
+    ix = fq.HashIndex(enc, fa)
+    reads = reads_from(g, 600, 19, lens=(150, 300, 511, 512, 513, 700, 1000, 5000))
+    want = orc.hash_align(reads)
+    got = ix.align(reads)
+    ix.close()
+    for nm, a, b in zip(["ret", "rev", "pos", "mispos", "mistype"], got, want):
+        assert np.array_equal(a, b), nm
+    lens = np.array([len(r) for r in reads])
+    assert ((want[0] >= 0) & (lens > 512)).sum() > 50   # long reads aligned, not only refused
