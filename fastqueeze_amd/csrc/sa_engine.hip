@@ -13,6 +13,7 @@
 #include <cstring>
 #include <condition_variable>
 #include <mutex>
+#include <optional>
 #include <sys/mman.h>
 #include <string>
 #include <vector>
@@ -209,6 +210,7 @@ struct sa_ctx {
     bool prep_wave = std::getenv("SA_PREP_WAVE") != nullptr;   // k_prep_sq instead of k_prep_sq16
     bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
     uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for
+    bool front_warm = false;       // a batch ran: its buffers exist (run_input's `early`)
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -1238,9 +1240,17 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // the front (prep up to the short model runs) holds the device's front
     // scratch.  (The prep before the turn, overlapping another context's
     // front, measured slower: 12.6 vs 13.9 GB/s, round 3 g3i -- the front
-    // kernels are throughput-bound together)
-    FrontTurn front_lock(F, st);
-    if (trace) fprintf(stderr, "[align] front turn taken\n");
+    // kernels are throughput-bound together.)  A context's first batch is the
+    // exception: its prep touches no front scratch, and its own buffers (~34
+    // GB for a 69-block batch) are allocated from the plan -- hipMalloc of
+    // tens of GB takes ~0.3 s, which inside the turn held up every other
+    // context (the command line's first batches: 1.4 s of allocations in
+    // series, round 4 r4c).  So the first batch preps, plans and allocates
+    // first, then takes its turn.
+    const bool early = !c->front_warm;
+    std::optional<FrontTurn> front_lock;
+    if (!early) front_lock.emplace(F, st);
+    if (trace && !early) fprintf(stderr, "[align] front turn taken\n");
     SA_CHECK(c, c->d_counts.ensure((size_t)std::max<uint32_t>(nr, 1) * NCOL * 4));
     SA_CHECK(c, c->d_dege_maxq.ensure((size_t)std::max<uint32_t>(nr, 1)));
     uint8_t* dege_maxq = c->prep_wave ? nullptr : c->d_dege_maxq.as<uint8_t>();   // (k_prep_sq: k_emit's serial path)
@@ -1279,7 +1289,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     } else {
         SA_CHECK(c, c->d_digests.ensure(16 * md5t.size()));
     }
-    if (F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));   // the previous front is done with it
+    if (!early && F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));   // the previous front is done with it
     ev_begin(c, PH_PREP, st);
     if (lossy && run_rblock(c, cfg->lossy, I->seq_bytes, bv)) return -1;
     // thread-per-read kernels: one thread per read (a grid-stride variant with
@@ -1346,35 +1356,54 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // slack: the replay loops read up to 2 chunks past a run's end, pass R one
     // 16-record chunk past a stream's last full segment
     const uint64_t stot = ps.total + KEY_SLACK, atot = pa.total + KEY_SLACK;
+    // AUX sort ping-pong: the sorted keys/values must land in this context's
+    // buffers (the long model runs read them after the front scratch is released)
+    const bool dense = c->aux_dense && aux_bits == (int)AUX_DENSE_BITS && pa.total;
+    const int aux_passes = dense ? 1 : (int)sort_digits(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits).size();
+    const uint64_t max_long = pa.total / LONG_RUN + 1;
+    const uint64_t max_seq_long = ps.total / (SEQ_HALVE_J + 1) + 1;
+    // at most one run per (block, model) and per symbol
+    const uint64_t max_short = std::max<uint64_t>(std::min<uint64_t>(pa.total, (uint64_t)nbk << aux_bits), 1);
+    uint64_t payload = bp.payload_bytes;
+    CoderView cv{};
+    auto ensure_ctx = [&]() -> int {   // this context's own buffers
+        SA_CHECK(c, c->d_auxp_k.ensure(atot * 4));
+        SA_CHECK(c, c->d_auxp_v.ensure(atot * 4));
+        SA_CHECK(c, c->d_prs_seq.ensure(stot * sizeof(PRec)));
+        SA_CHECK(c, c->d_prs_aux.ensure(atot * sizeof(PRec)));
+        SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
+        SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
+        SA_CHECK(c, c->d_huge_sorted.ensure((pa.total / HUGE_RUN + 1) * sizeof(LongRun)));
+        SA_CHECK(c, c->d_nlong.ensure(16));   // RunLists counters: short, huge, long, queue
+        SA_CHECK(c, c->d_tasks.ensure(sizeof(CoderTask) * tasks.size()));
+        SA_CHECK(c, c->d_out_len.ensure(4 * tasks.size()));
+        if (!exact) SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
+        SA_CHECK(c, c->d_asm.ensure(sizeof(AsmBlock) * nbk));
+        SA_CHECK(c, c->d_asm_copies.ensure(4ull * ASM_COPY_WORDS * nbk));
+        SA_CHECK(c, c->d_task_out_base.ensure(8 * tasks.size()));
+        SA_CHECK(c, c->d_final_len.ensure(8 * nbk));
+        return coder_buffers(c, tasks.size(), bp.total_segs, cv);
+    };
+    if (ensure_ctx()) return -1;
+    if (early) {   // (see `early`): now the turn, and the previous front's end on the device
+        front_lock.emplace(F, st);
+        if (trace) fprintf(stderr, "[align] front turn taken\n");
+        if (F->have_ev) SA_CHECK(c, hipStreamWaitEvent(st, F->ev_free, 0));
+    }
+    // the device's front scratch (shared by its contexts: inside the turn)
     for (int i = 0; i < 2; i++) {
         SA_CHECK(c, F->d_seq_k[i].ensure(stot * 4));
         SA_CHECK(c, F->d_seq_v[i].ensure(stot * 4));
     }
     SA_CHECK(c, F->d_auxs_k.ensure(atot * 4));
     SA_CHECK(c, F->d_auxs_v.ensure(atot * 4));
-    SA_CHECK(c, c->d_auxp_k.ensure(atot * 4));
-    SA_CHECK(c, c->d_auxp_v.ensure(atot * 4));
-    // AUX sort ping-pong: the sorted keys/values must land in this context's
-    // buffers (the long model runs read them after the front scratch is released)
-    const bool dense = c->aux_dense && aux_bits == (int)AUX_DENSE_BITS && pa.total;
-    const int aux_passes = dense ? 1 : (int)sort_digits(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits).size();
     DBuf* akb[2] = {aux_passes % 2 ? &F->d_auxs_k : &c->d_auxp_k, aux_passes % 2 ? &c->d_auxp_k : &F->d_auxs_k};
     DBuf* avb[2] = {aux_passes % 2 ? &F->d_auxs_v : &c->d_auxp_v, aux_passes % 2 ? &c->d_auxp_v : &F->d_auxs_v};
     DBuf* skb[2] = {&F->d_seq_k[0], &F->d_seq_k[1]};
     DBuf* svb[2] = {&F->d_seq_v[0], &F->d_seq_v[1]};
     int seq_sorted_buf = 0, aux_sorted_buf = 0;
-    SA_CHECK(c, c->d_prs_seq.ensure(stot * sizeof(PRec)));
-    SA_CHECK(c, c->d_prs_aux.ensure(atot * sizeof(PRec)));
-    SA_CHECK(c, c->d_cum_aux.ensure(atot * 2));
-    const uint64_t max_long = pa.total / LONG_RUN + 1;
-    SA_CHECK(c, c->d_longs.ensure(max_long * sizeof(LongRun)));
-    SA_CHECK(c, c->d_huge_sorted.ensure((pa.total / HUGE_RUN + 1) * sizeof(LongRun)));
-    const uint64_t max_seq_long = ps.total / (SEQ_HALVE_J + 1) + 1;
     SA_CHECK(c, F->d_seq_longs.ensure(max_seq_long * 8));
     SA_CHECK(c, F->d_nseq_long.ensure(4));
-    SA_CHECK(c, c->d_nlong.ensure(16));   // RunLists counters: short, huge, long, queue
-    // at most one run per (block, model) and per symbol
-    const uint64_t max_short = std::max<uint64_t>(std::min<uint64_t>(pa.total, (uint64_t)nbk << aux_bits), 1);
     SA_CHECK(c, F->d_short_at.ensure(max_short * 8));
     SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.tile_seg.size(), 1) * 4 *
                                      sort_hist_per_tile((int)seq_sh, ns > 1 ? (int)seq_sh + seq_bits : 0)));
@@ -1384,14 +1413,6 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, F->d_segs_aux.ensure(sizeof(SortSeg) * nbk));
     SA_CHECK(c, F->d_tile_seq.ensure(std::max<size_t>(ps.tile_seg.size(), 1) * 4));
     SA_CHECK(c, F->d_tile_aux.ensure(std::max<size_t>(pa.tile_seg.size(), 1) * 4));
-    SA_CHECK(c, c->d_tasks.ensure(sizeof(CoderTask) * tasks.size()));
-    SA_CHECK(c, c->d_out_len.ensure(4 * tasks.size()));
-    uint64_t payload = bp.payload_bytes;
-    if (!exact) SA_CHECK(c, c->d_payload.ensure(std::max<uint64_t>(payload, 16)));
-    SA_CHECK(c, c->d_asm.ensure(sizeof(AsmBlock) * nbk));
-    SA_CHECK(c, c->d_asm_copies.ensure(4ull * ASM_COPY_WORDS * nbk));
-    SA_CHECK(c, c->d_task_out_base.ensure(8 * tasks.size()));
-    SA_CHECK(c, c->d_final_len.ensure(8 * nbk));
 
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
     SA_CHECK(c, h2d(c, F->d_segs_seq.p, ps.segs.data(), sizeof(SortSeg) * nbk, st));
@@ -1403,7 +1424,6 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, h2d(c, c->d_tasks.p, tasks.data(), sizeof(CoderTask) * tasks.size(), st));
 
 
-    CoderView cv{};
     cv.tasks = c->d_tasks.as<CoderTask>();
     cv.prs[0] = c->d_prs_seq.as<PRec>();
     cv.prs[1] = c->d_prs_aux.as<PRec>();
@@ -1411,7 +1431,6 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     cv.cum[1] = c->d_cum_aux.as<uint16_t>();
     cv.out = c->d_payload.as<uint8_t>();
     cv.out_len = c->d_out_len.as<uint32_t>();
-    if (coder_buffers(c, tasks.size(), bp.total_segs, cv)) return -1;
 
     // ---- emit (main stream) ----
     ev_begin(c, PH_EMIT, st);
@@ -1547,8 +1566,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // the front scratch is free once the kernels enqueued so far on st are done
     SA_CHECK(c, hipEventRecord(F->ev_free, st));
     F->have_ev = true;
-    front_lock.freed = true;
-    front_lock.unlock();
+    front_lock->freed = true;
+    front_lock->unlock();
     hipStream_t st3 = c->st3, st4 = c->st4;
     if (c->host_waits) SA_CHECK(c, hipEventSynchronize(c->ev_fork_seq));
     else SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
@@ -1617,6 +1636,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     }
     if (trace) fprintf(stderr, "[align] batch queued\n");
     c->have_output = true;
+    c->front_warm = true;
     return 0;
 }
 
