@@ -707,6 +707,10 @@ struct TextPool {
     std::vector<void*> chunks;
     bool pinned = false;   // new windows in page-locked memory (device parse)
     size_t win = 0;        // window bytes of the arena (set before the first get)
+    // (-v) chunks pinned on demand by the reader, and when the last one was
+    std::atomic<uint32_t> on_demand{0};
+    std::atomic<double> last_on_demand{0.0};
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     ~TextPool()
     {
         free.clear();
@@ -739,7 +743,11 @@ struct TextPool {
     {
         std::lock_guard<std::mutex> g(mu);
         if (free.empty() && pinned && win)
-            if (uint8_t* c = static_cast<uint8_t*>(sa_host_alloc(kChunk * win))) add_locked(c);
+            if (uint8_t* c = static_cast<uint8_t*>(sa_host_alloc(kChunk * win))) {
+                add_locked(c);
+                on_demand++;
+                last_on_demand = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            }
         if (free.empty()) {
             Buf<uint8_t> b;
             b.pinned = pinned;
@@ -977,6 +985,7 @@ int compress(const Options& o)
                 else known = false;
             }
         if (known) wins = std::min(wins, (size_t)(pe ? 2 : 1) * (size_t)(tot / (texts.win - (64u << 10)) + 3));
+        if (const char* e = std::getenv("SA_CLI_PREFILL_WINDOWS")) wins = std::strtoull(e, nullptr, 10);   // (A/B)
         prefill_chunks = (wins + TextPool::kChunk - 1) / TextPool::kChunk;
     }
     // contexts: K per device; every device's contexts share one front scratch
@@ -1604,6 +1613,16 @@ int compress(const Options& o)
                     t_ctx, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
                     parse_busy.load(), nparse, fill_busy, cut_busy, stage_busy.load(),
                     dev_parse ? "device" : "host");
+        if (o.verbose && texts.pinned) {
+            size_t nch;
+            {
+                std::lock_guard<std::mutex> g(texts.mu);
+                nch = texts.chunks.size();
+            }
+            fprintf(stderr, "seqarc_amd: text windows: %zu chunks of %zu pinned (%zu ahead, %u on demand, the last at "
+                            "%.3f s)\n", nch, TextPool::kChunk, prefill_chunks, texts.on_demand.load(),
+                    texts.last_on_demand.load());
+        }
         if (o.ingest_only) fprintf(stderr, "seqarc_amd: ingest text crc32 %08x\n", text_crc);
         fprintf(stderr, "seqarc_amd: %zu block(s), %llu -> %llu bytes (%.2fx), %.3f s, %.1f MB/s\n", info.size(),
                 (unsigned long long)total_in, (unsigned long long)(16 + total + tl),
