@@ -38,7 +38,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 #include <zlib.h>
@@ -272,6 +274,15 @@ using Bytes = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
 // a slab of members, `workers` threads inflate them into their places (each
 // member's ISIZE gives its output size) and check their CRCs.  Other gzip files
 // (one member, or several concatenated) inflate on the producer thread.
+// Inflate threads run at a lower priority than the encoder threads: those
+// sleep on their streams and wake for a few host steps per batch, and with
+// every core inflating they woke late (BGZF short leg, r4i: encode busy 14.3 s
+// against 7.1 s on plain input).
+void lower_priority()
+{
+    (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 5);
+}
+
 struct GzStream {
     int fd = -1;
     int workers = 1;
@@ -295,6 +306,7 @@ struct GzStream {
         bgzf = r == 18 && h[0] == 0x1f && h[1] == 0x8b && h[2] == 8 && (h[3] & 4) && h[10] == 6 && h[11] == 0 &&
                h[12] == 'B' && h[13] == 'C' && h[14] == 2 && h[15] == 0;
         prod = std::thread([this]() {
+            lower_priority();
             const bool ok = bgzf ? run_bgzf() : run_plain();
             std::lock_guard<std::mutex> g(mu);
             failed = !ok;
@@ -403,6 +415,7 @@ struct GzStream {
         std::deque<std::unique_ptr<Slab>> jobs;   // in file order
         bool quit = false;
         auto work = [&]() {
+            lower_priority();
             z_stream z{};
             const bool ok = inflateInit2(&z, -15) == Z_OK;
             std::unique_lock<std::mutex> lk(pm);
