@@ -67,7 +67,7 @@ int usage()
     fprintf(stderr,
             "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
             "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
-            "                  [--block-size MiB] [--device D] [--share-device] [--no-ramp] [--release]\n"
+            "                  [--block-size MiB] [--device D] [--share-device] [--ramp] [--release]\n"
             "                  [--stage-ahead]\n"
             "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
             "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
@@ -841,7 +841,7 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_tex
 struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
-         verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = true,
+         verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = false,
          release = false, stage_ahead = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
@@ -1065,16 +1065,18 @@ int compress(const Options& o)
     }
     int64_t B = std::max(1, o.batch);
     const int64_t C = (int64_t)ctxs.size();
-    // batch k = blocks [bstart(k), bstart(k + 1)).  The first batch of each
-    // context ramps up (B (k+1) / (C+1) blocks: the first encode starts after a
-    // fraction of a batch is read, and the contexts' first tails are staggered);
-    // the contexts allocate for B from the start (sa_set_reserve).  --no-ramp: all B.
+    // batch k = blocks [bstart(k), bstart(k + 1)).  --ramp: the first batch of
+    // each context ramps up (B (k+1) / (C+1) blocks: the first encode starts
+    // after a fraction of a batch is read, and the contexts' first tails are
+    // staggered); the contexts allocate for B from the start (sa_set_reserve).
+    // Off by default since round 4: a batch's latency is its longest chain's
+    // whatever its size, so the ramp's five small batches cost a round of
+    // throughput (42.8 GB: 5,390 MB/s with it, 6,642 without, r4m).
     // A plain-file input that fits one round (C batches of B blocks, by its
-    // size) is dealt as C equal batches instead: with the ramp its last blocks
-    // waited for a second round of batch latencies (round 3 g4g: 17.8 GB, five
-    // ramp batches, then three more).
+    // size) is dealt as C equal batches (round 3 g4g: with the ramp its last
+    // blocks waited for a second round of batch latencies).
     bool ramp = o.ramp;
-    if (ramp && !o.host_only && !o.ingest_only && !in1.is_gz && (!pe || !in2.is_gz)) {
+    if (!o.host_only && !o.ingest_only && !in1.is_gz && (!pe || !in2.is_gz)) {
         uint64_t tot = 0;
         struct stat st;
         for (const char* f : {o.f1, pe ? o.f2 : nullptr})
@@ -1943,6 +1945,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--host-only")) o.host_only = true;
         else if (!strcmp(a, "--ingest-only")) o.ingest_only = true;
         else if (!strcmp(a, "--no-ramp")) o.ramp = false;
+        else if (!strcmp(a, "--ramp")) o.ramp = true;
         else if (!strcmp(a, "--release")) o.release = true;
         else if (!strcmp(a, "--stage-ahead")) o.stage_ahead = true;
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
