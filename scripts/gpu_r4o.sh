@@ -4,11 +4,18 @@
 # sonames); seqarc_amd links /opt/rocm's (7.2).  The CLI on 42.8 GB with the
 # pass-R probe on each runtime: is the clock drop the runtime's?
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r4o}
+TAG=${TAG:-r4o2}
 O=$R/gpurun_out/$TAG
 IN=/dev/shm/sa_bench_inputs
 E=/dev/shm/sa_cli_e2e
-TL=$(python3 -c "import os, torch; print(os.path.join(os.path.dirname(torch.__file__), 'lib'))")
+TL0=$(python3 -c "import os, torch; print(os.path.join(os.path.dirname(torch.__file__), 'lib'))")
+# torch ships libamdhip64.so / libhsa-runtime64.so (sonames .so.7 / .so.1):
+# a directory of links under the soname file names, then torch's own lib dir
+TL=/tmp/sa_torch_rt
+mkdir -p $TL
+ln -sf $TL0/libamdhip64.so $TL/libamdhip64.so.7
+ln -sf $TL0/libhsa-runtime64.so $TL/libhsa-runtime64.so.1
+TL=$TL:$TL0
 mkdir -p $O
 cd $R
 export TMPDIR=/tmp SA_NO_BUILD=1
