@@ -1522,6 +1522,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, hipGetLastError());
     ev_finish(c, PH_REPLAY_SEQ, st);
     ev_begin(c, PH_SORT_AUX, st);
+    bool runs_from_hist = false;   // one dense pass: the run lists from the scan (k_runs_dense)
     if (dense) {
         // (the counts were read back right after the emit: the SEQ sort and
         // replay queued above keep the device busy while the host waits here)
@@ -1529,6 +1530,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         uint32_t dmax = 0;
         for (uint32_t b = 0; b < nbk; b++) dmax = std::max(dmax, c->h_aux_nmod[b]);
         const int dbits = dmax > 512 ? (int)AUX_DENSE_BITS : 9;
+        runs_from_hist = dbits == 9 && !std::getenv("SA_FIND_RUNS");   // (SA_FIND_RUNS=1: k_find_runs, A/B)
         if (run_sort(c, st, pa, F->d_segs_aux, F->d_tile_aux, F->d_hist_aux, akb, avb, 0, dbits, aux_sorted_buf, true,
                      c->d_aux_tab.as<uint64_t>()))
             return -1;
@@ -1555,8 +1557,11 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                       c->d_huge_sorted.as<LongRun>()};
     SA_CHECK(c, hipMemsetAsync(ctr, 0, 16, st));
     if (pa.total) {
-        hipLaunchKernelGGL(k_find_runs, dim3((uint32_t)((pa.total / FIND_ITEMS + 255) / 256)), dim3(256), 0, st, sva,
-                           ak, rl);
+        if (runs_from_hist)
+            hipLaunchKernelGGL(k_runs_dense<9>, dim3((nbk * 512u + 255) / 256), dim3(256), 0, st, sva, ak, rl);
+        else
+            hipLaunchKernelGGL(k_find_runs, dim3((uint32_t)((pa.total / FIND_ITEMS + 255) / 256)), dim3(256), 0, st,
+                               sva, ak, rl);
         hipLaunchKernelGGL(k_sort_huge, dim3(1), dim3(1024), 0, st, rl);
         hipLaunchKernelGGL(k_replay_aux_short, dim3(SHORT_GRID), dim3(RP_THREADS), 0, st, sva, ak, av, sink_aux, rl,
                            d_err);

@@ -1676,6 +1676,37 @@ struct RunLists {
     LongRun* huge_sorted;  // the huge runs, longest first (k_sort_huge)
 };
 
+// The same run lists when the AUX space was sorted by ONE dense pass (§4.2):
+// the runs are then exactly the digit buckets, so their starts and lengths are
+// the scan's per-segment digit bases (hist row of the segment's first tile)
+// and no sorted key is read but each run's first (for its model id).  One
+// thread per (segment, digit); the pad keys sort into the last digit, after
+// the segment's symbols, and are cut off by the segment's count.
+template <int DB>
+__global__ __launch_bounds__(256) void k_runs_dense(const SortView sv, const uint32_t* __restrict__ keys,
+                                                    const RunLists rl)
+{
+    constexpr uint32_t ND = 1u << DB;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t seg = gid / ND, d = gid % ND;
+    if (seg >= sv.nsegs) return;
+    const SortSeg& sg = sv.segs[seg];
+    if (!sg.ntiles) return;
+    const uint32_t* H = sv.hist + (size_t)sg.tile0 * ND;
+    const uint32_t s = H[d];
+    uint32_t e = d + 1 < ND ? H[d + 1] : sg.ntiles * SORT_TILE;
+    if (e > sg.count) e = sg.count;
+    if (e <= s) return;
+    const size_t i = sg.base + s;
+    if (e - s >= LONG_RUN) {
+        const LongRun lr{i, sg.base + e, sg.base, keys[i] >> AUX_SYM_BITS, 0};
+        if (e - s >= HUGE_RUN) rl.longs[atomicAdd(rl.n_huge, 1u)] = lr;
+        else rl.longs[rl.cap_long - 1 - atomicAdd(rl.n_long, 1u)] = lr;
+    } else {
+        rl.short_at[atomicAdd(rl.n_short, 1u)] = i;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_find_runs(const SortView sv, const uint32_t* __restrict__ keys,
                                                    const RunLists rl)
 {
