@@ -211,6 +211,9 @@ struct sa_ctx {
     bool emit_wave = std::getenv("SA_EMIT_WAVE") != nullptr;
     uint32_t reserve_blocks = 0;   // sa_set_reserve: the batch size to allocate for
     bool front_warm = false;       // a batch ran: its buffers exist (run_input's `early`)
+    // records per chunk in the L passes (SA_L_CHUNK=16: 56 VGPRs, 8 waves per
+    // SIMD, half a line per chunk; 32: 88 VGPRs, 5 waves, a whole line)
+    uint32_t l_chunk = std::getenv("SA_L_CHUNK") && std::atoi(std::getenv("SA_L_CHUNK")) == 16 ? 16u : 32u;
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -670,7 +673,7 @@ void coder_launch_l12(sa_ctx* c, hipStream_t st, const TaskList& tl, const Coder
 {
     if (!tl.count) return;
     const uint32_t lgrid = (uint32_t)((tl.total_segs + 255) / 256);
-    hipLaunchKernelGGL(k_coder_l1, dim3(lgrid), dim3(256), 0, st, cv, tl);
+    hipLaunchKernelGGL(c->l_chunk == 16 ? k_coder_l1<16> : k_coder_l1<32>, dim3(lgrid), dim3(256), 0, st, cv, tl);
     hipLaunchKernelGGL(k_coder_l2, dim3(tl.count), dim3(L2_THREADS), 0, st, cv, tl);
 }
 
@@ -678,7 +681,7 @@ void coder_launch_l3(sa_ctx* c, hipStream_t st, const TaskList& tl, const CoderV
 {
     if (!tl.count) return;
     const uint32_t lgrid = (uint32_t)((tl.total_segs + 255) / 256);
-    hipLaunchKernelGGL(k_coder_l3, dim3(lgrid), dim3(256), 0, st, cv, tl);
+    hipLaunchKernelGGL(c->l_chunk == 16 ? k_coder_l3<16> : k_coder_l3<32>, dim3(lgrid), dim3(256), 0, st, cv, tl);
 }
 
 // Range coder driver (DESIGN.md "Coder"): pass R of every listed chain (on st,

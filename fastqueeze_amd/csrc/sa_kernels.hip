@@ -2618,6 +2618,7 @@ __device__ inline uint32_t list_find(const TaskList& tl, uint64_t gi)
 }
 
 // L1: one lane per segment -> its LowMap.
+template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_coder_l1(const CoderView cv, const TaskList tl)
 {
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2627,7 +2628,7 @@ __global__ __launch_bounds__(256) void k_coder_l1(const CoderView cv, const Task
     const uint32_t g = tl.run[li].start_seg + (uint32_t)(gi - tl.gbase[li]);
     const size_t at = tk.rec_base + (size_t)g * SEG_SYMS;
     cv.maps[tk.seg_base + g] =
-        seg_lowmap(cv.prs[tk.space] + at, cv.cum[tk.space] ? cv.cum[tk.space] + at : nullptr,
+        seg_lowmap<CH>(cv.prs[tk.space] + at, cv.cum[tk.space] ? cv.cum[tk.space] + at : nullptr,
                    cv.ck_r[tk.seg_base + g], seg_count(tk.n, g));
 }
 
@@ -2718,6 +2719,7 @@ __global__ __launch_bounds__(256) void k_task_ends(const CoderView cv, const Tas
 }
 
 // L3: one lane per segment: the exact coder from (range, low) at its offset.
+template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_coder_l3(const CoderView cv, const TaskList tl)
 {
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2730,7 +2732,7 @@ __global__ __launch_bounds__(256) void k_coder_l3(const CoderView cv, const Task
     const uint64_t sg = tk.seg_base + g;
     const uint32_t off = cv.off_at[sg];
     const bool last = g + 1 == tk.nseg;
-    const SegEnd e = seg_code(cv.prs[tk.space] + at, cv.cum[tk.space] ? cv.cum[tk.space] + at : nullptr,
+    const SegEnd e = seg_code<CH>(cv.prs[tk.space] + at, cv.cum[tk.space] ? cv.cum[tk.space] + at : nullptr,
                               cv.ck_r[sg], cv.low_at[sg],
                               seg_count(tk.n, g), cv.out + tk.out_base + off, tk.out_cap > off ? tk.out_cap - off : 0,
                               last);

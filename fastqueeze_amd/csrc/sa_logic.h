@@ -593,33 +593,33 @@ SA_HD LowMap lowmap_compose(const LowMap& a, const LowMap& b)
 // the chain), so the 32 records cost no more registers than 16 with their
 // reciprocals did (88 VGPRs).
 constexpr uint32_t RC_CHUNK = 32;
-template <bool PACKED, class Fn>
+template <bool PACKED, uint32_t CH = RC_CHUNK, class Fn>
 SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
 {
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    for (uint32_t b = 0; b < n; b += RC_CHUNK) {
-        PRec p[RC_CHUNK];
-        uint32_t c[PACKED ? 1 : RC_CHUNK];
+    for (uint32_t b = 0; b < n; b += CH) {
+        PRec p[CH];
+        uint32_t c[PACKED ? 1 : CH];
 #pragma unroll
-        for (uint32_t k = 0; k < RC_CHUNK; k++) {
+        for (uint32_t k = 0; k < CH; k++) {
             const uint32_t i = b + k < n ? b + k : n - 1;
             p[k] = P[i];
             if constexpr (!PACKED) c[k] = cum[i];
         }
 #pragma unroll
-        for (uint32_t k = 0; k < RC_CHUNK; k++)
+        for (uint32_t k = 0; k < CH; k++)
             if (b + k < n) fn(p[k], recip32z(p[k].tf & tmask), PACKED ? (p[k].tf >> 8) & 0xffu : c[PACKED ? 0 : k]);
     }
 }
 
-template <bool PACKED>
+template <bool PACKED, uint32_t CH = RC_CHUNK>
 SA_HD LowMap seg_lowmap_t(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
 {
     LowMap m{0ull, 0u, 0u};
     uint64_t low = 0;
     uint32_t sbits = 0;
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
+    seg_for_each<PACKED, CH>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
         uint32_t nb;
         const uint32_t q = range_step(r, pr, pm, tmask, nb);
         low = shl64(low + (uint64_t)c * q, 8 * nb);
@@ -644,14 +644,14 @@ struct SegEnd {
 
 SA_HD uint32_t seg_count(uint32_t n, uint32_t seg) { return n - seg * SEG_SYMS < SEG_SYMS ? n - seg * SEG_SYMS : SEG_SYMS; }
 
-template <bool PACKED>
+template <bool PACKED, uint32_t CH = RC_CHUNK>
 SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
                         uint64_t cap, bool finish)
 {
     SegEnd e{0, 0, 0, 0};
     uint32_t op = 0;
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    seg_for_each<PACKED>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
+    seg_for_each<PACKED, CH>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
         const uint32_t t = pr.tf & tmask, f = pr.tf >> 16;
         uint32_t q = mulhi32(r, pm);
         q -= (r < q * t) ? 1u : 0u;
@@ -682,14 +682,17 @@ SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t
 }
 
 // cum == nullptr: packed (SEQ) records
+template <uint32_t CH = RC_CHUNK>
 SA_HD LowMap seg_lowmap(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
 {
-    return cum ? seg_lowmap_t<false>(P, cum, r, n) : seg_lowmap_t<true>(P, cum, r, n);
+    return cum ? seg_lowmap_t<false, CH>(P, cum, r, n) : seg_lowmap_t<true, CH>(P, cum, r, n);
 }
+template <uint32_t CH = RC_CHUNK>
 SA_HD SegEnd seg_code(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
                       uint64_t cap, bool finish)
 {
-    return cum ? seg_code_t<false>(P, cum, r, low, n, o, cap, finish) : seg_code_t<true>(P, cum, r, low, n, o, cap, finish);
+    return cum ? seg_code_t<false, CH>(P, cum, r, low, n, o, cap, finish)
+               : seg_code_t<true, CH>(P, cum, r, low, n, o, cap, finish);
 }
 
 // ---- block assembly plan (k_assemble; doFqzEncode@0x42d2d0) ----------------
