@@ -466,15 +466,18 @@ void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const ui
     else
         hipLaunchKernelGGL((k_sort_hist<DB, false>), hgrid, dim3(SORT_THREADS), 0, st, sv, kin, shift);
     hipLaunchKernelGGL(k_sort_scan<DB>, dim3(sv.nsegs), dim3(1024), 0, st, sv);
-    if (wide)
-        hipLaunchKernelGGL((k_sort_scatter<DB, true, false>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin,
-                           kout, vout, shift);
-    else if (sv.dense)
-        hipLaunchKernelGGL((k_sort_scatter<DB, false, true>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin,
-                           kout, vout, shift);
-    else
-        hipLaunchKernelGGL((k_sort_scatter<DB, false, false>), dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin,
-                           kout, vout, shift);
+    // (vin = nullptr: the values are the elements' index, IDX)
+    auto scatter = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(sv.ntiles), dim3(SORT_THREADS), 0, st, sv, kin, vin, kout, vout, shift); };
+    if (wide) {
+        if (vin) scatter(k_sort_scatter<DB, true, false, false>);
+        else scatter(k_sort_scatter<DB, true, false, true>);
+    } else if (sv.dense) {
+        if (vin) scatter(k_sort_scatter<DB, false, true, false>);
+        else scatter(k_sort_scatter<DB, false, true, true>);
+    } else {
+        if (vin) scatter(k_sort_scatter<DB, false, false, false>);
+        else scatter(k_sort_scatter<DB, false, false, true>);
+    }
 }
 
 // sorts keys by bits [lo, hi) (bits below lo ride along); the result is in

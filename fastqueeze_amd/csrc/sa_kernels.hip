@@ -1369,7 +1369,9 @@ __global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
 
 // WIDE: a segment of >= 2^30 keys (the HASH index of a genome of > 2^31
 // bases sorts all its seeds as one segment): 64-bit element offsets
-template <int DB, bool WIDE, bool DENSE>
+// IDX: the input values are the elements' index in the segment (vin unused;
+// each value is computed where it is written, so no register holds it)
+template <int DB, bool WIDE, bool DENSE, bool IDX>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv,
                                                                const uint32_t* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin,
@@ -1391,14 +1393,16 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
     for (uint32_t i = threadIdx.x; i < NW * ND; i += SORT_THREADS) (&wc[0][0])[i] = 0;
     __syncthreads();
     const size_t wbase = sg.base + (size_t)lt * SORT_TILE + (size_t)w * (64 * SORT_ITEMS);
-    uint32_t k[SORT_ITEMS], v[SORT_ITEMS], rk[SORT_ITEMS];
+    uint32_t k[SORT_ITEMS], v[IDX ? 1 : SORT_ITEMS], rk[SORT_ITEMS];
+    // IDX: the values are the index in the segment (a space's first pass: the
+    // emitters leave the values out)
+    auto val = [&](int r) __attribute__((always_inline)) -> uint32_t {
+        return IDX ? lt * SORT_TILE + w * (64 * SORT_ITEMS) + (uint32_t)r * 64 + lane : v[IDX ? 0 : r];
+    };
 #pragma unroll
     for (int r = 0; r < SORT_ITEMS; r++) {
         k[r] = kin[wbase + (size_t)r * 64 + lane];
-        // vin = nullptr: the values are the index in the segment (the AUX
-        // space's first pass: the emitters leave the values out)
-        v[r] = vin ? vin[wbase + (size_t)r * 64 + lane]
-                   : lt * SORT_TILE + w * (64 * SORT_ITEMS) + (uint32_t)r * 64 + lane;
+        if constexpr (!IDX) v[r] = vin[wbase + (size_t)r * 64 + lane];
     }
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const uint64_t* T = DENSE ? sv.dense + (size_t)sv.tile_seg[t] * AUX_DENSE_WORDS : nullptr;
@@ -1481,7 +1485,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = v[r];
+        for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = val(r);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < SORT_ITEMS; r++) vo[(uint64_t)ro[r]] = sb[threadIdx.x + (uint32_t)r * SORT_THREADS];
@@ -1501,7 +1505,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = v[r];
+        for (int r = 0; r < SORT_ITEMS; r++) sb[rk[r]] = val(r);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < SORT_ITEMS; r++)
