@@ -1494,7 +1494,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             c->h_aux_nmod_cap = 2ull * nbk;
         }
         SA_CHECK(c, hipMemsetAsync(c->d_aux_bm.p, 0, 4ull * AUX_DENSE_WORDS * nbk, st));
-        hipLaunchKernelGGL(k_aux_presence, dim3((uint32_t)pa.tile_seg.size()), dim3(SORT_THREADS), 0, st, sva,
+        hipLaunchKernelGGL(k_aux_presence, dim3((uint32_t)((pa.tile_seg.size() + PRESENCE_TILES - 1) / PRESENCE_TILES)),
+                           dim3(SORT_THREADS), 0, st, sva,
                            akb[0]->as<uint32_t>(), c->d_aux_bm.as<uint32_t>());
         hipLaunchKernelGGL(k_aux_dense, dim3(nbk), dim3(256), 0, st, c->d_aux_bm.as<uint32_t>(),
                            c->d_aux_tab.as<uint64_t>(), c->d_aux_nmod.as<uint32_t>());

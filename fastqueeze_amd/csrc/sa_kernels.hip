@@ -840,12 +840,27 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
     __shared__ uint32_t comp[EMIT_WAVES][64];
     __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES) {
-        // (parts = EMIT_DEGE: only the reads with N / IUPAC bases have work)
-        if (parts == EMIT_DEGE && !read_col_count(bv, counts, totals, r, C_CH)) continue;
+    if (parts == EMIT_DEGE) {
+        // only the reads with N / IUPAC bases have work (~1 % of 150 bp reads):
+        // a wave tests 64 reads at once (each lane one read's CH count, four
+        // dependent loads) and walks the ones that have some (round 3 tested one
+        // read per wave step: 5.6 ms of dependent loads per batch, r4n)
+        const uint32_t stride = gridDim.x * EMIT_WAVES * 64;
+        for (uint32_t r0 = (blockIdx.x * EMIT_WAVES + w) * 64; r0 < bv.nreads_total; r0 += stride) {
+            const uint32_t r = r0 + lane;
+            uint64_t m = __ballot(r < bv.nreads_total && read_col_count(bv, counts, totals, r, C_CH) != 0);
+            while (m) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                emit_sq_read(bv, r0 + j, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals,
+                             dege_maxq, seq_sh, parts);
+            }
+        }
+        return;
+    }
+    for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
         emit_sq_read(bv, r, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals, dege_maxq,
                      seq_sh, parts);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1175,27 +1190,52 @@ constexpr int SORT_MIN_DB = 7, SORT_MAX_DB = 9;   // (SA_SORT_MIN_DB=8: round 1'
 constexpr uint32_t AUX_DENSE_BITS = 17;                             // model ids < 2^17
 constexpr uint32_t AUX_DENSE_WORDS = 1u << (AUX_DENSE_BITS - 5);    // 4096 bitmap words per block
 
+constexpr uint32_t PRESENCE_TILES = 16;   // tiles per k_aux_presence workgroup
+
 __global__ __launch_bounds__(SORT_THREADS) void k_aux_presence(const SortView sv, const uint32_t* __restrict__ keys,
                                                                uint32_t* __restrict__ bm)
 {
+    // PRESENCE_TILES consecutive tiles per workgroup (one block's, mostly):
+    // the LDS bitmap is flushed to the block's global bitmap once per block
+    // seen, not once per tile (a tile flushed up to one atomicOr per nonzero
+    // word, ~37 M global atomics per batch onto a few hot words); and a key
+    // whose model equals its left neighbour's (consecutive stream positions:
+    // quality contexts repeat) sets nothing
     __shared__ uint32_t lb[AUX_DENSE_WORDS];
+    const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i = threadIdx.x; i < AUX_DENSE_WORDS; i += SORT_THREADS) lb[i] = 0;
     __syncthreads();
-    const uint32_t t = blockIdx.x, seg = sv.tile_seg[t];
-    const SortSeg& sg = sv.segs[seg];
-    const uint32_t* K = keys + sg.base + (size_t)(t - sg.tile0) * SORT_TILE;
-    uint32_t k[SORT_ITEMS];
+    const uint32_t t0 = blockIdx.x * PRESENCE_TILES;
+    const uint32_t t1 = t0 + PRESENCE_TILES < sv.ntiles ? t0 + PRESENCE_TILES : sv.ntiles;
+    auto flush = [&](uint32_t seg) __attribute__((always_inline)) {
+        __syncthreads();
+        uint32_t* B = bm + (size_t)seg * AUX_DENSE_WORDS;
+        for (uint32_t i = threadIdx.x; i < AUX_DENSE_WORDS; i += SORT_THREADS) {
+            if (lb[i]) atomicOr(&B[i], lb[i]);
+            lb[i] = 0;
+        }
+        __syncthreads();
+    };
+    uint32_t cur = t0 < t1 ? sv.tile_seg[t0] : 0;
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t seg = sv.tile_seg[t];   // (workgroup-uniform)
+        if (seg != cur) {
+            flush(cur);
+            cur = seg;
+        }
+        const SortSeg& sg = sv.segs[seg];
+        const uint32_t* K = keys + sg.base + (size_t)(t - sg.tile0) * SORT_TILE;
+        uint32_t k[SORT_ITEMS];
 #pragma unroll
-    for (int r = 0; r < SORT_ITEMS; r++) k[r] = K[threadIdx.x + r * SORT_THREADS];
+        for (int r = 0; r < SORT_ITEMS; r++) k[r] = K[threadIdx.x + r * SORT_THREADS];
 #pragma unroll
-    for (int r = 0; r < SORT_ITEMS; r++) {
-        const uint32_t m = k[r] >> AUX_SYM_BITS;
-        if (k[r] != SORT_PAD && m < (1u << AUX_DENSE_BITS)) atomicOr(&lb[m >> 5], 1u << (m & 31));
+        for (int r = 0; r < SORT_ITEMS; r++) {
+            const uint32_t m = k[r] == SORT_PAD ? 0xffffffffu : k[r] >> AUX_SYM_BITS;
+            const uint32_t left = __shfl_up(m, 1, 64);
+            if (m < (1u << AUX_DENSE_BITS) && (lane == 0 || left != m)) atomicOr(&lb[m >> 5], 1u << (m & 31));
+        }
     }
-    __syncthreads();
-    uint32_t* B = bm + (size_t)seg * AUX_DENSE_WORDS;
-    for (uint32_t i = threadIdx.x; i < AUX_DENSE_WORDS; i += SORT_THREADS)
-        if (lb[i]) atomicOr(&B[i], lb[i]);
+    if (t0 < t1) flush(cur);
 }
 
 // per block (one workgroup): the rank table and the number of models
