@@ -163,6 +163,7 @@ struct CoderView {
     uint32_t* off_at;          // per segment: output offset of its first byte (L2)
     uint32_t* out_len;         // per task
     uint32_t* first_sq;        // per task: first segment whose exact coding squeezed
+    uint32_t lprio;            // the L passes at s_setprio 2 (SA_L_PRIO=1, A/B)
 };
 
 struct Md5Task {

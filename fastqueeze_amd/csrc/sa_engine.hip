@@ -214,6 +214,9 @@ struct sa_ctx {
     // records per chunk in the L passes (SA_L_CHUNK=16: 56 VGPRs, 8 waves per
     // SIMD, half a line per chunk; 32: 88 VGPRs, 5 waves, a whole line)
     uint32_t l_chunk = std::getenv("SA_L_CHUNK") && std::atoi(std::getenv("SA_L_CHUNK")) == 16 ? 16u : 32u;
+    // the L passes at issue priority 2 (they are on the batch's critical path,
+    // the other contexts' fronts beside them are not always; SA_L_PRIO=1, A/B)
+    uint32_t l_prio = std::getenv("SA_L_PRIO") && std::atoi(std::getenv("SA_L_PRIO")) != 0 ? 1u : 0u;
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
@@ -1437,6 +1440,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     cv.cum[1] = c->d_cum_aux.as<uint16_t>();
     cv.out = c->d_payload.as<uint8_t>();
     cv.out_len = c->d_out_len.as<uint32_t>();
+    cv.lprio = c->l_prio;
 
     // ---- emit (main stream) ----
     ev_begin(c, PH_EMIT, st);

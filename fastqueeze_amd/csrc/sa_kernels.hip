@@ -88,6 +88,16 @@ __device__ inline void wg256_excl_scan(uint32_t v, uint32_t& excl, uint32_t* sh 
 
 // s_setprio 3 when `prio` (a kernel argument, so uniform): the branch is scalar
 // code of its own, outside the compiler's control flow
+__device__ __forceinline__ void set_l_prio(uint32_t prio)
+{
+    asm volatile(
+        "s_cmp_eq_u32 %0, 0\n\t"
+        "s_cbranch_scc1 1f\n\t"
+        "s_setprio 2\n"
+        "1:" ::"s"(prio)
+        : "scc");
+}
+
 __device__ __forceinline__ void set_chain_prio(uint32_t prio)
 {
     asm volatile(
@@ -2665,6 +2675,7 @@ __device__ inline uint32_t list_find(const TaskList& tl, uint64_t gi)
 template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_coder_l1(const CoderView cv, const TaskList tl)
 {
+    set_l_prio(cv.lprio);
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= tl.total_segs) return;
     const uint32_t li = list_find(tl, gi);
@@ -2766,6 +2777,7 @@ __global__ __launch_bounds__(256) void k_task_ends(const CoderView cv, const Tas
 template <uint32_t CH>
 __global__ __launch_bounds__(256) void k_coder_l3(const CoderView cv, const TaskList tl)
 {
+    set_l_prio(cv.lprio);
     const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= tl.total_segs) return;
     const uint32_t li = list_find(tl, gi);
