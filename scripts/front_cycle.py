@@ -11,8 +11,8 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 
 
-def nm(r):
-    return r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sa::", "")
+def nm(r):   # (template arguments dropped: k_coder_l1<32u> -> k_coder_l1)
+    return r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sa::", "").split("<")[0]
 
 
 ks = sorted(({"n": nm(r), "s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"]), "th": r["Thread_Id"]}
