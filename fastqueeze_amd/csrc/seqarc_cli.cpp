@@ -39,6 +39,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
@@ -72,6 +73,7 @@ int usage()
             "                  [--stage-ahead]\n"
             "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
             "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
+            "       (-s with -i / -c / -d and ref.fa: the index image in /dev/shm/<ref file name>)\n"
             "       (-c / -d with ref.fa: the reference path; -I N insert size, --maxmis M)\n");
     return 2;
 }
@@ -880,11 +882,13 @@ struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
          verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = false,
-         release = false, stage_ahead = false;
+         release = false, stage_ahead = false, shm = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
 };
+
+bool shm_publish(const char* ref, const uint8_t* p, size_t n, bool verbose);
 
 // ---- SeqArc -i ref.fa: the HASH index (HashAlignment::buildRefIndex@0x410190,
 //      HashRefIndex32::writeIndexFile@0x41ed00 -> "<ref>.hash"; MD5File@0x405950 of
@@ -919,6 +923,7 @@ int build_index(const Options& o)
         fprintf(stderr, "seqarc_amd: cannot write the index files of %s\n", o.ref);
         rc = 1;
     }
+    if (rc == 0 && o.shm && !shm_publish(o.ref, file.data(), file.size(), o.verbose)) rc = 1;
     const double s_load = std::chrono::duration<double>(t1 - t0).count(),
                  s_build = std::chrono::duration<double>(t2 - t1).count(),
                  s_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -933,14 +938,129 @@ int build_index(const Options& o)
 // the MD5 the archive records (getMd5@0x416810 reads "<ref>.md5")
 struct RefFiles {
     std::vector<uint8_t> hash, fasta;
+    // the index image: hash's bytes, or (-s) a /dev/shm object mapped read-only
+    const uint8_t* hp = nullptr;
+    size_t hn = 0;
+    void* map = nullptr;
+    size_t map_len = 0;
     uint8_t md5[16] = {0};
+    bool have_hash() const { return hn > 16; }
+    void drop_hash()
+    {
+        hash.clear();
+        hash.shrink_to_fit();
+        if (map) munmap(map, map_len);
+        map = nullptr;
+        hp = nullptr;
+        hn = 0;
+    }
+    ~RefFiles() { drop_hash(); }
 };
 
-bool load_ref(const char* ref, bool need_fasta, RefFiles& rf)
+// the bytes an index image's header announces (HashRefIndex32::loadRefIndexShm@0x41ef80:
+// K, bases, words, positions; words, num[4^K], ind[4^K], positions), 0 if no header
+uint64_t hash_image_bytes(const uint8_t* p, size_t n)
+{
+    if (n < 16) return 0;
+    uint32_t h[4];
+    memcpy(h, p, 16);
+    if (h[0] < 1 || h[0] > 16) return 0;
+    return 16 + 4ull * (h[2] + 2 * (1ull << (2 * h[0])) + h[3]);
+}
+
+// -s: the index image in POSIX shared memory under the reference's file name
+// (IHashRefIndex::createShm@0x41f280: shm_open of the basename, an existing
+// object of the announced size is kept, one of another size replaced;
+// HashRefIndex32::createRefIndexShm@0x41f520 copies the image in after the
+// file was read).  Later runs map it instead of reading <ref>.hash.
+std::string shm_name(const char* ref)
 {
     const std::string r(ref);
-    const bool have_hash = slurp(r + ".hash", rf.hash) && rf.hash.size() > 16;
-    if (!have_hash) rf.hash.clear();
+    return r.substr(r.rfind('/') + 1);
+}
+
+bool shm_publish(const char* ref, const uint8_t* p, size_t n, bool verbose)
+{
+    const std::string nm = shm_name(ref);
+    int fd = shm_open(nm.c_str(), O_RDWR, 0);
+    if (fd >= 0) {
+        struct stat sb;
+        const bool same = fstat(fd, &sb) == 0 && (uint64_t)sb.st_size == n;
+        close(fd);
+        if (same) {
+            fprintf(stderr, "createHashShm %s has existed.\n", nm.c_str());
+            return true;
+        }
+        shm_unlink(nm.c_str());
+    }
+    fd = shm_open(nm.c_str(), O_CREAT | O_EXCL | O_RDWR, 0644);
+    if (fd < 0) {
+        fprintf(stderr, "shm_open fail.\n");
+        return false;
+    }
+    bool ok = ftruncate(fd, (off_t)n) == 0;
+    if (!ok) fprintf(stderr, "ftruncate fail.\n");
+    void* m = ok ? mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+    close(fd);
+    if (ok && m == MAP_FAILED) {
+        fprintf(stderr, "mmap fail.\n");
+        ok = false;
+    }
+    if (!ok) {
+        shm_unlink(nm.c_str());
+        return false;
+    }
+    memcpy(m, p, n);
+    munmap(m, n);
+    if (verbose) fprintf(stderr, "seqarc_amd: index image in /dev/shm/%s (%zu bytes)\n", nm.c_str(), n);
+    return true;
+}
+
+// 1: mapped, 0: no such object, -1: an object that is not an index image
+int shm_map(const char* ref, RefFiles& rf)
+{
+    const std::string nm = shm_name(ref);
+    const int fd = shm_open(nm.c_str(), O_RDONLY, 0);
+    if (fd < 0) return 0;
+    struct stat sb;
+    void* m = MAP_FAILED;
+    size_t n = 0;
+    if (fstat(fd, &sb) == 0 && sb.st_size >= 16) {
+        n = (size_t)sb.st_size;
+        m = mmap(nullptr, n, PROT_READ, MAP_SHARED, fd, 0);
+    }
+    close(fd);
+    if (m == MAP_FAILED || hash_image_bytes((const uint8_t*)m, n) != n) {
+        if (m != MAP_FAILED) munmap(m, n);
+        fprintf(stderr, "/dev/shm/ %s is wrong file, please delete\n", nm.c_str());
+        return -1;
+    }
+    rf.map = m;
+    rf.map_len = n;
+    rf.hp = (const uint8_t*)m;
+    rf.hn = n;
+    return 1;
+}
+
+bool load_ref(const char* ref, bool need_fasta, RefFiles& rf, bool use_shm = false, bool verbose = false)
+{
+    const std::string r(ref);
+    bool have_hash = false;
+    if (use_shm) {   // (HashAlignment::loadRefIndex: loadRefIndexShm, else loadRefIndexFile)
+        const int m = shm_map(ref, rf);
+        if (m < 0) return false;
+        have_hash = m == 1;
+        if (have_hash && verbose) fprintf(stderr, "seqarc_amd: index image from /dev/shm/%s\n", shm_name(ref).c_str());
+    }
+    if (!have_hash) {
+        have_hash = slurp(r + ".hash", rf.hash) && rf.hash.size() > 16;
+        if (!have_hash) rf.hash.clear();
+        if (have_hash) {
+            rf.hp = rf.hash.data();
+            rf.hn = rf.hash.size();
+            if (use_shm && hash_image_bytes(rf.hp, rf.hn) == rf.hn) (void)shm_publish(ref, rf.hp, rf.hn, verbose);
+        }
+    }
     std::vector<uint8_t> m;
     const bool have_md5 = slurp(r + ".md5", m) && m.size() == 16;
     if (!have_hash || !have_md5 || need_fasta) {
@@ -1078,14 +1198,14 @@ int compress(const Options& o)
     std::vector<sa_hash_index*> indexes;
     sa_align_chain* chain = nullptr;
     if (o.ref && !o.host_only && !o.ingest_only) {
-        if (!load_ref(o.ref, false, rf)) return 1;
+        if (!load_ref(o.ref, false, rf, o.shm, o.verbose)) return 1;
         const double ti = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
         sa_ctx* owner = nullptr;
         sa_hash_index* ix = nullptr;
         for (size_t k = 0; k < ctxs.size(); k++) {
             if (k % (size_t)o.contexts == 0 && !(o.share_device && ix)) {   // the first context of a device
                 owner = ctxs[k];
-                ix = !rf.hash.empty() ? sa_hash_load(owner, rf.hash.data(), rf.hash.size())
+                ix = rf.have_hash() ? sa_hash_load(owner, rf.hp, rf.hn)
                                       : sa_hash_build(owner, (const char*)rf.fasta.data(), rf.fasta.size(), 14, 2, 1u << 16);
                 if (!ix) {
                     fprintf(stderr, "seqarc_amd: reference index: %s\n", sa_last_error(owner));
@@ -1098,7 +1218,7 @@ int compress(const Options& o)
         chain = sa_align_chain_create(0, 0);   // a fresh encode thread's AlignParam (nmis 0)
         if (o.verbose)
             fprintf(stderr, "seqarc_amd: reference %s: index %s in %.3f s\n", o.ref,
-                    rf.hash.empty() ? "built" : "loaded",
+                    rf.have_hash() ? "loaded" : "built",
                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() - ti);
     }
     int64_t B = std::max(1, o.batch);
@@ -1814,22 +1934,22 @@ int decompress(const Options& o)
             fprintf(stderr, "seqarc_amd: %s was made with a reference: give ref.fa\n", o.arc);
             return 1;
         }
-        if (!load_ref(o.ref, false, rf)) return 1;
+        if (!load_ref(o.ref, false, rf, o.shm, o.verbose)) return 1;
         if (have_md5 && memcmp(arc_md5, rf.md5, 16)) {   // checkMd5@0x416c40
             fprintf(stderr, "seqarc_amd: the reference %s is not the one %s was made with (MD5)\n", o.ref, o.arc);
             return 1;
         }
-        if (!rf.hash.empty()) {   // K, bases, words, positions; words follow
+        if (rf.have_hash()) {   // K, bases, words, positions; words follow
             uint32_t hdr[4];
-            memcpy(hdr, rf.hash.data(), 16);
-            if (16 + 4ull * hdr[2] > rf.hash.size()) {
+            memcpy(hdr, rf.hp, 16);
+            if (16 + 4ull * hdr[2] > rf.hn) {
                 fprintf(stderr, "seqarc_amd: %s.hash is truncated\n", o.ref);
                 return 1;
             }
             gbases = hdr[1];
             gwords.resize(hdr[2]);
-            memcpy(gwords.data(), rf.hash.data() + 16, 4ull * hdr[2]);
-            rf.hash.clear();
+            memcpy(gwords.data(), rf.hp + 16, 4ull * hdr[2]);
+            rf.drop_hash();
         } else if (!pack_fasta(rf.fasta, gwords, gbases)) {
             fprintf(stderr, "seqarc_amd: %s: not a FASTA file\n", o.ref);
             return 1;
@@ -1989,6 +2109,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--host-parse")) o.host_parse = true;
         else if (!strcmp(a, "-v")) o.verbose = true;
         else if (!strcmp(a, "-i")) { o.index = true; if (!(o.ref = val())) return usage(); }
+        else if (!strcmp(a, "-s")) o.shm = true;
         else if (!strcmp(a, "-q")) {   // -q -i: the minimizer index (MINI_INDEX) is not part of this build
             fprintf(stderr, "seqarc_amd: -q (minimizer index) is not part of this build; the HASH index is\n");
             return 2;

@@ -157,3 +157,48 @@ def test_bin_mode_pe_types(kind):
     cfg = fq.Config(bin_mode=1)
     d, ok = fq.decode_block(oracle_py.encode_block(blk, bin_mode=1), blk.text1 + blk.text2, cfg, tmpl)
     assert ok and d.names.tobytes() == blk.names.tobytes() and np.array_equal(d.name_lens, blk.name_lens)
+
+
+def test_cli_decode_reference_shm(tmp_path):
+    """-s (README.md:32, IHashRefIndex::createShm@0x41f280 /
+    HashRefIndex32::loadRefIndexShm@0x41ef80): the first -d with -s copies
+    ref.fa.hash into /dev/shm/<ref file name>, later runs map it instead of
+    reading the file; an object of another size is refused ("is wrong file")."""
+    import hashlib
+    name = f"sa_shm_test_{os.getpid()}.fa"
+    shm = os.path.join("/dev/shm", name)
+    fa, g = synth.reference(300_000, 71, chroms=2)
+    fa = fa.upper()
+    (tmp_path / name).write_bytes(fa)
+    hfile = oracle_py.hash_index(fa)
+    (tmp_path / (name + ".hash")).write_bytes(hfile)
+    (tmp_path / (name + ".md5")).write_bytes(hashlib.md5(fa).digest())
+    r1, r2 = synth.aligned_reads(g, 1500, 72, paired=True, random_frac=0.1)
+    blocks = fq.blocks_from_fastq(r1, r2, 1 << 18)
+    tmpl = fq.analyze_ids(blocks[0], False)
+    cfg = fq.Config(bin_mode=int(tmpl[0]))
+    carry = [0, 0]
+    enc = [oracle_py.encode_block_hash(b, True, carry, bin_mode=cfg.bin_mode) for b in blocks]
+    arc = fq.arc_archive(enc, blocks, "a_1.fq", "a_2.fq", tmpl, cfg, plus_bare=fq.bare_plus(r1),
+                         ref_md5=hashlib.md5(fa).digest())
+    (tmp_path / "a.arc").write_bytes(arc)
+    run = lambda args: subprocess.run([CLI] + args, capture_output=True, text=True, cwd=tmp_path, timeout=120)
+    try:
+        if os.path.exists(shm):
+            os.remove(shm)
+        r = run(["-d", "-s", "-v", name, "a.arc", "b1"])
+        assert r.returncode == 0, r.stderr
+        assert open(shm, "rb").read() == hfile
+        assert (tmp_path / "b1_1.fastq").read_bytes() == r1 and (tmp_path / "b1_2.fastq").read_bytes() == r2
+        os.remove(tmp_path / (name + ".hash"))   # from now on only the shared-memory image has the index
+        r = run(["-d", "-s", "-v", name, "a.arc", "b2"])
+        assert r.returncode == 0, r.stderr
+        assert "from /dev/shm/" in r.stderr
+        assert (tmp_path / "b2_1.fastq").read_bytes() == r1 and (tmp_path / "b2_2.fastq").read_bytes() == r2
+        with open(shm, "r+b") as f:
+            f.truncate(len(hfile) - 4)
+        r = run(["-d", "-s", name, "a.arc", "b3"])
+        assert r.returncode != 0 and "is wrong file" in r.stderr
+    finally:
+        if os.path.exists(shm):
+            os.remove(shm)

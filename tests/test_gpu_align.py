@@ -214,6 +214,45 @@ def test_cli_reference_path(tmp_path):
     same([(tmp_path / "bi_1.fastq").read_bytes()], [r1])
 
 
+def test_cli_reference_shm(tmp_path):
+    """-i -s / -c -s (README.md:32): the index image goes to /dev/shm/<ref file
+    name> (IHashRefIndex::createShm@0x41f280) and -c -s encodes from it with no
+    ref.fa.hash on disk -- the same archive as from the file."""
+    import hashlib
+    import os
+    import subprocess
+    from fastqueeze_amd import build
+    name = f"sa_shm_gpu_{os.getpid()}.fa"
+    shm = os.path.join("/dev/shm", name)
+    fa, g = synth.reference(800_000, 81, chroms=2)
+    fa = fa.upper()
+    (tmp_path / name).write_bytes(fa)
+    run = lambda args: subprocess.run([build.CLI] + args, capture_output=True, cwd=tmp_path, timeout=300)
+    r1, r2 = synth.aligned_reads(g, 6000, 82, paired=True, random_frac=0.1)
+    (tmp_path / "a_1.fq").write_bytes(r1)
+    (tmp_path / "a_2.fq").write_bytes(r2)
+    base = ["-c", "-f", "--block-size", "1", "--batch", "2"]
+    try:
+        if os.path.exists(shm):
+            os.remove(shm)
+        r = run(["-s", "-i", name])
+        assert r.returncode == 0, r.stderr
+        assert open(shm, "rb").read() == (tmp_path / (name + ".hash")).read_bytes()
+        r = run(base + [name, "-1", "a_1.fq", "-2", "a_2.fq", "file"])
+        assert r.returncode == 0, r.stderr
+        os.remove(tmp_path / (name + ".hash"))
+        r = run(base + ["-s", "-v", name, "-1", "a_1.fq", "-2", "a_2.fq", "mem"])
+        assert r.returncode == 0, r.stderr
+        assert b"from /dev/shm/" in r.stderr
+        assert (tmp_path / "mem.arc").read_bytes() == (tmp_path / "file.arc").read_bytes()
+        r = run(["-d", "-s", name, "mem.arc", "back"])
+        assert r.returncode == 0, r.stderr
+        assert (tmp_path / "back_1.fastq").read_bytes() == r1
+    finally:
+        if os.path.exists(shm):
+            os.remove(shm)
+
+
 def test_cli_reference_maxmis_bailout_chain(tmp_path):
     """a non-default --maxmis is recorded in the archive (params field
     19) so -d rebuilds the same Mis model without the flag; blocks that bail out
