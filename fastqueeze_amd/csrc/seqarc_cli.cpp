@@ -316,29 +316,6 @@ void lower_priority()
     (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 5);
 }
 
-// The inflated bytes reach the reader's text window by a copy on the reader
-// thread; one thread copies ~5-8 GB/s, the inflate pool delivers more (BGZF),
-// so a large copy is split over a few threads.  SA_GZ_COPY_THREADS (A/B; 1: one).
-int g_copy_threads = std::getenv("SA_GZ_COPY_THREADS") ? std::max(1, atoi(std::getenv("SA_GZ_COPY_THREADS"))) : 4;
-
-void par_copy(uint8_t* dst, const uint8_t* src, size_t n)
-{
-    const size_t kMin = 8u << 20;   // bytes per thread at least
-    const int t = (int)std::min<size_t>((size_t)g_copy_threads, n / kMin);
-    if (t <= 1) {
-        memcpy(dst, src, n);
-        return;
-    }
-    const size_t per = (n / (size_t)t + 4095) & ~(size_t)4095;
-    std::vector<std::thread> th;
-    for (int i = 1; i < t; i++) {
-        const size_t a = per * (size_t)i, b = std::min(n, a + per);
-        if (a < b) th.emplace_back([=]() { memcpy(dst + a, src + a, b - a); });
-    }
-    memcpy(dst, src, std::min(n, per));
-    for (auto& x : th) x.join();
-}
-
 struct GzStream {
     int fd = -1;
     int workers = 1;
@@ -623,7 +600,7 @@ struct GzStream {
                 cv.notify_all();
             }
             const size_t k = std::min(n - got, cur.size() - cur_at);
-            par_copy(dst + got, cur.data() + cur_at, k);
+            memcpy(dst + got, cur.data() + cur_at, k);
             cur_at += k;
             got += k;
         }
