@@ -2533,241 +2533,33 @@ constexpr uint32_t CODER_LA = 6;
         "s_lshl_b32 %[r], %[q], %[p]\n\t" \
         ""
 
-// Variants of the step (SA_RV_VARIANT, A/B): 1 -- the quotient's correction
-// moved after the frequency multiply, rr = (r < q0*t) ? q0*f - f : q0*f with
-// both products issued back to back, so two multiplies instead of three are on
-// the dependent chain (12 instructions a step instead of 11); 2 -- the same
-// with the three v_readlane issued between the chain's dependent SALU steps
-// instead of ahead of them.
-#define SA_RV_STEP8_V1 \
-        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l0]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l0]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l1]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l1]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l2]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l2]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l3]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l3]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l4]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l4]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l5]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l5]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l6]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l6]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l7]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l7]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        ""
-#define SA_RV_STEP8_V2 \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l0]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l0]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l0]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l1]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l1]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l1]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l2]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l2]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l2]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l3]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l3]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l3]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l4]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l4]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l4]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l5]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l5]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l5]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[ma]\n\t" \
-        "v_readlane_b32 %[mb], %[cm], %[l6]\n\t" \
-        "s_mul_i32 %[p], %[q], %[ta]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fa]\n\t" \
-        "v_readlane_b32 %[tb], %[vt], %[l6]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fa]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fb], %[vf], %[l6]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        "s_mul_hi_u32 %[q], %[r], %[mb]\n\t" \
-        "v_readlane_b32 %[ma], %[cm], %[l7]\n\t" \
-        "s_mul_i32 %[p], %[q], %[tb]\n\t" \
-        "s_mul_i32 %[a], %[q], %[fb]\n\t" \
-        "v_readlane_b32 %[ta], %[vt], %[l7]\n\t" \
-        "s_sub_u32 %[b], %[a], %[fb]\n\t" \
-        "s_cmp_lt_u32 %[r], %[p]\n\t" \
-        "v_readlane_b32 %[fa], %[vf], %[l7]\n\t" \
-        "s_cselect_b32 %[q], %[b], %[a]\n\t" \
-        "s_flbit_i32_b32 %[p], %[q]\n\t" \
-        "s_and_b32 %[p], %[p], 24\n\t" \
-        "s_lshl_b32 %[r], %[q], %[p]\n\t" \
-        ""
-
-template <int V, int J>
+template <int J>
 __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& fa, uint32_t& mb,
                                          uint32_t& tb, uint32_t& fb, uint32_t cm, uint32_t vt, uint32_t vf)
 {
-    uint32_t q, p, a, b;
+    uint32_t q, p;
 #define SA_RV_OPERANDS                                                                                            \
     : [r] "+s"(r), [ma] "+s"(ma), [ta] "+s"(ta), [fa] "+s"(fa), [mb] "+s"(mb), [tb] "+s"(tb), [fb] "+s"(fb),     \
-      [q] "=&s"(q), [p] "=&s"(p), [a] "=&s"(a), [b] "=&s"(b)                                                      \
+      [q] "=&s"(q), [p] "=&s"(p)                                                                                  \
     : [cm] "v"(cm), [vt] "v"(vt), [vf] "v"(vf), [l0] "i"((J + 1) & 63), [l1] "i"((J + 2) & 63),                  \
       [l2] "i"((J + 3) & 63), [l3] "i"((J + 4) & 63), [l4] "i"((J + 5) & 63), [l5] "i"((J + 6) & 63),             \
       [l6] "i"((J + 7) & 63), [l7] "i"((J + 8) & 63)                                                             \
     : "scc"
-    if constexpr (V == 1) asm volatile(SA_RV_STEP8_V1 SA_RV_OPERANDS);
-    else if constexpr (V == 2) asm volatile(SA_RV_STEP8_V2 SA_RV_OPERANDS);
-    else asm volatile(SA_RV_STEP8 SA_RV_OPERANDS);
+    asm volatile(SA_RV_STEP8 SA_RV_OPERANDS);
 #undef SA_RV_OPERANDS
 }
 #undef SA_RV_STEP8
-#undef SA_RV_STEP8_V1
-#undef SA_RV_STEP8_V2
 
 // the 64 steps of one segment (records in lanes 0..63 of cm / ctf)
-template <int V, int... P>
+template <int... P>
 __device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t vt, uint32_t vf,
                                            std::integer_sequence<int, P...>)
 {
     uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(vt, 0),
              fa = __builtin_amdgcn_readlane(vf, 0), mb = 0, tb = 0, fb = 0;
-    (rv_step8<V, 8 * P>(r, ma, ta, fa, mb, tb, fb, cm, vt, vf), ...);
+    (rv_step8<8 * P>(r, ma, ta, fa, mb, tb, fb, cm, vt, vf), ...);
 }
 
-template <int V>
 __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
                                                const TaskList& tl, const PRec* __restrict__ prs0,
                                                const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
@@ -2808,7 +2600,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                 r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);   // (scalar for the asm: see k_coder_rv)
                 const uint32_t r_seg = r;
                 const uint32_t vt = ctf & tmask, cm = recip32z(vt);
-                rv_segment<V>(r, cm, vt, ctf >> 16, std::make_integer_sequence<int, 8>{});
+                rv_segment(r, cm, vt, ctf >> 16, std::make_integer_sequence<int, 8>{});
                 if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
                 g++;
             }
@@ -2830,7 +2622,6 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
 // 100 MHz clock (s_memrealtime), the shader-clock cycles between them
 // (s_memtime), and where it ran (HW_ID: wave slot, SIMD, CU, SE; XCC_ID) with
 // the number of chains it coded
-template <int V>
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
     const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio,
@@ -2849,7 +2640,7 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const uint32_t step = wi < nl ? 0u : gridDim.x * wpg - nl;
     uint32_t chains = 0;
     for (uint32_t li = wi; li < tl.count;) {
-        coder_rv_chain<V>(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+        coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
         chains++;
         if (!step) break;
         li += step;
