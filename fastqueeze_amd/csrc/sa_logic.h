@@ -612,23 +612,28 @@ SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
     }
 }
 
-template <bool PACKED, uint32_t CH = RC_CHUNK>
-SA_HD LowMap seg_lowmap_t(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
-{
-    LowMap m{0ull, 0u, 0u};
+// L1's per-symbol step: the affine map of low over the symbols so far
+struct LowMapAcc {
     uint64_t low = 0;
-    uint32_t sbits = 0;
-    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    seg_for_each<PACKED, CH>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
+    uint32_t sbits = 0, nbytes = 0;
+    SA_HD void step(uint32_t& r, const PRec pr, uint32_t pm, uint32_t c, uint32_t tmask)
+    {
         uint32_t nb;
         const uint32_t q = range_step(r, pr, pm, tmask, nb);
         low = shl64(low + (uint64_t)c * q, 8 * nb);
         sbits += 8 * nb;
-        m.nbytes += nb;
-    });
-    m.B = low;
-    m.s = sbits >= 64 ? 64u : sbits;
-    return m;
+        nbytes += nb;
+    }
+    SA_HD LowMap map() const { return LowMap{low, sbits >= 64 ? 64u : sbits, nbytes}; }
+};
+
+template <bool PACKED, uint32_t CH = RC_CHUNK>
+SA_HD LowMap seg_lowmap_t(const PRec* P, const uint16_t* cum, uint32_t r, uint32_t n)
+{
+    LowMapAcc a;
+    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
+    seg_for_each<PACKED, CH>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) { a.step(r, pr, pm, c, tmask); });
+    return a.map();
 }
 
 // L3: the exact coder over one segment from (r, low).  Writes the bytes to
@@ -644,14 +649,15 @@ struct SegEnd {
 
 SA_HD uint32_t seg_count(uint32_t n, uint32_t seg) { return n - seg * SEG_SYMS < SEG_SYMS ? n - seg * SEG_SYMS : SEG_SYMS; }
 
-template <bool PACKED, uint32_t CH = RC_CHUNK>
-SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
-                        uint64_t cap, bool finish)
-{
-    SegEnd e{0, 0, 0, 0};
-    uint32_t op = 0;
-    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
-    seg_for_each<PACKED, CH>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) {
+// L3's per-symbol step: the exact coder from (r, low), its bytes to o[0..cap)
+struct SegCoder {
+    uint32_t r;
+    uint64_t low;
+    uint8_t* o;
+    uint64_t cap;
+    uint32_t op = 0, squeezed = 0;
+    SA_HD void step(const PRec pr, uint32_t pm, uint32_t c, uint32_t tmask)
+    {
         const uint32_t t = pr.tf & tmask, f = pr.tf >> 16;
         uint32_t q = mulhi32(r, pm);
         q -= (r < q * t) ? 1u : 0u;
@@ -660,25 +666,35 @@ SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t
         while (r < (1u << 24)) {
             if ((low ^ (low + r)) >> 56) {
                 r = ((uint32_t)low | 0xffffffu) - (uint32_t)low;
-                e.squeezed = 1;
+                squeezed = 1;
             }
             if (op < cap) o[op] = (uint8_t)(low >> 56);
             op++;
             r <<= 8;
             low <<= 8;
         }
-    });
-    if (finish) {
-        for (int k = 0; k < 8; k++) {
-            if (op < cap) o[op] = (uint8_t)(low >> 56);
-            op++;
-            low <<= 8;
-        }
     }
-    e.low = low;
-    e.r = r;
-    e.nbytes = op;
-    return e;
+    SA_HD SegEnd end(bool finish)
+    {
+        if (finish) {
+            for (int k = 0; k < 8; k++) {
+                if (op < cap) o[op] = (uint8_t)(low >> 56);
+                op++;
+                low <<= 8;
+            }
+        }
+        return SegEnd{low, r, op, squeezed};
+    }
+};
+
+template <bool PACKED, uint32_t CH = RC_CHUNK>
+SA_HD SegEnd seg_code_t(const PRec* P, const uint16_t* cum, uint32_t r, uint64_t low, uint32_t n, uint8_t* o,
+                        uint64_t cap, bool finish)
+{
+    SegCoder sc{r, low, o, cap};
+    const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
+    seg_for_each<PACKED, CH>(P, cum, n, [&](const PRec pr, uint32_t pm, uint32_t c) { sc.step(pr, pm, c, tmask); });
+    return sc.end(finish);
 }
 
 // cum == nullptr: packed (SEQ) records
