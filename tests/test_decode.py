@@ -167,14 +167,14 @@ def test_cli_decode_reference_shm(tmp_path):
     import hashlib
     name = f"sa_shm_test_{os.getpid()}.fa"
     shm = os.path.join("/dev/shm", name)
-    fa, g = synth.reference(300_000, 71, chroms=2)
+    fa, g = synth.reference(150_000, 71, chroms=2)
     fa = fa.upper()
     (tmp_path / name).write_bytes(fa)
-    hfile = oracle_py.hash_index(fa)
+    hfile = oracle_py.hash_index(fa, k=10)   # (the decoder reads the genome words; K = 10 keeps the image at 8 MB)
     (tmp_path / (name + ".hash")).write_bytes(hfile)
     (tmp_path / (name + ".md5")).write_bytes(hashlib.md5(fa).digest())
-    r1, r2 = synth.aligned_reads(g, 1500, 72, paired=True, random_frac=0.1)
-    blocks = fq.blocks_from_fastq(r1, r2, 1 << 18)
+    r1, r2 = synth.aligned_reads(g, 500, 72, paired=True, random_frac=0.1)
+    blocks = fq.blocks_from_fastq(r1, r2, 1 << 16)
     tmpl = fq.analyze_ids(blocks[0], False)
     cfg = fq.Config(bin_mode=int(tmpl[0]))
     carry = [0, 0]
