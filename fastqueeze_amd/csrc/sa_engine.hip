@@ -235,6 +235,10 @@ struct sa_ctx {
     // (pass R, L passes).  SA_HOST_WAITS=0: device-side waits, for A/B.
     bool host_waits = !(std::getenv("SA_HOST_WAITS") && std::atoi(std::getenv("SA_HOST_WAITS")) == 0);
     uint32_t coder_waves = 4;
+    // the pass-R step order (k_coder_rv<V>): 5 = the 24 v_readlane of eight steps
+    // issued together ahead of their SALU steps (r4z3: pass R 671-675 against
+    // 767-776 ms); SA_RV_VARIANT=0: a step's three v_readlane ahead of it (A/B)
+    int rv_variant = std::getenv("SA_RV_VARIANT") ? std::atoi(std::getenv("SA_RV_VARIANT")) : 5;
     uint32_t rv_short_waves = std::getenv("SA_RV_SHORT_WAVES") ? (uint32_t)std::atoi(std::getenv("SA_RV_SHORT_WAVES")) : 32u;
     // k_replay_aux_long workgroups: what the long-run CUs hold at once (6 per CU;
     // SA_LONG_GRID overrides, round 2 used 2048)
@@ -645,7 +649,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
         c->probe_waves = grid * c->coder_waves;
         (void)hipMemsetAsync(probe, 0, 32ull * c->probe_waves, st);
     }
-    hipLaunchKernelGGL(k_coder_rv, dim3(grid), dim3(64 * c->coder_waves),
+    hipLaunchKernelGGL(c->rv_variant == 5 ? k_coder_rv<5> : k_coder_rv<0>, dim3(grid), dim3(64 * c->coder_waves),
                        c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio, probe);
     if (ph >= 0) ev_finish(c, ph, st);
@@ -848,8 +852,10 @@ sa_ctx* sa_create(int device)
     }
     if (const char* e = std::getenv("SA_CODER_LDS")) c->coder_lds = (uint32_t)std::min(std::max(std::atoi(e), 0), 160 * 1024);
     if (c->coder_lds > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)c->coder_lds) != hipSuccess) {
+        (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess ||
+         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<5>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess)) {
         std::fprintf(stderr, "seqarc_amd: cannot reserve %u B of LDS for pass R\n", c->coder_lds);
         delete c;
         return nullptr;

@@ -2533,6 +2533,35 @@ constexpr uint32_t CODER_LA = 6;
         "s_lshl_b32 %[r], %[q], %[p]\n\t" \
         ""
 
+// (A/B, SA_RV_VARIANT=5) the eight steps' 24 v_readlane issued together ahead
+// of their 64 SALU instructions: one switch from the vector to the scalar unit
+// per eight steps instead of one per step.
+#define SA_RV_RL(k)                                                                                           \
+    "v_readlane_b32 %[m" #k "], %[cm], %[l" #k "]\n\tv_readlane_b32 %[t" #k "], %[vt], %[l" #k "]\n\t" \
+    "v_readlane_b32 %[f" #k "], %[vf], %[l" #k "]\n\t"
+#define SA_RV_ST(k)                                                                                           \
+    "s_mul_hi_u32 %[q], %[r], %[m" #k "]\n\ts_mul_i32 %[p], %[q], %[t" #k "]\n\ts_cmp_lt_u32 %[r], %[p]\n\t"   \
+    "s_subb_u32 %[q], %[q], 0\n\ts_mul_i32 %[q], %[q], %[f" #k "]\n\ts_flbit_i32_b32 %[p], %[q]\n\t"           \
+    "s_and_b32 %[p], %[p], 24\n\ts_lshl_b32 %[r], %[q], %[p]\n\t"
+
+template <int J>
+__device__ __forceinline__ void rv_step8_batched(uint32_t& r, uint32_t cm, uint32_t vt, uint32_t vf)
+{
+    uint32_t q, p, m0, m1, m2, m3, m4, m5, m6, m7, t0, t1, t2, t3, t4, t5, t6, t7, f0, f1, f2, f3, f4, f5, f6, f7;
+    asm volatile(SA_RV_RL(0) SA_RV_RL(1) SA_RV_RL(2) SA_RV_RL(3) SA_RV_RL(4) SA_RV_RL(5) SA_RV_RL(6) SA_RV_RL(7)
+                 SA_RV_ST(0) SA_RV_ST(1) SA_RV_ST(2) SA_RV_ST(3) SA_RV_ST(4) SA_RV_ST(5) SA_RV_ST(6) SA_RV_ST(7)
+                 : [r] "+s"(r), [q] "=&s"(q), [p] "=&s"(p), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
+                   [m3] "=&s"(m3), [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [t0] "=&s"(t0),
+                   [t1] "=&s"(t1), [t2] "=&s"(t2), [t3] "=&s"(t3), [t4] "=&s"(t4), [t5] "=&s"(t5), [t6] "=&s"(t6),
+                   [t7] "=&s"(t7), [f0] "=&s"(f0), [f1] "=&s"(f1), [f2] "=&s"(f2), [f3] "=&s"(f3), [f4] "=&s"(f4),
+                   [f5] "=&s"(f5), [f6] "=&s"(f6), [f7] "=&s"(f7)
+                 : [cm] "v"(cm), [vt] "v"(vt), [vf] "v"(vf), [l0] "i"(J), [l1] "i"(J + 1), [l2] "i"(J + 2),
+                   [l3] "i"(J + 3), [l4] "i"(J + 4), [l5] "i"(J + 5), [l6] "i"(J + 6), [l7] "i"(J + 7)
+                 : "scc");
+}
+#undef SA_RV_RL
+#undef SA_RV_ST
+
 template <int J>
 __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta, uint32_t& fa, uint32_t& mb,
                                          uint32_t& tb, uint32_t& fb, uint32_t cm, uint32_t vt, uint32_t vf)
@@ -2551,15 +2580,20 @@ __device__ __forceinline__ void rv_step8(uint32_t& r, uint32_t& ma, uint32_t& ta
 #undef SA_RV_STEP8
 
 // the 64 steps of one segment (records in lanes 0..63 of cm / ctf)
-template <int... P>
+template <int V, int... P>
 __device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t vt, uint32_t vf,
                                            std::integer_sequence<int, P...>)
 {
-    uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(vt, 0),
-             fa = __builtin_amdgcn_readlane(vf, 0), mb = 0, tb = 0, fb = 0;
-    (rv_step8<8 * P>(r, ma, ta, fa, mb, tb, fb, cm, vt, vf), ...);
+    if constexpr (V == 5) {
+        (rv_step8_batched<8 * P>(r, cm, vt, vf), ...);
+    } else {
+        uint32_t ma = __builtin_amdgcn_readlane(cm, 0), ta = __builtin_amdgcn_readlane(vt, 0),
+                 fa = __builtin_amdgcn_readlane(vf, 0), mb = 0, tb = 0, fb = 0;
+        (rv_step8<8 * P>(r, ma, ta, fa, mb, tb, fb, cm, vt, vf), ...);
+    }
 }
 
+template <int V>
 __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
                                                const TaskList& tl, const PRec* __restrict__ prs0,
                                                const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
@@ -2600,7 +2634,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                 r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);   // (scalar for the asm: see k_coder_rv)
                 const uint32_t r_seg = r;
                 const uint32_t vt = ctf & tmask, cm = recip32z(vt);
-                rv_segment(r, cm, vt, ctf >> 16, std::make_integer_sequence<int, 8>{});
+                rv_segment<V>(r, cm, vt, ctf >> 16, std::make_integer_sequence<int, 8>{});
                 if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
                 g++;
             }
@@ -2622,6 +2656,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
 // 100 MHz clock (s_memrealtime), the shader-clock cycles between them
 // (s_memtime), and where it ran (HW_ID: wave slot, SIMD, CU, SE; XCC_ID) with
 // the number of chains it coded
+template <int V>
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
     const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio,
@@ -2640,7 +2675,7 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const uint32_t step = wi < nl ? 0u : gridDim.x * wpg - nl;
     uint32_t chains = 0;
     for (uint32_t li = wi; li < tl.count;) {
-        coder_rv_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+        coder_rv_chain<V>(li, tasks, tl, prs0, prs1, ck_r, err, prio);
         chains++;
         if (!step) break;
         li += step;
