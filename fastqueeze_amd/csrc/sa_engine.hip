@@ -237,8 +237,13 @@ struct sa_ctx {
     uint32_t coder_waves = 4;
     // the pass-R step order (k_coder_rv<V>): 5 = the 24 v_readlane of eight steps
     // issued together ahead of their SALU steps (r4z3: pass R 671-675 against
-    // 767-776 ms); SA_RV_VARIANT=0: a step's three v_readlane ahead of it (A/B)
-    int rv_variant = std::getenv("SA_RV_VARIANT") ? std::atoi(std::getenv("SA_RV_VARIANT")) : 5;
+    // 767-776 ms, the bench +3-5 %); 0 = a step's three v_readlane ahead of it.
+    // The batched moves hold the vector unit of their SIMD longer, and batches
+    // of long reads (mean > 1000 bp), whose fronts are VALU-heavy and set the
+    // pace, ran 11 % slower with them (r4z5: ONT shape 7,187 / 7,281 against
+    // 8,081 / 8,260 MB/s), so those keep 0.  SA_RV_VARIANT=0 / 5: one for all.
+    int rv_variant = std::getenv("SA_RV_VARIANT") ? std::atoi(std::getenv("SA_RV_VARIANT")) : -1;
+    int rv_batch = 5;   // the current batch's (run_input)
     uint32_t rv_short_waves = std::getenv("SA_RV_SHORT_WAVES") ? (uint32_t)std::atoi(std::getenv("SA_RV_SHORT_WAVES")) : 32u;
     // k_replay_aux_long workgroups: what the long-run CUs hold at once (6 per CU;
     // SA_LONG_GRID overrides, round 2 used 2048)
@@ -649,7 +654,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
         c->probe_waves = grid * c->coder_waves;
         (void)hipMemsetAsync(probe, 0, 32ull * c->probe_waves, st);
     }
-    hipLaunchKernelGGL(c->rv_variant == 5 ? k_coder_rv<5> : k_coder_rv<0>, dim3(grid), dim3(64 * c->coder_waves),
+    hipLaunchKernelGGL(c->rv_batch == 5 ? k_coder_rv<5> : k_coder_rv<0>, dim3(grid), dim3(64 * c->coder_waves),
                        c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
                        c->chain_prio, probe);
     if (ph >= 0) ev_finish(c, ph, st);
@@ -1221,6 +1226,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
     FrontShare* F = c->fs;
+    c->rv_batch = c->rv_variant >= 0 ? c->rv_variant : (nr && I->seq_bytes / nr > 1000 ? 0 : 5);   // (see rv_variant)
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
