@@ -29,8 +29,9 @@ out = {}
 for k in sorted(set(fetch) | set(write)):
     b = 2 * fetch.get(k, 0.0) * 1024 + write.get(k, 0.0) * 1024   # KB -> B; FETCH doubled
     out[k] = {"bytes": round(b), "fetch_kb_raw": round(fetch.get(k, 0.0)), "write_kb": round(write.get(k, 0.0))}
-    if k in PHASE:
-        out[PHASE[k]] = round(b)
+    base = k.split("<")[0]   # (k_coder_rv<5>: a template instance)
+    if base in PHASE:
+        out[PHASE[base]] = round(b)
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 for k, v in out.items():
     if isinstance(v, dict):
