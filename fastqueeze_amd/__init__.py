@@ -50,7 +50,7 @@ class _SaArcBlock(C.Structure):
 class _SaArcInfo(C.Structure):
     _fields_ = [("file1", C.c_char_p), ("file2", C.c_char_p), ("paired", C.c_int32), ("gz1", C.c_int32),
                 ("bare_plus", C.c_int32), ("md5", C.c_int32), ("lossy", C.c_int32), ("id_template", C.c_void_p),
-                ("ref_md5", C.c_void_p), ("insert_size", C.c_uint32), ("maxmis", C.c_int32)]
+                ("ref_md5", C.c_void_p), ("insert_size", C.c_uint32)]
 
 
 class _SaDecoded(C.Structure):
@@ -113,6 +113,7 @@ def load_library(path: str | None = None):
         "sa_create_shared": ([I32, P], P),
         "sa_input_create": ([I32, P, I32], P), "sa_input_destroy": ([P], None), "sa_run_input": ([P, P, P], I32),
         "sa_arc_header": ([U64, P], I32), "sa_arc_trailer": ([P, P, C.c_uint32, P, U64], I64),
+        "sa_arc_trailer2": ([P, C.c_int32, P, C.c_uint32, P, U64], I64),
         "sa_decode_block": ([P, U64, P, P, I32, P], I64),
         "sa_host_register": ([P, U64], I32), "sa_host_unregister": ([P], I32),
         "sa_stage_text": ([P, P, I32, P], I32), "sa_host_alloc": ([U64], P), "sa_host_free": ([P], None),
@@ -508,10 +509,10 @@ def arc_archive(encaps: list[bytes], blocks: list[Block], file1: str, file2: str
     rm = None if ref_md5 is None else np.frombuffer(ref_md5, np.uint8)
     info = _SaArcInfo(file1.encode(), (file2 or "").encode(), 1 if file2 else 0, 1 if gz1 else 0, int(plus_bare),
                       1 if cfg.md5 else 0, 1 if cfg.lossy > 0 else 0, _ptr(tmpl), None if rm is None else _ptr(rm),
-                      int(insert_size), int(maxmis))
+                      int(insert_size))
     cap = 4096 + 40 * len(encaps)
     tr = np.empty(cap, np.uint8)
-    n = lib.sa_arc_trailer(C.byref(info), recs, len(encaps), _ptr(tr), cap)
+    n = lib.sa_arc_trailer2(C.byref(info), int(maxmis), recs, len(encaps), _ptr(tr), cap)
     if n < 0:
         raise SeqArcError("sa_arc_trailer failed")
     hdr = np.zeros(16, np.uint8)

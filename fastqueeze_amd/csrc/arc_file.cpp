@@ -111,7 +111,8 @@ int sa_arc_header(uint64_t block_bytes, uint8_t out[16])
     return 7 + n + 8 == 16 ? 0 : -1;
 }
 
-int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t n, uint8_t* out, uint64_t cap)
+int64_t sa_arc_trailer2(const sa_arc_info* in, int32_t maxmis, const sa_arc_block* blk, uint32_t n, uint8_t* out,
+                        uint64_t cap)
 {
     if (!in || (!blk && n) || !out) return -1;
     Out o{out, out + cap};
@@ -149,8 +150,8 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     field_bool(o, 16, in->lossy);               // param+0x1870
     field_bool(o, 17, in->md5);                 // param+0x1880
     field_bool(o, 18, 0);                       // param+0xd: file list (-m)
-    if (in->ref_md5 && in->maxmis != 7)         // (ours: a non-default maxmis, see sa_arc_info)
-        field_uint(o, 19, 1, (uint32_t)in->maxmis);
+    if (in->ref_md5 && maxmis != 7)             // (ours: a non-default maxmis, see sa_arc_trailer2)
+        field_uint(o, 19, 1, (uint32_t)maxmis);
     if (!o.ok) return -1;
     put_size((uint64_t)(o.p - pbeg), 2, ph + 1);
     if (in->ref_md5) {   // writeMd5@0x416b10: setID(8), 1-byte size 0x10, the 16 bytes
@@ -191,6 +192,11 @@ int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t 
     }
     put_size((uint64_t)(o.p - top - 5), 4, top + 1);
     return o.p - out;
+}
+
+int64_t sa_arc_trailer(const sa_arc_info* in, const sa_arc_block* blk, uint32_t n, uint8_t* out, uint64_t cap)
+{
+    return sa_arc_trailer2(in, 7, blk, n, out, cap);
 }
 
 }  // extern "C"

@@ -882,13 +882,13 @@ struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
          verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = false,
-         release = false, stage_ahead = false, shm = false;
+         release = false, stage_ahead = false, shm = false, maxmis_set = false;
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
 };
 
-bool shm_publish(const char* ref, const uint8_t* p, size_t n, bool verbose);
+bool shm_publish(const char* ref, const uint8_t* p, size_t n, const uint8_t* md5, bool verbose);
 
 // ---- SeqArc -i ref.fa: the HASH index (HashAlignment::buildRefIndex@0x410190,
 //      HashRefIndex32::writeIndexFile@0x41ed00 -> "<ref>.hash"; MD5File@0x405950 of
@@ -923,7 +923,7 @@ int build_index(const Options& o)
         fprintf(stderr, "seqarc_amd: cannot write the index files of %s\n", o.ref);
         rc = 1;
     }
-    if (rc == 0 && o.shm && !shm_publish(o.ref, file.data(), file.size(), o.verbose)) rc = 1;
+    if (rc == 0 && o.shm && !shm_publish(o.ref, file.data(), file.size(), md, o.verbose)) rc = 1;
     const double s_load = std::chrono::duration<double>(t1 - t0).count(),
                  s_build = std::chrono::duration<double>(t2 - t1).count(),
                  s_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -979,7 +979,61 @@ std::string shm_name(const char* ref)
     return r.substr(r.rfind('/') + 1);
 }
 
-bool shm_publish(const char* ref, const uint8_t* p, size_t n, bool verbose)
+// The object is bound to its reference by a sidecar object "<name>.sa_ref":
+// the FASTA's MD5 (the archive's encap 8) and the image size.  The reference
+// keys the object by the file's basename alone, so two references of the same
+// name would otherwise share one image (and -c would align against the wrong
+// genome while recording the right MD5).
+struct ShmTag {
+    char magic[8];
+    uint8_t md5[16];
+    uint64_t bytes;
+};
+constexpr char kShmTagMagic[8] = {'S', 'A', 'R', 'E', 'F', '0', '0', '1'};
+
+std::string shm_tag_name(const char* ref) { return shm_name(ref) + ".sa_ref"; }
+
+// 1: the tag names this reference and size, 0: no tag, -1: another reference or size
+int shm_tag_check(const char* ref, const uint8_t* md5, uint64_t bytes)
+{
+    const int fd = shm_open(shm_tag_name(ref).c_str(), O_RDONLY, 0);
+    if (fd < 0) return 0;
+    ShmTag t{};
+    const bool got = ::pread(fd, &t, sizeof t, 0) == (ssize_t)sizeof t;
+    close(fd);
+    return got && !memcmp(t.magic, kShmTagMagic, 8) && !memcmp(t.md5, md5, 16) && t.bytes == bytes ? 1 : -1;
+}
+
+bool shm_tag_write(const char* ref, const uint8_t* md5, uint64_t bytes)
+{
+    const std::string nm = shm_tag_name(ref);
+    shm_unlink(nm.c_str());
+    const int fd = shm_open(nm.c_str(), O_CREAT | O_EXCL | O_RDWR, 0644);
+    if (fd < 0) return false;
+    ShmTag t{};
+    memcpy(t.magic, kShmTagMagic, 8);
+    memcpy(t.md5, md5, 16);
+    t.bytes = bytes;
+    const bool ok = ::pwrite(fd, &t, sizeof t, 0) == (ssize_t)sizeof t;
+    close(fd);
+    return ok;
+}
+
+// <ref>.hash on disk: 1 its header and size equal the image's, 0 no file, -1 they differ
+int hash_file_matches(const char* ref, const uint8_t* p, size_t n)
+{
+    const std::string f = std::string(ref) + ".hash";
+    const int fd = ::open(f.c_str(), O_RDONLY);
+    if (fd < 0) return 0;
+    struct stat sb;
+    uint8_t h[16];
+    const bool same = fstat(fd, &sb) == 0 && (uint64_t)sb.st_size == n && n >= 16 &&
+                      ::pread(fd, h, 16, 0) == 16 && !memcmp(h, p, 16);
+    close(fd);
+    return same ? 1 : -1;
+}
+
+bool shm_publish(const char* ref, const uint8_t* p, size_t n, const uint8_t* md5, bool verbose)
 {
     const std::string nm = shm_name(ref);
     int fd = shm_open(nm.c_str(), O_RDWR, 0);
@@ -987,7 +1041,9 @@ bool shm_publish(const char* ref, const uint8_t* p, size_t n, bool verbose)
         struct stat sb;
         const bool same = fstat(fd, &sb) == 0 && (uint64_t)sb.st_size == n;
         close(fd);
-        if (same) {
+        // kept only when it is this reference's image (an object of the same
+        // size but another reference, or an untagged one, is replaced)
+        if (same && shm_tag_check(ref, md5, n) == 1) {
             fprintf(stderr, "createHashShm %s has existed.\n", nm.c_str());
             return true;
         }
@@ -1012,12 +1068,20 @@ bool shm_publish(const char* ref, const uint8_t* p, size_t n, bool verbose)
     }
     memcpy(m, p, n);
     munmap(m, n);
+    if (!shm_tag_write(ref, md5, n)) {
+        fprintf(stderr, "shm_open fail.\n");
+        shm_unlink(nm.c_str());
+        return false;
+    }
     if (verbose) fprintf(stderr, "seqarc_amd: index image in /dev/shm/%s (%zu bytes)\n", nm.c_str(), n);
     return true;
 }
 
-// 1: mapped, 0: no such object, -1: an object that is not an index image
-int shm_map(const char* ref, RefFiles& rf)
+// 1: mapped, 0: no such object, or the object of another reference while
+// <ref>.hash exists (the caller reads the file and republishes), -1: an object
+// that is not an index image, or one that cannot be shown to be this
+// reference's (md5: the FASTA's, from <ref>.md5 or the FASTA itself)
+int shm_map(const char* ref, const uint8_t* md5, RefFiles& rf)
 {
     const std::string nm = shm_name(ref);
     const int fd = shm_open(nm.c_str(), O_RDONLY, 0);
@@ -1035,6 +1099,17 @@ int shm_map(const char* ref, RefFiles& rf)
         fprintf(stderr, "/dev/shm/ %s is wrong file, please delete\n", nm.c_str());
         return -1;
     }
+    // bound to this reference: its tag, else (an object without one, e.g. made
+    // by SeqArc itself) <ref>.hash's header and size
+    const int tag = shm_tag_check(ref, md5, n);
+    const int file = tag == 1 ? 1 : hash_file_matches(ref, (const uint8_t*)m, n);
+    if (tag < 0 || file < 0 || (tag == 0 && file == 0)) {
+        munmap(m, n);
+        if (file != 0) return 0;   // (stale or another reference's image: <ref>.hash is read and republished)
+        fprintf(stderr, "/dev/shm/ %s is not the index of %s (another reference of the same name?), please delete\n",
+                nm.c_str(), ref);
+        return -1;
+    }
     rf.map = m;
     rf.map_len = n;
     rf.hp = (const uint8_t*)m;
@@ -1045,11 +1120,25 @@ int shm_map(const char* ref, RefFiles& rf)
 bool load_ref(const char* ref, bool need_fasta, RefFiles& rf, bool use_shm = false, bool verbose = false)
 {
     const std::string r(ref);
+    auto read_fasta = [&]() {
+        if (!rf.fasta.empty()) return true;
+        if (!slurp(r, rf.fasta) || rf.fasta.empty()) {
+            fprintf(stderr, "Error:The file %s may be not exist or empty!\n", ref);
+            return false;
+        }
+        return true;
+    };
+    // the reference's MD5 first: the shared-memory image must be this reference's
+    std::vector<uint8_t> m;
+    const bool have_md5 = slurp(r + ".md5", m) && m.size() == 16;
+    if ((!have_md5 || need_fasta) && !read_fasta()) return false;
+    if (have_md5) memcpy(rf.md5, m.data(), 16);
+    else sa_md5(rf.fasta.data(), rf.fasta.size(), rf.md5);
     bool have_hash = false;
     if (use_shm) {   // (HashAlignment::loadRefIndex: loadRefIndexShm, else loadRefIndexFile)
-        const int m = shm_map(ref, rf);
-        if (m < 0) return false;
-        have_hash = m == 1;
+        const int sm = shm_map(ref, rf.md5, rf);
+        if (sm < 0) return false;
+        have_hash = sm == 1;
         if (have_hash && verbose) fprintf(stderr, "seqarc_amd: index image from /dev/shm/%s\n", shm_name(ref).c_str());
     }
     if (!have_hash) {
@@ -1058,20 +1147,10 @@ bool load_ref(const char* ref, bool need_fasta, RefFiles& rf, bool use_shm = fal
         if (have_hash) {
             rf.hp = rf.hash.data();
             rf.hn = rf.hash.size();
-            if (use_shm && hash_image_bytes(rf.hp, rf.hn) == rf.hn) (void)shm_publish(ref, rf.hp, rf.hn, verbose);
+            if (use_shm && hash_image_bytes(rf.hp, rf.hn) == rf.hn) (void)shm_publish(ref, rf.hp, rf.hn, rf.md5, verbose);
         }
     }
-    std::vector<uint8_t> m;
-    const bool have_md5 = slurp(r + ".md5", m) && m.size() == 16;
-    if (!have_hash || !have_md5 || need_fasta) {
-        if (!slurp(r, rf.fasta) || rf.fasta.empty()) {
-            fprintf(stderr, "Error:The file %s may be not exist or empty!\n", ref);
-            return false;
-        }
-    }
-    if (have_md5) memcpy(rf.md5, m.data(), 16);
-    else sa_md5(rf.fasta.data(), rf.fasta.size(), rf.md5);
-    return true;
+    return have_hash || read_fasta();
 }
 
 // ---- compression: the streaming pipeline ------------------------------------
@@ -1753,9 +1832,9 @@ int compress(const Options& o)
         return 1;
     }
     sa_arc_info ai{o.f1, pe ? o.f2 : nullptr, pe ? 1 : 0, in1.is_gz ? 1 : 0, plus_bare, cfg.md5,
-                   cfg.lossy > 0.0 ? 1 : 0, tmpl, o.ref ? rf.md5 : nullptr, (uint32_t)o.insert, o.maxmis};
+                   cfg.lossy > 0.0 ? 1 : 0, tmpl, o.ref ? rf.md5 : nullptr, (uint32_t)o.insert};
     std::vector<uint8_t> tr(4096 + 40 * info.size());
-    const int64_t tl = sa_arc_trailer(&ai, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
+    const int64_t tl = sa_arc_trailer2(&ai, o.maxmis, info.data(), (uint32_t)info.size(), tr.data(), tr.size());
     if (tl < 0) {
         fprintf(stderr, "seqarc_amd: trailer failed\n");
         rc = 1;
@@ -1891,7 +1970,10 @@ int decompress(const Options& o)
     uint8_t tmpl[512] = {0};
     int bare = 1, paired = 0, lossy = 0, md5 = 1, gz1 = 0, noref = 1;
     uint32_t nblocks = 0, insert = 0;
-    int maxmis = 7;   // SeqArc's default (param+0x1b60); field 19 when the archive was made with another
+    // SeqArc's default (param+0x1b60); field 19 when the archive was made with
+    // another; an archive without field 19 (SeqArc's own, made with a
+    // seqarc.config maxmis, or an earlier build of this tool) takes -d --maxmis
+    int maxmis = o.maxmis_set ? o.maxmis : 7;
     std::string name1, name2;
     while (t < pend) {
         const uint64_t id = vint(t, pend, w);
@@ -2120,6 +2202,7 @@ int main(int argc, char** argv)
                 fprintf(stderr, "seqarc_amd: --maxmis takes 0..8\n");
                 return usage();
             }
+            o.maxmis_set = true;
         }
         else if (a[0] != '-') pos.push_back(a);
         else return usage();

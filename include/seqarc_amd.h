@@ -212,11 +212,7 @@ typedef struct {
      * the MD5 of the FASTA file, getMd5@0x416810) */
     const uint8_t *ref_md5;        /* NULL: no reference                                 */
     uint32_t insert_size;          /* param+0x28 (-I)                                    */
-    int32_t maxmis;                /* reference path: param+0x1b60 (0..8).  SeqArc reads it
-                                    * from ./seqarc.config and stores none; a value other
-                                    * than its default 7 is written as params field 19 so
-                                    * that -d rebuilds the same Mis model                   */
-} sa_arc_info;
+} sa_arc_info;   /* (layout unchanged since round 1: maxmis is sa_arc_trailer2's argument) */
 
 /* ---- block decoder (SeqArc -d; host) ------------------------------------ */
 /* The inverse of sa_encode_blocks for one block: EncapFqzComp::doFqzDecode@0x42c680
@@ -259,9 +255,16 @@ void sa_md5(const uint8_t *data, uint64_t len, uint8_t digest[16]);
 
 /* 16-byte header; block_bytes = sum of the blocks' sizes. Returns 0. */
 int sa_arc_header(uint64_t block_bytes, uint8_t out[16]);
-/* Trailer bytes written to out (written at offset 16 + block_bytes), or -1. */
+/* Trailer bytes written to out (written at offset 16 + block_bytes), or -1
+ * (writeParam@0x416450 + writeMd5@0x416b10 + writeBlockLenArry{SE,PE}@0x416d60/0x416e90). */
 int64_t sa_arc_trailer(const sa_arc_info *info, const sa_arc_block *blocks, uint32_t nblocks,
                        uint8_t *out, uint64_t cap);
+/* The same with the reference path's maxmis (param+0x1b60, 0..8).  SeqArc reads it
+ * from ./seqarc.config and stores none; a value other than its default 7 is
+ * written as params field 19 so that -d rebuilds the same Mis model.
+ * sa_arc_trailer(...) == sa_arc_trailer2(info, 7, ...). */
+int64_t sa_arc_trailer2(const sa_arc_info *info, int32_t maxmis, const sa_arc_block *blocks, uint32_t nblocks,
+                        uint8_t *out, uint64_t cap);
 
 /* ---- HASH reference index and gapless seed alignment ----
  * The index `SeqArc -i ref.fa` builds (HashAlignment::buildRefIndex@0x410190

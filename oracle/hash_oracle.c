@@ -247,10 +247,13 @@ int ho_index_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32
             pos++;
             if (isn[ch]) run = 0;
             else if (run + 1 == K) {
-                if (pos % step == 0) sk[ns++] = kmer;
+                if (pos % step == 0) {
+                    sk[ns++] = kmer;
+                    /* (flushed inside the line: an unwrapped chromosome is one line) */
+                    if (ns == HO_SEEDBUF) ns = ho_count_seeds(ix->num, sk, ns, maxcount, ix->nkmers);
+                }
             } else run++;
         }
-        if (ns > HO_SEEDBUF - 65536) ns = ho_count_seeds(ix->num, sk, ns, maxcount, ix->nkmers);
     }
     ns = ho_count_seeds(ix->num, sk, ns, maxcount, ix->nkmers);
     if (!headers) { free(sk); free(sp); return -1; }
@@ -293,10 +296,10 @@ int ho_index_build(const char* fa, uint64_t n, uint32_t K, uint32_t step, uint32
                 if (pos % step == 0) {
                     sk[ns] = kmer;
                     sp[ns++] = (uint32_t)(pos - (K - 1));
+                    if (ns == HO_SEEDBUF) ns = ho_place_seeds(ix->pos, cur, sk, sp, ns, ix->nkmers);
                 }
             } else run++;
         }
-        if (ns > HO_SEEDBUF - 65536) ns = ho_place_seeds(ix->pos, cur, sk, sp, ns, ix->nkmers);
     }
     ho_place_seeds(ix->pos, cur, sk, sp, ns, ix->nkmers);
     ho_free(cur, ix->nkmers * 4);

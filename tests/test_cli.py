@@ -108,11 +108,13 @@ def test_compress_usage_errors(tmp_path):
     assert r.returncode == 2 and b"0..8" in r.stderr
 
 
-@pytest.mark.parametrize("maxmis", [0, 3, 8])
-def test_decode_reference_maxmis_from_archive(tmp_path, maxmis):
+@pytest.mark.parametrize("maxmis,field19", [(0, True), (3, True), (8, True), (8, False), (0, False)])
+def test_decode_reference_maxmis_from_archive(tmp_path, maxmis, field19):
     """An archive of the reference path made with a non-default maxmis carries it
     (params field 19, ours; SeqArc keeps maxmis in ./seqarc.config and stores
-    none): -d rebuilds the Mis model without being told."""
+    none): -d rebuilds the Mis model without being told.  An archive without
+    field 19 (SeqArc's own, or an earlier build's) takes -d --maxmis M (ADVICE
+    r4: the option was accepted and ignored)."""
     fa, g = synth.reference(600_000, 73, chroms=2)
     fa = fa.upper()
     (tmp_path / "ref.fa").write_bytes(fa)
@@ -124,11 +126,15 @@ def test_decode_reference_maxmis_from_archive(tmp_path, maxmis):
     carry = [0, 0]
     enc = [oracle_py.encode_block_hash(b, False, carry, bin_mode=cfg.bin_mode, maxmis=maxmis) for b in blocks]
     data = fq.arc_archive(enc, blocks, "s.fq", None, tmpl, cfg, plus_bare=fq.bare_plus(r1),
-                          ref_md5=hashlib.md5(fa).digest(), maxmis=maxmis)
+                          ref_md5=hashlib.md5(fa).digest(), maxmis=maxmis if field19 else 7)
     (tmp_path / "a.arc").write_bytes(data)
-    r = _run(["-d", "-t", "2", "ref.fa", "a.arc", "back"], tmp_path)
+    r = _run(["-d", "-t", "2"] + ([] if field19 else ["--maxmis", str(maxmis)]) + ["ref.fa", "a.arc", "back"],
+             tmp_path)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "back.fastq").read_bytes() == r1
+    if not field19 and maxmis == 8:   # (without the option: the Mis model of 8 symbols, not 9)
+        r = _run(["-d", "-f", "-t", "2", "ref.fa", "a.arc", "back"], tmp_path)
+        assert r.returncode != 0 or (tmp_path / "back.fastq").read_bytes() != r1
 
 
 @pytest.mark.parametrize("paired,with_hash", [(False, True), (True, False), (True, True)])

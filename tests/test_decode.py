@@ -200,5 +200,64 @@ def test_cli_decode_reference_shm(tmp_path):
         r = run(["-d", "-s", name, "a.arc", "b3"])
         assert r.returncode != 0 and "is wrong file" in r.stderr
     finally:
-        if os.path.exists(shm):
-            os.remove(shm)
+        for f in (shm, shm + ".sa_ref"):
+            if os.path.exists(f):
+                os.remove(f)
+
+
+def test_cli_shm_two_references_same_name(tmp_path):
+    """the shared-memory image is keyed by the reference's file name
+    (loadRefIndexShm@0x41ef80), so two references of one name -- a/ref.fa and
+    b/ref.fa -- would share it.  The object is bound to its FASTA's MD5 (the
+    /dev/shm/<name>.sa_ref tag): -d -s with b/ref.fa does not decode against
+    a's genome; it reads b's .hash and republishes; with b's image in /dev/shm
+    and a's .hash gone, -d -s with a/ref.fa is refused."""
+    import hashlib
+    name = f"sa_shm_two_{os.getpid()}.fa"
+    shm = os.path.join("/dev/shm", name)
+    run = lambda args: subprocess.run([CLI] + args, capture_output=True, text=True, cwd=tmp_path, timeout=120)
+    arcs = {}
+    for d, seed in (("a", 81), ("b", 82)):
+        (tmp_path / d).mkdir()
+        fa, g = synth.reference(150_000, seed, chroms=2)
+        fa = fa.upper()
+        (tmp_path / d / name).write_bytes(fa)
+        (tmp_path / d / (name + ".hash")).write_bytes(oracle_py.hash_index(fa, k=10))
+        (tmp_path / d / (name + ".md5")).write_bytes(hashlib.md5(fa).digest())
+        r1, r2 = synth.aligned_reads(g, 400, seed + 10, paired=True, random_frac=0.1)
+        blocks = fq.blocks_from_fastq(r1, r2, 1 << 16)
+        tmpl = fq.analyze_ids(blocks[0], False)
+        cfg = fq.Config(bin_mode=int(tmpl[0]))
+        carry = [0, 0]
+        enc = [oracle_py.encode_block_hash(b, True, carry, bin_mode=cfg.bin_mode) for b in blocks]
+        (tmp_path / f"{d}.arc").write_bytes(fq.arc_archive(enc, blocks, "x_1.fq", "x_2.fq", tmpl, cfg,
+                                                           plus_bare=fq.bare_plus(r1),
+                                                           ref_md5=hashlib.md5(fa).digest()))
+        arcs[d] = (r1, r2)
+    try:
+        for f in (shm, shm + ".sa_ref"):
+            if os.path.exists(f):
+                os.remove(f)
+        r = run(["-d", "-s", f"a/{name}", "a.arc", "ra"])
+        assert r.returncode == 0, r.stderr
+        assert (tmp_path / "ra_1.fastq").read_bytes() == arcs["a"][0]
+        # b's reference under the same name: not decoded against a's image
+        r = run(["-d", "-s", "-v", f"b/{name}", "b.arc", "rb"])
+        assert r.returncode == 0, r.stderr
+        assert "from /dev/shm/" not in r.stderr
+        assert (tmp_path / "rb_1.fastq").read_bytes() == arcs["b"][0]
+        assert (tmp_path / "rb_2.fastq").read_bytes() == arcs["b"][1]
+        assert open(shm, "rb").read() == (tmp_path / "b" / (name + ".hash")).read_bytes()   # republished
+        # a's .hash gone, b's image in /dev/shm: refused, not decoded wrongly
+        os.remove(tmp_path / "a" / (name + ".hash"))
+        r = run(["-d", "-s", f"a/{name}", "a.arc", "ra2"])
+        assert r.returncode != 0 and "is not the index of" in r.stderr, r.stderr
+        # b maps its own image with its .hash gone
+        os.remove(tmp_path / "b" / (name + ".hash"))
+        r = run(["-d", "-s", "-v", f"b/{name}", "b.arc", "rb2"])
+        assert r.returncode == 0 and "from /dev/shm/" in r.stderr, r.stderr
+        assert (tmp_path / "rb2_1.fastq").read_bytes() == arcs["b"][0]
+    finally:
+        for f in (shm, shm + ".sa_ref"):
+            if os.path.exists(f):
+                os.remove(f)

@@ -117,3 +117,19 @@ def test_unalignable_reads():
     ret, *_ = orc.hash_align([far, many_n, b"ACGT" * 30])
     assert ret[1] == -1          # more N than maxmis
     assert ret[0] == -1 and ret[2] == -1
+
+
+def test_unwrapped_chromosome_line():
+    """A chromosome on one FASTA line (the seed buffer was flushed
+    only between lines): 36 M bases give 18 M sampled seeds in that line, more
+    than the oracle's 2^24-entry buffer.  Line wrapping does not change the
+    index (positions count bases, the reference's getdelim loop keeps the
+    K-mer across lines), so the unwrapped FASTA's index equals the wrapped
+    one's."""
+    k = 10
+    chroms = [genome(36_000_000, 11), genome(300_000, 12)]
+    wrapped = orc.hash_index(fasta(chroms), k=k, step=2, maxcount=1 << 16)
+    one_line = orc.hash_index(fasta(chroms, width=1 << 40), k=k, step=2, maxcount=1 << 16)
+    assert one_line == wrapped
+    total, _, num, _, pos = parse_index(one_line, k)
+    assert total == 36_300_000 and len(pos) > (1 << 24)
