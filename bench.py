@@ -113,6 +113,9 @@ def parse_args(argv=None):
                     help="only the in-HBM line (no e2e / gzip / ingest / ONT / HASH legs, no CPU baselines)")
     ap.add_argument("--ont-leg", type=int, default=1, help="configs[4] leg: ONT-shape SE long reads, -l 1.15 (0: skip)")
     ap.add_argument("--ont-reads", type=int, default=60_000, help="reads of the ONT leg's batch (10-50 kbp)")
+    ap.add_argument("--se-leg", type=int, default=1,
+                    help="configs[1] leg: 150 bp SE, default Slevel and Slevel 8 (0: skip)")
+    ap.add_argument("--se-reads", type=int, default=10_000_000, help="reads of the SE leg's batch")
     ap.add_argument("--hash-leg", type=int, default=1, help="configs[3] leg: the HASH reference path (0: skip)")
     ap.add_argument("--hash-genome-mb", type=float, default=3100.0, help="synthetic genome of the HASH leg (GRCh38: 3100)")
     ap.add_argument("--hash-pairs", type=int, default=5_000_000,
@@ -144,7 +147,7 @@ def parse_args(argv=None):
     if a.e2e_batches < 0:   # (N ranks: rank 0's first batch, N x 2 times over, one seqarc_amd --devices N run)
         a.e2e_batches = a.batches if int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.gpus == 1 else 1
     if a.no_legs:
-        a.e2e_batches, a.cpu_seconds, a.ont_leg, a.hash_leg, a.ingest_devices = 0, 0.0, 0, 0, 0
+        a.e2e_batches, a.cpu_seconds, a.ont_leg, a.hash_leg, a.ingest_devices, a.se_leg = 0, 0.0, 0, 0, 0, 0
     if a.dry_run:
         a.pairs = min(a.pairs, 3000)
         a.block_size = min(a.block_size, 300_000)
@@ -405,6 +408,53 @@ def ont_leg(args, workers: int, local: int) -> dict:
             "phase_ms": phase_medians(W), "generate_s": round(gen_s, 1),
             "check": "first and last block bit-identical to oracle/fqz_oracle.c with -l 1.15",
             "data": "synthetic (tests/synth.py, 10/20/30/40/50 kbp SE, seed 1000 + k), inputs resident in HBM"}
+
+
+def se_leg(args, workers: int, local: int) -> dict:
+    """configs[1]: 10 M x 150 bp single-end reads, no reference, one batch
+    resident in HBM (~70 blocks of 50 MiB), the contexts' pipeline as in the
+    headline, at the default Slevel and at Slevel 8 (k = 15: the 2^30-context
+    base model, the README's "16-order" path, compressSeq@0x4248a0 /
+    BASE_MODEL ctor@0x42f63e); first and last block of each checked against
+    the CPU restatement."""
+    import copy
+    import fastqueeze_amd as fq
+    import oracle_py
+    a = copy.copy(args)
+    a.se, a.ont, a.pairs, a.inputs = True, False, args.se_reads, None
+    t0 = time.perf_counter()
+    blocks = make_batch(0, a, workers)
+    gen_s = time.perf_counter() - t0
+    tmpl = fq.analyze_ids(blocks[0], True)
+    inp = fq.Input(blocks, local)
+    tb = inp.text_bytes
+    out = {"metric": "MB/s FASTQ compressed, 150 bp SE, no-ref (configs[1], 1 MI355X)", "unit": "MB/s",
+           "reads": a.pairs, "fastq_bytes_per_batch": tb, "blocks": len(blocks), "contexts": args.contexts,
+           "steps": args.leg_steps, "generate_s": round(gen_s, 1),
+           "data": "synthetic (tests/synth.py, 150 bp SE, seed 1000), inputs resident in HBM", "slevels": {}}
+    try:
+        for sl in sorted({args.slevel, 8}):
+            cfg = fq.Config(slevel=sl, qlevel=args.qlevel, bin_mode=int(tmpl[0]))
+            encs = make_contexts(local, args.contexts)
+            try:
+                el, W = pipeline(encs, [inp], cfg, args.leg_steps, 2, local)
+                encs[0].run_input(inp, cfg)
+                outs = encs[0].fetch()
+            finally:
+                for e in encs:
+                    e.close()
+            for i in sorted({0, len(blocks) - 1}):
+                if outs[i] != oracle_py.encode_block(blocks[i], cfg.slevel, cfg.qlevel, cfg.md5, cfg.bin_mode):
+                    raise SystemExit(f"SE leg: Slevel {sl} block {i} differs from the CPU restatement")
+            out["slevels"][str(sl)] = {
+                "value": round(tb * args.leg_steps / el / 1e6, 1), "ms_per_step": round(el / args.leg_steps * 1e3, 2),
+                "order_k": sl + 7 if sl < 9 else 0, "ratio": round(tb / sum(map(len, outs)), 3),
+                "phase_ms": phase_medians(W),
+                "check": f"first and last block bit-identical to oracle/fqz_oracle.c at Slevel {sl}"}
+    finally:
+        inp.close()
+    out["value"] = out["slevels"][str(args.slevel)]["value"]
+    return out
 
 
 def hash_leg(args, local: int) -> dict:
@@ -1119,12 +1169,13 @@ def main():
         finally:
             shutil.rmtree(os.path.dirname(e2e_files[0]), True)
     if rank == 0 and world == 1:
-        for name, leg, on in (("ont_lossy", ont_leg, args.ont_leg), ("hash_path", hash_leg, args.hash_leg)):
+        for name, leg, on in (("se_leg", se_leg, args.se_leg), ("ont_lossy", ont_leg, args.ont_leg),
+                              ("hash_path", hash_leg, args.hash_leg)):
             if not on:
                 continue
             t0 = time.perf_counter()
             try:
-                res[name] = ont_leg(args, workers, local) if leg is ont_leg else hash_leg(args, local)
+                res[name] = hash_leg(args, local) if leg is hash_leg else leg(args, workers, local)
             except SystemExit:
                 raise
             except Exception as e:   # (recorded: the headline line stands on its own)

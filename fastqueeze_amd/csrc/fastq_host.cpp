@@ -191,6 +191,25 @@ int sa_cut_next_pe(const uint8_t* w1, uint64_t avail1, int eof1, const uint8_t* 
     std::future<uint64_t> f2 = std::async(std::launch::async, [&]() { return count_nl_par(w2, a2, 2); });
     const uint64_t k1 = count_nl_par(w1, a1, 2);
     const uint64_t k2 = f2.get();
+    return sa_cut_next_pe_nl(w1, avail1, eof1, k1, w2, avail2, eof2, k2, bs, first, flen, end1, end2);
+}
+
+// sa_cut_next_pe with the windows' newline counts given (k1 / k2: newlines in
+// the first min(avail, bs / 2) bytes of each window), e.g. counted by the
+// threads that read the input
+int sa_cut_next_pe_nl(const uint8_t* w1, uint64_t avail1, int eof1, uint64_t k1, const uint8_t* w2, uint64_t avail2,
+                      int eof2, uint64_t k2, uint64_t bs, const uint8_t* first, uint64_t flen, uint64_t* end1,
+                      uint64_t* end2)
+{
+    if (!w1 || !w2 || !end1 || !end2 || bs < 2 || !first || flen == 0) return -1;
+    const uint64_t half = (uint64_t)((uint32_t)bs >> 1);
+    if ((avail1 < half && !eof1) || (avail2 < half && !eof2)) return -1;
+    const uint64_t a1 = std::min<uint64_t>(avail1, half), a2 = std::min<uint64_t>(avail2, half);
+    if (a1 < half && a2 < half) {
+        *end1 = avail1;
+        *end2 = avail2;
+        return 0;
+    }
     const uint64_t k = std::min(k1, k2);
     if (k < 2) return -1;
     int64_t j = (int64_t)k - 2;

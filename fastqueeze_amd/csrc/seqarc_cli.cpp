@@ -21,6 +21,9 @@
 //   --share-device   all contexts on one GPU (tests of the multi-GPU gather)
 //   --host-only      read, cut and parse only (no device; measures the host pipeline)
 //   --host-parse     parse the blocks on host threads (default: on the device, sa_stage_text)
+//   --read-threads N plain-file reader threads (default 8; 0: the per-block window reader)
+//   --ingest-only    the reader and block cut alone, batches dealt to devices x contexts
+//                    consumers (no device); --ingest-crc: the consumers CRC the texts
 //
 // Compression mirrors SeqArc-1.6 main@0x41fd40 -> SeqArcContext::doReadAndEncode
 // @0x41a4e0 as a stream: one reader thread cuts 50 MiB blocks as the input
@@ -33,6 +36,7 @@
 // (SeqArcFile::writeFileInfo@0x4171b0).  The blocks in flight are bounded
 // (ReadBufPool@0x4341e0 plays that role in the reference).
 #include <dlfcn.h>
+#include <emmintrin.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <stdint.h>
@@ -714,6 +718,276 @@ struct Input {
     }
 };
 
+// Newlines in t[0, len): 64 bytes a step (compare, movemask, popcount).
+uint64_t count_newlines(const uint8_t* t, uint64_t len)
+{
+    uint64_t n = 0, i = 0;
+    const __m128i nl = _mm_set1_epi8('\n');
+    for (; i + 64 <= len; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(t + i));
+        const __m128i b = _mm_loadu_si128((const __m128i*)(t + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i*)(t + i + 32));
+        const __m128i d = _mm_loadu_si128((const __m128i*)(t + i + 48));
+        const uint64_t m = (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(a, nl)) |
+                           (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(b, nl)) << 16 |
+                           (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(c, nl)) << 32 |
+                           (uint64_t)(uint16_t)_mm_movemask_epi8(_mm_cmpeq_epi8(d, nl)) << 48;
+        n += (uint64_t)__builtin_popcountll(m);
+    }
+    for (; i < len; i++) n += t[i] == '\n';
+    return n;
+}
+
+// ---- plain files: read ahead in segments (round 5) -------------------------
+// The input files are read in segments of S bytes plus an overlap of W bytes
+// (one block window: bs / 2 + 64 KiB for PE, bs + 64 KiB for SE), so that every
+// window that starts inside a segment lies inside it, into a ring of R
+// page-locked buffers per file.  A pool of fill threads copies 4 MiB slices out
+// of the page cache (pread: one thread copies ~7 GB/s, eight ~58 GB/s on the
+// GPU box, profiles/round5_r5a_ingest_probe.txt) and counts the newlines of
+// every 256 KiB chunk of the slice while it is in cache.  The cut then reads a
+// window's newline count off the chunk counts (cultPEbuf@0x432180 counts both
+// windows' newlines: sa_cut_next_pe_nl) and walks back from the window's end as
+// before, and a block is a view into its segment -- no per-block window, no
+// carry copy.  A segment's slot is refilled once the cut has moved past it and
+// every block in it was staged (its text copied to the device) or parsed.
+struct SegReader {
+    static constexpr uint64_t kSlice = 4ull << 20, kChunk = 256ull << 10;
+    struct Seg {
+        uint8_t* p = nullptr;
+        uint64_t cap = 0;           // bytes of p
+        int64_t idx = -1;           // segment number held (-1: none yet)
+        uint64_t base = 0, len = 0;
+        uint32_t nslices = 0, next_slice = 0, done = 0;
+        int refs = 0;               // blocks (and the cut) still reading it
+        bool ready = false;         // p is allocated for this segment
+        bool filled = false;
+    };
+    struct File {
+        int fd = -1;
+        uint64_t size = 0;
+        int64_t nseg = 0;
+        int64_t next_start = 0;     // next segment number to start filling
+        int64_t low = 0;            // the cut's segment (the lower ones are free once their refs are 0)
+        std::vector<uint32_t> nl;   // newlines per kChunk of the file (the segments' primary parts)
+        std::vector<Seg> ring;
+    };
+    File f[2];
+    int nf = 1;
+    uint64_t S = 0, W = 0;
+    bool pinned = false, failed = false, stop = false;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::thread> workers;
+    std::atomic<uint64_t> alloc_bytes{0};
+    double fill_s = 0;   // fill threads' busy time (under mu)
+
+    // fds: open plain regular files; W: the cut's window
+    bool start(const int* fds, const uint64_t* sizes, int n, uint64_t window, int64_t ahead_bytes, int threads,
+               bool pin)
+    {
+        nf = n;
+        W = window;
+        pinned = pin;
+        uint64_t mx = 0;
+        for (int i = 0; i < n; i++) mx = std::max(mx, sizes[i]);
+        // segments of 512 MiB (a small input: one segment; SA_CLI_SEG_SLICES=n: n slices, for the tests)
+        S = std::max<uint64_t>(kSlice, std::min<uint64_t>(512ull << 20, (mx + kSlice - 1) / kSlice * kSlice));
+        if (const char* e = std::getenv("SA_CLI_SEG_SLICES")) S = kSlice * std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+        const int R = (int)std::max<int64_t>(3, (ahead_bytes + (int64_t)S - 1) / (int64_t)S + 3);
+        for (int i = 0; i < n; i++) {
+            File& F = f[i];
+            F.fd = fds[i];
+            F.size = sizes[i];
+            F.nseg = (int64_t)((F.size + S - 1) / S);
+            F.nl.assign((size_t)(F.size / kChunk + 1), 0);
+            F.ring.resize((size_t)std::max<int64_t>(1, std::min<int64_t>(R, F.nseg)));
+        }
+        for (int t = 0; t < std::max(1, threads); t++) workers.emplace_back([this]() { work(); });
+        return true;
+    }
+    ~SegReader() { free_all(); }
+    // the fill threads stopped, the segments' page-locked memory released (once
+    // every block was staged: off the exit, where unpinning ~10 GB took ~0.5 s)
+    void free_all()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        for (auto& t : workers) t.join();
+        workers.clear();
+        for (int i = 0; i < nf; i++)
+            for (Seg& s : f[i].ring) free_buf(s);
+    }
+    void free_buf(Seg& s)
+    {
+        if (!s.p) return;
+        if (pinned) sa_host_free(s.p);
+        else free(s.p);
+        s.p = nullptr;
+        s.cap = 0;
+    }
+    // under mu: a slice to fill (file, segment slot, slice), starting a segment when its slot is free
+    bool pick(int& fi, Seg*& sg, uint32_t& sl, bool& must_alloc)
+    {
+        int best = -1;
+        uint64_t best_off = ~0ull;
+        for (int i = 0; i < nf; i++) {
+            File& F = f[i];
+            // the lowest segment with slices left, else the next one to start
+            Seg* cand = nullptr;
+            for (int64_t k = std::max<int64_t>(0, F.next_start - (int64_t)F.ring.size()); k < F.next_start; k++) {
+                Seg& s = F.ring[(size_t)(k % (int64_t)F.ring.size())];
+                if (s.idx == k && s.ready && s.next_slice < s.nslices) {
+                    cand = &s;
+                    break;
+                }
+            }
+            uint64_t off;
+            if (cand) {
+                off = cand->base + (uint64_t)cand->next_slice * kSlice;
+            } else {
+                if (F.next_start >= F.nseg) continue;
+                Seg& s = F.ring[(size_t)(F.next_start % (int64_t)F.ring.size())];
+                const bool free_slot = s.idx < 0 || (s.refs == 0 && s.idx < F.low && s.filled);
+                if (!free_slot) continue;
+                off = (uint64_t)F.next_start * S;
+            }
+            if (off < best_off) {
+                best_off = off;
+                best = i;
+                sg = cand;
+            }
+        }
+        if (best < 0) return false;
+        fi = best;
+        File& F = f[best];
+        must_alloc = false;
+        if (!sg) {   // start segment next_start in its slot
+            Seg& s = F.ring[(size_t)(F.next_start % (int64_t)F.ring.size())];
+            s.idx = F.next_start++;
+            s.base = (uint64_t)s.idx * S;
+            s.len = std::min<uint64_t>(S + W, F.size - s.base);
+            s.nslices = (uint32_t)((s.len + kSlice - 1) / kSlice);
+            s.next_slice = s.done = 0;
+            s.filled = false;
+            s.ready = s.cap >= s.len;
+            must_alloc = !s.ready;
+            sg = &s;
+        }
+        sl = sg->next_slice++;
+        return true;
+    }
+    void work()
+    {
+        for (;;) {
+            int fi = 0;
+            Seg* sg = nullptr;
+            uint32_t sl = 0;
+            bool must_alloc = false;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || failed || pick(fi, sg, sl, must_alloc); });
+                if (stop || failed) return;
+            }
+            const auto t0 = std::chrono::steady_clock::now();
+            if (must_alloc) {   // (one worker per segment; the others wait for `ready`)
+                free_buf(*sg);
+                const uint64_t want = std::max<uint64_t>(sg->len, std::min<uint64_t>(S + W, f[fi].size));
+                void* p = pinned ? sa_host_alloc(want) : nullptr;
+                if (!p) {   // (no device: pageable, on huge pages where the kernel has them)
+                    if (posix_memalign(&p, 2u << 20, want) != 0) p = nullptr;
+                    else (void)madvise(p, want, MADV_HUGEPAGE);
+                }
+                std::lock_guard<std::mutex> g(mu);
+                if (!p) {
+                    failed = true;
+                    cv.notify_all();
+                    return;
+                }
+                alloc_bytes += want;
+                sg->p = static_cast<uint8_t*>(p);
+                sg->cap = want;
+                sg->ready = true;
+                cv.notify_all();
+            }
+            const uint64_t a = (uint64_t)sl * kSlice, n = std::min<uint64_t>(kSlice, sg->len - a);
+            uint64_t got = 0;
+            while (got < n) {
+                const ssize_t r = ::pread(f[fi].fd, sg->p + a + got, n - got, (off_t)(sg->base + a + got));
+                if (r < 0 && errno == EINTR) continue;
+                if (r <= 0) break;
+                got += (uint64_t)r;
+            }
+            // newlines of the slice's whole chunks in the segment's primary part
+            const uint64_t fa = sg->base + a, fe = std::min(sg->base + a + got, std::min(sg->base + S, f[fi].size));
+            for (uint64_t c = fa / kChunk; (c + 1) * kChunk <= fe && c * kChunk >= fa; c++)
+                f[fi].nl[(size_t)c] = (uint32_t)count_newlines(sg->p + (c * kChunk - sg->base), kChunk);
+            std::lock_guard<std::mutex> g(mu);
+            fill_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (got < n) {
+                failed = true;   // (the file shrank under us)
+            } else if (++sg->done == sg->nslices) {
+                sg->filled = true;
+            }
+            cv.notify_all();
+        }
+    }
+    // the cut's window at file offset off: waits for its segment, takes a
+    // reference for the block (release(fi, seg)), returns the bytes available
+    // from off within the segment; nullptr on a read failure
+    const uint8_t* window(int fi, uint64_t off, uint64_t& avail, int64_t& seg)
+    {
+        File& F = f[fi];
+        const int64_t k = std::min<int64_t>((int64_t)(off / S), std::max<int64_t>(F.nseg - 1, 0));
+        std::unique_lock<std::mutex> lk(mu);
+        F.low = k;
+        cv.notify_all();
+        Seg& s = F.ring[(size_t)(k % (int64_t)F.ring.size())];
+        cv.wait(lk, [&] { return failed || (s.idx == k && s.filled); });
+        if (failed) return nullptr;
+        s.refs++;
+        seg = k;
+        avail = s.base + s.len - off;
+        return s.p + (off - s.base);
+    }
+    void release(int fi, int64_t seg)
+    {
+        if (seg < 0) return;
+        std::lock_guard<std::mutex> g(mu);
+        Seg& s = f[fi].ring[(size_t)(seg % (int64_t)f[fi].ring.size())];
+        if (s.idx == seg && s.refs > 0) s.refs--;
+        cv.notify_all();
+    }
+    // the cut has passed every segment (the end of the input)
+    void finish()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (int i = 0; i < nf; i++) f[i].low = f[i].nseg;
+        cv.notify_all();
+    }
+    // newlines in [off, off + len) of file fi, inside the segment that holds off
+    // (filled): whole chunks of its primary part from the chunk counts, the rest counted
+    uint64_t newlines(int fi, uint64_t off, uint64_t len, const uint8_t* at_off)
+    {
+        const uint64_t seg_base = off / S * S, prim_end = seg_base + S, e = off + len;
+        const uint64_t e1 = std::min(e, prim_end);
+        uint64_t n = 0;
+        const uint64_t ca = (off + kChunk - 1) / kChunk, cb = e1 / kChunk;
+        if (ca >= cb) {
+            n += count_newlines(at_off, e1 - off);
+        } else {
+            n += count_newlines(at_off, ca * kChunk - off);
+            for (uint64_t c = ca; c < cb; c++) n += f[fi].nl[(size_t)c];
+            n += count_newlines(at_off + (cb * kChunk - off), e1 - cb * kChunk);
+        }
+        if (e > prim_end) n += count_newlines(at_off + (prim_end - off), e - prim_end);
+        return n;
+    }
+};
+
 struct Parsed {
     // (not page-locked: hipHostRegister from the parser threads serialised in
     // the driver -- 129 s of parser time for 14 GB, r2p; pageable staging from
@@ -821,7 +1095,9 @@ struct TextPool {
 };
 
 struct Job {                     // one block between the reader and the writer
-    Buf<uint8_t> t1, t2;          // its FASTQ text (recycled once parsed / staged)
+    Buf<uint8_t> t1, t2;          // its FASTQ text (recycled once parsed / staged; a view into a SegReader segment)
+    SegReader* segr = nullptr;    // (views: the segments' references, released with the text)
+    int64_t seg[2] = {-1, -1};
     uint64_t text1 = 0, text2 = 0;   // its text bytes in input 1 / 2
     uint32_t nreads = 0, len_long = 0;
     std::unique_ptr<Parsed> p;     // host parse (--host-parse; block 0 for the ID template)
@@ -831,14 +1107,26 @@ struct Job {                     // one block between the reader and the writer
 };
 
 // getFirstLine@0x431eb0: the '+' line of the first record carries no ID
-int bare_plus(const Buf<uint8_t>& t)
+int bare_plus(const uint8_t* t, size_t n)
 {
     size_t nl[3] = {0, 0, 0};
     int k = 0;
-    for (size_t i = 0; i < t.size() && k < 3; i++)
+    for (size_t i = 0; i < n && k < 3; i++)
         if (t[i] == '\n') nl[k++] = i + 1;
     if (k < 3) return 1;
     return nl[2] - nl[1] > 2 ? 0 : 1;
+}
+
+// a block's text back to the reader: its windows recycled, its segment references dropped
+void give_back(Job& j, TextPool& texts)
+{
+    texts.put(j.t1);
+    texts.put(j.t2);
+    if (j.segr) {
+        j.segr->release(0, j.seg[0]);
+        j.segr->release(1, j.seg[1]);
+    }
+    j.seg[0] = j.seg[1] = -1;
 }
 
 bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_text)
@@ -871,10 +1159,7 @@ bool parse_job(Job& j, bool pe, ParsedPool& pool, TextPool& texts, bool keep_tex
     p.sl.n = p.nreads;
     j.nreads = p.nreads;
     for (uint32_t r = 0; r < p.nreads; r++) j.len_long |= p.sl[r] > 0xffff;
-    if (!keep_text) {
-        texts.put(j.t1);
-        texts.put(j.t2);
-    }
+    if (!keep_text) give_back(j, texts);
     return true;
 }
 
@@ -882,7 +1167,8 @@ struct Options {
     const char *f1 = nullptr, *f2 = nullptr, *out = nullptr, *arc = nullptr, *ref = nullptr;
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
          verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = false,
-         release = false, stage_ahead = false, shm = false, maxmis_set = false;
+         release = false, stage_ahead = false, shm = false, maxmis_set = false, ingest_crc = false;
+    int read_threads = 8;   // --read-threads: the plain-file reader's fill threads (SegReader)
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -1223,8 +1509,17 @@ int compress(const Options& o)
             if (t.joinable()) t.join();
         }
     } prefill;
+    // plain regular files (not gzip, not a pipe) are read by the segment reader
+    // (SegReader, started below), the others in per-block windows (TextPool)
+    uint64_t fsize[2] = {0, 0};
+    bool seg_plain = o.read_threads > 0 && !in1.is_gz && (!pe || !in2.is_gz) && !std::getenv("SA_CLI_WINDOWS");
+    for (int i = 0; i < (pe ? 2 : 1) && seg_plain; i++) {
+        struct stat st;
+        if (fstat(i ? in2.fd : in1.fd, &st) != 0 || !S_ISREG(st.st_mode)) seg_plain = false;
+        else fsize[i] = (uint64_t)st.st_size;
+    }
     size_t prefill_chunks = 0;
-    if (texts.pinned) {
+    if (texts.pinned && !seg_plain) {
         size_t wins = (size_t)(pe ? 2 : 1) * (2 * (size_t)std::max(1, o.batch) + 4);
         uint64_t tot = 0;
         bool known = true;
@@ -1365,8 +1660,113 @@ int compress(const Options& o)
         if (chain) sa_align_chain_fail(chain);
     };
 
+    // plain regular files (not gzip, not a pipe): the segment reader (SegReader)
+    std::unique_ptr<SegReader> segr;
+    {
+        if (seg_plain) {
+            const uint64_t win = pe ? (uint64_t)((uint32_t)bs >> 1) : bs;
+            segr.reset(new SegReader());
+            const int fds[2] = {in1.fd, in2.fd};
+            // the reader runs at most two batches of blocks ahead of the staging (below)
+            segr->start(fds, fsize, pe ? 2 : 1, win + (64u << 10), (int64_t)(2 * B + 2) * (int64_t)win,
+                        o.read_threads, dev_parse);   // (page-locked for the device parse; --ingest-only too)
+        }
+    }
+    // the segments are released as soon as every block is staged (device parse)
+    std::thread seg_free;
+    bool seg_stop = false;
+    if (segr && dev_parse)
+        seg_free = std::thread([&]() {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return failed || seg_stop || (nblocks >= 0 && staged >= nblocks); });
+                if (failed || seg_stop) return;
+            }
+            segr->free_all();
+        });
     // reader: cuts blocks as the input arrives
     std::thread reader([&]() {
+        if (segr) {   // blocks are views into the segments
+            const uint64_t want = pe ? (uint64_t)((uint32_t)bs >> 1) : bs;
+            std::vector<uint8_t> first;
+            uint64_t o1 = 0, o2 = 0;
+            for (int64_t i = 0;; i++) {
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] {
+                        return failed || ((size_t)(nread - written) < max_inflight && (!dev_parse || nread - staged < 2 * B));
+                    });
+                    if (failed) return;
+                }
+                if (o1 >= fsize[0] && (!pe || o2 >= fsize[1])) {   // the input ended on a block boundary
+                    segr->finish();
+                    std::lock_guard<std::mutex> g(mu);
+                    nblocks = i;
+                    cv.notify_all();
+                    return;
+                }
+                const double tf0 = now_s();
+                uint64_t av1 = 0, av2 = 0;
+                int64_t s1 = -1, s2 = -1;
+                const uint8_t* w1 = segr->window(0, o1, av1, s1);
+                const uint8_t* w2 = pe ? segr->window(1, o2, av2, s2) : nullptr;
+                if (!w1 || (pe && !w2)) return fail("read error on the input");
+                const bool eof1 = o1 + av1 >= fsize[0], eof2 = pe && o2 + av2 >= fsize[1];
+                if (i == 0) {
+                    const void* nl = memchr(w1, '\n', (size_t)std::min(av1, want));
+                    first.assign(w1, nl ? (const uint8_t*)nl + 1 : w1 + std::min(av1, want));
+                    plus_bare = pe ? bare_plus(w2, (size_t)std::min(av2, want)) : bare_plus(w1, (size_t)std::min(av1, want));
+                }
+                const double tc0 = now_s();
+                fill_busy += tc0 - tf0;   // (waiting for the fill threads)
+                uint64_t e1 = 0, e2 = 0;
+                if (pe) {
+                    const uint64_t k1 = segr->newlines(0, o1, std::min(av1, want), w1);
+                    const uint64_t k2 = segr->newlines(1, o2, std::min(av2, want), w2);
+                    if (sa_cut_next_pe_nl(w1, av1, eof1, k1, w2, av2, eof2, k2, bs, first.data(), first.size(), &e1,
+                                          &e2) != 0)
+                        return fail("PE block cut failed (mates out of step)");
+                } else {
+                    const int64_t e = sa_cut_next_se(w1, av1, eof1, bs, first.data(), first.size());
+                    if (e < 0) return fail("block cut failed");
+                    e1 = (uint64_t)e;
+                }
+                cut_busy += now_s() - tc0;
+                if (e1 + e2 == 0) return fail("block cut made no progress");
+                std::unique_ptr<Job> j(new Job());
+                auto view = [](Buf<uint8_t>& b, const uint8_t* p, uint64_t n) {
+                    b.d = const_cast<uint8_t*>(p);
+                    b.n = n;
+                    b.cap = 0;   // (not a window: TextPool::put leaves it)
+                    b.external = true;
+                };
+                view(j->t1, w1, e1);
+                if (pe) view(j->t2, w2, e2);
+                j->segr = segr.get();
+                j->seg[0] = s1;
+                j->seg[1] = s2;
+                o1 += e1;
+                o2 += e2;
+                const bool last = o1 >= fsize[0] && (!pe || o2 >= fsize[1]);
+                if (last) {
+                    t_read_done = now_s();
+                    segr->finish();
+                }
+                j->text1 = e1;
+                j->text2 = e2;
+                if (dev_parse && i > 0) j->state = 1;   // (parsed on the device when staged)
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    total_in += e1 + e2;
+                    jobs[i] = std::move(j);
+                    if (!dev_parse || i == 0) to_parse.push_back(i);
+                    nread = i + 1;
+                    if (last) nblocks = nread;
+                }
+                cv.notify_all();
+                if (last) return;
+            }
+        }
         Buf<uint8_t> b1 = texts.get(), b2 = texts.get();
         std::vector<uint8_t> first;
         const uint64_t want = pe ? (uint64_t)((uint32_t)bs >> 1) : bs;
@@ -1401,7 +1801,7 @@ int compress(const Options& o)
                 const void* nl = memchr(b1.data(), '\n', b1.size());
                 const uint8_t* f0 = b1.data();
                 first.assign(f0, nl ? (const uint8_t*)nl + 1 : f0 + b1.size());
-                plus_bare = bare_plus(pe ? b2 : b1);
+                plus_bare = pe ? bare_plus(b2.data(), b2.size()) : bare_plus(b1.data(), b1.size());
             }
             const double tc0 = now_s();
             fill_busy += tc0 - tf0;
@@ -1555,8 +1955,7 @@ int compress(const Options& o)
             std::lock_guard<std::mutex> g(mu);
             staged += (int64_t)js.size();
             for (size_t i = 0; i < js.size(); i++) {
-                texts.put(js[i]->t1);   // (the device holds the text now)
-                texts.put(js[i]->t2);
+                give_back(*js[i], texts);   // (the device holds the text now)
                 js[i]->nreads = ti[i].nreads;
                 js[i]->len_long = ti[i].len_long;
                 js[i]->out.resize(ti[i].out_bound);
@@ -1663,17 +2062,18 @@ int compress(const Options& o)
                     while (te < cur && !t_first_enc.compare_exchange_weak(cur, te)) {}
                 }
                 if (dev_parse && !ctx) {   // --ingest-only: the batch is taken, its windows recycled
+                    for (size_t i = 0; i < js.size(); i++) {
+                        if (o.ingest_crc) {   // (a check of the delivered bytes, for the tests: CPU work no device path does)
+                            uint32_t c = (uint32_t)crc32(0L, js[i]->t1.data(), (uInt)js[i]->t1.size());
+                            if (pe) c = (uint32_t)crc32(c, js[i]->t2.data(), (uInt)js[i]->t2.size());
+                            js[i]->crc = c;
+                        }
+                        give_back(*js[i], texts);
+                        outs[i] = sa_out{nullptr, 0, 0};
+                    }
                     {
                         std::lock_guard<std::mutex> g(mu);
                         staged += (int64_t)js.size();
-                    }
-                    for (size_t i = 0; i < js.size(); i++) {
-                        uint32_t c = (uint32_t)crc32(0L, js[i]->t1.data(), (uInt)js[i]->t1.size());
-                        if (pe) c = (uint32_t)crc32(c, js[i]->t2.data(), (uInt)js[i]->t2.size());
-                        js[i]->crc = c;
-                        texts.put(js[i]->t1);
-                        texts.put(js[i]->t2);
-                        outs[i] = sa_out{nullptr, 0, 0};
                     }
                     cv.notify_all();
                 } else if (dev_parse) {
@@ -1694,8 +2094,7 @@ int compress(const Options& o)
                         staged += (int64_t)js.size();
                     }
                     for (size_t i = 0; i < js.size(); i++) {
-                        texts.put(js[i]->t1);   // (the device holds the text now)
-                        texts.put(js[i]->t2);
+                        give_back(*js[i], texts);   // (the device holds the text now)
                         js[i]->nreads = ti[i].nreads;
                         js[i]->len_long = ti[i].len_long;
                         js[i]->out.resize(ti[i].out_bound);
@@ -1803,6 +2202,14 @@ int compress(const Options& o)
     reader.join();
     for (auto& t : parsers) t.join();
     for (auto& t : encoders) t.join();
+    if (seg_free.joinable()) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            seg_stop = true;   // (wakes it when the run ended early)
+            cv.notify_all();
+        }
+        seg_free.join();
+    }
     const double t_joined = now_s();
     // the archive is finished (trailer, header, closed) before the contexts'
     // device buffers are released (~1.4 s for five contexts' ~200 GB)
@@ -2184,6 +2591,8 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--share-device")) o.share_device = true;
         else if (!strcmp(a, "--host-only")) o.host_only = true;
         else if (!strcmp(a, "--ingest-only")) o.ingest_only = true;
+        else if (!strcmp(a, "--ingest-crc")) o.ingest_crc = true;
+        else if (!strcmp(a, "--read-threads")) { if (!ival(o.read_threads, 0)) return usage(); }
         else if (!strcmp(a, "--no-ramp")) o.ramp = false;
         else if (!strcmp(a, "--ramp")) o.ramp = true;
         else if (!strcmp(a, "--release")) o.release = true;

@@ -174,6 +174,12 @@ int64_t sa_cut_next_se(const uint8_t *win, uint64_t avail, int eof, uint64_t blo
                        const uint8_t *first, uint64_t flen);
 int sa_cut_next_pe(const uint8_t *w1, uint64_t avail1, int eof1, const uint8_t *w2, uint64_t avail2, int eof2,
                    uint64_t block_size, const uint8_t *first, uint64_t flen, uint64_t *end1, uint64_t *end2);
+/* sa_cut_next_pe with the newline counts of both windows given: k1 / k2 =
+ * newlines in the first min(avail, block_size / 2) bytes of each window (the
+ * command line's reader threads count them as they read the input). */
+int sa_cut_next_pe_nl(const uint8_t *w1, uint64_t avail1, int eof1, uint64_t k1, const uint8_t *w2,
+                      uint64_t avail2, int eof2, uint64_t k2, uint64_t block_size, const uint8_t *first,
+                      uint64_t flen, uint64_t *end1, uint64_t *end2);
 /* Block parse: getBlockRead@0x411b60 (SE) / getBlockReadPE@0x412920 (PE).
  * Output arrays sized >= text bytes (names/seq/qual) and text/4+1 (lens). */
 int64_t sa_parse_se(const uint8_t *text, uint64_t len, uint8_t *names, uint16_t *name_lens,

@@ -32,8 +32,9 @@ def _write_archive(tmp_path, texts, names, arc="t.arc", block_size=fq.BLOCK_SIZE
     return str(path), len(blocks)
 
 
-def _run(args, cwd):
-    return subprocess.run([EXE] + args, capture_output=True, cwd=cwd, timeout=300)
+def _run(args, cwd, env=None):
+    return subprocess.run([EXE] + args, capture_output=True, cwd=cwd, timeout=300,
+                          env=None if env is None else dict(os.environ, **env))
 
 
 def _records(text):
@@ -294,7 +295,8 @@ def test_gzip_ingest_plain_multimember_bgzf(tmp_path, capsys):
     a truncated gzip file is an error.  The ingest MB/s of each is reported."""
     import gzip
     a, b = synth.generate(40_000, paired=True, seed=65)
-    files = {"plain": (a, b), "gz": (gzip.compress(a, 1), gzip.compress(b, 1)),
+    files = {"plain": (a, b), "plain_windows": (a, b), "plain_segments": (a, b),
+             "gz": (gzip.compress(a, 1), gzip.compress(b, 1)),
              "multi": (gzip.compress(a[:len(a) // 3], 1) + gzip.compress(a[len(a) // 3:], 1),
                        gzip.compress(b[:7], 1) + gzip.compress(b[7:], 1)),
              "bgzf": (_bgzf(a), _bgzf(b))}
@@ -303,8 +305,13 @@ def test_gzip_ingest_plain_multimember_bgzf(tmp_path, capsys):
         p1, p2 = tmp_path / f"{k}_1.fq", tmp_path / f"{k}_2.fq"
         p1.write_bytes(x)
         p2.write_bytes(y)
-        r = _run(["-c", "-f", "--ingest-only", "--devices", "2", "--contexts", "2", "--batch", "2", "--block-size",
-                  "1", "-t", "8", "-1", str(p1), "-2", str(p2), "-o", str(tmp_path / k)], tmp_path)
+        # plain: the segment reader (SegReader); plain_windows: the per-block window reader;
+        # plain_segments: 4 MiB segments in a ring of 4 (every slot refilled)
+        extra = ["--read-threads", "0"] if k == "plain_windows" else []
+        env = {"SA_CLI_SEG_SLICES": "1"} if k == "plain_segments" else None
+        r = _run(["-c", "-f", "--ingest-only", "--ingest-crc", "--devices", "2", "--contexts", "2", "--batch", "2",
+                  "--block-size", "1", "-t", "8"] + extra + ["-1", str(p1), "-2", str(p2), "-o", str(tmp_path / k)],
+                 tmp_path, env=env)
         assert r.returncode == 0, (k, r.stderr)
         err = r.stderr.decode()
         crc = [ln for ln in err.splitlines() if "crc32" in ln][0].split()[-1]
