@@ -158,11 +158,9 @@ SA_HD uint32_t base_code(uint8_t c)
 // (e.g. 'A'-0x20 = '!' stays '!'); only letters can reach the cases above
 // because `c|0x20` equals a lowercase letter iff c is that letter in either case.
 
-SA_HD int nbits_u32(uint32_t v)
+SA_HD int nbits_u32(uint32_t v)   // bits of v (0 for 0)
 {
-    int n = 0;
-    while (v) { n++; v >>= 1; }
-    return n;
+    return v ? 32 - __builtin_clz(v) : 0;
 }
 
 // ---- per-read statistics (pass 1) ------------------------------------------

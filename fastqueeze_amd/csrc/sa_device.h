@@ -150,6 +150,7 @@ struct TaskList {
     uint32_t count;
     uint32_t nlong;          // pass R: entries [0, nlong) get a wave each, the rest are shared (k_coder_rv)
     uint64_t total_segs;
+    uint32_t wait_ticks;     // pass R: how long a wave waits for unwritten records (100 MHz ticks; 0: 20 s)
 };
 
 struct CoderView {

@@ -202,6 +202,14 @@ struct sa_ctx {
     hipEvent_t ev_dense = nullptr;
     hipEvent_t ev_fork = nullptr, ev_fork_seq = nullptr, ev_md5_done = nullptr, ev_r[2] = {nullptr, nullptr};
     hipEvent_t ev_seq_done = nullptr, ev_long_done = nullptr;
+    // the AUX record array is all zero between batches (pass R's unwritten-record
+    // test): zeroed in the tail of the batch that used it (st3, after the L
+    // passes), not in the front turn; prs_zero_cap = its bytes known zero,
+    // ev_prs_zero = that tail memset
+    hipEvent_t ev_prs_zero = nullptr;
+    size_t prs_zero_cap = 0;
+    void* prs_zero_p = nullptr;
+    bool prs_zero_pending = false;
     uint32_t long_lds = 0;
     bool serial_seq = false;
     uint32_t chain_prio = 1;   // s_setprio 3 in the latency-bound chain kernels (SA_CHAIN_PRIO=0: off)
@@ -244,6 +252,13 @@ struct sa_ctx {
     // 8,081 / 8,260 MB/s), so those keep 0.  SA_RV_VARIANT=0 / 5: one for all.
     int rv_variant = std::getenv("SA_RV_VARIANT") ? std::atoi(std::getenv("SA_RV_VARIANT")) : -1;
     int rv_batch = 5;   // the current batch's (run_input)
+    // pass R's wait for records the long runs have not written (SA_RV_WAIT_MS, default 20 s: the
+    // long runs take ~0.4 s; a wave that waits longer gives up and the batch fails with E_CODER)
+    uint32_t rv_wait_ticks = std::getenv("SA_RV_WAIT_MS")
+                                 ? (uint32_t)std::min<uint64_t>(100000ull * (uint64_t)std::max(1, std::atoi(std::getenv("SA_RV_WAIT_MS"))),
+                                                                4000000000ull)
+                                 : 2000000000u;
+    bool test_skip_long = std::getenv("SA_TEST_SKIP_LONG") != nullptr;   // (tests: starve pass R)
     uint32_t rv_short_waves = std::getenv("SA_RV_SHORT_WAVES") ? (uint32_t)std::atoi(std::getenv("SA_RV_SHORT_WAVES")) : 32u;
     // k_replay_aux_long workgroups: what the long-run CUs hold at once (6 per CU;
     // SA_LONG_GRID overrides, round 2 used 2048)
@@ -348,7 +363,7 @@ struct sa_ctx {
             if (ev_beg[i]) (void)hipEventDestroy(ev_beg[i]);
             if (ev_end[i]) (void)hipEventDestroy(ev_end[i]);
         }
-        for (hipEvent_t e : {ev_fork, ev_fork_seq, ev_md5_done, ev_r[0], ev_r[1], ev_seq_done, ev_long_done})
+        for (hipEvent_t e : {ev_fork, ev_fork_seq, ev_md5_done, ev_r[0], ev_r[1], ev_seq_done, ev_long_done, ev_prs_zero})
             if (e) (void)hipEventDestroy(e);
         if (mail) (void)hipHostFree(mail);
         for (uint8_t* m : mail_retired) (void)hipHostFree(m);
@@ -647,6 +662,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
         waves = nlong + c->rv_short_waves;
     }
     if (ph >= 0) ev_begin(c, ph, st);
+    tl.wait_ticks = c->rv_wait_ticks;
     const uint32_t grid = (waves + c->coder_waves - 1) / c->coder_waves;
     uint64_t* probe = nullptr;
     if (c->rv_probe && ph >= 0 && c->d_probe.ensure(32ull * grid * c->coder_waves) == hipSuccess) {
@@ -745,7 +761,9 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         hipLaunchKernelGGL(k_task_ends, dim3((tl.count + 255) / 256), dim3(256), 0, st, cv, tl,
                            c->d_task_ends.as<uint32_t>());
         std::vector<uint32_t> ends(tasks.size());
+        uint32_t perr[4] = {0, 0, 0, 0};
         SA_CHECK(c, d2h(c, ends.data(), c->d_task_ends.p, 4 * tasks.size(), st));
+        SA_CHECK(c, d2h(c, perr, c->d_err.p, 16, st));
         std::vector<uint64_t> probe;
         if (c->rv_probe && c->probe_waves) {
             probe.resize(4ull * c->probe_waves);
@@ -753,6 +771,10 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         }
         SA_CHECK(c, sync_d2h(c, st));
         if (!probe.empty()) write_rv_probe(c, probe);
+        if (perr[0] & E_CODER) {   // (pass R gave up on unwritten records: L3 is not run on them)
+            c->err = "range coder: pass R timed out waiting for model records (E_CODER)";
+            return -1;
+        }
         uint64_t payload = 0, slack = 4096;
         if (const char* e = std::getenv("SA_PAYLOAD_SLACK")) slack = std::strtoull(e, nullptr, 10);   // (tests)
         for (size_t t = 0; t < tasks.size(); t++) {
@@ -898,6 +920,7 @@ sa_ctx* sa_create(int device)
         hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_seq_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_long_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_prs_zero, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork_seq, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_md5_done, hipEventDisableTiming) != hipSuccess ||
@@ -1525,7 +1548,15 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     //      runs (latency-bound, st4: CU set B) and pass R of every coder chain
     //      (st3: the other CUs) start together: pass R waits per segment for
     //      records the long runs have not written yet (k_coder_r) ----
-    SA_CHECK(c, hipMemsetAsync(c->d_prs_aux.p, 0, atot * sizeof(PRec), st));
+    if (c->prs_zero_p != c->d_prs_aux.p || c->prs_zero_cap < atot * sizeof(PRec)) {
+        // (a new buffer, or the last batch did not end normally: zeroed here, all of it)
+        SA_CHECK(c, hipMemsetAsync(c->d_prs_aux.p, 0, c->d_prs_aux.cap, st));
+    } else if (c->prs_zero_pending) {   // (the previous batch's tail memset: long done by now)
+        SA_CHECK(c, hipStreamWaitEvent(st, c->ev_prs_zero, 0));
+    }
+    c->prs_zero_p = c->d_prs_aux.p;
+    c->prs_zero_cap = 0;   // (until this batch's tail zeroes what it wrote)
+    c->prs_zero_pending = false;
     ev_begin(c, PH_SORT_SEQ, st);
     if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, (int)seq_sh,
                  ns > 1 ? (int)seq_sh + seq_bits : 0, seq_sorted_buf, seq_sh != 0))
@@ -1599,7 +1630,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     hipStream_t st3 = c->st3, st4 = c->st4;
     if (c->host_waits) SA_CHECK(c, hipEventSynchronize(c->ev_fork_seq));
     else SA_CHECK(c, hipStreamWaitEvent(st4, c->ev_fork_seq, 0));
-    if (pa.total)
+    if (pa.total && !c->test_skip_long)
         hipLaunchKernelGGL(k_replay_aux_long, dim3(c->long_grid), dim3(128), c->long_lds, st4, rl, ak, av, sink_aux,
                            d_err, c->chain_prio);
     SA_CHECK(c, hipGetLastError());
@@ -1615,6 +1646,11 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         const int rc = coder_run(c, tasks, cv, st3, PH_CODER_R, PH_CODER_L, c->ev_long_done, exact, out_len, payload);
         if (rc) return rc;
     }
+    // the records this batch wrote back to zero, in its tail (after the L passes on st3)
+    SA_CHECK(c, hipMemsetAsync(c->d_prs_aux.p, 0, atot * sizeof(PRec), st3));
+    SA_CHECK(c, hipEventRecord(c->ev_prs_zero, st3));
+    c->prs_zero_cap = c->d_prs_aux.cap;
+    c->prs_zero_pending = true;
     // the final arena from the streams' real sizes: per block its encaps
     // (<= 32 header bytes each), count / MD5s, and the ID-bin first ID
     uint64_t final_bytes = 0;

@@ -458,7 +458,8 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
         uint32_t exc = 0, nsym = 0;
         if (__ballot(hasn != 0)) {   // (rows without such a base take no bytes: cnt = 0)
             uint32_t cg = 0;         // the row's carry from the previous step: gap after its last eligible ACGT
-            const int mq = (int)(maxq & 0xffu);
+            const int mq = (int)(maxq & 0xffu);   // (0..127: the max of signed qualities, from 0)
+            const uint32_t mq4 = 0x80808080u | ((uint32_t)mq * 0x01010101u);
             for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * PREP_ROW) {
                 const uint32_t pos = i0 + 16 * rl;
                 uint32_t sw[4] = {0, 0, 0, 0}, qw[4] = {0, 0, 0, 0}, cnt = 0;
@@ -467,18 +468,27 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
                     load16(s + pos, sw);
                     load16(q + pos, qw);
                 }
-                // the lane's summary
-                uint32_t g = 0, h = 0;
-                for (uint32_t j = 0; j < cnt; j++) {
-                    const int qi = (int)(int8_t)(qw[j >> 2] >> (8 * (j & 3)));
-                    if (qi > mq) continue;
-                    if (base_code((uint8_t)(sw[j >> 2] >> (8 * (j & 3)))) > 3) {
-                        g++;
-                    } else {
-                        g = 0;
-                        h = 1;
-                    }
+                // the lane's 16 bytes as bit masks (round 5: SWAR instead of a
+                // byte loop): E = eligible (signed quality <= maxq: a byte with
+                // the top bit set is negative, else (0x80 + maxq) - q keeps the
+                // top bit), A = ACGT; Y = eligible ACGT, N = eligible other bases
+                uint32_t E = 0, A = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t nb = cnt > 4u * k ? (cnt - 4u * k < 4 ? cnt - 4u * k : 4) : 0;
+                    const uint32_t inm = nb >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * nb)) - 1u));
+                    const uint32_t x = sw[k] | 0x20202020u;
+                    const uint32_t acgt = ~(bytes_nonzero(x ^ 0x61616161u) & bytes_nonzero(x ^ 0x63636363u) &
+                                            bytes_nonzero(x ^ 0x67676767u) & bytes_nonzero(x ^ 0x74747474u)) & inm;
+                    const uint32_t el = ((mq4 - (qw[k] & 0x7f7f7f7fu)) | qw[k]) & inm;
+                    // the four top bits -> four mask bits (bit 7 + 8j -> bit j)
+                    E |= ((((el >> 7) & 0x01010101u) * 0x01020408u) >> 24 & 0xfu) << (4 * k);
+                    A |= ((((acgt >> 7) & 0x01010101u) * 0x01020408u) >> 24 & 0xfu) << (4 * k);
                 }
+                const uint32_t Y = E & A, N = E & ~A;
+                // the lane's summary: eligible non-ACGT after its last eligible ACGT, and whether it has one
+                const uint32_t h = Y ? 1u : 0u;
+                const uint32_t g = Y ? (uint32_t)__popc(N >> (32 - __clz(Y))) : (uint32_t)__popc(N);
                 // inclusive row scan of (g, h): (A then B) = (hB ? gB : gA + gB, hA | hB)
                 uint32_t ig = g, ih = h;
 #pragma unroll
@@ -492,16 +502,20 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
                 uint32_t eg = __shfl_up(ig, 1, PREP_ROW), eh = __shfl_up(ih, 1, PREP_ROW);
                 if (rl == 0) eg = eh = 0;
                 // the gap entering this lane: the carry, then the lanes before it
-                uint32_t gap = eh ? eg : cg + eg;
-                for (uint32_t j = 0; j < cnt; j++) {
-                    const int qi = (int)(int8_t)(qw[j >> 2] >> (8 * (j & 3)));
-                    if (qi > mq) continue;
-                    if (base_code((uint8_t)(sw[j >> 2] >> (8 * (j & 3)))) > 3) {
-                        gap++;
-                    } else {
-                        exc++;
-                        nsym += 1 + (uint32_t)nbits_u32(gap);
-                        gap = 0;
+                const uint32_t gap = eh ? eg : cg + eg;
+                // each eligible ACGT base: 1 + bits(gap before it) symbols; only the
+                // first one of the lane and those after an eligible N have a gap
+                exc += (uint32_t)__popc(Y);
+                nsym += (uint32_t)__popc(Y);
+                if (Y) nsym += (uint32_t)nbits_u32(gap + (uint32_t)__popc(N & ((Y & (0u - Y)) - 1u)));
+                if (N && (Y & (Y - 1u))) {
+                    // (rare: eligible N bases between eligible ACGT bases of the lane)
+                    uint32_t yy = Y & (Y - 1u), from = (uint32_t)__ffs(Y);   // bits below `from` are done
+                    while (yy) {
+                        const uint32_t y = (uint32_t)__ffs(yy) - 1u;
+                        nsym += (uint32_t)nbits_u32((uint32_t)__popc(N & ((1u << y) - 1u) & ~((1u << from) - 1u)));
+                        from = y + 1u;
+                        yy &= yy - 1u;
                     }
                 }
                 // the row's total (lane 15's inclusive value) continues the carry
@@ -2399,10 +2413,18 @@ __device__ __forceinline__ void rc_range_salu(uint32_t& r, uint32_t m, uint32_t 
 // range to 0, where it stays -- a range chain never reaches 0 otherwise
 // (q >= 1, f >= 1).  So a segment that ends with r == 0 is re-coded from its
 // start once its records are in, read through L2.
-__device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t tmask, uint32_t& bad)
+// (round 5) The wait is bounded in time, on the constant 100 MHz clock:
+// `wait_ticks` per segment, and after one timeout the wave waits no more -- a
+// long-run kernel that never ran (tests/test_gpu_parity.py::
+// test_pass_r_starved_long_runs) ends the batch with E_CODER in about that
+// time, not after 2^22 polls for every segment it left unwritten.
+__device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t tmask, uint32_t& bad,
+                              uint32_t wait_ticks)
 {
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+    if (bad) return r0;
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + (wait_ticks ? wait_ticks : 2000000000u);
+    for (;;) {
         const uint32_t tf = __hip_atomic_load(reinterpret_cast<const uint32_t*>(P + lane), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t m = recip32z(tf & tmask);
@@ -2411,6 +2433,7 @@ __device__ uint32_t seg_retry(const PRec* __restrict__ P, uint32_t r0, uint32_t 
         for (int k = 0; k < 64; k++)
             rc_range_salu(r, __builtin_amdgcn_readlane(m, k), __builtin_amdgcn_readlane(tf, k), tmask);
         if (r != 0) return r;
+        if (__builtin_amdgcn_s_memrealtime() > t_end) break;
         __builtin_amdgcn_s_sleep(32);
     }
     bad = 1;
@@ -2635,7 +2658,7 @@ __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTas
                 const uint32_t r_seg = r;
                 const uint32_t vt = ctf & tmask, cm = recip32z(vt);
                 rv_segment<V>(r, cm, vt, ctf >> 16, std::make_integer_sequence<int, 8>{});
-                if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad);
+                if (r == 0) r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad, tl.wait_ticks);
                 g++;
             }
         }
