@@ -170,6 +170,35 @@ def test_deterministic_rerun(enc):
     assert enc.fetch() == first
 
 
+def test_pass_r_starved_long_runs(enc, monkeypatch):
+    """Pass R codes while the long SIMPLE_MODEL runs are still replayed and
+    waits for records they have not written (seg_retry).  With the long-run
+    kernel never launched (SA_TEST_SKIP_LONG, a test hook) every such wait
+    times out: the batch fails with E_CODER in about SA_RV_WAIT_MS, the L3 pass
+    does not run on the missing records, and a context made afterwards encodes
+    the same blocks exactly."""
+    import time
+    a, b = synth.generate(40_000, paired=True, seed=81)
+    blocks = fq.blocks_from_fastq(a, b, 4 << 20)
+    monkeypatch.setenv("SA_TEST_SKIP_LONG", "1")
+    monkeypatch.setenv("SA_RV_WAIT_MS", "300")
+    starved = fq.Encoder(0)
+    try:
+        t0 = time.perf_counter()
+        with pytest.raises(fq.SeqArcError, match="E_CODER|0x"):
+            starved.encode(blocks, fq.Config())
+        assert time.perf_counter() - t0 < 20
+    finally:
+        starved.close()
+    monkeypatch.delenv("SA_TEST_SKIP_LONG")
+    monkeypatch.delenv("SA_RV_WAIT_MS")
+    fresh = fq.Encoder(0)
+    try:
+        _check(fresh, blocks, fq.Config())
+    finally:
+        fresh.close()
+
+
 def test_rejects_out_of_model_quality(enc):
     bad = fq.parse_se(b"@r\nACGT\n+\nII\x7fI\n")
     with pytest.raises(fq.SeqArcError):
