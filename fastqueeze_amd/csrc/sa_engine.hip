@@ -308,7 +308,10 @@ struct sa_ctx {
     DBuf d_longs, d_huge_sorted, d_nlong;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
-    DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess;   // -l (rblock)
+    DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess, d_rb_tab;   // -l (rblock)
+    std::vector<uint32_t> rb_tab_host;   // the R decision tables (RbTab) of rb_tab_r
+    double rb_tab_r = -1.0;
+    bool rb_tab_sent = false;
     // reference path: per read the alignment of both carried states, status, the
     // alignment columns, the SEQ skip flags (sa_hash.hip, align_front)
     // per-read counts of every column (k_prep, k_prep_sq16 -> k_scan_reads ->
@@ -332,7 +335,7 @@ struct sa_ctx {
         return {&d_blocks, &d_totals, &d_err, &d_auxp_k, &d_auxp_v, &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux,
                 &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
                 &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_first_sq,
+                &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_rb_tab, &d_first_sq,
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
@@ -595,16 +598,31 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     SA_CHECK(c, c->d_rb_guess.ensure(sizeof(RbRun) * nck));
     SA_CHECK(c, h2d(c, c->d_rb_chunks.p, ck.data(), sizeof(RbChunk) * nck, st));
     SA_CHECK(c, h2d(c, c->d_rb_ck0.p, ck0.data(), 4ull * (nbk + 1), st));
+    // the decision tables of this R (rebuilt when R changes)
+    if (c->rb_tab_r != ratio || c->rb_tab_host.empty()) {
+        c->rb_tab_host.assign(2 * RB_TAB_WORDS, 0u);
+        rb_tab_build(ratio, c->rb_tab_host.data(), c->rb_tab_host.data() + RB_TAB_WORDS);
+        c->rb_tab_r = ratio;
+        c->rb_tab_sent = false;
+    }
+    if (!c->d_rb_tab.p) c->rb_tab_sent = false;
+    SA_CHECK(c, c->d_rb_tab.ensure(8ull * RB_TAB_WORDS));
+    if (!c->rb_tab_sent) {   // (through the mailbox, once per R)
+        SA_CHECK(c, h2d(c, c->d_rb_tab.p, c->rb_tab_host.data(), 8ull * RB_TAB_WORDS, st));
+        c->rb_tab_sent = true;
+    }
+    const uint32_t* tab = c->d_rb_tab.as<uint32_t>();
     const RbChunk* dck = c->d_rb_chunks.as<RbChunk>();
-    hipLaunchKernelGGL(k_rb_spec, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, dck, nck, ratio,
+    const uint32_t rgrid = (nck + RB_THREADS - 1) / RB_THREADS;
+    hipLaunchKernelGGL(k_rb_spec, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>());
-    hipLaunchKernelGGL(k_rb_guess, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, dck, nck, ratio,
+    hipLaunchKernelGGL(k_rb_guess, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>());
     hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk,
-                       ratio, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
+                       tab, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
                        c->d_rb_entry.as<RbRun>());
-    hipLaunchKernelGGL(k_rb_apply, dim3((nck + 63) / 64), dim3(64), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck, nck,
-                       ratio, c->d_rb_entry.as<RbRun>());
+    hipLaunchKernelGGL(k_rb_apply, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck, nck,
+                       tab, c->d_rb_entry.as<RbRun>());
     SA_CHECK(c, hipGetLastError());
     return 0;
 }

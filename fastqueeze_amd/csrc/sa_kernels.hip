@@ -557,13 +557,27 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
 // R-Block lossy pre-pass (rblock@0x426c10; sa_logic.h): speculative chunk
 // passes, one carry lane per block, chunk replay writing every run once.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_rb_spec(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
-                                                uint32_t nck, double R, uint32_t* __restrict__ opens,
-                                                RbRun* __restrict__ spec_exit)
+// (round 5) the R decision tables (sa_logic.h RbTab) in LDS, 16 KB per
+// workgroup of four waves; k_rb_fix (a lane per block, rarely past a compare)
+// reads them from global memory
+constexpr uint32_t RB_THREADS = 256;
+
+__device__ __forceinline__ RbTab rb_stage_tab(const uint32_t* __restrict__ tab, uint32_t* sh)
 {
-    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    for (uint32_t k = threadIdx.x; k < 2 * RB_TAB_WORDS; k += blockDim.x) sh[k] = tab[k];
+    __syncthreads();
+    return RbTab{sh, sh + RB_TAB_WORDS};
+}
+
+__global__ __launch_bounds__(RB_THREADS) void k_rb_spec(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
+                                                        uint32_t nck, const uint32_t* __restrict__ tab,
+                                                        uint32_t* __restrict__ opens, RbRun* __restrict__ spec_exit)
+{
+    __shared__ uint32_t sh[2 * RB_TAB_WORDS];
+    const RbTab t = rb_stage_tab(tab, sh);
+    const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck) return;
-    spec_exit[c] = rb_spec(q, ck[c], R, opens + (size_t)c * RB_WORDS);
+    spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * RB_WORDS);
 }
 
 // k_rb_guess: one lane per chunk, the chunk's exit if the run open before it
@@ -571,23 +585,27 @@ __global__ __launch_bounds__(64) void k_rb_spec(const uint8_t* __restrict__ q, c
 // chunk converged, i.e. nearly always.  k_rb_fix then only compares states,
 // and runs rb_carry itself (serial byte loads at memory latency: ~50 us per
 // chunk, 214 ms per ONT batch, r3r) where the guess does not apply.
-__global__ __launch_bounds__(64) void k_rb_guess(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
-                                                 uint32_t nck, double R, const uint32_t* __restrict__ opens,
-                                                 const RbRun* __restrict__ spec_exit, RbRun* __restrict__ guess)
+__global__ __launch_bounds__(RB_THREADS) void k_rb_guess(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
+                                                         uint32_t nck, const uint32_t* __restrict__ tab,
+                                                         const uint32_t* __restrict__ opens,
+                                                         const RbRun* __restrict__ spec_exit, RbRun* __restrict__ guess)
 {
-    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    __shared__ uint32_t sh[2 * RB_TAB_WORDS];
+    const RbTab t = rb_stage_tab(tab, sh);
+    const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck || c == 0 || (ck[c].flags & RB_FIRST)) return;
-    guess[c] = rb_carry(q, ck[c], spec_exit[c - 1], R, opens + (size_t)c * RB_WORDS, spec_exit[c]);
+    guess[c] = rb_carry(q, ck[c], spec_exit[c - 1], t, opens + (size_t)c * RB_WORDS, spec_exit[c]);
 }
 
 __global__ __launch_bounds__(64) void k_rb_fix(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
-                                               const uint32_t* __restrict__ ck0, uint32_t nblk, double R,
-                                               const uint32_t* __restrict__ opens,
+                                               const uint32_t* __restrict__ ck0, uint32_t nblk,
+                                               const uint32_t* __restrict__ tab, const uint32_t* __restrict__ opens,
                                                const RbRun* __restrict__ spec_exit, const RbRun* __restrict__ guess,
                                                RbRun* __restrict__ entry)
 {
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
     if (b >= nblk) return;
+    const RbTab t{tab, tab + RB_TAB_WORDS};
     const uint32_t c0 = ck0[b], c1 = ck0[b + 1];
     if (c0 == c1) return;
     RbRun cur = spec_exit[c0];
@@ -595,18 +613,21 @@ __global__ __launch_bounds__(64) void k_rb_fix(const uint8_t* __restrict__ q, co
         entry[c] = cur;
         const RbRun sp = spec_exit[c - 1];
         if (cur.start == sp.start && cur.mn == sp.mn && cur.mx == sp.mx) cur = guess[c];
-        else cur = rb_carry(q, ck[c], cur, R, opens + (size_t)c * RB_WORDS, spec_exit[c]);
+        else cur = rb_carry(q, ck[c], cur, t, opens + (size_t)c * RB_WORDS, spec_exit[c]);
     }
 }
 
-__global__ __launch_bounds__(64) void k_rb_apply(const uint8_t* __restrict__ q, uint8_t* __restrict__ out,
-                                                 const RbChunk* __restrict__ ck, uint32_t nck, double R,
-                                                 const RbRun* __restrict__ entry)
+__global__ __launch_bounds__(RB_THREADS) void k_rb_apply(const uint8_t* __restrict__ q, uint8_t* __restrict__ out,
+                                                         const RbChunk* __restrict__ ck, uint32_t nck,
+                                                         const uint32_t* __restrict__ tab,
+                                                         const RbRun* __restrict__ entry)
 {
-    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    __shared__ uint32_t sh[2 * RB_TAB_WORDS];
+    const RbTab t = rb_stage_tab(tab, sh);
+    const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck) return;
     const RbChunk k = ck[c];
-    rb_apply(q, out, k, (k.flags & RB_FIRST) ? RbRun{k.base, 0u, 0u} : entry[c], R);
+    rb_apply(q, out, k, (k.flags & RB_FIRST) ? RbRun{k.base, 0u, 0u} : entry[c], t);
 }
 
 // ---------------------------------------------------------------------------

@@ -749,16 +749,48 @@ SA_HD uint32_t rb_round_sqrt(uint32_t n)
     return n > g * g + g ? g + 1 : g;
 }
 
+// The two decisions of a character outside the open run depend on two
+// bytes each, so they are tables of 256 x 256 bits per R (round 5; built once
+// per batch on the host with the reference's double arithmetic, staged in LDS
+// by the kernels): lo[c][mx] -- c below the run extends it (R > g/c and
+// R > mx/g, g = round(sqrt(c*mx)), @0x426d48), hi[c][mn] -- c above it does
+// (R > g/mn and R > c/g, g = round(sqrt(c*mn)), @0x426cc0).  The per-byte
+// step is then two compares and one bit test instead of an integer square root
+// and two double divisions in divergent lanes.
+constexpr uint32_t RB_TAB_WORDS = 256 * 256 / 32;
+struct RbTab {
+    const uint32_t* lo;
+    const uint32_t* hi;
+};
+
+SA_HD bool rb_tab_bit(const uint32_t* t, uint32_t c, uint32_t v)
+{
+    const uint32_t i = (c << 8) | (v & 0xffu);
+    return (t[i >> 5] >> (i & 31)) & 1u;
+}
+
+// lo / hi: RB_TAB_WORDS words each
+SA_HD void rb_tab_build(double R, uint32_t* lo, uint32_t* hi)
+{
+    for (uint32_t w = 0; w < RB_TAB_WORDS; w++) lo[w] = hi[w] = 0;
+    for (uint32_t c = 0; c < 256; c++)
+        for (uint32_t v = 0; v < 256; v++) {
+            const uint32_t i = (c << 8) | v;
+            uint32_t g = rb_round_sqrt(c * v);   // v = mx
+            if (R > (double)g / (double)c && R > (double)v / (double)g) lo[i >> 5] |= 1u << (i & 31);
+            g = rb_round_sqrt(c * v);            // v = mn
+            if (R > (double)g / (double)v && R > (double)c / (double)g) hi[i >> 5] |= 1u << (i & 31);
+        }
+}
+
 // One character c of the open run; false: the run closes before c.
-SA_HD bool rb_extend(RbRun& s, uint32_t c, double R)
+SA_HD bool rb_extend(RbRun& s, uint32_t c, const RbTab& t)
 {
     if (s.mx >= c) {
         if (s.mn <= c) return true;
-        const uint32_t g = rb_round_sqrt(c * s.mx);
-        if (R > (double)g / (double)c && R > (double)s.mx / (double)g) { s.mn = c; return true; }
+        if (rb_tab_bit(t.lo, c, s.mx)) { s.mn = c; return true; }
     } else {
-        const uint32_t g = rb_round_sqrt(c * s.mn);
-        if (R > (double)g / (double)s.mn && R > (double)c / (double)g) { s.mx = c; return true; }
+        if (rb_tab_bit(t.hi, c, s.mn)) { s.mx = c; return true; }
     }
     return false;
 }
@@ -796,7 +828,7 @@ SA_HD void rb_for_bytes(const uint8_t* q, uint64_t base, uint32_t from, uint32_t
 }
 
 // Speculative pass over one chunk: bit i of opens = a run opens at byte i.
-SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, double R, uint32_t* opens)
+SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_t* opens)
 {
     RbRun s{ck.base, q[ck.base], q[ck.base]};
     uint32_t w = 1u;   // a run opens at the chunk's first byte
@@ -814,7 +846,8 @@ SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, double R, uint32_t* ope
 }
 
 // The true open run after chunk ck, given the true run open before it.
-SA_HD RbRun rb_carry(const uint8_t* q, const RbChunk& ck, RbRun s, double R, const uint32_t* opens, const RbRun& spec_exit)
+SA_HD RbRun rb_carry(const uint8_t* q, const RbChunk& ck, RbRun s, const RbTab& R, const uint32_t* opens,
+                     const RbRun& spec_exit)
 {
     bool conv = false;
     rb_for_bytes(q, ck.base, 0, ck.len, [&](uint32_t i, uint32_t c) {
@@ -832,7 +865,7 @@ SA_HD RbRun rb_carry(const uint8_t* q, const RbChunk& ck, RbRun s, double R, con
 
 // Writes every run that closes inside chunk ck (and, in the block's last
 // chunk, the final run); entry = the true run open before the chunk.
-SA_HD void rb_apply(const uint8_t* q, uint8_t* out, const RbChunk& ck, RbRun s, double R)
+SA_HD void rb_apply(const uint8_t* q, uint8_t* out, const RbChunk& ck, RbRun s, const RbTab& R)
 {
     uint32_t from = 0;
     if (ck.flags & RB_FIRST) {

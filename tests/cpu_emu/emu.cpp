@@ -334,6 +334,9 @@ int main(int argc, char** argv)
     std::vector<uint8_t> qual_q;
     if (lossy > 0.0) {
         qual_q.assign(qual.size(), 0);
+        std::vector<uint32_t> tabw(2 * RB_TAB_WORDS);   // (the R decision tables the kernels stage in LDS)
+        rb_tab_build(lossy, tabw.data(), tabw.data() + RB_TAB_WORDS);
+        const RbTab tab{tabw.data(), tabw.data() + RB_TAB_WORDS};
         for (int64_t b = 0; b < nb; b++) {
             const DevBlock& d = blocks[(size_t)b];
             std::vector<RbChunk> ck;
@@ -344,13 +347,13 @@ int main(int argc, char** argv)
             if (ck.empty()) continue;
             std::vector<uint32_t> opens(ck.size() * RB_WORDS);
             std::vector<RbRun> spec(ck.size()), entry(ck.size());
-            for (size_t c = 0; c < ck.size(); c++) spec[c] = rb_spec(qual.data(), ck[c], lossy, &opens[c * RB_WORDS]);
+            for (size_t c = 0; c < ck.size(); c++) spec[c] = rb_spec(qual.data(), ck[c], tab, &opens[c * RB_WORDS]);
             RbRun cur = spec[0];
             for (size_t c = 1; c < ck.size(); c++) {
                 entry[c] = cur;
-                cur = rb_carry(qual.data(), ck[c], cur, lossy, &opens[c * RB_WORDS], spec[c]);
+                cur = rb_carry(qual.data(), ck[c], cur, tab, &opens[c * RB_WORDS], spec[c]);
             }
-            for (size_t c = ck.size(); c-- > 0;) rb_apply(qual.data(), qual_q.data(), ck[c], entry[c], lossy);
+            for (size_t c = ck.size(); c-- > 0;) rb_apply(qual.data(), qual_q.data(), ck[c], entry[c], tab);
             std::vector<uint8_t> ref(qual.begin() + (long)d.seq_base, qual.begin() + (long)(d.seq_base + d.seq_bytes));
             orc_rblock(ref.data(), ref.size(), lossy);
             if (std::memcmp(ref.data(), qual_q.data() + d.seq_base, ref.size())) {
