@@ -308,6 +308,7 @@ struct sa_ctx {
     DBuf d_longs, d_huge_sorted, d_nlong;
     DBuf d_ck, d_maps, d_low_at, d_off_at, d_first_sq;
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
+    DBuf d_dege_list;   // the reads with N / IUPAC bases (k_dege_list -> k_emit_sq)
     DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess, d_rb_tab;   // -l (rblock)
     std::vector<uint32_t> rb_tab_host;   // the R decision tables (RbTab) of rb_tab_r
     double rb_tab_r = -1.0;
@@ -335,7 +336,7 @@ struct sa_ctx {
         return {&d_blocks, &d_totals, &d_err, &d_auxp_k, &d_auxp_v, &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux,
                 &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
                 &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_rb_tab, &d_first_sq,
+                &d_dege_list, &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_rb_tab, &d_first_sq,
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
@@ -1516,16 +1517,23 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                                akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh,
-                               (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE));
+                               (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE), nullptr);
         } else {
             hipLaunchKernelGGL(seq_sh ? k_emit_sq16<2> : k_emit_sq16<0>, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0,
                                st, bv, c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
                                F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr);
-            if (dege_maxq && n_ch)   // the N / IUPAC side streams of the reads that have such bases
+            if (dege_maxq && n_ch) {   // the N / IUPAC side streams of the reads that have such bases
+                SA_CHECK(c, c->d_dege_list.ensure(4ull * ((uint64_t)nr + 1)));
+                SA_CHECK(c, hipMemsetAsync(c->d_dege_list.p, 0, 4, st));
+                hipLaunchKernelGGL(k_dege_list, dim3(std::max<uint32_t>(1, std::min<uint32_t>((nr + 255) / 256, c->n_cu * 4))),
+                                   dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(), c->d_totals.as<uint32_t>(),
+                                   c->d_dege_list.as<uint32_t>());
                 hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                    c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
                                    F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr,
-                                   c->d_totals.as<uint32_t>(), dege_maxq, seq_sh, (uint32_t)EMIT_DEGE);
+                                   c->d_totals.as<uint32_t>(), dege_maxq, seq_sh, (uint32_t)EMIT_DEGE,
+                                   c->d_dege_list.as<uint32_t>());
+            }
         }
         if (al)   // the alignment streams (AlignInfoProcess[PE], decomposeAlignInfo)
             hipLaunchKernelGGL(k_align_emit, dim3(rgrid), dim3(256), 0, st, bv, alv, c->d_acounts.as<uint32_t>(),

@@ -873,6 +873,27 @@ __device__ __forceinline__ void emit_sq_read(const BatchView& bv, const uint32_t
     }
 }
 
+// The reads with N / IUPAC bases (a nonzero CH count): a wave tests 64 reads
+// at once (each lane one read's CH count, four dependent loads; one read per
+// wave step was 5.6 ms of dependent loads per batch, r4n) and appends the
+// flagged ones to list[1..] (list[0]: their number; zeroed before).
+__global__ __launch_bounds__(256) void k_dege_list(const BatchView bv, const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ totals, uint32_t* __restrict__ list)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * (blockDim.x >> 6) * 64;
+    for (uint32_t r0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < bv.nreads_total; r0 += stride) {
+        const uint32_t r = r0 + lane;
+        const bool has = r < bv.nreads_total && read_col_count(bv, counts, totals, r, C_CH) != 0;
+        const uint64_t m = __ballot(has);
+        if (!m) continue;
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(list, (uint32_t)__popcll(m));
+        at = (uint32_t)__shfl((int)at, 0, 64);
+        if (has) list[1 + at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = r;
+    }
+}
+
 __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv, const uint32_t* __restrict__ counts,
                                                               uint32_t* __restrict__ seq_key,
                                                               uint32_t* __restrict__ seq_val,
@@ -880,27 +901,22 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
                                                               uint32_t* __restrict__ aux_val,
                                                               const uint32_t* __restrict__ totals,
                                                               const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh,
-                                                              const uint32_t parts)
+                                                              const uint32_t parts,
+                                                              const uint32_t* __restrict__ dege_list)
 {
     __shared__ uint32_t comp[EMIT_WAVES][64];
     __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (parts == EMIT_DEGE) {
-        // only the reads with N / IUPAC bases have work (~1 % of 150 bp reads):
-        // a wave tests 64 reads at once (each lane one read's CH count, four
-        // dependent loads) and walks the ones that have some (round 3 tested one
-        // read per wave step: 5.6 ms of dependent loads per batch, r4n)
-        const uint32_t stride = gridDim.x * EMIT_WAVES * 64;
-        for (uint32_t r0 = (blockIdx.x * EMIT_WAVES + w) * 64; r0 < bv.nreads_total; r0 += stride) {
-            const uint32_t r = r0 + lane;
-            uint64_t m = __ballot(r < bv.nreads_total && read_col_count(bv, counts, totals, r, C_CH) != 0);
-            while (m) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                emit_sq_read(bv, r0 + j, lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val, totals,
-                             dege_maxq, seq_sh, parts);
-            }
-        }
+        // only the reads with N / IUPAC bases have work: k_dege_list listed
+        // them, a wave per listed read (round 5: the waves had walked the
+        // flagged reads of their own 64-read group -- for long reads, where
+        // nearly every read has some, 60,000 reads on ~940 waves, 76 ms per
+        // ONT batch, profiles/round5_r5b_ont_kernel_stats.txt)
+        const uint32_t n = dege_list[0];
+        for (uint32_t i = blockIdx.x * EMIT_WAVES + w; i < n; i += gridDim.x * EMIT_WAVES)
+            emit_sq_read(bv, dege_list[1 + i], lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val,
+                         totals, dege_maxq, seq_sh, parts);
         return;
     }
     for (uint32_t r = blockIdx.x * EMIT_WAVES + w; r < bv.nreads_total; r += gridDim.x * EMIT_WAVES)
