@@ -226,6 +226,10 @@ struct sa_ctx {
     // the other contexts' fronts beside them are not always; SA_L_PRIO=1, A/B)
     uint32_t l_prio = std::getenv("SA_L_PRIO") && std::atoi(std::getenv("SA_L_PRIO")) != 0 ? 1u : 0u;
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
+    // the SEQ space sorted by the context's top bits only and replayed per
+    // bucket with the models in LDS (k_replay_seq_bkt, contexts of <= 22 bits);
+    // SA_SEQ_BUCKET=0: the full sort and k_replay_seq (A/B)
+    bool seq_bucket = !(std::getenv("SA_SEQ_BUCKET") && std::atoi(std::getenv("SA_SEQ_BUCKET")) == 0);
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
     // k_md5<true> reads the next block's words while the chain runs: 148 VGPRs instead
@@ -1264,6 +1268,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // equal the sort pad) and order 0 has no sort pass, so they keep values
     // position << 2 | base (SA_SEQ_PACK=0: always)
     const uint32_t seq_sh = (ns > 1 && seq_bits <= 28 && !c->seq_unpacked) ? 2u : 0u;
+    // contexts of <= 22 bits (Slevel <= 4): one sort pass over the context's top
+    // 8 (9) bits, the low bkt_sb bits replayed per bucket with the models in LDS
+    // (k_replay_seq_bkt); longer contexts: the full sort and k_replay_seq
+    const bool seq_bkt = c->seq_bucket && seq_sh == 2 && seq_bits >= 12 && seq_bits <= 22;
+    const int bkt_sb = seq_bits <= 20 ? seq_bits - 8 : seq_bits - 9;
+    const int seq_lo = (int)seq_sh + (seq_bkt ? bkt_sb : 0), seq_hi = ns > 1 ? (int)seq_sh + seq_bits : 0;
     const int aux_bits = cfg->qlevel > 2 ? 21 : 17;
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
@@ -1469,7 +1479,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, F->d_nseq_long.ensure(4));
     SA_CHECK(c, F->d_short_at.ensure(max_short * 8));
     SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.tile_seg.size(), 1) * 4 *
-                                     sort_hist_per_tile((int)seq_sh, ns > 1 ? (int)seq_sh + seq_bits : 0)));
+                                     sort_hist_per_tile(seq_lo, seq_hi)));
     SA_CHECK(c, F->d_hist_aux.ensure(std::max<uint64_t>(pa.tile_seg.size(), 1) * 4 *
                                      sort_hist_per_tile(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits)));
     SA_CHECK(c, F->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
@@ -1584,12 +1594,21 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     c->prs_zero_cap = 0;   // (until this batch's tail zeroes what it wrote)
     c->prs_zero_pending = false;
     ev_begin(c, PH_SORT_SEQ, st);
-    if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, (int)seq_sh,
-                 ns > 1 ? (int)seq_sh + seq_bits : 0, seq_sorted_buf, seq_sh != 0))
+    if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, seq_lo, seq_hi, seq_sorted_buf,
+                 seq_sh != 0))
         return -1;
     ev_finish(c, PH_SORT_SEQ, st);
     ev_begin(c, PH_REPLAY_SEQ, st);
-    if (ps.total) {
+    if (ps.total && seq_bkt) {
+        const std::vector<int> dg = sort_digits(seq_lo, seq_hi);   // (one pass: its digit width)
+        if (dg.size() != 1) {
+            c->err = "internal: the SEQ bucket sort is not one pass";
+            return -1;
+        }
+        hipLaunchKernelGGL(k_replay_seq_bkt, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
+                           F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
+                           sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb);
+    } else if (ps.total) {
         SA_CHECK(c, hipMemsetAsync(F->d_nseq_long.p, 0, 4, st));
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,
                            F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),

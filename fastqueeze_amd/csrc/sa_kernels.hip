@@ -1749,6 +1749,138 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
 }
 
 // ---------------------------------------------------------------------------
+// k_replay_seq_bkt (round 5): BASE_MODEL replay after ONE sort pass.  The SEQ
+// space is sorted stably by the top TB bits of the context only -- a bucket;
+// inside it the symbols stay in stream order -- and one wave walks each
+// (block, bucket) in stream order with the models of the bucket's 2^SB
+// contexts in LDS (4 x u8 counts each, init 3, updated exactly as
+// replay_seq_run / encode_seq@0x421f30 do, the halving inline: no run goes to
+// k_replay_seq_long).  64 symbols a step: a lane writes its lane id to its
+// context's tag and reads it back; the lanes whose context no other lane of the
+// step has update their model directly (the common case), the lanes that share
+// one take their counts before them from ballots, or one after the other where
+// the shared run crosses a halving.  This replaces the further sort passes
+// (hist, scan, scatter each) and the tile-wide replay.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bm_tot(uint32_t s) { return (s * 0x01010101u) >> 24; }   // byte sum (< 256)
+
+// the record of base b under model s (tot | cum << 8 | freq << 16); s halved
+// first when its total is above 253 (replay_seq_run)
+__device__ __forceinline__ uint32_t bm_rec(uint32_t& s, uint32_t b)
+{
+    uint32_t tot = bm_tot(s);
+    if (tot > 253) {
+        s -= (s >> 1) & 0x7f7f7f7fu;
+        tot = bm_tot(s);
+    }
+    const uint32_t below = b ? (s & (0xffffffffu >> (32 - 8 * b))) : 0u;
+    return tot | (bm_tot(below) << 8) | (((s >> (8 * b)) & 0xffu) << 16);
+}
+
+__device__ __forceinline__ uint32_t bm_counts(uint64_t m, uint64_t b0, uint64_t b1, uint64_t b2, uint64_t b3)
+{
+    return (uint32_t)__popcll(m & b0) | (uint32_t)__popcll(m & b1) << 8 | (uint32_t)__popcll(m & b2) << 16 |
+           (uint32_t)__popcll(m & b3) << 24;
+}
+
+// grid: nsegs << tb workgroups of one wave; dynamic LDS (4 + 1) << sb bytes.
+// hist: the bucket pass's scanned histogram (row tile0 of a segment = its
+// digit starts); keys = context << 2 | base, values = stream positions.
+__global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const uint32_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ vals, const SymSink rec,
+                                                       uint32_t tb, uint32_t sb)
+{
+    extern __shared__ uint32_t bkt_lds[];
+    __shared__ uint32_t fl[64];
+    const uint32_t nsub = 1u << sb, nd = 1u << tb;
+    volatile uint32_t* mst = bkt_lds;
+    volatile uint8_t* tag = reinterpret_cast<volatile uint8_t*>(bkt_lds + nsub);
+    volatile uint32_t* vfl = fl;
+    const uint32_t seg = blockIdx.x >> tb, d = blockIdx.x & (nd - 1);
+    const SortSeg& sg = sv.segs[seg];
+    if (sg.count == 0) return;
+    const uint32_t* H = sv.hist + (size_t)sg.tile0 * nd;
+    const uint32_t start = H[d];
+    const uint32_t end = d + 1 < nd ? H[d + 1] : sg.count;   // (the pad keys sort last)
+    if (start >= end) return;
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < nsub; i += 64) mst[i] = 0x03030303u;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const uint32_t* K = keys + sg.base;
+    const uint32_t* V = vals + sg.base;
+    PRec* out = rec.prs + sg.base;
+    const uint32_t smask = nsub - 1;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t kn = 0, pn = 0;
+    if (start + lane < end) {
+        kn = K[start + lane];
+        pn = V[start + lane];
+    }
+    for (uint32_t i = start; i < end; i += 64) {
+        const bool act = i + lane < end;
+        const uint32_t k = kn, p = pn;
+        if (i + 64 + lane < end) {   // (the next step's symbols in flight during this one)
+            kn = K[i + 64 + lane];
+            pn = V[i + 64 + lane];
+        }
+        const uint32_t sub = (k >> 2) & smask, b = k & 3u;
+        if (act) tag[sub] = (uint8_t)lane;
+        asm volatile("" ::: "memory");   // (LDS operations of a wave complete in order)
+        const uint32_t t = act ? tag[sub] : lane;
+        uint32_t s = act ? mst[sub] : 0u;
+        const bool loser = t != lane;   // another lane of the step has this context
+        const uint64_t lm = __ballot(loser);
+        bool member = false;            // shares its context with another lane
+        if (lm) {
+            vfl[lane] = 0u;
+            asm volatile("" ::: "memory");
+            if (loser) vfl[t] = 1u;
+            asm volatile("" ::: "memory");
+            member = loser || vfl[lane] != 0u;
+        }
+        if (act && !member) {
+            const uint32_t r = bm_rec(s, b);
+            mst[sub] = s + (1u << (8 * b));
+            out[p] = PRec{r};
+        }
+        if (lm) {
+            const uint64_t b0 = __ballot(member && b == 0), b1 = __ballot(member && b == 1),
+                           b2 = __ballot(member && b == 2), b3 = __ballot(member && b == 3);
+            uint64_t M = __ballot(member);
+            while (M) {   // one group of lanes with the same context at a time
+                const uint32_t L = (uint32_t)__builtin_ctzll(M);
+                const uint32_t gs = (uint32_t)__shfl((int)sub, (int)L, 64);
+                const uint64_t G = __ballot(member && sub == gs);
+                const uint32_t s0 = (uint32_t)__shfl((int)s, (int)L, 64);
+                const uint32_t glen = (uint32_t)__popcll(G);
+                const bool in_g = (G >> lane) & 1ull;
+                if (bm_tot(s0) + glen - 1u <= 253u) {   // no halving inside the group
+                    if (in_g) {
+                        uint32_t si = s0 + bm_counts(G & below, b0, b1, b2, b3);
+                        out[p] = PRec{bm_rec(si, b)};
+                    }
+                    if (lane == L) mst[gs] = s0 + bm_counts(G, b0, b1, b2, b3);
+                } else {   // (rare) the group crosses a halving: in lane order
+                    uint32_t cur = s0, mine = 0;
+                    for (uint64_t g = G; g; g &= g - 1ull) {
+                        const uint32_t j = (uint32_t)__builtin_ctzll(g);
+                        const uint32_t bj = (uint32_t)__shfl((int)b, (int)j, 64);
+                        const uint32_t r = bm_rec(cur, bj);
+                        if (lane == j) mine = r;
+                        cur += 1u << (8 * bj);
+                    }
+                    if (in_g) out[p] = PRec{mine};
+                    if (lane == L) mst[gs] = cur;
+                }
+                M &= ~G;
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+}
+
+// ---------------------------------------------------------------------------
 // AUX model replay: SIMPLE_MODEL<N> (kModelEncode@0x42ccb0 and every inlined
 // copy), one model run = the symbols of one (block, model) in stream order.
 //   k_replay_aux_short: one lane per run start; runs of >= LONG_RUN symbols are
