@@ -243,13 +243,26 @@ extern "C" {
 // instead of 1.38 s and the process exit released it in 0.54 s instead of
 // 1.27 s (scripts/micro/exit_probe.hip, round 3 g4i); the DMA from it ran at
 // the same rate (35 vs 31 GB/s H2D, g3y).
+// (A/B knobs, round 5: SA_HOST_THP=0 leaves out the huge-page hint;
+// SA_HOST_MALLOC=1 takes hipHostMalloc memory instead of registered memory)
+namespace {
+int host_mode()   // 0: register + THP hint, 1: register only, 2: hipHostMalloc
+{
+    static const int m = std::getenv("SA_HOST_MALLOC") && std::atoi(std::getenv("SA_HOST_MALLOC")) != 0 ? 2
+                         : std::getenv("SA_HOST_THP") && std::atoi(std::getenv("SA_HOST_THP")) == 0 ? 1
+                                                                                                     : 0;
+    return m;
+}
+}  // namespace
+
 void* sa_host_alloc(uint64_t bytes)
 {
     constexpr uint64_t kHuge = 2ull << 20;
     const uint64_t n = ((bytes ? bytes : 1) + kHuge - 1) & ~(kHuge - 1);
     void* p = nullptr;
+    if (host_mode() == 2) return hipHostMalloc(&p, n, hipHostMallocPortable) == hipSuccess ? p : nullptr;
     if (posix_memalign(&p, kHuge, n) != 0) return nullptr;
-    (void)madvise(p, n, MADV_HUGEPAGE);   // (a hint: without THP the pages are 4 KiB)
+    if (host_mode() == 0) (void)madvise(p, n, MADV_HUGEPAGE);   // (a hint: without THP the pages are 4 KiB)
     if (hipHostRegister(p, n, hipHostRegisterPortable) != hipSuccess) {
         free(p);
         return nullptr;
@@ -260,6 +273,10 @@ void* sa_host_alloc(uint64_t bytes)
 void sa_host_free(void* p)
 {
     if (!p) return;
+    if (host_mode() == 2) {
+        (void)hipHostFree(p);
+        return;
+    }
     (void)hipHostUnregister(p);
     free(p);
 }
