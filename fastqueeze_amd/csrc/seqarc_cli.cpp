@@ -1536,67 +1536,86 @@ int compress(const Options& o)
     // contexts: K per device; every device's contexts share one front scratch
     std::vector<sa_ctx*> ctxs;
     std::vector<int> ctx_dev;   // (the device of each context)
-    // --ingest-only: the reader and the block cut alone, feeding devices x
-    // contexts consumers that take batches as the device parse would (no device)
-    if (o.host_only || o.ingest_only) ctxs.assign((size_t)o.contexts * (o.ingest_only ? o.devices : 1), nullptr);
-    for (int d = 0; d < o.devices && !o.host_only && !o.ingest_only; d++) {
-        sa_ctx* first = nullptr;
-        for (int k = 0; k < o.contexts; k++) {
-            const int dev = o.device + (o.share_device ? 0 : d);
-            sa_ctx* c = first ? sa_create_shared(dev, first) : sa_create(dev);
-            if (!c) break;
-            if (!first) first = c;
-            ctxs.push_back(c);
-            ctx_dev.push_back(dev);
-        }
-        if (!first) break;
-    }
-    // (started once the contexts exist: pinning beside their creation held
-    // it up, 0.25 -> 0.83 s, round 3 g4j)
-    if (prefill_chunks && !ctxs.empty() && ctxs[0])
-        prefill.t = std::thread([&texts, prefill_chunks]() {
-            for (size_t i = 0; i < prefill_chunks; i++)
-                if (!texts.grow()) break;
-        });
-    if (o.verbose)
-        for (sa_ctx* c : ctxs)
-            if (c) sa_set_timing(c, 1);
-    if (ctxs.empty()) {
-        fprintf(stderr, "seqarc_amd: no usable gfx950 device %d\n", o.device);
-        return 1;
-    }
     // reference path: the index on every device in use, one align_info chain
     // through all batches in input order (the reference's -t 1 thread)
     RefFiles rf;
     std::map<sa_ctx*, sa_align_cfg> acfg;
     std::vector<sa_hash_index*> indexes;
     sa_align_chain* chain = nullptr;
-    if (o.ref && !o.host_only && !o.ingest_only) {
-        if (!load_ref(o.ref, false, rf, o.shm, o.verbose)) return 1;
-        const double ti = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-        sa_ctx* owner = nullptr;
-        sa_hash_index* ix = nullptr;
-        for (size_t k = 0; k < ctxs.size(); k++) {
-            if (k % (size_t)o.contexts == 0 && !(o.share_device && ix)) {   // the first context of a device
-                owner = ctxs[k];
-                ix = rf.have_hash() ? sa_hash_load(owner, rf.hp, rf.hn)
-                                      : sa_hash_build(owner, (const char*)rf.fasta.data(), rf.fasta.size(), 14, 2, 1u << 16);
-                if (!ix) {
-                    fprintf(stderr, "seqarc_amd: reference index: %s\n", sa_last_error(owner));
-                    return 1;
-                }
-                indexes.push_back(ix);
+    // The plain-file reader starts before the device contexts exist (round 5):
+    // creating five contexts takes ~0.35 s, which the reader's first batch
+    // then overlaps instead of following.  (SA_CLI_EARLY_READ=0: contexts
+    // first, A/B.)  The contexts and the reference index: false with a message.
+    const bool early_read =
+        !(std::getenv("SA_CLI_EARLY_READ") && std::atoi(std::getenv("SA_CLI_EARLY_READ")) == 0) && seg_plain;
+    std::string ctx_err;
+    auto create_contexts = [&]() -> bool {
+        // --ingest-only: the reader and the block cut alone, feeding devices x
+        // contexts consumers that take batches as the device parse would (no device)
+        if (o.host_only || o.ingest_only) ctxs.assign((size_t)o.contexts * (o.ingest_only ? o.devices : 1), nullptr);
+        for (int d = 0; d < o.devices && !o.host_only && !o.ingest_only; d++) {
+            sa_ctx* first = nullptr;
+            for (int k = 0; k < o.contexts; k++) {
+                const int dev = o.device + (o.share_device ? 0 : d);
+                sa_ctx* c = first ? sa_create_shared(dev, first) : sa_create(dev);
+                if (!c) break;
+                if (!first) first = c;
+                ctxs.push_back(c);
+                ctx_dev.push_back(dev);
             }
-            acfg[ctxs[k]] = sa_align_cfg{ix, pe ? 1 : 0, o.maxmis, 1, (uint32_t)o.insert};
+            if (!first) break;
         }
-        chain = sa_align_chain_create(0, 0);   // a fresh encode thread's AlignParam (nmis 0)
+        // (started once the contexts exist: pinning beside their creation held
+        // it up, 0.25 -> 0.83 s, round 3 g4j)
+        if (prefill_chunks && !ctxs.empty() && ctxs[0])
+            prefill.t = std::thread([&texts, prefill_chunks]() {
+                for (size_t i = 0; i < prefill_chunks; i++)
+                    if (!texts.grow()) break;
+            });
         if (o.verbose)
-            fprintf(stderr, "seqarc_amd: reference %s: index %s in %.3f s\n", o.ref,
-                    rf.have_hash() ? "loaded" : "built",
-                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() - ti);
+            for (sa_ctx* c : ctxs)
+                if (c) sa_set_timing(c, 1);
+        if (ctxs.empty()) {
+            ctx_err = "no usable gfx950 device " + std::to_string(o.device);
+            return false;
+        }
+        if (o.ref && !o.host_only && !o.ingest_only) {
+            if (!load_ref(o.ref, false, rf, o.shm, o.verbose)) {
+                ctx_err = std::string("cannot load the reference ") + o.ref;
+                return false;
+            }
+            const double ti = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+            sa_ctx* owner = nullptr;
+            sa_hash_index* ix = nullptr;
+            for (size_t k = 0; k < ctxs.size(); k++) {
+                if (k % (size_t)o.contexts == 0 && !(o.share_device && ix)) {   // the first context of a device
+                    owner = ctxs[k];
+                    ix = rf.have_hash() ? sa_hash_load(owner, rf.hp, rf.hn)
+                                          : sa_hash_build(owner, (const char*)rf.fasta.data(), rf.fasta.size(), 14, 2,
+                                                          1u << 16);
+                    if (!ix) {
+                        ctx_err = std::string("reference index: ") + sa_last_error(owner);
+                        return false;
+                    }
+                    indexes.push_back(ix);
+                }
+                acfg[ctxs[k]] = sa_align_cfg{ix, pe ? 1 : 0, o.maxmis, 1, (uint32_t)o.insert};
+            }
+            chain = sa_align_chain_create(0, 0);   // a fresh encode thread's AlignParam (nmis 0)
+            if (o.verbose)
+                fprintf(stderr, "seqarc_amd: reference %s: index %s in %.3f s\n", o.ref,
+                        rf.have_hash() ? "loaded" : "built",
+                        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() - ti);
+        }
+        return true;
+    };
+    if (!early_read && !create_contexts()) {
+        fprintf(stderr, "seqarc_amd: %s\n", ctx_err.c_str());
+        return 1;
     }
     int64_t B = std::max(1, o.batch);
-    const int64_t C = (int64_t)ctxs.size();
+    // (the contexts the options ask for: with early_read they do not exist yet)
+    const int64_t C = early_read ? (int64_t)o.contexts * (o.host_only ? 1 : o.devices) : (int64_t)ctxs.size();
     // batch k = blocks [bstart(k), bstart(k + 1)).  --ramp: the first batch of
     // each context ramps up (B (k+1) / (C+1) blocks: the first encode starts
     // after a fraction of a batch is read, and the contexts' first tails are
@@ -1620,16 +1639,19 @@ int compress(const Options& o)
             B = (est + C - 1) / C;
         }
     }
-    const size_t max_inflight = (size_t)B * (ctxs.size() + 2);   // blocks read but not yet written
+    const size_t max_inflight = (size_t)B * ((size_t)C + 2);   // blocks read but not yet written
     std::vector<int64_t> ramp_start{0};
     for (int64_t k = 0; ramp && k < C; k++) ramp_start.push_back(ramp_start.back() + std::max<int64_t>(1, B * (k + 1) / (C + 1)));
     auto bstart = [&](int64_t k) -> int64_t {
         const int64_t r = (int64_t)ramp_start.size() - 1;
         return k <= r ? ramp_start[(size_t)k] : ramp_start.back() + (k - r) * B;
     };
-    if (ramp)
-        for (sa_ctx* c : ctxs)
-            if (c) sa_set_reserve(c, (uint32_t)B);
+    auto reserve = [&]() {
+        if (ramp)
+            for (sa_ctx* c : ctxs)
+                if (c) sa_set_reserve(c, (uint32_t)B);
+    };
+    if (!early_read) reserve();
 
     std::mutex mu;
     std::condition_variable cv;
@@ -1637,7 +1659,7 @@ int compress(const Options& o)
     std::map<int64_t, std::unique_ptr<Job>> jobs;
     // -v: when the stages first / last did something (seconds from the start)
     auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
-    const double t_ctx = now_s();
+    double t_ctx = now_s();   // (early_read: set once the contexts exist)
     std::atomic<double> t_read_done{0}, t_first_enc{1e30}, t_last_enc{0}, enc_busy{0}, parse_busy{0};
     double fill_busy = 0, cut_busy = 0;   // (reader thread only)
     std::deque<int64_t> to_parse;
@@ -1884,6 +1906,15 @@ int compress(const Options& o)
             }
         });
 
+    // early_read: the contexts now, beside the reader's first batch
+    if (early_read) {
+        if (create_contexts()) {
+            reserve();
+            t_ctx = now_s();
+        } else {
+            fail(ctx_err);
+        }
+    }
     // encoders: one host thread per context, batches of B blocks in order
     auto batch_ready = [&](int64_t k) {   // under mu
         if (!tmpl_ready) return false;
