@@ -1812,18 +1812,8 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
     PRec* out = rec.prs + sg.base;
     const uint32_t smask = nsub - 1;
     const uint64_t below = (1ull << lane) - 1ull;
-    uint32_t kn = 0, pn = 0;
-    if (start + lane < end) {
-        kn = K[start + lane];
-        pn = V[start + lane];
-    }
-    for (uint32_t i = start; i < end; i += 64) {
-        const bool act = i + lane < end;
-        const uint32_t k = kn, p = pn;
-        if (i + 64 + lane < end) {   // (the next step's symbols in flight during this one)
-            kn = K[i + 64 + lane];
-            pn = V[i + 64 + lane];
-        }
+    // one step: 64 symbols of the bucket in stream order (k: key, p: position)
+    auto step = [&](const uint32_t k, const uint32_t p, const bool act) __attribute__((always_inline)) {
         const uint32_t sub = (k >> 2) & smask, b = k & 3u;
         if (act) tag[sub] = (uint8_t)lane;
         asm volatile("" ::: "memory");   // (LDS operations of a wave complete in order)
@@ -1877,6 +1867,36 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
             }
         }
         asm volatile("" ::: "memory");
+    };
+    // BKT_AHEAD steps of symbols are loaded a chunk ahead: the wait for them
+    // (vmcnt, which counts the record stores too) comes once per chunk, when
+    // the previous chunk's scattered stores are mostly done, not once per step
+    constexpr uint32_t BKT_AHEAD = 8;
+    uint32_t ck[BKT_AHEAD], cp[BKT_AHEAD];
+#pragma unroll
+    for (uint32_t j = 0; j < BKT_AHEAD; j++) {
+        const uint32_t i = min(start + 64 * j + lane, end - 1);   // (branch-free loads)
+        ck[j] = K[i];
+        cp[j] = V[i];
+    }
+    for (uint32_t base = start; base < end; base += 64 * BKT_AHEAD) {
+        uint32_t nk[BKT_AHEAD], np[BKT_AHEAD];
+#pragma unroll
+        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
+            const uint32_t i = min(base + 64 * (BKT_AHEAD + j) + lane, end - 1);
+            nk[j] = K[i];
+            np[j] = V[i];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
+            const uint32_t i = base + 64 * j;
+            if (i < end) step(ck[j], cp[j], i + lane < end);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
+            ck[j] = nk[j];
+            cp[j] = np[j];
+        }
     }
 }
 
@@ -2883,6 +2903,128 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
             probe[4 * wi + 2] = c1 - c0;
             probe[4 * wi + 3] = hw | (uint64_t)(xcc & 0xffu) << 32 | (uint64_t)chains << 40;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_coder_rl (round 5): pass R with one chain per LANE.  k_coder_rv runs a
+// chain per wave on the scalar unit -- one scalar unit per CU, so its ~600
+// waves in flight (three to four batches of 172) held the scalar issue of
+// three quarters of the CUs, and the front kernels beside them, whose loops
+// and address arithmetic are scalar instructions, ran 2.5-6x slower than alone
+// (k_prep_sq16 4.4 -> 26.5 ms, k_emit_sq16 17 -> 43 ms; profiles/round5_r5e_*).
+// Here the same step runs in the VALU, 64 chains per wave, a batch's ~760
+// chains in ~12 workgroups.  A workgroup is two waves on two SIMDs: the
+// feeder (wave 0) loads each lane's next 64-record segment, waits for records
+// the long model runs have not written yet (tot 0; bounded as in seg_retry),
+// looks up the reciprocals (a 2^16-entry table of recip32z) and writes
+// (m, tf) pairs into one half of an LDS ring; the chain wave (wave 1) codes
+// the other half, one ds_read_b64 and the step per symbol.  One s_barrier per
+// segment hands the halves over.  Lanes whose chain has ended idle (exec).
+// Checkpoints (ck_r): each lane stores its range at the start of every
+// segment of its chain, first..last, as k_coder_rv does.
+// ---------------------------------------------------------------------------
+constexpr uint32_t RL_WAVES = 2;
+
+__global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __restrict__ tasks, const TaskList tl,
+                                                            const PRec* __restrict__ prs0,
+                                                            const PRec* __restrict__ prs1,
+                                                            const uint32_t* __restrict__ rtab,
+                                                            uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err,
+                                                            const uint32_t prio)
+{
+    __shared__ uint2 ring[2][SEG_SYMS][64];   // 64 KB: (m, tf) per segment step and lane
+    const uint32_t lane = threadIdx.x & 63;
+    const bool feeder = threadIdx.x < 64;
+    const uint32_t li = blockIdx.x * 64 + lane;
+    const bool has = li < tl.count;
+    uint32_t first = 0, last = 0, r = 0, tmask = 0xffu;
+    uint64_t seg_base = 0;
+    const PRec* P = prs0;
+    if (has) {
+        const CoderTask tk = tasks[tl.ids[li]];
+        const CoderRun run = tl.run[li];
+        P = (tk.space ? prs1 : prs0) + tk.rec_base;
+        tmask = tk.space ? 0xffffu : 0xffu;
+        first = run.start_seg;
+        last = tk.nseg - 1;
+        r = run.r0;
+        seg_base = tk.seg_base;
+    }
+    // segments coded by this lane: first .. last - 1 (the last is L3's alone)
+    const uint32_t nj = has && last > first ? last - first : 0u;
+    uint32_t J = nj;   // the workgroup's longest chain, in segments (both waves agree)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)J, d, 64);
+        J = J > o ? J : o;
+    }
+    J = (uint32_t)__builtin_amdgcn_readfirstlane((int)J);
+    if (feeder) {
+        uint32_t bad = 0;
+        const uint64_t wait = tl.wait_ticks ? tl.wait_ticks : 2000000000u;
+        // segment j of the lane's chain into ring half (j & 1)
+        auto fill = [&](uint32_t j) __attribute__((always_inline)) {
+            if (j >= nj) return;
+            // (a stream starts at any record: dword loads, each lane its own 256 B)
+            const uint32_t* S = reinterpret_cast<const uint32_t*>(P + (size_t)(first + j) * SEG_SYMS);
+            uint32_t v[SEG_SYMS];
+#pragma unroll
+            for (uint32_t k = 0; k < SEG_SYMS; k++) v[k] = S[k];
+            uint32_t zero = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < SEG_SYMS; k++) zero |= (v[k] & tmask) == 0;
+            if (zero && !bad) {   // records not written yet (long runs replayed concurrently)
+                const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
+                for (;;) {
+                    zero = 0;
+#pragma unroll
+                    for (uint32_t k = 0; k < SEG_SYMS; k++) {
+                        v[k] = __hip_atomic_load(S + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        zero |= (v[k] & tmask) == 0;
+                    }
+                    if (!zero) break;
+                    if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                        bad = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(32);
+                }
+            }
+            uint2* R = &ring[j & 1][0][lane];
+#pragma unroll
+            for (uint32_t k = 0; k < SEG_SYMS; k++) R[k * 64] = make_uint2(rtab[v[k] & tmask], v[k]);
+        };
+        fill(0);
+        __syncthreads();
+        for (uint32_t j = 0; j < J; j++) {
+            fill(j + 1);
+            __syncthreads();
+        }
+        if (__ballot(bad != 0) && lane == 0) atomicOr(err, (uint32_t)E_CODER);
+    } else {
+        set_chain_prio(prio);
+        uint32_t* ck = ck_r + seg_base;
+        __syncthreads();
+        for (uint32_t j = 0; j < J; j++) {
+            if (j < nj) {
+                ck[first + j] = r;
+                const uint2* R = &ring[j & 1][0][lane];
+                uint32_t rr = r;
+#pragma unroll 16
+                for (uint32_t k = 0; k < SEG_SYMS; k++) {
+                    const uint2 e = R[k * 64];
+                    const uint32_t t = e.y & tmask, f = e.y >> 16;
+                    uint32_t q = __umulhi(rr, e.x);
+                    q -= rr < q * t ? 1u : 0u;
+                    const uint32_t x = q * f;
+                    rr = x << (__builtin_clz(x) & 24);   // (x > 0: records are written)
+                }
+                r = rr;
+            }
+            __syncthreads();
+        }
+        if (has) ck[first + nj] = r;   // (the range entering segment `last`)
     }
 }
 
