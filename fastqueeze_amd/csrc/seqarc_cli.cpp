@@ -794,7 +794,12 @@ struct SegReader {
         // segments of 512 MiB (a small input: one segment; SA_CLI_SEG_SLICES=n: n slices, for the tests)
         S = std::max<uint64_t>(kSlice, std::min<uint64_t>(512ull << 20, (mx + kSlice - 1) / kSlice * kSlice));
         if (const char* e = std::getenv("SA_CLI_SEG_SLICES")) S = kSlice * std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
-        const int R = (int)std::max<int64_t>(3, (ahead_bytes + (int64_t)S - 1) / (int64_t)S + 3);
+        int R = (int)std::max<int64_t>(3, (ahead_bytes + (int64_t)S - 1) / (int64_t)S + 3);
+        // (A/B) SA_CLI_RING_SEGS=n: n segments per file.  The ring is page-locked
+        // once, at ~12 GB/s for the whole process (hipHostRegister does not scale
+        // with threads, profiles/round5_r5a_ingest_probe.txt): a smaller ring
+        // costs less of it before the first pass over it completes
+        if (const char* e = std::getenv("SA_CLI_RING_SEGS")) R = std::max(3, std::atoi(e));
         for (int i = 0; i < n; i++) {
             File& F = f[i];
             F.fd = fds[i];
@@ -2069,6 +2074,7 @@ int compress(const Options& o)
                 te = te2;
             }
         });
+    const double t_enc_start = now_s();
     for (size_t ci = 0; !stage_ahead && ci < ctxs.size(); ci++)
         encoders.emplace_back([&, ctx = ctxs[ci]]() {
             for (;;) {
@@ -2297,10 +2303,10 @@ int compress(const Options& o)
     if (tl >= 0) {
         if (o.verbose)
             fprintf(stderr,
-                    "seqarc_amd: contexts ready %.3f s, input read %.3f s, first encode %.3f s, last encode "
+                    "seqarc_amd: contexts ready %.3f s, encoders started %.3f s, input read %.3f s, first encode %.3f s, last encode "
                     "done %.3f s; encode busy %.3f s over %zu contexts, parse busy %.3f s over %d threads; "
                     "reader: fill %.3f s, cut %.3f s; stage %.3f s (%s parse)\n",
-                    t_ctx, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
+                    t_ctx, t_enc_start, t_read_done.load(), t_first_enc.load(), t_last_enc.load(), enc_busy.load(), ctxs.size(),
                     parse_busy.load(), nparse, fill_busy, cut_busy, stage_busy.load(),
                     dev_parse ? "device" : "host");
         if (o.verbose && texts.pinned) {
