@@ -51,7 +51,7 @@ cli() {   # name dir [env...]
     rm -f $d/e2e.arc
     return $rc
 }
-cli short $E/s X=1 && cli short_noearly $E/s SA_CLI_EARLY_READ=0 && cli short_ring4 $E/s SA_CLI_RING_SEGS=4 && cli short_ring6 $E/s SA_CLI_RING_SEGS=6 && cli short_lanes $E/s SA_RV_LANES=1 && cli long $E/l X=1 && cli long_nothp $E/l SA_HOST_THP=0 && cli long_hostmalloc $E/l SA_HOST_MALLOC=1 && cli short2 $E/s X=1 || exit 1
+cli short $E/s X=1 && cli short_noearly $E/s SA_CLI_EARLY_READ=0 && cli short_ring4 $E/s SA_CLI_RING_SEGS=4 && cli short_ring6 $E/s SA_CLI_RING_SEGS=6 && cli short_lanes $E/s SA_RV_LANES=1 && cli long $E/l X=1 && cli long_lanes $E/l SA_RV_LANES=1 && cli long_nothp $E/l SA_HOST_THP=0 && cli long_hostmalloc $E/l SA_HOST_MALLOC=1 && cli short2 $E/s X=1 || exit 1
 for t in 8 12 16; do
     (cd $E/l && timeout -k 10 120 $R/fastqueeze_amd/bin/seqarc_amd -c -f -v -t 16 -1 r1.fq -2 r2.fq -o ing --contexts 5 --batch 69 \
         --block-size 50 --ingest-only --devices 8 --read-threads $t) > $O/ingest_$t.log 2>&1
