@@ -236,6 +236,48 @@ def test_low_complexity_context_runs(enc):
         _check(enc, blocks, fq.Config(slevel=slevel))
 
 
+def _low_complexity_fastq(seed, n):
+    rng = np.random.default_rng(seed)
+    recs = []
+    motifs = [b"A", b"AC", b"CAG", b"GATTACA", b"TTTTTTTTTG"]
+    for i in range(n):
+        m = motifs[i % len(motifs)]
+        s = (m * 200)[: 100 + (i % 51)]
+        if i % 7 == 0:
+            arr = bytearray(s)
+            for p in rng.integers(0, len(arr), 3):
+                arr[int(p)] = b"ACGTN"[int(rng.integers(0, 5))]
+            s = bytes(arr)
+        q = bytes(rng.choice(np.frombuffer(b"F:,#", np.uint8), size=len(s), p=[0.7, 0.2, 0.08, 0.02]))
+        recs.append(b"@lc%d\n%s\n+\n%s\n" % (i, s, q))
+    return b"".join(recs)
+
+
+@pytest.mark.parametrize("lanes,bucket", [(0, 0), (1, 1), (1, 0), (0, 1)])
+def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket):
+    """Both pass-R kernels (k_coder_rv: a chain per wave on the scalar unit;
+    k_coder_rl: a chain per lane in the VALU fed through an LDS ring,
+    SA_RV_LANES) and both SEQ replays (the full sort + k_replay_seq; one bucket
+    sort pass + k_replay_seq_bkt, SA_SEQ_BUCKET) give the oracle's bytes:
+    multi-block PE batches (chains of ~2.9 M symbols and of a few), low-complexity
+    reads (context runs far past the first halving, contexts shared inside a
+    64-symbol step), Slevel 1 / 3 / 4 (8 / 12 / 13 low context bits per bucket)."""
+    monkeypatch.setenv("SA_RV_LANES", str(lanes))
+    monkeypatch.setenv("SA_SEQ_BUCKET", str(bucket))
+    e = fq.Encoder(0)
+    try:
+        a, b = synth.generate(40_000, paired=True, seed=91)
+        pe = fq.blocks_from_fastq(a, b, 4 << 20)
+        assert len(pe) >= 4
+        _check(e, pe, fq.Config())
+        _check(e, pe[:2], fq.Config(slevel=4, qlevel=3))
+        lc = fq.blocks_from_fastq(_low_complexity_fastq(33, 4000), None, 200_000)
+        for slevel in (3, 1):
+            _check(e, lc, fq.Config(slevel=slevel))
+    finally:
+        e.close()
+
+
 def _long_read_fastq(seed, n):
     """Reads whose lengths straddle the 64-position steps of k_emit_sq, with N /
     IUPAC bases anywhere (so a step compacts its ACGT bases) and '#' runs that
