@@ -319,6 +319,9 @@ struct sa_ctx {
     DBuf d_list_ids[2], d_list_gbase[2], d_list_run[2];
     DBuf d_dege_list;   // the reads with N / IUPAC bases (k_dege_list -> k_emit_sq)
     DBuf d_qual_q, d_rb_chunks, d_rb_ck0, d_rb_opens, d_rb_spec, d_rb_entry, d_rb_guess, d_rb_tab;   // -l (rblock)
+    DBuf d_rb_vals, d_rb_info;   // (round 5: run values per chunk byte, RbInfo per chunk)
+    // SA_RB_APPLY=1: the round-4 second full walk (k_rb_apply) instead of k_rb_true + k_rb_fill (A/B)
+    bool rb_apply_walk = std::getenv("SA_RB_APPLY") && std::atoi(std::getenv("SA_RB_APPLY")) != 0;
     std::vector<uint32_t> rb_tab_host;   // the R decision tables (RbTab) of rb_tab_r
     double rb_tab_r = -1.0;
     bool rb_tab_sent = false;
@@ -345,7 +348,7 @@ struct sa_ctx {
         return {&d_blocks, &d_totals, &d_err, &d_auxp_k, &d_auxp_v, &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux,
                 &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
                 &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_rtab, &d_ck, &d_maps, &d_low_at, &d_off_at,
-                &d_dege_list, &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_rb_tab, &d_first_sq,
+                &d_dege_list, &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_rb_tab, &d_rb_vals, &d_rb_info, &d_first_sq,
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
@@ -624,15 +627,29 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     const uint32_t* tab = c->d_rb_tab.as<uint32_t>();
     const RbChunk* dck = c->d_rb_chunks.as<RbChunk>();
     const uint32_t rgrid = (nck + RB_THREADS - 1) / RB_THREADS;
+    const bool walk = c->rb_apply_walk;
+    if (!walk) {
+        SA_CHECK(c, c->d_rb_vals.ensure((uint64_t)RB_CHUNK * nck));
+        SA_CHECK(c, c->d_rb_info.ensure(sizeof(RbInfo) * nck));
+    }
+    uint8_t* vals = walk ? nullptr : c->d_rb_vals.as<uint8_t>();
+    RbInfo* info = walk ? nullptr : c->d_rb_info.as<RbInfo>();
     hipLaunchKernelGGL(k_rb_spec, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
-                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>());
+                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), vals, info);
     hipLaunchKernelGGL(k_rb_guess, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>());
     hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk,
                        tab, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
                        c->d_rb_entry.as<RbRun>());
-    hipLaunchKernelGGL(k_rb_apply, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck, nck,
-                       tab, c->d_rb_entry.as<RbRun>());
+    if (walk) {
+        hipLaunchKernelGGL(k_rb_apply, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck,
+                           nck, tab, c->d_rb_entry.as<RbRun>());
+    } else {
+        hipLaunchKernelGGL(k_rb_true, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
+                           c->d_rb_opens.as<uint32_t>(), vals, info, c->d_rb_entry.as<RbRun>());
+        hipLaunchKernelGGL(k_rb_fill, dim3(nck), dim3(RB_WORDS), 0, st, c->d_qual_q.as<uint8_t>(), dck,
+                           c->d_rb_opens.as<uint32_t>(), vals, info);
+    }
     SA_CHECK(c, hipGetLastError());
     return 0;
 }

@@ -571,13 +571,15 @@ __device__ __forceinline__ RbTab rb_stage_tab(const uint32_t* __restrict__ tab, 
 
 __global__ __launch_bounds__(RB_THREADS) void k_rb_spec(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
                                                         uint32_t nck, const uint32_t* __restrict__ tab,
-                                                        uint32_t* __restrict__ opens, RbRun* __restrict__ spec_exit)
+                                                        uint32_t* __restrict__ opens, RbRun* __restrict__ spec_exit,
+                                                        uint8_t* __restrict__ vals, RbInfo* __restrict__ info)
 {
     __shared__ uint32_t sh[2 * RB_TAB_WORDS];
     const RbTab t = rb_stage_tab(tab, sh);
     const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck) return;
-    spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * RB_WORDS);
+    if (vals) spec_exit[c] = rb_spec_vals(q, ck[c], t, opens + (size_t)c * RB_WORDS, vals + (size_t)c * RB_CHUNK, info[c]);
+    else spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * RB_WORDS);
 }
 
 // k_rb_guess: one lane per chunk, the chunk's exit if the run open before it
@@ -628,6 +630,51 @@ __global__ __launch_bounds__(RB_THREADS) void k_rb_apply(const uint8_t* __restri
     if (c >= nck) return;
     const RbChunk k = ck[c];
     rb_apply(q, out, k, (k.flags & RB_FIRST) ? RbRun{k.base, 0u, 0u} : entry[c], t);
+}
+
+// (round 5) k_rb_true: a lane per chunk after a block's first, the true pass
+// from its entry until it converges with the speculative one (rb_true);
+// k_rb_fill: a workgroup of RB_WORDS threads per chunk, 32 output bytes each
+// from the open bits and the run values (rb_fill_word): the last open before
+// each thread's word is an exclusive max-scan over the workgroup's words.
+__global__ __launch_bounds__(RB_THREADS) void k_rb_true(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
+                                                        uint32_t nck, const uint32_t* __restrict__ tab,
+                                                        uint32_t* __restrict__ opens, uint8_t* __restrict__ vals,
+                                                        RbInfo* __restrict__ info, const RbRun* __restrict__ entry)
+{
+    __shared__ uint32_t sh[2 * RB_TAB_WORDS];
+    const RbTab t = rb_stage_tab(tab, sh);
+    const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
+    if (c >= nck || (ck[c].flags & RB_FIRST)) return;
+    rb_true(q, ck[c], entry[c], t, opens + (size_t)c * RB_WORDS, vals + (size_t)c * RB_CHUNK, info[c]);
+}
+
+__global__ __launch_bounds__(RB_WORDS) void k_rb_fill(uint8_t* __restrict__ out, const RbChunk* __restrict__ ck,
+                                                      const uint32_t* __restrict__ opens,
+                                                      const uint8_t* __restrict__ vals, const RbInfo* __restrict__ info)
+{
+    __shared__ int32_t wl[RB_WORDS / 64];
+    __shared__ uint32_t ev[2];
+    const uint32_t c = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const RbChunk k = ck[c];
+    if (t == 0) {
+        ev[0] = info[c].entry_val & 0xffu;
+        ev[1] = rb_chase(info, ck, c);
+    }
+    const uint32_t word = opens[(size_t)c * RB_WORDS + t];
+    // the last open at or before the end of each word, then exclusive over the words
+    int32_t m = word ? (int32_t)(32 * t + 31 - __clz(word)) : -1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t o = __shfl_up(m, d, 64);
+        if (lane >= (uint32_t)d) m = m > o ? m : o;
+    }
+    if (lane == 63) wl[w] = m;
+    __syncthreads();
+    int32_t prev = __shfl_up(m, 1, 64);
+    if (lane == 0) prev = -1;
+    for (uint32_t k2 = 0; k2 < w; k2++) prev = prev > wl[k2] ? prev : wl[k2];
+    if (32 * t < k.len) rb_fill_word(out, k, t, word, prev, vals + (size_t)c * RB_CHUNK, info[c], ev[0], ev[1]);
 }
 
 // ---------------------------------------------------------------------------

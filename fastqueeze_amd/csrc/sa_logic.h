@@ -886,6 +886,138 @@ SA_HD void rb_apply(const uint8_t* q, uint8_t* out, const RbChunk& ck, RbRun s, 
     }
 }
 
+// ---- R-Block output without a second full walk (round 5) ------------------
+// rb_apply walked every chunk a second time from its true entry and wrote each
+// closed run byte by byte (a divergent loop per close in lanes that close at
+// different bytes).  Instead: the speculative pass also records the value of
+// every run that closes inside the chunk at the run's start (vals, one byte
+// per chunk byte); rb_true re-walks a chunk from its true entry only until it
+// converges with the speculative pass, fixing the open bits and values of that
+// prefix; rb_fill_word then writes every byte from the open bits (the run a
+// byte belongs to starts at the last open at or before it) and the values --
+// 32 bytes per thread, no walk.  Per chunk (RbInfo): the value of the run
+// entering it if that run closes inside it (known), and where the run open at
+// its end starts (RB_OPEN_NONE in a block's last chunk, where the final run
+// closes; RB_OPEN_ENTRY if the entering run spans the chunk).  A run open at a
+// chunk's end takes its value from the chunks after it (rb_chase).
+constexpr uint32_t RB_OPEN_NONE = 0xffffffffu, RB_OPEN_ENTRY = 0xfffffffeu;
+struct RbInfo {
+    uint32_t entry_val;    // value of the run entering the chunk | known << 8
+    uint32_t last_start;   // start (chunk offset) of the run open at the chunk's end
+};
+
+// Speculative pass (rb_spec) recording run values: vals = the chunk's
+// RB_CHUNK bytes, vals[s] = the value of the run starting at s if it closes in
+// the chunk.  The speculative pass opens a run at byte 0, so no run enters.
+SA_HD RbRun rb_spec_vals(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_t* opens, uint8_t* vals,
+                         RbInfo& info)
+{
+    RbRun s{ck.base, q[ck.base], q[ck.base]};
+    uint32_t w = 1u;   // a run opens at the chunk's first byte
+    rb_for_bytes(q, ck.base, 1, ck.len, [&](uint32_t i, uint32_t c) {
+        if (!rb_extend(s, c, R)) {
+            vals[s.start - ck.base] = (uint8_t)rb_round_sqrt(s.mn * s.mx);
+            s = RbRun{ck.base + i, c, c};
+            w |= 1u << (i & 31);
+        }
+        if ((i & 31) == 31) { opens[i >> 5] = w; w = 0; }
+        return true;
+    });
+    if ((ck.len & 31) != 0) opens[(ck.len - 1) >> 5] = w;
+    for (uint32_t k = (ck.len + 31) >> 5; k < RB_WORDS; k++) opens[k] = 0;
+    info.entry_val = 0;
+    if (ck.flags & RB_LAST) {   // the final run closes at the block's end
+        vals[s.start - ck.base] = (uint8_t)rb_round_sqrt(s.mn * s.mx);
+        info.last_start = RB_OPEN_NONE;
+    } else {
+        info.last_start = (uint32_t)(s.start - ck.base);
+    }
+    return s;
+}
+
+// The true pass over chunk ck from its true entry run s (not the block's first
+// chunk: there the speculative pass is the true one), until it closes a run
+// where the speculative pass opened one -- from there both agree -- or to the
+// chunk's end.  Rewrites the open bits of that prefix, records the values of
+// the runs closing in it (the entering run's in info.entry_val) and, without
+// convergence, where the run open at the chunk's end starts.
+SA_HD void rb_true(const uint8_t* q, const RbChunk& ck, RbRun s, const RbTab& R, uint32_t* opens, uint8_t* vals,
+                   RbInfo& info)
+{
+    uint32_t w = 0;            // true open bits of the current word
+    uint32_t conv = ck.len;    // first byte from which both passes agree
+    bool entry_open = true;    // the run entering the chunk has not closed
+    info.entry_val = 0;
+    rb_for_bytes(q, ck.base, 0, ck.len, [&](uint32_t i, uint32_t c) {
+        if (!rb_extend(s, c, R)) {
+            const uint8_t g = (uint8_t)rb_round_sqrt(s.mn * s.mx);
+            if (entry_open) {
+                info.entry_val = (uint32_t)g | 0x100u;
+                entry_open = false;
+            } else {
+                vals[s.start - ck.base] = g;
+            }
+            if ((opens[i >> 5] >> (i & 31)) & 1u) {   // converged at i
+                conv = i;
+                return false;
+            }
+            s = RbRun{ck.base + i, c, c};
+            w |= 1u << (i & 31);
+        }
+        if ((i & 31) == 31) { opens[i >> 5] = w; w = 0; }
+        return true;
+    });
+    if (conv < ck.len) {   // the word holding conv: true bits below it, the speculative ones from it
+        const uint32_t k = conv >> 5, lo = (conv & 31) ? (1u << (conv & 31)) - 1u : 0u;
+        opens[k] = (w & lo) | (opens[k] & ~lo);
+        return;            // (info.last_start: the speculative pass's)
+    }
+    if ((ck.len & 31) != 0) opens[(ck.len - 1) >> 5] = w;
+    const uint8_t g = (uint8_t)rb_round_sqrt(s.mn * s.mx);
+    if (ck.flags & RB_LAST) {   // the final run closes at the block's end
+        if (entry_open) info.entry_val = (uint32_t)g | 0x100u;
+        else vals[s.start - ck.base] = g;
+        info.last_start = RB_OPEN_NONE;
+    } else {
+        info.last_start = entry_open ? RB_OPEN_ENTRY : (uint32_t)(s.start - ck.base);
+    }
+}
+
+// The value of the run open at the end of chunk c: the run entering c + 1,
+// which closes in c + 1 or, spanning it, later (a block's last chunk closes it).
+SA_HD uint32_t rb_chase(const RbInfo* info, const RbChunk* ck, uint32_t c)
+{
+    if (ck[c].flags & RB_LAST) return 0;   // (no run is open at a block's end)
+    for (uint32_t k = c + 1;; k++) {
+        if (info[k].entry_val & 0x100u) return info[k].entry_val & 0xffu;
+        if (ck[k].flags & RB_LAST) return 0;   // (unreachable: the last chunk closes it)
+    }
+}
+
+// Bytes [32 t, 32 t + 32) of chunk ck into out, t < RB_WORDS: prev = the last
+// open before the word (chunk offset, or -1: none), entry / tail = the values
+// of the entering run and of the run open at the chunk's end.
+SA_HD void rb_fill_word(uint8_t* out, const RbChunk& ck, uint32_t t, uint32_t word, int32_t prev, const uint8_t* vals,
+                        const RbInfo& info, uint32_t entry, uint32_t tail)
+{
+    uint32_t o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t cur = prev;
+    for (uint32_t i = 0; i < 32; i++) {
+        if ((word >> i) & 1u) cur = (int32_t)(32 * t + i);
+        uint32_t v;
+        if (cur < 0) v = info.last_start == RB_OPEN_ENTRY ? tail : entry;
+        else if ((uint32_t)cur == info.last_start) v = tail;
+        else v = vals[cur];
+        o[i >> 2] |= v << (8 * (i & 3));
+    }
+    const uint32_t at = 32 * t;
+    if (at + 32 <= ck.len) {
+        __builtin_memcpy(out + ck.base + at, o, 32);
+    } else {
+        for (uint32_t i = 0; at + i < ck.len; i++) out[ck.base + at + i] = (uint8_t)(o[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
 // Writes every header, MD5 and the ID-bin payload of block b into o, and lists
 // the coder payloads still to copy (destination offset, coder task, length).
 // Returns the block's total length.

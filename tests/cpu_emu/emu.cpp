@@ -347,13 +347,34 @@ int main(int argc, char** argv)
             if (ck.empty()) continue;
             std::vector<uint32_t> opens(ck.size() * RB_WORDS);
             std::vector<RbRun> spec(ck.size()), entry(ck.size());
-            for (size_t c = 0; c < ck.size(); c++) spec[c] = rb_spec(qual.data(), ck[c], tab, &opens[c * RB_WORDS]);
+            std::vector<uint8_t> vals(ck.size() * RB_CHUNK);
+            std::vector<RbInfo> info(ck.size());
+            // k_rb_spec (with the run values, round 5), k_rb_fix's carry,
+            // then k_rb_true + k_rb_fill -- or (SA_RB_APPLY=1) the round-4 k_rb_apply
+            const bool walk = std::getenv("SA_RB_APPLY") != nullptr;
+            for (size_t c = 0; c < ck.size(); c++)
+                spec[c] = walk ? rb_spec(qual.data(), ck[c], tab, &opens[c * RB_WORDS])
+                               : rb_spec_vals(qual.data(), ck[c], tab, &opens[c * RB_WORDS], &vals[c * RB_CHUNK], info[c]);
             RbRun cur = spec[0];
             for (size_t c = 1; c < ck.size(); c++) {
                 entry[c] = cur;
                 cur = rb_carry(qual.data(), ck[c], cur, tab, &opens[c * RB_WORDS], spec[c]);
             }
-            for (size_t c = ck.size(); c-- > 0;) rb_apply(qual.data(), qual_q.data(), ck[c], entry[c], tab);
+            if (walk) {
+                for (size_t c = ck.size(); c-- > 0;) rb_apply(qual.data(), qual_q.data(), ck[c], entry[c], tab);
+            } else {
+                for (size_t c = 1; c < ck.size(); c++)
+                    rb_true(qual.data(), ck[c], entry[c], tab, &opens[c * RB_WORDS], &vals[c * RB_CHUNK], info[c]);
+                for (size_t c = 0; c < ck.size(); c++) {
+                    const uint32_t ev = info[c].entry_val & 0xffu, tv = rb_chase(info.data(), ck.data(), (uint32_t)c);
+                    int32_t prev = -1;
+                    for (uint32_t t = 0; t < RB_WORDS && 32 * t < ck[c].len; t++) {
+                        const uint32_t w = opens[c * RB_WORDS + t];
+                        rb_fill_word(qual_q.data(), ck[c], t, w, prev, &vals[c * RB_CHUNK], info[c], ev, tv);
+                        if (w) prev = (int32_t)(32 * t + 31 - (uint32_t)__builtin_clz(w));
+                    }
+                }
+            }
             std::vector<uint8_t> ref(qual.begin() + (long)d.seq_base, qual.begin() + (long)(d.seq_base + d.seq_bytes));
             orc_rblock(ref.data(), ref.size(), lossy);
             if (std::memcmp(ref.data(), qual_q.data() + d.seq_base, ref.size())) {

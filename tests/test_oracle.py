@@ -98,12 +98,23 @@ def test_cpu_decomposition(tmp_path):
     (tmp_path / "b.fq").write_bytes(pe2)
     (tmp_path / "e.fq").write_bytes(synth.edge_cases())
     (tmp_path / "long.fq").write_bytes(synth.generate(12, read_len=70000, seed=5)[0])
+    # R-Block runs that span whole 8 KiB chunks (constant or two-level qualities):
+    # the run values reach the chunks' bytes through rb_chase
+    rng = np.random.default_rng(1)
+    recs = []
+    for i in range(6):
+        n = 30000 + 1000 * i
+        s = bytes(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)])
+        q = b"I" * n if i % 2 == 0 else bytes(b"5?"[(j // 9000) % 2] for j in range(n))
+        recs.append(b"@c%d\n%s\n+\n%s\n" % (i, s, q))
+    (tmp_path / "const.fq").write_bytes(b"".join(recs))
     runs = [[TEST1, TEST2], [TEST1], ["-b", "600000", TEST1, TEST2], [str(tmp_path / "a.fq"), str(tmp_path / "b.fq")],
             ["-s", "4", "-b", "300000", str(tmp_path / "a.fq"), str(tmp_path / "b.fq")],
             ["-q", "3", str(tmp_path / "a.fq")], [str(tmp_path / "e.fq")], ["-s", "9", str(tmp_path / "e.fq")],
             ["-l", "1.15", TEST1, TEST2], ["-l", "1.3", "-b", "300000", str(tmp_path / "a.fq")],
             ["-l", "1.05", str(tmp_path / "e.fq")], [str(tmp_path / "long.fq")],
-            ["-l", "1.6", str(tmp_path / "long.fq")]]
+            ["-l", "1.6", str(tmp_path / "long.fq")], ["-l", "1.15", str(tmp_path / "const.fq")],
+            ["-l", "1.6", str(tmp_path / "const.fq")]]
     for args in runs:
         r = subprocess.run([str(exe)] + args, capture_output=True, text=True)
         assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
