@@ -249,7 +249,8 @@ def _low_complexity_fastq(seed, n):
                 arr[int(p)] = b"ACGTN"[int(rng.integers(0, 5))]
             s = bytes(arr)
         q = bytes(rng.choice(np.frombuffer(b"F:,#", np.uint8), size=len(s), p=[0.7, 0.2, 0.08, 0.02]))
-        recs.append(b"@lc%d\n%s\n+\n%s\n" % (i, s, q))
+        # (a common name prefix of more than five bytes: the block cut's record test)
+        recs.append(b"@LOWCPLX%d\n%s\n+\n%s\n" % (i, s, q))
     return b"".join(recs)
 
 
