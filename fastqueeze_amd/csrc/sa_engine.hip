@@ -226,6 +226,9 @@ struct sa_ctx {
     // the other contexts' fronts beside them are not always; SA_L_PRIO=1, A/B)
     uint32_t l_prio = std::getenv("SA_L_PRIO") && std::atoi(std::getenv("SA_L_PRIO")) != 0 ? 1u : 0u;
     bool seq_unpacked = std::getenv("SA_SEQ_PACK") && std::atoi(std::getenv("SA_SEQ_PACK")) == 0;
+    // k_prep_sq16 / k_emit_sq16 with the round-4 static grid stride instead of
+    // reads taken from a counter (WaveReads; SA_FRONT_STATIC=1, A/B)
+    bool front_static = std::getenv("SA_FRONT_STATIC") && std::atoi(std::getenv("SA_FRONT_STATIC")) != 0;
     // pass R with one chain per lane in the VALU (k_coder_rl: the scalar units
     // stay free for the front kernels of the other batches) instead of one
     // chain per wave on the scalar unit (k_coder_rv); SA_RV_LANES=1 / 0
@@ -1368,10 +1371,13 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, c->d_name_p.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
     SA_CHECK(c, c->d_name_s.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
     SA_CHECK(c, c->d_maxlen.ensure((size_t)std::max<uint32_t>(nr, 1) * 2));
-    SA_CHECK(c, c->d_err.ensure(16));
-    SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 16, st));
+    SA_CHECK(c, c->d_err.ensure(64));   // error words 0-3, the front kernels' read counters (WaveReads) 8-9
+    SA_CHECK(c, hipMemsetAsync(c->d_err.p, 0, 64, st));
 
     uint32_t* d_err = c->d_err.as<uint32_t>();
+    // the front kernels' dynamic read counters (nullptr: the static grid stride)
+    uint32_t* wq_prep = c->front_static ? nullptr : d_err + 8;
+    uint32_t* wq_emit = c->front_static ? nullptr : d_err + 9;
 
     ev_begin(c, PH_TOTAL, st);
     // ---- MD5 of every block's IDs/bases/quals (calcBlockMd5@0x414d90) on st2,
@@ -1412,9 +1418,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         // faster under load (prep 38 vs 32 ms, same GB/s, round 3 g3r / g3s);
         // SA_PREP_WAVE=1: round 2's wave-per-read k_prep_sq
         if (c->prep_fused) {
-            hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                               c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(),
-                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>());
+            hipLaunchKernelGGL(wq_prep ? k_prep_sq16<true> : k_prep_sq16<false>, dim3(wave_grid(c, (nr + 3) / 4)),
+                               dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(),
+                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), wq_prep);
         } else {
             hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
                                c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
@@ -1422,9 +1428,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                 hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                    c->d_counts.as<uint32_t>(), d_err);
             else
-                hipLaunchKernelGGL(k_prep_sq16, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv,
-                                   c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(), nullptr,
-                                   nullptr);
+                hipLaunchKernelGGL(wq_prep ? k_prep_sq16<true> : k_prep_sq16<false>,
+                                   dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
+                                   d_err, c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr, wq_prep);
         }
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
@@ -1566,9 +1572,11 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                                akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh,
                                (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE), nullptr);
         } else {
-            hipLaunchKernelGGL(seq_sh ? k_emit_sq16<2> : k_emit_sq16<0>, dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0,
+            hipLaunchKernelGGL(seq_sh ? (wq_emit ? k_emit_sq16<2, true> : k_emit_sq16<2, false>)
+                                      : (wq_emit ? k_emit_sq16<0, true> : k_emit_sq16<0, false>),
+                               dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0,
                                st, bv, c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
-                               F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr);
+                               F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr, wq_emit);
             if (dege_maxq && n_ch) {   // the N / IUPAC side streams of the reads that have such bases
                 SA_CHECK(c, c->d_dege_list.ensure(4ull * ((uint64_t)nr + 1)));
                 SA_CHECK(c, hipMemsetAsync(c->d_dege_list.p, 0, 4, st));

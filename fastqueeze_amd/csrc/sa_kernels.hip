@@ -381,17 +381,52 @@ __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint
     if ((int)nl - sfx - p < 0) sfx = (int)nl - p;
 }
 
+// (round 5) Reads handed to a wave of four 16-lane rows, four at a time.
+// Static: grid stride (the round-4 form, wq == nullptr).  Dynamic: the wave
+// takes WQ_CHUNK reads at a time from a counter, so the waves on CUs whose
+// scalar unit other batches' pass-R chains keep busy (their loops and address
+// arithmetic wait for it) take fewer reads instead of finishing last: a
+// grid-stride kernel's time is its slowest CU's.
+constexpr uint32_t WQ_CHUNK = 64;
+template <bool DYN>
+struct WaveReads {
+    uint32_t* wq;
+    uint32_t base, stride, cur = 0, lim = 0;
+    __device__ WaveReads(uint32_t* q, uint32_t wrow0, uint32_t rows) : wq(q), base(wrow0), stride(rows) {}
+    // the wave's next first row (wave-uniform); false when the reads are done
+    __device__ __forceinline__ bool next(uint32_t nr, uint32_t& b)
+    {
+        if constexpr (!DYN) {
+            b = base;
+            base += stride;
+            return b < nr;
+        } else {
+            if (cur >= lim) {
+                uint32_t g = 0;
+                if ((threadIdx.x & 63) == 0) g = atomicAdd(wq, WQ_CHUNK);
+                cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0, 64));
+                lim = cur + WQ_CHUNK;
+            }
+            b = cur;
+            cur += 4;
+            return b < nr;
+        }
+    }
+};
+
+template <bool DYN>
 __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ err, uint8_t* __restrict__ dege_maxq,
-                                                   int16_t* __restrict__ name_p, int16_t* __restrict__ name_s)
+                                                   int16_t* __restrict__ name_p, int16_t* __restrict__ name_s,
+                                                   uint32_t* __restrict__ wq)
 {
     const uint32_t rl = threadIdx.x & (PREP_ROW - 1);
     const uint32_t rows = gridDim.x * (blockDim.x / PREP_ROW);
     const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / PREP_ROW;
     const uint32_t nr = bv.nreads_total;
     // wave-uniform trip count: every row of the wave loops while any row has a read
-    const uint32_t wrow0 = row0 & ~3u;
-    for (uint32_t base = wrow0; base < nr; base += rows) {
+    WaveReads<DYN> wr(wq, row0 & ~3u, rows);
+    for (uint32_t base; wr.next(nr, base);) {
         const uint32_t r = base + (row0 & 3u);
         const bool live = r < nr;
         uint32_t len = 0;
@@ -999,10 +1034,13 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[4], uint32_t j)
     return (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
 }
 
-template <uint32_t SH>   // seq_sh: 2 = the base in the SEQ key, values implicit; 0 = values position << 2 | base
-__global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uint32_t* __restrict__ counts,
+// seq_sh SH: 2 = the base in the SEQ key, values implicit; 0 = values position << 2 | base.
+// DYN: reads from a counter (WaveReads)
+template <uint32_t SH, bool DYN>
+__global__ __launch_bounds__(256, 4) void k_emit_sq16(const BatchView bv, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
-                                                   uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val)
+                                                   uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
+                                                   uint32_t* __restrict__ wq)
 {
     // (one slot past each row's ER_STEP: the stores of the branch-free loops
     // below that carry no symbol land there)
@@ -1020,8 +1058,8 @@ __global__ __launch_bounds__(256) void k_emit_sq16(const BatchView bv, const uin
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
     };
-    const uint32_t wrow0 = row0 & ~3u;   // wave-uniform trip count (rows of a wave shuffle together)
-    for (uint32_t base = wrow0; base < nr; base += rows) {
+    WaveReads<DYN> wr(wq, row0 & ~3u, rows);   // (wave-uniform: the rows of a wave shuffle together)
+    for (uint32_t base; wr.next(nr, base);) {
         const uint32_t r = base + (row0 & 3u);
         const bool live = r < nr;
         uint32_t len = 0;
@@ -1840,9 +1878,12 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
     extern __shared__ uint32_t bkt_lds[];
     __shared__ uint32_t fl[64];
     const uint32_t nsub = 1u << sb, nd = 1u << tb;
-    volatile uint32_t* mst = bkt_lds;
-    volatile uint8_t* tag = reinterpret_cast<volatile uint8_t*>(bkt_lds + nsub);
-    volatile uint32_t* vfl = fl;
+    // (plain LDS pointers and compiler barriers, not volatile ones: a volatile
+    // access becomes a flat access, and every flat access waits for all the
+    // wave's outstanding global stores -- the scattered records -- r5e / r5g)
+    uint32_t* mst = bkt_lds;
+    uint8_t* tag = reinterpret_cast<uint8_t*>(bkt_lds + nsub);
+    uint32_t* vfl = fl;
     const uint32_t seg = blockIdx.x >> tb, d = blockIdx.x & (nd - 1);
     const SortSeg& sg = sv.segs[seg];
     if (sg.count == 0) return;
