@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5, call r5f: the command line's host side and clock.
+#  (0) chain_probe: cycles per pass-R step in the VALU (k_coder_rl) and on the scalar unit;
 #  (1) exit_probe: process teardown time against device / page-locked memory held;
 #  (2) seqarc_amd -c on the 17.8 GB (5 batches) and 42.8 GB (12 batches) files,
 #      KFD's per-process eviction time (kfd_sample.py), amd-smi's throttle record
@@ -29,6 +30,7 @@ sampler() {
         sleep 0.3
     done
 }
+step chain_probe timeout -k 10 60 scripts/bin/chain_probe > $O/chain_probe.txt 2>&1
 step exit_probe timeout -k 10 240 scripts/bin/exit_probe 0 50 100 200 > $O/exit_probe.txt 2>&1
 step write_inputs timeout -k 10 300 python -u bench.py --write-inputs $IN > $O/write_inputs.log 2>&1
 mkdir -p $E/s $E/l
