@@ -235,9 +235,10 @@ struct sa_ctx {
     bool rv_lanes = std::getenv("SA_RV_LANES") && std::atoi(std::getenv("SA_RV_LANES")) != 0;
     DBuf d_rtab;   // recip32z(t) for t < 2^16 (k_coder_rl)
     // the SEQ space sorted by the context's top bits only and replayed per
-    // bucket with the models in LDS (k_replay_seq_bkt, contexts of <= 22 bits);
-    // SA_SEQ_BUCKET=0: the full sort and k_replay_seq (A/B)
-    bool seq_bucket = !(std::getenv("SA_SEQ_BUCKET") && std::atoi(std::getenv("SA_SEQ_BUCKET")) == 0);
+    // bucket with the models in LDS (k_replay_seq_bkt, contexts of <= 22 bits,
+    // SA_SEQ_BUCKET=1); default: the full sort and k_replay_seq (r5e-r5h: the
+    // bucket replay measured slower, 14.9-15.4 against 15.9-16.8 GB/s)
+    bool seq_bucket = std::getenv("SA_SEQ_BUCKET") && std::atoi(std::getenv("SA_SEQ_BUCKET")) != 0;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
     // k_md5<true> reads the next block's words while the chain runs: 148 VGPRs instead

@@ -1928,29 +1928,25 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
             uint64_t M = __ballot(member);
             while (M) {   // one group of lanes with the same context at a time
                 const uint32_t L = (uint32_t)__builtin_ctzll(M);
-                const uint32_t gs = (uint32_t)__shfl((int)sub, (int)L, 64);
+                const uint32_t gs = (uint32_t)__builtin_amdgcn_readlane((int)sub, (int)L);
                 const uint64_t G = __ballot(member && sub == gs);
-                const uint32_t s0 = (uint32_t)__shfl((int)s, (int)L, 64);
-                const uint32_t glen = (uint32_t)__popcll(G);
+                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)L);
                 const bool in_g = (G >> lane) & 1ull;
-                if (bm_tot(s0) + glen - 1u <= 253u) {   // no halving inside the group
-                    if (in_g) {
-                        uint32_t si = s0 + bm_counts(G & below, b0, b1, b2, b3);
-                        out[p] = PRec{bm_rec(si, b)};
-                    }
-                    if (lane == L) mst[gs] = s0 + bm_counts(G, b0, b1, b2, b3);
-                } else {   // (rare) the group crosses a halving: in lane order
-                    uint32_t cur = s0, mine = 0;
-                    for (uint64_t g = G; g; g &= g - 1ull) {
-                        const uint32_t j = (uint32_t)__builtin_ctzll(g);
-                        const uint32_t bj = (uint32_t)__shfl((int)b, (int)j, 64);
-                        const uint32_t r = bm_rec(cur, bj);
-                        if (lane == j) mine = r;
-                        cur += 1u << (8 * bj);
-                    }
-                    if (in_g) out[p] = PRec{mine};
-                    if (lane == L) mst[gs] = cur;
+                // at most one halving inside a group: the symbol with group index
+                // h = 254 - tot halves the model (tot > 253), and after it the
+                // total is ~127, which 63 more symbols cannot take past 253
+                const uint32_t tot0 = bm_tot(s0), h = tot0 >= 254 ? 0u : 254u - tot0;
+                const uint32_t gi = (uint32_t)__popcll(G & below);
+                const uint64_t lo = __ballot(in_g && gi < h);   // the members before the halving
+                uint32_t sh = s0 + bm_counts(lo, b0, b1, b2, b3);
+                sh -= (sh >> 1) & 0x7f7f7f7fu;   // (the model at the halving symbol, halved)
+                if (in_g) {
+                    uint32_t si = gi < h ? s0 + bm_counts(G & below, b0, b1, b2, b3)
+                                         : sh + bm_counts(G & below & ~lo, b0, b1, b2, b3);
+                    out[p] = PRec{bm_rec(si, b)};   // (no halving left for bm_rec: total <= 253)
                 }
+                if (lane == L)
+                    mst[gs] = G == lo ? s0 + bm_counts(G, b0, b1, b2, b3) : sh + bm_counts(G & ~lo, b0, b1, b2, b3);
                 M &= ~G;
             }
         }
