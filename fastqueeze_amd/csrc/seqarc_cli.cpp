@@ -784,7 +784,7 @@ struct SegReader {
 
     // fds: open plain regular files; W: the cut's window
     bool start(const int* fds, const uint64_t* sizes, int n, uint64_t window, int64_t ahead_bytes, int threads,
-               bool pin)
+               bool pin, uint64_t batch_blocks = 1)
     {
         nf = n;
         W = window;
@@ -800,6 +800,10 @@ struct SegReader {
         // with threads, profiles/round5_r5a_ingest_probe.txt): a smaller ring
         // costs less of it before the first pass over it completes
         if (const char* e = std::getenv("SA_CLI_RING_SEGS")) R = std::max(3, std::atoi(e));
+        // (at least a batch of windows and two segments of slack: the blocks of
+        // a batch keep their segments until the batch is staged; r5i: a ring of
+        // four 512 MiB segments deadlocked a 69-block batch)
+        R = std::max<int>(R, (int)(((uint64_t)batch_blocks * window + S - 1) / S) + 2);
         for (int i = 0; i < n; i++) {
             File& F = f[i];
             F.fd = fds[i];
@@ -1696,10 +1700,11 @@ int compress(const Options& o)
             const int fds[2] = {in1.fd, in2.fd};
             // the reader runs at most two batches of blocks ahead of the staging (below)
             segr->start(fds, fsize, pe ? 2 : 1, win + (64u << 10), (int64_t)(2 * B + 2) * (int64_t)win,
-                        o.read_threads, dev_parse);   // (page-locked for the device parse; --ingest-only too)
+                        o.read_threads, dev_parse, (uint64_t)B);   // (page-locked for the device parse; --ingest-only too)
         }
     }
     // the segments are released as soon as every block is staged (device parse)
+    std::atomic<double> t_seg_freed{0};
     std::thread seg_free;
     bool seg_stop = false;
     if (segr && dev_parse)
@@ -1710,6 +1715,7 @@ int compress(const Options& o)
                 if (failed || seg_stop) return;
             }
             segr->free_all();
+            t_seg_freed = now_s();
         });
     // reader: cuts blocks as the input arrives
     std::thread reader([&]() {
@@ -2236,6 +2242,7 @@ int compress(const Options& o)
         }
         cv.notify_all();
     }
+    const double t_written = now_s();
     reader.join();
     for (auto& t : parsers) t.join();
     for (auto& t : encoders) t.join();
@@ -2298,8 +2305,8 @@ int compress(const Options& o)
     else g_fast_exit = true;
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     if (o.verbose)
-        fprintf(stderr, "seqarc_amd: encoders done %.3f s, archive closed %.3f s, contexts %s %.3f s\n", t_joined,
-                t_closed, o.release ? "released" : "left to the exit", secs);
+        fprintf(stderr, "seqarc_amd: blocks written %.3f s, segment ring freed %.3f s, encoders done %.3f s, archive closed %.3f s, contexts %s %.3f s\n",
+                t_written, t_seg_freed.load(), t_joined, t_closed, o.release ? "released" : "left to the exit", secs);
     if (tl >= 0) {
         if (o.verbose)
             fprintf(stderr,
