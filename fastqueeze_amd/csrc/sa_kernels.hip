@@ -3047,18 +3047,27 @@ __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __r
     if (feeder) {
         uint32_t bad = 0;
         const uint64_t wait = tl.wait_ticks ? tl.wait_ticks : 2000000000u;
-        // segment j of the lane's chain into ring half (j & 1)
-        auto fill = [&](uint32_t j) __attribute__((always_inline)) {
-            if (j >= nj) return;
-            // (a stream starts at any record: dword loads, each lane its own 256 B)
-            const uint32_t* S = reinterpret_cast<const uint32_t*>(P + (size_t)(first + j) * SEG_SYMS);
-            uint32_t v[SEG_SYMS];
+        // Pipelined: in the iteration that the chain wave codes segment j, the
+        // feeder looks up the reciprocals of segment j + 1 (its records were
+        // loaded one iteration earlier), issues the loads of segment j + 2, and
+        // writes segment j + 1 into the other ring half once the lookups are in
+        // -- one memory round trip per segment instead of two.  A stream starts
+        // at any record: dword loads, each lane its own 256 B; loads past a
+        // lane's chain re-read its last segment (branch-free, so the waits for
+        // the lookups need not wait for the loads issued after them).
+        const uint32_t* S0 = reinterpret_cast<const uint32_t*>(P + (size_t)first * SEG_SYMS);
+        auto load = [&](uint32_t j, uint32_t (&v)[SEG_SYMS]) __attribute__((always_inline)) {
+            const uint32_t* S = S0 + (size_t)(j < nj ? j : (nj ? nj - 1 : 0)) * SEG_SYMS;
 #pragma unroll
             for (uint32_t k = 0; k < SEG_SYMS; k++) v[k] = S[k];
+        };
+        // segment j's records in v (loaded); the unwritten ones waited for
+        auto written = [&](uint32_t j, uint32_t (&v)[SEG_SYMS]) __attribute__((always_inline)) {
             uint32_t zero = 0;
 #pragma unroll
             for (uint32_t k = 0; k < SEG_SYMS; k++) zero |= (v[k] & tmask) == 0;
-            if (zero && !bad) {   // records not written yet (long runs replayed concurrently)
+            if (zero && j < nj && !bad) {   // records not written yet (long runs replayed concurrently)
+                const uint32_t* S = S0 + (size_t)j * SEG_SYMS;
                 const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
                 for (;;) {
                     zero = 0;
@@ -3075,15 +3084,43 @@ __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __r
                     __builtin_amdgcn_s_sleep(32);
                 }
             }
-            uint2* R = &ring[j & 1][0][lane];
-#pragma unroll
-            for (uint32_t k = 0; k < SEG_SYMS; k++) R[k * 64] = make_uint2(rtab[v[k] & tmask], v[k]);
         };
-        fill(0);
+        // iteration j: segment j + 1 (records in cur) into its ring half, the
+        // loads of segment j + 2 into nxt
+        auto pipe = [&](uint32_t j, uint32_t (&cur)[SEG_SYMS], uint32_t (&nxt)[SEG_SYMS]) __attribute__((always_inline)) {
+            written(j + 1, cur);
+            uint32_t m[SEG_SYMS];
+#pragma unroll
+            for (uint32_t k = 0; k < SEG_SYMS; k++) m[k] = rtab[cur[k] & tmask];
+            load(j + 2, nxt);
+            if (j + 1 < nj) {
+                uint2* R = &ring[(j + 1) & 1][0][lane];
+#pragma unroll
+                for (uint32_t k = 0; k < SEG_SYMS; k++) R[k * 64] = make_uint2(m[k], cur[k]);
+            }
+        };
+        uint32_t va[SEG_SYMS], vb[SEG_SYMS];
+        load(0, va);
+        written(0, va);
+        {
+            uint32_t m[SEG_SYMS];
+#pragma unroll
+            for (uint32_t k = 0; k < SEG_SYMS; k++) m[k] = rtab[va[k] & tmask];
+            load(1, vb);
+            if (nj) {
+                uint2* R = &ring[0][0][lane];
+#pragma unroll
+                for (uint32_t k = 0; k < SEG_SYMS; k++) R[k * 64] = make_uint2(m[k], va[k]);
+            }
+        }
         __syncthreads();
-        for (uint32_t j = 0; j < J; j++) {
-            fill(j + 1);
+        for (uint32_t j = 0; j < J; j += 2) {
+            pipe(j, vb, va);
             __syncthreads();
+            if (j + 1 < J) {
+                pipe(j + 1, va, vb);
+                __syncthreads();
+            }
         }
         if (__ballot(bad != 0) && lane == 0) atomicOr(err, (uint32_t)E_CODER);
     } else {
