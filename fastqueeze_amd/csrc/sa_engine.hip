@@ -1309,12 +1309,14 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // equal the sort pad) and order 0 has no sort pass, so they keep values
     // position << 2 | base (SA_SEQ_PACK=0: always)
     const uint32_t seq_sh = (ns > 1 && seq_bits <= 28 && !c->seq_unpacked) ? 2u : 0u;
-    // contexts of <= 22 bits (Slevel <= 4): one sort pass over the context's top
-    // 8 (9) bits, the low bkt_sb bits replayed per bucket with the models in LDS
+    // contexts of <= 22 bits (Slevel <= 4): one sort pass over the context's low
+    // 8 (9) bits, the high bkt_sb bits replayed per bucket with the models in LDS
     // (k_replay_seq_bkt); longer contexts: the full sort and k_replay_seq
     const bool seq_bkt = c->seq_bucket && seq_sh == 2 && seq_bits >= 12 && seq_bits <= 22;
     const int bkt_sb = seq_bits <= 20 ? seq_bits - 8 : seq_bits - 9;
-    const int seq_lo = (int)seq_sh + (seq_bkt ? bkt_sb : 0), seq_hi = ns > 1 ? (int)seq_sh + seq_bits : 0;
+    // (the bucket pass sorts by the context's LOW bits: k_replay_seq_bkt)
+    const int seq_lo = (int)seq_sh,
+              seq_hi = ns > 1 ? (int)seq_sh + (seq_bkt ? seq_bits - bkt_sb : seq_bits) : 0;
     const int aux_bits = cfg->qlevel > 2 ? 21 : 17;
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
@@ -1653,7 +1655,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         }
         hipLaunchKernelGGL(k_replay_seq_bkt, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
                            F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
-                           sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb);
+                           sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]));
     } else if (ps.total) {
         SA_CHECK(c, hipMemsetAsync(F->d_nseq_long.p, 0, 4, st));
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,

@@ -1835,7 +1835,10 @@ __global__ __launch_bounds__(SORT_THREADS) void k_replay_seq(const SortView sv, 
 
 // ---------------------------------------------------------------------------
 // k_replay_seq_bkt (round 5): BASE_MODEL replay after ONE sort pass.  The SEQ
-// space is sorted stably by the top TB bits of the context only -- a bucket;
+// space is sorted stably by the low TB bits of the context only -- a bucket
+// (the low bits: the first bases of every read have contexts made of the seed
+// 0x7616c7's bits, so by the top bits the first seven positions of all reads
+// would share one bucket, many to one context);
 // inside it the symbols stay in stream order -- and one wave walks each
 // (block, bucket) in stream order with the models of the bucket's 2^SB
 // contexts in LDS (4 x u8 counts each, init 3, updated exactly as
@@ -1873,7 +1876,7 @@ __device__ __forceinline__ uint32_t bm_counts(uint64_t m, uint64_t b0, uint64_t 
 // digit starts); keys = context << 2 | base, values = stream positions.
 __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals, const SymSink rec,
-                                                       uint32_t tb, uint32_t sb)
+                                                       uint32_t tb, uint32_t sb, uint32_t subsh)
 {
     extern __shared__ uint32_t bkt_lds[];
     __shared__ uint32_t fl[64];
@@ -1902,7 +1905,7 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
     const uint64_t below = (1ull << lane) - 1ull;
     // one step: 64 symbols of the bucket in stream order (k: key, p: position)
     auto step = [&](const uint32_t k, const uint32_t p, const bool act) __attribute__((always_inline)) {
-        const uint32_t sub = (k >> 2) & smask, b = k & 3u;
+        const uint32_t sub = (k >> subsh) & smask, b = k & 3u;
         if (act) tag[sub] = (uint8_t)lane;
         asm volatile("" ::: "memory");   // (LDS operations of a wave complete in order)
         const uint32_t t = act ? tag[sub] : lane;
