@@ -19,6 +19,7 @@ step() {
     echo "$name rc=$rc $((SECONDS - t0))s" >> $O/steps.txt
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
+step pin_probe timeout -k 10 120 scripts/bin/pin_probe 8 > $O/pin_probe.txt 2>&1
 SA_RV_LANES=1 step tests timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -o cache_dir=/tmp/pyc > $O/tests.log 2>&1
 step write_inputs timeout -k 10 300 python -u bench.py --write-inputs $IN > $O/write_inputs.log 2>&1
 for rep in 1 2; do
