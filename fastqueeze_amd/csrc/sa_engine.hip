@@ -231,14 +231,18 @@ struct sa_ctx {
     bool front_static = std::getenv("SA_FRONT_STATIC") && std::atoi(std::getenv("SA_FRONT_STATIC")) != 0;
     // pass R with one chain per lane in the VALU (k_coder_rl: the scalar units
     // stay free for the front kernels of the other batches) instead of one
-    // chain per wave on the scalar unit (k_coder_rv); SA_RV_LANES=1 / 0
+    // chain per wave on the scalar unit (k_coder_rv); SA_RV_LANES=1 / 0.  Off:
+    // pass R 1,835-1,864 against 679-689 ms under the bench's load, the bench
+    // 7,971-8,064 against 16,849-16,908 MB/s (r5k)
     bool rv_lanes = std::getenv("SA_RV_LANES") && std::atoi(std::getenv("SA_RV_LANES")) != 0;
     DBuf d_rtab;   // recip32z(t) for t < 2^16 (k_coder_rl)
-    // the SEQ space sorted by the context's top bits only and replayed per
-    // bucket with the models in LDS (k_replay_seq_bkt, contexts of <= 22 bits,
-    // SA_SEQ_BUCKET=1); default: the full sort and k_replay_seq (r5e-r5h: the
-    // bucket replay measured slower, 14.9-15.4 against 15.9-16.8 GB/s)
-    bool seq_bucket = std::getenv("SA_SEQ_BUCKET") && std::atoi(std::getenv("SA_SEQ_BUCKET")) != 0;
+    // the SEQ space sorted by the context's low 8-9 bits only and replayed per
+    // bucket with the models in LDS (k_replay_seq_bkt, contexts of <= 22 bits);
+    // SA_SEQ_BUCKET=0: the full sort and k_replay_seq.  By the low bits the
+    // bench gained 1-3 % (r5k: 17,039 / 17,349 against 16,908 / 16,849 MB/s,
+    // SEQ sort + replay 84 against 88-98 ms); by the top bits it had lost
+    // (r5e-r5h: 14.9-15.4 against 15.9-16.8 GB/s)
+    bool seq_bucket = !(std::getenv("SA_SEQ_BUCKET") && std::atoi(std::getenv("SA_SEQ_BUCKET")) == 0);
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
     // k_md5<true> reads the next block's words while the chain runs: 148 VGPRs instead
