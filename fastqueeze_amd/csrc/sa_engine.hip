@@ -16,6 +16,7 @@
 #include <optional>
 #include <sys/mman.h>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/seqarc_amd.h"

@@ -245,7 +245,29 @@ extern "C" {
 // the same rate (35 vs 31 GB/s H2D, g3y).
 // (A/B knobs, round 5: SA_HOST_THP=0 leaves out the huge-page hint;
 // SA_HOST_MALLOC=1 takes hipHostMalloc memory instead of registered memory)
+// Round 5: the pages are faulted in first, by up to eight threads, and then
+// registered -- hipHostRegister faults an untouched range in itself, one
+// thread, at ~23 GB/s; 8 GB of touched huge pages took 0.066 s to touch and
+// 0.016 s to register (scripts/micro/pin_probe.hip, r5k; with 4 KiB pages
+// touching first saves nothing).  SA_HOST_TOUCH=0: the runtime faults them.
 namespace {
+bool host_touch()
+{
+    static const bool t = !(std::getenv("SA_HOST_TOUCH") && std::atoi(std::getenv("SA_HOST_TOUCH")) == 0);
+    return t;
+}
+void touch_pages(void* p, uint64_t n)
+{
+    const uint64_t nt = std::min<uint64_t>(8, std::max<uint64_t>(1, n >> 27));   // (a thread per 128 MiB, up to 8)
+    const uint64_t per = ((n / nt) + 4095) & ~4095ull;
+    std::vector<std::thread> th;
+    for (uint64_t t = 0; t < nt; t++)
+        th.emplace_back([=]() {
+            volatile uint8_t* b = static_cast<volatile uint8_t*>(p);
+            for (uint64_t o = t * per; o < std::min(n, (t + 1) * per); o += 4096) b[o] = 0;
+        });
+    for (auto& x : th) x.join();
+}
 int host_mode()   // 0: register + THP hint, 1: register only, 2: hipHostMalloc
 {
     static const int m = std::getenv("SA_HOST_MALLOC") && std::atoi(std::getenv("SA_HOST_MALLOC")) != 0 ? 2
@@ -262,7 +284,10 @@ void* sa_host_alloc(uint64_t bytes)
     void* p = nullptr;
     if (host_mode() == 2) return hipHostMalloc(&p, n, hipHostMallocPortable) == hipSuccess ? p : nullptr;
     if (posix_memalign(&p, kHuge, n) != 0) return nullptr;
-    if (host_mode() == 0) (void)madvise(p, n, MADV_HUGEPAGE);   // (a hint: without THP the pages are 4 KiB)
+    if (host_mode() == 0) {
+        (void)madvise(p, n, MADV_HUGEPAGE);   // (a hint: without THP the pages are 4 KiB)
+        if (host_touch()) touch_pages(p, n);
+    }
     if (hipHostRegister(p, n, hipHostRegisterPortable) != hipSuccess) {
         free(p);
         return nullptr;
