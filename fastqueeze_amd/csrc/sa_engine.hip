@@ -15,6 +15,8 @@
 #include <mutex>
 #include <optional>
 #include <sys/mman.h>
+#include <unistd.h>
+#include <cerrno>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1090,6 +1092,73 @@ uint64_t sa_output_bound(const sa_block* b)
 }
 
 }  // extern "C"
+
+// ---- the command line's clock keeper (sa_clock_keeper) ----
+// The firmware lowers the shader clock when few waves are resident (amd-smi's
+// throttle record: the low-utilization flag, 1.0-2.0 GHz while only pass R's
+// chains of the last batches ran; r5b, r5j).  A wave per CU that sleeps keeps
+// the measured activity up without issuing: r5l, the CLI's pass-R chains at
+// 2,356-2,386 MHz beside it against 1,685-2,152 without (rv_probe), the same
+// with FMA-issuing waves (r5k) -- but those delayed the chains on the SIMDs
+// they shared, the sleeping ones do not.
+namespace {
+__global__ void __launch_bounds__(64) k_keep_resident(uint32_t naps)
+{
+    for (uint32_t i = 0; i < naps; i++) __builtin_amdgcn_s_sleep(127);   // (~8k cycles a nap)
+}
+}  // namespace
+
+extern "C" int sa_clock_keeper(const int* devices, int n, int fd)
+{
+    struct Dev {
+        int id;
+        uint32_t cus;
+        hipStream_t st;
+    };
+    std::vector<Dev> ds;
+    for (int i = 0; i < n; i++) {
+        hipDeviceProp_t p;
+        hipStream_t st = nullptr;
+        if (hipSetDevice(devices[i]) != hipSuccess || hipGetDeviceProperties(&p, devices[i]) != hipSuccess ||
+            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+            continue;
+        ds.push_back(Dev{devices[i], (uint32_t)p.multiProcessorCount, st});
+    }
+    if (ds.empty()) return -1;
+    // (~3 ms per launch at 2.4 GHz; the next launch is queued before the host
+    // thread sleeps on the previous one's event, so the waves stay resident
+    // without a gap)
+    constexpr uint32_t kNaps = 1000;
+    std::vector<hipEvent_t> prev(ds.size(), nullptr);
+    for (;;) {
+        for (size_t i = 0; i < ds.size(); i++) {
+            Dev& d = ds[i];
+            (void)hipSetDevice(d.id);
+            hipLaunchKernelGGL(k_keep_resident, dim3(d.cus), dim3(64), 0, d.st, kNaps);
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess ||
+                hipEventRecord(e, d.st) != hipSuccess)
+                return -1;
+            if (prev[i]) {
+                (void)hipEventSynchronize(prev[i]);
+                (void)hipEventDestroy(prev[i]);
+            }
+            prev[i] = e;
+        }
+        char b;
+        const ssize_t r = ::read(fd, &b, 1);   // (fd non-blocking: -1 / EAGAIN while the pipe is open)
+        if (r == 0 || (r < 0 && errno != EAGAIN && errno != EINTR)) break;
+    }
+    for (size_t i = 0; i < ds.size(); i++) {
+        (void)hipSetDevice(ds[i].id);
+        if (prev[i]) {
+            (void)hipEventSynchronize(prev[i]);
+            (void)hipEventDestroy(prev[i]);
+        }
+        (void)hipStreamDestroy(ds[i].st);
+    }
+    return 0;
+}
 
 namespace {
 

@@ -23,6 +23,7 @@
 //   --host-parse     parse the blocks on host threads (default: on the device, sa_stage_text)
 //   --read-threads N plain-file reader threads (default 8; 0: the per-block window reader)
 //   --writers N      archive writer threads (default 8: page maps at the blocks' offsets; 1: write(2))
+//   --keep-clock 0|1 a companion process holding the GPU's clock while the encoders run (default 1)
 //   --ingest-only    the reader and block cut alone, batches dealt to devices x contexts
 //                    consumers (no device); --ingest-crc: the consumers CRC the texts
 //
@@ -44,7 +45,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <signal.h>
 #include <sys/mman.h>
+#include <sys/prctl.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
@@ -76,7 +79,7 @@ int usage()
             "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
             "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
             "                  [--block-size MiB] [--device D] [--share-device] [--ramp] [--release]\n"
-            "                  [--stage-ahead]\n"
+            "                  [--stage-ahead] [--writers N] [--keep-clock 0|1] [--read-threads N]\n"
             "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
             "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
             "       (-s with -i / -c / -d and ref.fa: the index image in /dev/shm/<ref file name>)\n"
@@ -1327,6 +1330,7 @@ struct Options {
          release = false, stage_ahead = false, shm = false, maxmis_set = false, ingest_crc = false;
     int read_threads = 8;   // --read-threads: the plain-file reader's fill threads (SegReader)
     int writers = 8;        // --writers: the archive writer's copy threads (ArcWriter; 1: write(2) in order)
+    int keep_clock = 1;     // --keep-clock: the companion process holding the GPU's clock (ClockKeeper; 0: none)
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -1621,6 +1625,57 @@ double g_main_s = 0.0;
     std::_Exit(rc);
 }
 
+// The GPU's clock under the latency-bound phases (round-5 VERDICT item 2).
+// amd-smi's throttle record names the limiter: the firmware's activity-based
+// clock control (its low-utilization flag) lowered the shader clock to
+// 1.0-2.0 GHz while few waves were resident -- the phases where only the last
+// batches' pass-R chains, MD5 and long runs run (r5b, r5j) -- and pass R, a
+// dependent chain, slowed with it.  A companion process keeps one sleeping
+// wave per CU resident (sa_clock_keeper: the waves issue nothing) for as long
+// as the encoders run: the chains then ran at 2,356-2,386 MHz instead of
+// 1,685-2,152 (r5l, rv_probe).  It is forked before this process starts a
+// thread or touches a GPU, and ends when its pipe closes (the encoders are
+// done, or this process exits).  --keep-clock 0: none.
+struct ClockKeeper {
+    pid_t pid = -1;
+    int wfd = -1;
+    void start(const std::vector<int>& devs)
+    {
+        int p[2];
+        if (devs.empty() || pipe(p) != 0) return;
+        const pid_t c = fork();
+        if (c < 0) {
+            close(p[0]);
+            close(p[1]);
+            return;
+        }
+        if (c == 0) {   // the keeper: no output, gone with its parent
+            close(p[1]);
+            (void)prctl(PR_SET_PDEATHSIG, SIGKILL);
+            if (getppid() == 1) _exit(0);
+            const int nul = ::open("/dev/null", O_RDWR);
+            if (nul >= 0) {
+                dup2(nul, 0);
+                dup2(nul, 1);
+                dup2(nul, 2);
+                close(nul);
+            }
+            (void)fcntl(p[0], F_SETFL, O_NONBLOCK);
+            _exit(sa_clock_keeper(devs.data(), (int)devs.size(), p[0]) == 0 ? 0 : 1);
+        }
+        close(p[0]);
+        (void)fcntl(p[1], F_SETFD, FD_CLOEXEC);
+        pid = c;
+        wfd = p[1];
+    }
+    void stop()
+    {
+        if (wfd >= 0) close(wfd);   // (the keeper sees end of file and ends)
+        wfd = -1;
+    }
+    ~ClockKeeper() { stop(); }
+};
+
 int compress(const Options& o)
 {
     const auto t_start = std::chrono::steady_clock::now();
@@ -1634,6 +1689,13 @@ int compress(const Options& o)
             fprintf(stderr, "Error:The Src file %s may be not exist or empty!\n", f);
             return 1;
         }
+    }
+    ClockKeeper keeper;
+    if (o.keep_clock && !o.host_only && !o.ingest_only) {
+        std::vector<int> devs;
+        for (int d = 0; d < (o.share_device ? 1 : o.devices); d++) devs.push_back(o.device + d);
+        keeper.start(devs);
+        if (o.verbose && keeper.pid > 0) fprintf(stderr, "seqarc_amd: clock keeper pid %d\n", (int)keeper.pid);
     }
     if (!in1.open(o.f1) || (pe && !in2.open(o.f2))) {
         fprintf(stderr, "seqarc_amd: cannot open the input\n");
@@ -2399,6 +2461,7 @@ int compress(const Options& o)
     reader.join();
     for (auto& t : parsers) t.join();
     for (auto& t : encoders) t.join();
+    keeper.stop();
     if (seg_free.joinable()) {
         {
             std::lock_guard<std::mutex> g(mu);
@@ -2791,6 +2854,7 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--ingest-crc")) o.ingest_crc = true;
         else if (!strcmp(a, "--read-threads")) { if (!ival(o.read_threads, 0)) return usage(); }
         else if (!strcmp(a, "--writers")) { if (!ival(o.writers, 1)) return usage(); }
+        else if (!strcmp(a, "--keep-clock")) { if (!ival(o.keep_clock, 0)) return usage(); }
         else if (!strcmp(a, "--no-ramp")) o.ramp = false;
         else if (!strcmp(a, "--ramp")) o.ramp = true;
         else if (!strcmp(a, "--release")) o.release = true;
