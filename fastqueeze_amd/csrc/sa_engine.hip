@@ -238,7 +238,6 @@ struct sa_ctx {
     // pass R 1,835-1,864 against 679-689 ms under the bench's load, the bench
     // 7,971-8,064 against 16,849-16,908 MB/s (r5k)
     bool rv_lanes = std::getenv("SA_RV_LANES") && std::atoi(std::getenv("SA_RV_LANES")) != 0;
-    DBuf d_rtab;   // recip32z(t) for t < 2^16 (k_coder_rl)
     // the SEQ space sorted by the context's low 8-9 bits only and replayed per
     // bucket with the models in LDS (k_replay_seq_bkt, contexts of <= 22 bits);
     // SA_SEQ_BUCKET=0: the full sort and k_replay_seq.  By the low bits the
@@ -358,7 +357,7 @@ struct sa_ctx {
     {
         return {&d_blocks, &d_totals, &d_err, &d_auxp_k, &d_auxp_v, &d_prs_seq, &d_prs_aux, &d_cum_seq, &d_cum_aux,
                 &d_task_ends, &d_tasks, &d_out_len, &d_payload, &d_md5tasks, &d_digests, &d_asm, &d_asm_copies, &d_task_out_base,
-                &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_rtab, &d_ck, &d_maps, &d_low_at, &d_off_at,
+                &d_final, &d_final_len, &d_longs, &d_huge_sorted, &d_nlong, &d_ck, &d_maps, &d_low_at, &d_off_at,
                 &d_dege_list, &d_qual_q, &d_rb_chunks, &d_rb_ck0, &d_rb_opens, &d_rb_spec, &d_rb_entry, &d_rb_guess, &d_rb_tab, &d_rb_vals, &d_rb_info, &d_first_sq,
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
@@ -721,7 +720,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
     tl.wait_ticks = c->rv_wait_ticks;
     if (c->rv_lanes) {   // a chain per lane, 64 per workgroup, longest first
         hipLaunchKernelGGL(k_coder_rl, dim3((tl.count + 63) / 64), dim3(64 * RL_WAVES), 0, st, cv.tasks, tl, cv.prs[0],
-                           cv.prs[1], c->d_rtab.as<uint32_t>(), cv.ck_r, c->d_err.as<uint32_t>(), c->chain_prio);
+                           cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(), c->chain_prio);
         if (ph >= 0) ev_finish(c, ph, st);
         return;
     }
@@ -952,15 +951,6 @@ sa_ctx* sa_create(int device)
     c->device = device;
     c->timing = c->trace;
     c->n_cu = (uint32_t)prop.multiProcessorCount;
-    if (c->rv_lanes) {   // k_coder_rl's reciprocal table: recip32z(t), t < 2^16
-        std::vector<uint32_t> tab(1u << 16);
-        for (uint32_t t = 0; t < (1u << 16); t++) tab[t] = recip32z(t);
-        if (c->d_rtab.ensure(4u << 16) != hipSuccess ||
-            hipMemcpy(c->d_rtab.p, tab.data(), 4u << 16, hipMemcpyHostToDevice) != hipSuccess) {
-            delete c;
-            return nullptr;
-        }
-    }
     for (int i = 0; i < PH_N; i++) c->ev_beg[i] = c->ev_end[i] = nullptr;
     // st carries the critical path (AUX symbols -> QUAL coder chain).  While the
     // long AUX model runs replay (latency-bound, st4: every 4th CU), the SEQ path

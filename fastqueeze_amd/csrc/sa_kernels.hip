@@ -3000,132 +3000,158 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
 // three quarters of the CUs, and the front kernels beside them, whose loops
 // and address arithmetic are scalar instructions, ran 2.5-6x slower than alone
 // (k_prep_sq16 4.4 -> 26.5 ms, k_emit_sq16 17 -> 43 ms; profiles/round5_r5e_*).
-// Here the same step runs in the VALU, 64 chains per wave, a batch's ~760
-// chains in ~12 workgroups.  A workgroup is two waves on two SIMDs: the
-// feeder (wave 0) loads each lane's next 64-record segment, waits for records
-// the long model runs have not written yet (tot 0; bounded as in seg_retry),
-// looks up the reciprocals (a 2^16-entry table of recip32z) and writes
-// (m, tf) pairs into one half of an LDS ring; the chain wave (wave 1) codes
-// the other half, one ds_read_b64 and the step per symbol.  One s_barrier per
-// segment hands the halves over.  Lanes whose chain has ended idle (exec).
-// Checkpoints (ck_r): each lane stores its range at the start of every
-// segment of its chain, first..last, as k_coder_rv does.
+// Here the same step runs in the VALU, 64 chains per workgroup (a batch's ~760
+// chains in ~12 workgroups, longest first).  Wave 4 codes: lane c is chain c,
+// one ds_read_b64 of (m, record) and the step per symbol.  Waves 0-3 feed it
+// through a two-half LDS ring, one 64-record segment of every chain per
+// round: for chain c (c = w, w + 4, ...) the wave loads the segment whole --
+// lane k its record k, 256 contiguous bytes -- derives m (BASE_MODEL totals
+// < 256 from an LDS table; wider totals by an exact double division), and
+// writes the pairs transposed, at [k][c] of a 65-wide row (2-way bank
+// conflicts at most).  The first version had each lane load its own chain's
+// records and look m up in a 2^16-entry table in memory: 128 gathers of 64
+// lines per round, pass R 1,835-1,864 ms under the bench's load (r5k).  The
+// loads of round j + 1 are issued before round j is converted; one barrier per
+// round hands the halves over.  Records the long model runs have not written
+// yet (total 0) are waited for as in seg_retry (agent-scope loads, bounded by
+// tl.wait_ticks, then E_CODER).  Checkpoints (ck_r): each lane stores its
+// range at the start of every segment of its chain, first..last, as
+// k_coder_rv does.
 // ---------------------------------------------------------------------------
-constexpr uint32_t RL_WAVES = 2;
+constexpr uint32_t RL_FEEDERS = 4, RL_WAVES = RL_FEEDERS + 1, RL_ROW = SEG_SYMS + 1;
+constexpr uint32_t RL_PER_FEEDER = 64 / RL_FEEDERS;
+
+// m for a record of one chain (tmask wave-uniform): recip32z of its total
+__device__ __forceinline__ uint32_t rl_recip(uint32_t v, uint32_t tmask, const uint32_t* tab)
+{
+    if (tmask == 0xffu) return tab[v & 0xffu];
+    const uint32_t t = v & 0xffffu;
+    // (2^32 - 1) / t rounded to nearest in double truncates to the integer
+    // quotient: below 2^32 a double's spacing is <= 2^-21, a non-integer
+    // quotient is >= 1/t >= 2^-16 from the next integer (recip32 for t >= 1;
+    // t = 1 wraps to 0 as recip32 does)
+    return t ? (uint32_t)(4294967295.0 / (double)t) + 1u : 0u;
+}
 
 __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __restrict__ tasks, const TaskList tl,
                                                             const PRec* __restrict__ prs0,
                                                             const PRec* __restrict__ prs1,
-                                                            const uint32_t* __restrict__ rtab,
                                                             uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err,
                                                             const uint32_t prio)
 {
-    __shared__ uint2 ring[2][SEG_SYMS][64];   // 64 KB: (m, tf) per segment step and lane
-    const uint32_t lane = threadIdx.x & 63;
-    const bool feeder = threadIdx.x < 64;
+    __shared__ uint2 ring[2][SEG_SYMS * RL_ROW];   // 66,560 B: (m, tf) at [step][chain]
+    __shared__ uint32_t tab[256];                  // recip32z(t), t < 256
+    typedef const __attribute__((address_space(1))) uint32_t g_u32;   // (global loads: vmcnt only, not lgkmcnt)
+    __shared__ g_u32* cbase[64];                   // chain c's first coded segment
+    __shared__ uint32_t cnj[64], cmask[64], cmax;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) tab[t] = recip32z(t);
     const uint32_t li = blockIdx.x * 64 + lane;
-    const bool has = li < tl.count;
-    uint32_t first = 0, last = 0, r = 0, tmask = 0xffu;
+    uint32_t first = 0, nj = 0, r = 0, tmask = 0xffu;
     uint64_t seg_base = 0;
-    const PRec* P = prs0;
-    if (has) {
-        const CoderTask tk = tasks[tl.ids[li]];
-        const CoderRun run = tl.run[li];
-        P = (tk.space ? prs1 : prs0) + tk.rec_base;
-        tmask = tk.space ? 0xffffu : 0xffu;
-        first = run.start_seg;
-        last = tk.nseg - 1;
-        r = run.r0;
-        seg_base = tk.seg_base;
-    }
-    // segments coded by this lane: first .. last - 1 (the last is L3's alone)
-    const uint32_t nj = has && last > first ? last - first : 0u;
-    uint32_t J = nj;   // the workgroup's longest chain, in segments (both waves agree)
+    if (wave == RL_FEEDERS) {
+        uint32_t last = 0;
+        const PRec* P = prs0;
+        if (li < tl.count) {
+            const CoderTask tk = tasks[tl.ids[li]];
+            const CoderRun run = tl.run[li];
+            P = (tk.space ? prs1 : prs0) + tk.rec_base;
+            tmask = tk.space ? 0xffffu : 0xffu;
+            first = run.start_seg;
+            last = tk.nseg - 1;
+            r = run.r0;
+            seg_base = tk.seg_base;
+        }
+        // segments coded by this lane: first .. last - 1 (the last is L3's alone)
+        nj = li < tl.count && last > first ? last - first : 0u;
+        cbase[lane] = (g_u32*)(P + (size_t)first * SEG_SYMS);
+        cnj[lane] = nj;
+        cmask[lane] = tmask;
+        uint32_t J = nj;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)J, d, 64);
-        J = J > o ? J : o;
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)J, d, 64);
+            J = J > o ? J : o;
+        }
+        if (lane == 0) cmax = J;
     }
-    J = (uint32_t)__builtin_amdgcn_readfirstlane((int)J);
-    if (feeder) {
+    __syncthreads();
+    const uint32_t J = cmax;
+    if (wave < RL_FEEDERS) {
         uint32_t bad = 0;
         const uint64_t wait = tl.wait_ticks ? tl.wait_ticks : 2000000000u;
-        // Pipelined: in the iteration that the chain wave codes segment j, the
-        // feeder looks up the reciprocals of segment j + 1 (its records were
-        // loaded one iteration earlier), issues the loads of segment j + 2, and
-        // writes segment j + 1 into the other ring half once the lookups are in
-        // -- one memory round trip per segment instead of two.  A stream starts
-        // at any record: dword loads, each lane its own 256 B; loads past a
-        // lane's chain re-read its last segment (branch-free, so the waits for
-        // the lookups need not wait for the loads issued after them).
-        const uint32_t* S0 = reinterpret_cast<const uint32_t*>(P + (size_t)first * SEG_SYMS);
-        auto load = [&](uint32_t j, uint32_t (&v)[SEG_SYMS]) __attribute__((always_inline)) {
-            const uint32_t* S = S0 + (size_t)(j < nj ? j : (nj ? nj - 1 : 0)) * SEG_SYMS;
+        // this wave's chains c = wave + RL_FEEDERS i: their record bases, segment
+        // counts and total masks in registers (the LDS copies are read once)
+        g_u32* base[RL_PER_FEEDER];
+        uint32_t cn[RL_PER_FEEDER], cm[RL_PER_FEEDER];
 #pragma unroll
-            for (uint32_t k = 0; k < SEG_SYMS; k++) v[k] = S[k];
+        for (uint32_t i = 0; i < RL_PER_FEEDER; i++) {
+            const uint32_t c = wave + RL_FEEDERS * i;
+            base[i] = cbase[c] + lane;
+            cn[i] = cnj[c];
+            cm[i] = cmask[c];
+        }
+        // a round's loads of segment j (clamped to the chain's last coded
+        // segment: branch-free)
+        auto load = [&](uint32_t j, uint32_t (&v)[RL_PER_FEEDER]) __attribute__((always_inline)) {
+#pragma unroll
+            for (uint32_t i = 0; i < RL_PER_FEEDER; i++) {
+                const uint32_t jj = j < cn[i] ? j : (cn[i] ? cn[i] - 1 : 0u);
+                v[i] = base[i][(size_t)jj * SEG_SYMS];
+            }
         };
-        // segment j's records in v (loaded); the unwritten ones waited for
-        auto written = [&](uint32_t j, uint32_t (&v)[SEG_SYMS]) __attribute__((always_inline)) {
-            uint32_t zero = 0;
+        // round j's records (in v) waited for where the long model runs have
+        // not written them yet (total 0; replayed concurrently) -- before the
+        // next round's loads are issued, so the wait for v is the only one
+        auto check = [&](uint32_t j, uint32_t (&v)[RL_PER_FEEDER]) __attribute__((always_inline)) {
+            bool zero = false;
 #pragma unroll
-            for (uint32_t k = 0; k < SEG_SYMS; k++) zero |= (v[k] & tmask) == 0;
-            if (zero && j < nj && !bad) {   // records not written yet (long runs replayed concurrently)
-                const uint32_t* S = S0 + (size_t)j * SEG_SYMS;
+            for (uint32_t i = 0; i < RL_PER_FEEDER; i++) zero |= j < cn[i] && (v[i] & cm[i]) == 0;
+            if (__ballot(zero) && !bad) {
                 const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + wait;
-                for (;;) {
-                    zero = 0;
 #pragma unroll
-                    for (uint32_t k = 0; k < SEG_SYMS; k++) {
-                        v[k] = __hip_atomic_load(S + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        zero |= (v[k] & tmask) == 0;
+                for (uint32_t i = 0; i < RL_PER_FEEDER; i++) {   // (unrolled: v, cn, cm stay in registers)
+                    if (j < cn[i] && !bad) {
+                        g_u32* S = base[i] + (size_t)j * SEG_SYMS;
+                        while (__ballot((v[i] & cm[i]) == 0)) {
+                            if (__builtin_amdgcn_s_memrealtime() > t_end) {
+                                bad = 1;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(32);
+                            v[i] = __hip_atomic_load((const uint32_t*)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
                     }
-                    if (!zero) break;
-                    if (__builtin_amdgcn_s_memrealtime() > t_end) {
-                        bad = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(32);
                 }
             }
         };
-        // iteration j: segment j + 1 (records in cur) into its ring half, the
-        // loads of segment j + 2 into nxt
-        auto pipe = [&](uint32_t j, uint32_t (&cur)[SEG_SYMS], uint32_t (&nxt)[SEG_SYMS]) __attribute__((always_inline)) {
-            written(j + 1, cur);
-            uint32_t m[SEG_SYMS];
+        // round j's records converted into ring half j & 1 (pairs of chains
+        // past their end are written too: their lanes do not read them)
+        auto put = [&](uint32_t j, const uint32_t (&v)[RL_PER_FEEDER]) __attribute__((always_inline)) {
+            uint2* R = ring[j & 1] + lane * RL_ROW + wave;
 #pragma unroll
-            for (uint32_t k = 0; k < SEG_SYMS; k++) m[k] = rtab[cur[k] & tmask];
-            load(j + 2, nxt);
-            if (j + 1 < nj) {
-                uint2* R = &ring[(j + 1) & 1][0][lane];
-#pragma unroll
-                for (uint32_t k = 0; k < SEG_SYMS; k++) R[k * 64] = make_uint2(m[k], cur[k]);
-            }
+            for (uint32_t i = 0; i < RL_PER_FEEDER; i++)
+                R[RL_FEEDERS * i] = make_uint2(rl_recip(v[i], cm[i], tab), v[i]);
         };
-        uint32_t va[SEG_SYMS], vb[SEG_SYMS];
+        uint32_t va[RL_PER_FEEDER], vb[RL_PER_FEEDER];
         load(0, va);
-        written(0, va);
-        {
-            uint32_t m[SEG_SYMS];
-#pragma unroll
-            for (uint32_t k = 0; k < SEG_SYMS; k++) m[k] = rtab[va[k] & tmask];
-            load(1, vb);
-            if (nj) {
-                uint2* R = &ring[0][0][lane];
-#pragma unroll
-                for (uint32_t k = 0; k < SEG_SYMS; k++) R[k * 64] = make_uint2(m[k], va[k]);
-            }
-        }
+        check(0, va);
+        load(1, vb);
+        put(0, va);
         __syncthreads();
-        for (uint32_t j = 0; j < J; j += 2) {
-            pipe(j, vb, va);
+        for (uint32_t j = 1; j <= J; j += 2) {   // round j into its half while the chain codes round j - 1
+            check(j, vb);
+            load(j + 1, va);
+            put(j, vb);
             __syncthreads();
-            if (j + 1 < J) {
-                pipe(j + 1, va, vb);
+            if (j + 1 <= J) {
+                check(j + 1, va);
+                load(j + 2, vb);
+                put(j + 1, va);
                 __syncthreads();
             }
         }
-        if (__ballot(bad != 0) && lane == 0) atomicOr(err, (uint32_t)E_CODER);
+        if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
     } else {
         set_chain_prio(prio);
         uint32_t* ck = ck_r + seg_base;
@@ -3133,11 +3159,11 @@ __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __r
         for (uint32_t j = 0; j < J; j++) {
             if (j < nj) {
                 ck[first + j] = r;
-                const uint2* R = &ring[j & 1][0][lane];
+                const uint2* R = ring[j & 1] + lane;
                 uint32_t rr = r;
 #pragma unroll 16
                 for (uint32_t k = 0; k < SEG_SYMS; k++) {
-                    const uint2 e = R[k * 64];
+                    const uint2 e = R[k * RL_ROW];
                     const uint32_t t = e.y & tmask, f = e.y >> 16;
                     uint32_t q = __umulhi(rr, e.x);
                     q -= rr < q * t ? 1u : 0u;
@@ -3148,7 +3174,7 @@ __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __r
             }
             __syncthreads();
         }
-        if (has) ck[first + nj] = r;   // (the range entering segment `last`)
+        if (li < tl.count) ck[first + nj] = r;   // (the range entering segment `last`)
     }
 }
 
