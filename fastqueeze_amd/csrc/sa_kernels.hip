@@ -3021,6 +3021,15 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
 constexpr uint32_t RL_FEEDERS = 4, RL_WAVES = RL_FEEDERS + 1, RL_ROW = SEG_SYMS + 1;
 constexpr uint32_t RL_PER_FEEDER = 64 / RL_FEEDERS;
 
+// The ring hand-over: LDS writes done, then the barrier -- without
+// __syncthreads' release fence, which waits for every outstanding global
+// access of the wave (vmcnt(0)): the feeders' loads of the next round and the
+// chain's checkpoint store would each cost a memory round trip per round.
+__device__ __forceinline__ void rl_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // m for a record of one chain (tmask wave-uniform): recip32z of its total
 __device__ __forceinline__ uint32_t rl_recip(uint32_t v, uint32_t tmask, const uint32_t* tab)
 {
@@ -3138,24 +3147,24 @@ __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __r
         check(0, va);
         load(1, vb);
         put(0, va);
-        __syncthreads();
+        rl_barrier();
         for (uint32_t j = 1; j <= J; j += 2) {   // round j into its half while the chain codes round j - 1
             check(j, vb);
             load(j + 1, va);
             put(j, vb);
-            __syncthreads();
+            rl_barrier();
             if (j + 1 <= J) {
                 check(j + 1, va);
                 load(j + 2, vb);
                 put(j + 1, va);
-                __syncthreads();
+                rl_barrier();
             }
         }
         if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
     } else {
         set_chain_prio(prio);
         uint32_t* ck = ck_r + seg_base;
-        __syncthreads();
+        rl_barrier();
         for (uint32_t j = 0; j < J; j++) {
             if (j < nj) {
                 ck[first + j] = r;
@@ -3172,7 +3181,7 @@ __global__ __launch_bounds__(64 * RL_WAVES) void k_coder_rl(const CoderTask* __r
                 }
                 r = rr;
             }
-            __syncthreads();
+            rl_barrier();
         }
         if (li < tl.count) ck[first + nj] = r;   // (the range entering segment `last`)
     }

@@ -74,9 +74,50 @@ int main(int argc, char** argv)
         const double t1 = now();
         for (int i = 0; i < c.threads; i++) hipHostUnregister((char*)p + part * i);
         const double tu = now() - t1;
+        const double t2 = now();
         free(p);
-        printf("%-52s %zu GB: touch %.3f s, register %.3f s (%.1f GB/s)%s, unregister %.3f s, AnonHugePages %ld MB\n",
-               c.name, gb, tt, tr, gb / tr, ok ? "" : " FAILED", tu, huge / 1024);
+        printf("%-52s %zu GB: touch %.3f s, register %.3f s (%.1f GB/s)%s, unregister %.3f s, free %.3f s, AnonHugePages %ld MB\n",
+               c.name, gb, tt, tr, gb / tr, ok ? "" : " FAILED", tu, now() - t2, huge / 1024);
+    }
+    // the command line's segment ring: 512 MiB segments, touched, registered,
+    // each the source of an H2D copy; then released (unregister + free) on one
+    // thread or on eight
+    for (int rel_threads : {1, 8}) {
+        const size_t seg = 512ull << 20, ns = n / seg;
+        std::vector<void*> segs(ns, nullptr);
+        void* d = nullptr;
+        if (hipMalloc(&d, seg) != hipSuccess) return 1;
+        for (size_t k = 0; k < ns; k++) {
+            if (posix_memalign(&segs[k], 2u << 20, seg) != 0) return 1;
+            madvise(segs[k], seg, MADV_HUGEPAGE);
+            memset(segs[k], 1, seg);
+            if (hipHostRegister(segs[k], seg, hipHostRegisterPortable) != hipSuccess) return 1;
+            if (hipMemcpy(d, segs[k], seg, hipMemcpyHostToDevice) != hipSuccess) return 1;
+        }
+        const double t0 = now();
+        std::vector<std::thread> th;
+        double tu_sum[8] = {0}, tf_sum[8] = {0};
+        for (int i = 0; i < rel_threads; i++)
+            th.emplace_back([&, i]() {
+                for (size_t k = i; k < ns; k += rel_threads) {
+                    const double a = now();
+                    hipHostUnregister(segs[k]);
+                    const double b = now();
+                    free(segs[k]);
+                    tu_sum[i] += b - a;
+                    tf_sum[i] += now() - b;
+                }
+            });
+        for (auto& t : th) t.join();
+        const double tr = now() - t0;
+        double tu = 0, tf = 0;
+        for (int i = 0; i < rel_threads; i++) {
+            tu += tu_sum[i];
+            tf += tf_sum[i];
+        }
+        (void)hipFree(d);
+        printf("segment ring %zu x 512 MiB, released on %d thread(s): %.3f s (unregister %.3f s, free %.3f s summed)\n",
+               ns, rel_threads, tr, tu, tf);
     }
     {
         void* p = nullptr;
