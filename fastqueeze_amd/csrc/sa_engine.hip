@@ -969,13 +969,32 @@ sa_ctx* sa_create(int device)
     for (int cu = 0; cu < prop.multiProcessorCount; cu++)
         ((cu % every) == 0 || every == 1 ? m_long : m_seq)[cu / 32] |= 1u << (cu % 32);
     if (every == 1) m_seq = m_long;   // (st3: the coder chains; st4: the long model runs)
+    // (A/B, round 5) SA_RV_CUS=n (1..5, with every = 4): pass R and the L passes
+    // (st3) on n of each 8 CUs only, the front (st) on the others -- the scalar
+    // units of the front's CUs free of chain waves (k_coder_rl showed the
+    // fronts 2-3x faster beside a pass R that leaves the scalar units alone)
+    std::vector<uint32_t> m_front;
+    if (const char* rc = std::getenv("SA_RV_CUS")) {
+        const int n = std::atoi(rc);
+        if (every == 4 && n >= 1 && n <= 5) {
+            m_front.assign(m_long.size(), 0u);
+            std::fill(m_seq.begin(), m_seq.end(), 0u);
+            static const int order[6] = {1, 5, 2, 6, 3, 7};   // (the non-long CUs of each 8, spread)
+            for (int cu = 0; cu < prop.multiProcessorCount; cu++) {
+                bool r = false;
+                for (int k = 0; k < n; k++) r |= (cu % 8) == order[k];
+                (r ? m_seq : m_front)[cu / 32] |= 1u << (cu % 32);
+            }
+        }
+    }
     {
         uint32_t ncu_long = 0;
         for (uint32_t w : m_long) ncu_long += (uint32_t)__builtin_popcount(w);
         c->long_grid = std::max(1u, 6u * ncu_long);
         if (const char* lg = std::getenv("SA_LONG_GRID")) c->long_grid = (uint32_t)std::max(1, std::atoi(lg));
     }
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+    if ((m_front.empty() ? hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)
+                         : hipExtStreamCreateWithCUMask(&c->st, (uint32_t)m_front.size(), m_front.data())) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st2, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st3, (uint32_t)m_seq.size(), m_seq.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->st4, (uint32_t)m_long.size(), m_long.data()) != hipSuccess ||
