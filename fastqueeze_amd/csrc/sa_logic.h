@@ -806,47 +806,24 @@ constexpr uint32_t RB_WORDS = RB_CHUNK / 32;
 template <class F>
 SA_HD void rb_for_bytes(const uint8_t* q, uint64_t base, uint32_t from, uint32_t len, F f)
 {
-    // 64 bytes a step, the next step's loads issued before this step's bytes
-    // are walked (round 5: 16-byte steps waited a memory round trip every 16
-    // bytes, and a lane came back to each 128-byte line eight times)
-    constexpr uint32_t G = 64;
-    auto fetch = [&](uint32_t i0, uint32_t(&w)[G / 4]) {
+    for (uint32_t i0 = from & ~15u; i0 < len; i0 += 16) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
         const uint8_t* p = q + base + i0;
-        if (i0 + G <= len && ((base + i0) & 15) == 0) {
-#pragma unroll
-            for (uint32_t k = 0; k < G / 16; k++) __builtin_memcpy(&w[4 * k], __builtin_assume_aligned(p + 16 * k, 16), 16);
+        if (i0 + 16 <= len && ((base + i0) & 15) == 0) {
+            __builtin_memcpy(w, __builtin_assume_aligned(p, 16), 16);
         } else {
-#pragma unroll
-            for (uint32_t k = 0; k < G / 4; k++) w[k] = 0u;
-            for (uint32_t j = 0; j < G && i0 + j < len; j++) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+            for (uint32_t j = 0; j < 16 && i0 + j < len; j++) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
         }
-    };
-    auto walk = [&](uint32_t i0, const uint32_t(&w)[G / 4]) -> bool {
 #pragma unroll
-        for (uint32_t k = 0; k < G / 4; k++) {
+        for (uint32_t k = 0; k < 4; k++) {
             uint32_t x = w[k];
             for (uint32_t j = 0; j < 4; j++, x >>= 8) {
                 const uint32_t i = i0 + 4 * k + j;
                 if (i < from) continue;
-                if (i >= len) return false;
-                if (!f(i, x & 0xffu)) return false;
+                if (i >= len) return;
+                if (!f(i, x & 0xffu)) return;
             }
         }
-        return true;
-    };
-    uint32_t wa[G / 4], wb[G / 4];
-    uint32_t i0 = from & ~(G - 1);
-    if (i0 >= len) return;
-    fetch(i0, wa);
-    for (;;) {
-        if (i0 + G < len) fetch(i0 + G, wb);
-        if (!walk(i0, wa)) return;
-        i0 += G;
-        if (i0 >= len) return;
-        if (i0 + G < len) fetch(i0 + G, wa);
-        if (!walk(i0, wb)) return;
-        i0 += G;
-        if (i0 >= len) return;
     }
 }
 
