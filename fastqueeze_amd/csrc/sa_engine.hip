@@ -332,6 +332,14 @@ struct sa_ctx {
     DBuf d_rb_vals, d_rb_info;   // (round 5: run values per chunk byte, RbInfo per chunk)
     // SA_RB_APPLY=1: the round-4 second full walk (k_rb_apply) instead of k_rb_true + k_rb_fill (A/B)
     bool rb_apply_walk = std::getenv("SA_RB_APPLY") && std::atoi(std::getenv("SA_RB_APPLY")) != 0;
+    // R-Block chunk length (A/B, round 5): SA_RB_CHUNK=n, a multiple of 32 up
+    // to RB_CHUNK (the arrays keep RB_CHUNK's stride; a shorter chunk is what
+    // a block's last chunk always was): shorter serial walks, more lanes
+    uint32_t rb_chunk = [] {
+        const char* e = std::getenv("SA_RB_CHUNK");
+        const uint32_t n = e ? (uint32_t)std::atoi(e) : RB_CHUNK;
+        return n >= 32 && n <= RB_CHUNK && n % 32 == 0 ? n : RB_CHUNK;
+    }();
     std::vector<uint32_t> rb_tab_host;   // the R decision tables (RbTab) of rb_tab_r
     double rb_tab_r = -1.0;
     bool rb_tab_sent = false;
@@ -602,8 +610,8 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     std::vector<uint32_t> ck0;
     for (const DevBlock& d : c->blocks) {
         ck0.push_back((uint32_t)ck.size());
-        for (uint64_t o = 0; o < d.seq_bytes; o += RB_CHUNK) {
-            const uint32_t len = (uint32_t)std::min<uint64_t>(RB_CHUNK, d.seq_bytes - o);
+        for (uint64_t o = 0; o < d.seq_bytes; o += c->rb_chunk) {
+            const uint32_t len = (uint32_t)std::min<uint64_t>(c->rb_chunk, d.seq_bytes - o);
             uint32_t fl = (o == 0 ? RB_FIRST : 0u) | (o + len == d.seq_bytes ? RB_LAST : 0u);
             ck.push_back(RbChunk{d.seq_base + o, len, fl});
         }

@@ -340,8 +340,11 @@ int main(int argc, char** argv)
         for (int64_t b = 0; b < nb; b++) {
             const DevBlock& d = blocks[(size_t)b];
             std::vector<RbChunk> ck;
-            for (uint64_t o = 0; o < d.seq_bytes; o += RB_CHUNK) {
-                const uint32_t len = (uint32_t)std::min<uint64_t>(RB_CHUNK, d.seq_bytes - o);
+            // (SA_RB_CHUNK: the engine's shorter chunk length, the same arrays' stride)
+            const char* rce = std::getenv("SA_RB_CHUNK");
+            const uint64_t rc = rce && std::atoi(rce) >= 32 && (uint32_t)std::atoi(rce) <= RB_CHUNK ? (uint64_t)std::atoi(rce) : RB_CHUNK;
+            for (uint64_t o = 0; o < d.seq_bytes; o += rc) {
+                const uint32_t len = (uint32_t)std::min<uint64_t>(rc, d.seq_bytes - o);
                 ck.push_back(RbChunk{d.seq_base + o, len, (o == 0 ? RB_FIRST : 0u) | (o + len == d.seq_bytes ? RB_LAST : 0u)});
             }
             if (ck.empty()) continue;

@@ -118,6 +118,13 @@ def test_cpu_decomposition(tmp_path):
     for args in runs:
         r = subprocess.run([str(exe)] + args, capture_output=True, text=True)
         assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
+    # the engine's shorter R-Block chunks (SA_RB_CHUNK, the arrays keep RB_CHUNK's stride)
+    for chunk in ("4096", "1024"):
+        for args in (["-l", "1.15", TEST1, TEST2], ["-l", "1.6", str(tmp_path / "long.fq")],
+                     ["-l", "1.15", str(tmp_path / "const.fq")]):
+            r = subprocess.run([str(exe)] + args, capture_output=True, text=True,
+                               env=dict(os.environ, SA_RB_CHUNK=chunk))
+            assert r.returncode == 0 and r.stdout.startswith("OK"), (chunk, args, r.stdout, r.stderr)
 
 
 def test_cpu_decomposition_reference_path(tmp_path):
