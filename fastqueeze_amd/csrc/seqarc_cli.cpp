@@ -785,14 +785,6 @@ struct SegReader {
     std::condition_variable cv;
     std::vector<std::thread> workers;
     std::atomic<uint64_t> alloc_bytes{0};
-    // segments retired early (round 5): a slot that no later segment of its
-    // file will use is released as soon as its segment is cut past and no
-    // block holds it -- by a thread of its own, beside the last reads --
-    // instead of all of them after the last block (releasing ~10 GB of
-    // page-locked memory took ~0.5 s at the end of --ingest-only, r5v)
-    std::vector<void*> retired;
-    std::thread retirer;
-    bool retire_stop = false;
     double fill_s = 0;   // fill threads' busy time (under mu)
 
     // fds: open plain regular files; W: the cut's window
@@ -826,21 +818,6 @@ struct SegReader {
             F.ring.resize((size_t)std::max<int64_t>(1, std::min<int64_t>(R, F.nseg)));
         }
         for (int t = 0; t < std::max(1, threads); t++) workers.emplace_back([this]() { work(); });
-        retirer = std::thread([this]() {
-            for (;;) {
-                std::vector<void*> batch;
-                {
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return retire_stop || !retired.empty(); });
-                    if (retired.empty()) return;
-                    batch.swap(retired);
-                }
-                for (void* q : batch) {
-                    if (pinned) sa_host_free(q);
-                    else free(q);
-                }
-            }
-        });
         return true;
     }
     ~SegReader() { free_all(); }
@@ -855,12 +832,6 @@ struct SegReader {
         }
         for (auto& t : workers) t.join();
         workers.clear();
-        {
-            std::lock_guard<std::mutex> g(mu);
-            retire_stop = true;
-            cv.notify_all();
-        }
-        if (retirer.joinable()) retirer.join();   // (it drains its queue first)
         // (on up to SA_CLI_FREE_THREADS threads, default 8: releasing ~10 GB of
         // page-locked segments one by one took ~0.47 s past the last encode, r5m)
         std::vector<Seg*> all;
@@ -990,23 +961,6 @@ struct SegReader {
             cv.notify_all();
         }
     }
-    // under mu: slot s of file F handed to the retirer once nothing needs it
-    // again (cut past, no block holds it, no later segment maps to the slot)
-    void maybe_retire(File& F, Seg& s)
-    {
-        if (!s.p || s.idx < 0 || s.refs != 0 || !s.filled || s.idx >= F.low ||
-            s.idx + (int64_t)F.ring.size() < F.nseg)
-            return;
-        retired.push_back(s.p);
-        s.p = nullptr;
-        s.cap = 0;
-        s.ready = false;
-        cv.notify_all();
-    }
-    void retire_passed(File& F)
-    {
-        for (Seg& s : F.ring) maybe_retire(F, s);
-    }
     // the cut's window at file offset off: waits for its segment, takes a
     // reference for the block (release(fi, seg)), returns the bytes available
     // from off within the segment; nullptr on a read failure
@@ -1016,7 +970,6 @@ struct SegReader {
         const int64_t k = std::min<int64_t>((int64_t)(off / S), std::max<int64_t>(F.nseg - 1, 0));
         std::unique_lock<std::mutex> lk(mu);
         F.low = k;
-        retire_passed(F);
         cv.notify_all();
         Seg& s = F.ring[(size_t)(k % (int64_t)F.ring.size())];
         cv.wait(lk, [&] { return failed || (s.idx == k && s.filled); });
@@ -1032,17 +985,13 @@ struct SegReader {
         std::lock_guard<std::mutex> g(mu);
         Seg& s = f[fi].ring[(size_t)(seg % (int64_t)f[fi].ring.size())];
         if (s.idx == seg && s.refs > 0) s.refs--;
-        if (s.idx == seg) maybe_retire(f[fi], s);
         cv.notify_all();
     }
     // the cut has passed every segment (the end of the input)
     void finish()
     {
         std::lock_guard<std::mutex> g(mu);
-        for (int i = 0; i < nf; i++) {
-            f[i].low = f[i].nseg;
-            retire_passed(f[i]);
-        }
+        for (int i = 0; i < nf; i++) f[i].low = f[i].nseg;
         cv.notify_all();
     }
     // newlines in [off, off + len) of file fi, inside the segment that holds off
