@@ -1120,6 +1120,36 @@ struct TextPool {
     }
 };
 
+// The encoded blocks' host buffers, recycled (round 5): a fresh buffer per
+// block is a fresh mapping that the runtime's device-to-host copy faults in
+// (and may page-lock) and that is unmapped again once the block is written,
+// every batch.  The pool keeps them for the next batch's blocks; the virtual
+// size is the output bound (~2x the block's symbols), only the written bytes
+// are ever touched.  SA_CLI_OUT_POOL=0: a fresh buffer per block (A/B).
+struct OutPool {
+    std::mutex mu;
+    std::vector<Buf<uint8_t>> free;
+    const bool on = !(std::getenv("SA_CLI_OUT_POOL") && std::atoi(std::getenv("SA_CLI_OUT_POOL")) == 0);
+    void take(Buf<uint8_t>& b, size_t n)
+    {
+        if (on && !b.cap) {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free.empty()) {
+                b = std::move(free.back());
+                free.pop_back();
+            }
+        }
+        if (on && b.cap < n) b.reserve(n + n / 8);   // (slack: the next block's bound may be a little larger)
+        b.resize(n);
+    }
+    void give(Buf<uint8_t>& b)
+    {
+        if (!on || !b.cap) return;
+        std::lock_guard<std::mutex> g(mu);
+        free.push_back(std::move(b));
+    }
+};
+
 struct Job {                     // one block between the reader and the writer
     Buf<uint8_t> t1, t2;          // its FASTQ text (recycled once parsed / staged; a view into a SegReader segment)
     SegReader* segr = nullptr;    // (views: the segments' references, released with the text)
@@ -1728,6 +1758,7 @@ int compress(const Options& o)
     // template.  --host-parse / --host-only: -t parser threads build the SoA.
     const bool dev_parse = !o.host_parse && !o.host_only;
     ParsedPool pool;   // (declared before the jobs: outlive them)
+    OutPool outpool;
     TextPool texts;
     texts.pinned = dev_parse && !o.ingest_only;
     texts.win = (pe ? (size_t)((uint32_t)bs >> 1) : (size_t)bs) + (64u << 10);   // a window + slack for the carry
@@ -2223,7 +2254,7 @@ int compress(const Options& o)
                 give_back(*js[i], texts);   // (the device holds the text now)
                 js[i]->nreads = ti[i].nreads;
                 js[i]->len_long = ti[i].len_long;
-                js[i]->out.resize(ti[i].out_bound);
+                outpool.take(js[i]->out, ti[i].out_bound);
             }
         }
         cv.notify_all();
@@ -2363,7 +2394,7 @@ int compress(const Options& o)
                         give_back(*js[i], texts);   // (the device holds the text now)
                         js[i]->nreads = ti[i].nreads;
                         js[i]->len_long = ti[i].len_long;
-                        js[i]->out.resize(ti[i].out_bound);
+                        outpool.take(js[i]->out, ti[i].out_bound);
                         outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
                     }
                     cv.notify_all();   // (text windows are free for the reader)
@@ -2396,7 +2427,7 @@ int compress(const Options& o)
                     std::vector<sa_block> in(js.size());
                     for (size_t i = 0; i < js.size(); i++) {
                         in[i] = js[i]->p->view();
-                        js[i]->out.resize(sa_output_bound(&in[i]));   // (uninitialised: only the real bytes are touched)
+                        outpool.take(js[i]->out, sa_output_bound(&in[i]));   // (uninitialised: only the real bytes are touched)
                         outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
                     }
                     if (!ctx) {   // --host-only
@@ -2439,6 +2470,7 @@ int compress(const Options& o)
     const int nwriters = std::max(1, std::min(8, o.writers));
     const bool opened = aw.open(path, nwriters, [&](std::unique_ptr<Job> j) {
         if (j->p) pool.put(std::move(j->p));
+        outpool.give(j->out);
         j.reset();
         {
             std::lock_guard<std::mutex> g(mu);
