@@ -1961,7 +1961,9 @@ int compress(const Options& o)
     std::atomic<double> t_seg_freed{0};
     std::thread seg_free;
     bool seg_stop = false;
-    if (segr && dev_parse)
+    // (SA_CLI_RING_FREE=0, A/B: the ring is left to the process exit)
+    const bool ring_free = !(std::getenv("SA_CLI_RING_FREE") && std::atoi(std::getenv("SA_CLI_RING_FREE")) == 0);
+    if (segr && dev_parse && ring_free)
         seg_free = std::thread([&]() {
             {
                 std::unique_lock<std::mutex> lk(mu);
