@@ -797,7 +797,12 @@ struct SegReader {
         uint64_t mx = 0;
         for (int i = 0; i < n; i++) mx = std::max(mx, sizes[i]);
         // segments of 512 MiB (a small input: one segment; SA_CLI_SEG_SLICES=n: n slices, for the tests)
-        S = std::max<uint64_t>(kSlice, std::min<uint64_t>(512ull << 20, (mx + kSlice - 1) / kSlice * kSlice));
+        // (round 5: 256 MiB, SA_CLI_SEG_MIB to change: the ring is unmapped at the
+        // end, ~25 GB/s of page-locked memory, and while device work runs the
+        // unmapping stalls it -- a smaller ring costs less of both, r5x)
+        const char* sm = std::getenv("SA_CLI_SEG_MIB");
+        const uint64_t smax = (uint64_t)(sm ? std::max(4, std::atoi(sm)) : 256) << 20;
+        S = std::max<uint64_t>(kSlice, std::min<uint64_t>(smax, (mx + kSlice - 1) / kSlice * kSlice));
         if (const char* e = std::getenv("SA_CLI_SEG_SLICES")) S = kSlice * std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
         int R = (int)std::max<int64_t>(3, (ahead_bytes + (int64_t)S - 1) / (int64_t)S + 3);
         // (A/B) SA_CLI_RING_SEGS=n: n segments per file.  The ring is page-locked
@@ -1953,7 +1958,12 @@ int compress(const Options& o)
             segr.reset(new SegReader());
             const int fds[2] = {in1.fd, in2.fd};
             // the reader runs at most two batches of blocks ahead of the staging (below)
-            segr->start(fds, fsize, pe ? 2 : 1, win + (64u << 10), (int64_t)(2 * B + 2) * (int64_t)win,
+            // (one batch of windows ahead of the staging, SA_CLI_AHEAD_BATCHES to change;
+            // two until round 5: the contexts take batches as fast as the reader
+            // cuts them until all are busy, then the device sets the pace)
+            const char* ab = std::getenv("SA_CLI_AHEAD_BATCHES");
+            const int64_t ahead = ab ? std::max(1, std::atoi(ab)) : 1;
+            segr->start(fds, fsize, pe ? 2 : 1, win + (64u << 10), (int64_t)(ahead * B + 2) * (int64_t)win,
                         o.read_threads, dev_parse, (uint64_t)B);   // (page-locked for the device parse; --ingest-only too)
         }
     }
