@@ -327,11 +327,18 @@ class Encoder:
         if self._staged is None:
             raise SeqArcError("fetch(): nothing staged (encode_blocks() fetched its own output; stage() or "
                               "run_input() first)")
+        # (the host buffers are kept for the next fetch: freeing memory the
+        # device-to-host copies page-locked stalls the GPU's queues while other
+        # contexts run -- DESIGN.md, round 5)
+        bufs = self.__dict__.setdefault("_fetch_bufs", [])
         outs, keep = [], []
-        for cap in self._staged:
-            buf = np.empty(cap, dtype=np.uint8)
-            keep.append(buf)
-            outs.append(_SaOut(_ptr(buf), cap, 0))
+        for i, cap in enumerate(self._staged):
+            if i == len(bufs):
+                bufs.append(np.empty(0, dtype=np.uint8))
+            if bufs[i].size < cap:
+                bufs[i] = np.empty(cap + cap // 8, dtype=np.uint8)
+            keep.append(bufs[i])
+            outs.append(_SaOut(_ptr(bufs[i]), cap, 0))
         arr = (_SaOut * max(1, len(outs)))(*outs)
         if self._lib.sa_fetch(self._ctx, arr, len(outs)) != 0:
             self._err("sa_fetch")
