@@ -23,7 +23,7 @@
 //   --host-parse     parse the blocks on host threads (default: on the device, sa_stage_text)
 //   --read-threads N plain-file reader threads (default 8; 0: the per-block window reader)
 //   --writers N      archive writer threads (default 8: page maps at the blocks' offsets; 1: write(2))
-//   --keep-clock 0|1 a companion process holding the GPU's clock while the encoders run (default 1)
+//   --keep-clock 0|1 a companion process holding the GPU's clock while the encoders run (default 0)
 //   --ingest-only    the reader and block cut alone, batches dealt to devices x contexts
 //                    consumers (no device); --ingest-crc: the consumers CRC the texts
 //
@@ -1390,7 +1390,7 @@ struct Options {
          release = false, stage_ahead = false, shm = false, maxmis_set = false, ingest_crc = false;
     int read_threads = 8;   // --read-threads: the plain-file reader's fill threads (SegReader)
     int writers = 8;        // --writers: the archive writer's copy threads (ArcWriter; 1: write(2) in order)
-    int keep_clock = 1;     // --keep-clock: the companion process holding the GPU's clock (ClockKeeper; 0: none)
+    int keep_clock = 0;     // --keep-clock 1: the companion process holding the GPU's clock (ClockKeeper)
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -1695,7 +1695,10 @@ double g_main_s = 0.0;
 // as the encoders run: the chains then ran at 2,356-2,386 MHz instead of
 // 1,685-2,152 (r5l, rv_probe).  It is forked before this process starts a
 // thread or touches a GPU, and ends when its pipe closes (the encoders are
-// done, or this process exits).  --keep-clock 0: none.
+// done, or this process exits).  Off by default since the output pool: with
+// the device pipeline no longer stalled the chains keep the clock busy enough,
+// and the companion's own start-up delayed this process's (r5z3: 42.8 GB in
+// 4.03 / 4.19 s without it against 4.64 / 4.25 with it).  --keep-clock 1: on.
 struct ClockKeeper {
     pid_t pid = -1;
     int wfd = -1;
