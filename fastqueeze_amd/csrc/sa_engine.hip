@@ -269,6 +269,14 @@ struct sa_ctx {
     // of long reads (mean > 1000 bp), whose fronts are VALU-heavy and set the
     // pace, ran 11 % slower with them (r4z5: ONT shape 7,187 / 7,281 against
     // 8,081 / 8,260 MB/s), so those keep 0.  SA_RV_VARIANT=0 / 5: one for all.
+    // Round 6: 6 = the operands through SMEM from a per-wave ring the lanes fill
+    // (k_coder_rv<6>, coder_rg_chain): the chain itself is faster (r6b: one
+    // context alone 504 against 630 ms; under the bench's load 626-644 against
+    // 665-691) but it issues 10 SALU per symbol instead of 8 and holds its SIMD's
+    // scalar issue ~90 % of the time, so the kernels that share those SIMDs
+    // slow (L passes 89 against 52 ms, prep 16 against 10) and the bench lost
+    // 3 % (r6b / r6c: 16,623-16,904 against 17,281-17,493 MB/s).  Off by
+    // default; SA_RV_VARIANT=6 (A/B).
     int rv_variant = std::getenv("SA_RV_VARIANT") ? std::atoi(std::getenv("SA_RV_VARIANT")) : -1;
     int rv_batch = 5;   // the current batch's (run_input)
     // pass R's wait for records the long runs have not written (SA_RV_WAIT_MS, default 20 s: the
@@ -312,6 +320,7 @@ struct sa_ctx {
     const char* rv_probe = std::getenv("SA_RV_PROBE");
     DBuf d_probe;
     uint32_t probe_waves = 0;
+    DBuf d_ring;   // pass R's per-wave operand rings (k_coder_rv<6>)
 
     // the batch sa_stage uploads (sa_run encodes it); blocks = the working copy
     // of the batch being encoded (its symbol spaces filled by plan_batch)
@@ -370,7 +379,7 @@ struct sa_ctx {
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
-                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe, &d_aux_bm,
+                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe, &d_ring, &d_aux_bm,
                 &d_aux_tab, &d_aux_nmod};
     }
     uint64_t held_bytes()
@@ -715,9 +724,9 @@ int coder_list(sa_ctx* c, hipStream_t st, int slot, const std::vector<CoderTask>
 // share rv_short_waves waves (k_coder_rv; SA_RV_SHORT_WAVES=0: a wave per chain)
 constexpr uint32_t RV_LONG_SYMS = 1u << 21;
 
-void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv, int ph, uint32_t nlong)
+int coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv, int ph, uint32_t nlong)
 {
-    if (!tl.count) return;
+    if (!tl.count) return 0;
     uint32_t waves = tl.count;
     tl.nlong = tl.count;
     if (c->rv_short_waves && nlong + c->rv_short_waves < tl.count) {
@@ -730,7 +739,7 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
         hipLaunchKernelGGL(k_coder_rl, dim3((tl.count + 63) / 64), dim3(64 * RL_WAVES), 0, st, cv.tasks, tl, cv.prs[0],
                            cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(), c->chain_prio);
         if (ph >= 0) ev_finish(c, ph, st);
-        return;
+        return 0;
     }
     const uint32_t grid = (waves + c->coder_waves - 1) / c->coder_waves;
     uint64_t* probe = nullptr;
@@ -739,10 +748,20 @@ void coder_launch_r(sa_ctx* c, hipStream_t st, TaskList tl, const CoderView& cv,
         c->probe_waves = grid * c->coder_waves;
         (void)hipMemsetAsync(probe, 0, 32ull * c->probe_waves, st);
     }
-    hipLaunchKernelGGL(c->rv_batch == 5 ? k_coder_rv<5> : k_coder_rv<0>, dim3(grid), dim3(64 * c->coder_waves),
-                       c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1], cv.ck_r, c->d_err.as<uint32_t>(),
-                       c->chain_prio, probe);
+    // (V = 6) a 2 KiB ring per wave, sized for 1024 waves from the start (a
+    // re-allocation's hipFree would synchronise the device)
+    if (c->rv_batch == 6 &&
+        c->d_ring.ensure(4ull * RING_DW * std::max<uint32_t>(1024u, grid * c->coder_waves)) != hipSuccess) {
+        c->err = "pass R: cannot allocate the operand ring";
+        return -1;
+    }
+    hipLaunchKernelGGL(c->rv_batch == 6   ? k_coder_rv<6>
+                       : c->rv_batch == 5 ? k_coder_rv<5>
+                                          : k_coder_rv<0>,
+                       dim3(grid), dim3(64 * c->coder_waves), c->coder_lds, st, cv.tasks, tl, cv.prs[0], cv.prs[1],
+                       cv.ck_r, c->d_err.as<uint32_t>(), c->chain_prio, probe, c->d_ring.as<uint32_t>());
     if (ph >= 0) ev_finish(c, ph, st);
+    return 0;
 }
 
 // SA_RV_PROBE: one line per pass-R wave of this batch: context, batch, wave,
@@ -812,7 +831,7 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         if (coder_list(c, st, 0, tasks, ids, runs, gb, tl)) return -1;
         for (const uint32_t t : ids) nlong += tasks[t].n >= RV_LONG_SYMS ? 1u : 0u;
     }
-    coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1, nlong);
+    if (coder_launch_r(c, st, tl, cv, c->timing ? ph_r : -1, nlong)) return -1;
     if (c->st5) {   // (SA_L_CU_EVERY) the L passes on their own CUs once pass R is done
         SA_CHECK(c, hipEventRecord(c->ev_r_done, st));
         SA_CHECK(c, hipEventSynchronize(c->ev_r_done));
@@ -891,7 +910,7 @@ int coder_run(sa_ctx* c, std::vector<CoderTask>& tasks, CoderView& cv, hipStream
         }
         c->coder_restarts += (uint32_t)ids.size();
         if (coder_list(c, st, 0, tasks, ids, runs, gb, tl)) return -1;
-        coder_launch_r(c, st, tl, cv, -1, 0);
+        if (coder_launch_r(c, st, tl, cv, -1, 0)) return -1;
         coder_launch_l12(c, st, tl, cv);
         coder_launch_l3(c, st, tl, cv);
         SA_CHECK(c, hipGetLastError());
@@ -951,6 +970,8 @@ sa_ctx* sa_create(int device)
         (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)c->coder_lds) != hipSuccess ||
          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<5>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)c->coder_lds) != hipSuccess ||
+         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_coder_rv<6>), hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)c->coder_lds) != hipSuccess)) {
         std::fprintf(stderr, "seqarc_amd: cannot reserve %u B of LDS for pass R\n", c->coder_lds);
         delete c;
@@ -1020,7 +1041,15 @@ sa_ctx* sa_create(int device)
     }
     if (const char* le = std::getenv("SA_L_CU_EVERY")) {
         const int n = std::atoi(le);
-        if (n >= 2) {
+        if (n == 1) {   // (A/B, round 6) the L passes on the front's CUs (all of them without SA_RV_CUS)
+            if ((m_front.empty() ? hipStreamCreateWithFlags(&c->st5, hipStreamNonBlocking)
+                                 : hipExtStreamCreateWithCUMask(&c->st5, (uint32_t)m_front.size(), m_front.data())) !=
+                    hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_r_done, hipEventDisableTiming) != hipSuccess) {
+                delete c;
+                return nullptr;
+            }
+        } else if (n >= 2) {
             std::vector<uint32_t> m_l(m_long.size(), 0u);
             for (int cu = 0; cu < prop.multiProcessorCount; cu++)
                 if (cu % n == n / 2) m_l[cu / 32] |= 1u << (cu % 32);   // (offset: not the long runs' CUs when n = 4)
@@ -1109,73 +1138,6 @@ uint64_t sa_output_bound(const sa_block* b)
 }
 
 }  // extern "C"
-
-// ---- the command line's clock keeper (sa_clock_keeper) ----
-// The firmware lowers the shader clock when few waves are resident (amd-smi's
-// throttle record: the low-utilization flag, 1.0-2.0 GHz while only pass R's
-// chains of the last batches ran; r5b, r5j).  A wave per CU that sleeps keeps
-// the measured activity up without issuing: r5l, the CLI's pass-R chains at
-// 2,356-2,386 MHz beside it against 1,685-2,152 without (rv_probe), the same
-// with FMA-issuing waves (r5k) -- but those delayed the chains on the SIMDs
-// they shared, the sleeping ones do not.
-namespace {
-__global__ void __launch_bounds__(64) k_keep_resident(uint32_t naps)
-{
-    for (uint32_t i = 0; i < naps; i++) __builtin_amdgcn_s_sleep(127);   // (~8k cycles a nap)
-}
-}  // namespace
-
-extern "C" int sa_clock_keeper(const int* devices, int n, int fd)
-{
-    struct Dev {
-        int id;
-        uint32_t cus;
-        hipStream_t st;
-    };
-    std::vector<Dev> ds;
-    for (int i = 0; i < n; i++) {
-        hipDeviceProp_t p;
-        hipStream_t st = nullptr;
-        if (hipSetDevice(devices[i]) != hipSuccess || hipGetDeviceProperties(&p, devices[i]) != hipSuccess ||
-            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
-            continue;
-        ds.push_back(Dev{devices[i], (uint32_t)p.multiProcessorCount, st});
-    }
-    if (ds.empty()) return -1;
-    // (~3 ms per launch at 2.4 GHz; the next launch is queued before the host
-    // thread sleeps on the previous one's event, so the waves stay resident
-    // without a gap)
-    constexpr uint32_t kNaps = 1000;
-    std::vector<hipEvent_t> prev(ds.size(), nullptr);
-    for (;;) {
-        for (size_t i = 0; i < ds.size(); i++) {
-            Dev& d = ds[i];
-            (void)hipSetDevice(d.id);
-            hipLaunchKernelGGL(k_keep_resident, dim3(d.cus), dim3(64), 0, d.st, kNaps);
-            hipEvent_t e = nullptr;
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess ||
-                hipEventRecord(e, d.st) != hipSuccess)
-                return -1;
-            if (prev[i]) {
-                (void)hipEventSynchronize(prev[i]);
-                (void)hipEventDestroy(prev[i]);
-            }
-            prev[i] = e;
-        }
-        char b;
-        const ssize_t r = ::read(fd, &b, 1);   // (fd non-blocking: -1 / EAGAIN while the pipe is open)
-        if (r == 0 || (r < 0 && errno != EAGAIN && errno != EINTR)) break;
-    }
-    for (size_t i = 0; i < ds.size(); i++) {
-        (void)hipSetDevice(ds[i].id);
-        if (prev[i]) {
-            (void)hipEventSynchronize(prev[i]);
-            (void)hipEventDestroy(prev[i]);
-        }
-        (void)hipStreamDestroy(ds[i].st);
-    }
-    return 0;
-}
 
 namespace {
 
@@ -1412,7 +1374,9 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     hipStream_t st = c->st;
     const uint32_t nr = I->nreads;
     FrontShare* F = c->fs;
-    c->rv_batch = c->rv_variant >= 0 ? c->rv_variant : (nr && I->seq_bytes / nr > 1000 ? 0 : 5);   // (see rv_variant)
+    c->rv_batch = c->rv_variant == 0 || c->rv_variant == 5 || c->rv_variant == 6
+                      ? c->rv_variant
+                      : (nr && I->seq_bytes / nr > 1000 ? 0 : 5);   // (see rv_variant)
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
@@ -1888,6 +1852,18 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     return 0;
 }
 
+// A batch that failed part-way (E_CODER, a device error bit, a failed call)
+// may still have work in flight on the context's streams -- e.g. the long-run
+// replay writing d_prs_aux after pass R gave up: the next batch's full memset
+// of that buffer (prs_zero_cap is 0 after a failure) must not race it.
+void drain_after_error(sa_ctx* c)
+{
+    for (hipStream_t s : {c->st, c->st2, c->st3, c->st4, c->st5})
+        if (s) (void)hipStreamSynchronize(s);
+    c->prs_zero_cap = 0;
+    c->prs_zero_pending = false;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1900,6 +1876,7 @@ int sa_run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg)
         for (hipStream_t s : {c->st, c->st2, c->st3, c->st4}) SA_CHECK(c, hipStreamSynchronize(s));
         rc = run_input(c, I, cfg, false);
     }
+    if (rc) drain_after_error(c);
     return rc ? -1 : 0;
 }
 

@@ -1508,7 +1508,10 @@ int sa_run_input_aligned(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, const 
     }
     // any failure ends the chain: the contexts waiting on later batches return
     // an error instead of waiting for this batch forever
-    if (rc) align_chain_fail(chain);
+    if (rc) {
+        align_chain_fail(chain);
+        drain_after_error(c);
+    }
     return rc ? -1 : 0;
 }
 

@@ -2892,6 +2892,163 @@ __device__ __forceinline__ void rv_segment(uint32_t& r, uint32_t cm, uint32_t vt
     }
 }
 
+// ---------------------------------------------------------------------------
+// (round 6) V = 6: the operands reach the scalar unit through SMEM instead of
+// v_readlane.  The lanes derive (m, tf) of segment g+2 from its records and
+// store them to the wave's ring in global memory (4 segment slots, 2 KiB); the
+// chain reads 16 symbols' pairs per group with two s_load_dwordx16 (glc: the
+// scalar cache does not see the vector stores), the next group's loads issued
+// at the start of the current group's steps, so a load has one group's steps
+// (~700 cycles) to return (SMEM returns out of order: every wait is
+// lgkmcnt(0)).  Per symbol the scalar unit issues the step's eight
+// instructions plus the split of tf into t and f: 10 SALU and 1/8 of a load
+// against 8 SALU and three v_readlane (scripts/micro/feed_probe.hip, r6a: 44-45
+// against 50-63 cycles per symbol; the step alone 39).  The two buffers live
+// at fixed SGPRs (A = s[36:67], B = s[68:99]); no code between the groups uses
+// them (tests/test_isa.py checks the compiled kernel).
+constexpr uint32_t RING_SLOT = 2 * SEG_SYMS;   // dwords per segment slot
+constexpr uint32_t RING_DW = 4 * RING_SLOT;    // dwords per wave
+
+#define SA_RG_STEP(M, TF)                                                                                     \
+    "s_and_b32 %[t], " TF ", %[mk]\n\ts_lshr_b32 %[f], " TF ", 16\n\ts_mul_hi_u32 %[q], %[r], " M "\n\t"      \
+    "s_mul_i32 %[p], %[q], %[t]\n\ts_cmp_lt_u32 %[r], %[p]\n\ts_subb_u32 %[q], %[q], 0\n\t"                    \
+    "s_mul_i32 %[q], %[q], %[f]\n\ts_flbit_i32_b32 %[p], %[q]\n\ts_and_b32 %[p], %[p], 24\n\t"                 \
+    "s_lshl_b32 %[r], %[q], %[p]\n\t"
+#define SA_RG_A                                                                                               \
+    SA_RG_STEP("s36", "s37") SA_RG_STEP("s38", "s39") SA_RG_STEP("s40", "s41") SA_RG_STEP("s42", "s43")         \
+    SA_RG_STEP("s44", "s45") SA_RG_STEP("s46", "s47") SA_RG_STEP("s48", "s49") SA_RG_STEP("s50", "s51")         \
+    SA_RG_STEP("s52", "s53") SA_RG_STEP("s54", "s55") SA_RG_STEP("s56", "s57") SA_RG_STEP("s58", "s59")         \
+    SA_RG_STEP("s60", "s61") SA_RG_STEP("s62", "s63") SA_RG_STEP("s64", "s65") SA_RG_STEP("s66", "s67")
+#define SA_RG_B                                                                                               \
+    SA_RG_STEP("s68", "s69") SA_RG_STEP("s70", "s71") SA_RG_STEP("s72", "s73") SA_RG_STEP("s74", "s75")         \
+    SA_RG_STEP("s76", "s77") SA_RG_STEP("s78", "s79") SA_RG_STEP("s80", "s81") SA_RG_STEP("s82", "s83")         \
+    SA_RG_STEP("s84", "s85") SA_RG_STEP("s86", "s87") SA_RG_STEP("s88", "s89") SA_RG_STEP("s90", "s91")         \
+    SA_RG_STEP("s92", "s93") SA_RG_STEP("s94", "s95") SA_RG_STEP("s96", "s97") SA_RG_STEP("s98", "s99")
+#define SA_RG_LOAD_A "s_load_dwordx16 s[36:51], %[nx], 0x0 glc\n\ts_load_dwordx16 s[52:67], %[nx], 0x40 glc\n\t"
+#define SA_RG_LOAD_B "s_load_dwordx16 s[68:83], %[nx], 0x0 glc\n\ts_load_dwordx16 s[84:99], %[nx], 0x40 glc\n\t"
+#define SA_RG_CLOBBER                                                                                         \
+    "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",   \
+        "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", \
+        "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", \
+        "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", \
+        "s96", "s97", "s98", "s99"
+
+__device__ __forceinline__ const uint32_t* wave_ptr(const uint32_t* p)
+{
+    const uint64_t x = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return (const uint32_t*)((uint64_t)hi << 32 | lo);
+}
+// the first group of a segment into buffer A
+__device__ __forceinline__ void rg_first(const uint32_t* p)
+{
+    asm volatile("; sa_rg_first\n\t" SA_RG_LOAD_A ::[nx] "s"(wave_ptr(p)) : "memory", SA_RG_CLOBBER);
+}
+// every load in (before code that may use the buffers' registers)
+__device__ __forceinline__ void rg_drain()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\t; sa_rg_drained" ::: "memory", SA_RG_CLOBBER);
+}
+// one group: buffer A (ODD = 0) or B coded while the other one loads from nx
+template <int ODD>
+__device__ __forceinline__ void rg_group(uint32_t& r, const uint32_t* nx, const uint32_t tmask)
+{
+    uint32_t q, p, t, f;
+    if constexpr (ODD == 0)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\t" SA_RG_LOAD_B SA_RG_A
+                     : [r] "+s"(r), [q] "=&s"(q), [p] "=&s"(p), [t] "=&s"(t), [f] "=&s"(f)
+                     : [nx] "s"(wave_ptr(nx)), [mk] "s"(tmask)
+                     : "scc", SA_RG_CLOBBER);
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\t" SA_RG_LOAD_A SA_RG_B
+                     : [r] "+s"(r), [q] "=&s"(q), [p] "=&s"(p), [t] "=&s"(t), [f] "=&s"(f)
+                     : [nx] "s"(wave_ptr(nx)), [mk] "s"(tmask)
+                     : "scc", SA_RG_CLOBBER);
+}
+#undef SA_RG_STEP
+#undef SA_RG_A
+#undef SA_RG_B
+#undef SA_RG_LOAD_A
+#undef SA_RG_LOAD_B
+
+// the lanes' part: segment g's (m, tf) pairs into its slot
+__device__ __forceinline__ void rg_put(uint32_t* R, uint32_t g, uint32_t ctf, uint32_t tmask)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    *reinterpret_cast<uint2*>(R + (g & 3) * RING_SLOT + 2 * lane) = make_uint2(recip32z(ctf & tmask), ctf);
+}
+
+__device__ __forceinline__ void coder_rg_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
+                                               const TaskList& tl, const PRec* __restrict__ prs0,
+                                               const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r,
+                                               uint32_t* __restrict__ err, const uint32_t prio, uint32_t* R)
+{
+    typedef const __attribute__((address_space(1))) uint32_t g_u32;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t t = tl.ids[li];
+    const CoderTask tk = tasks[t];
+    const CoderRun run = tl.run[li];
+    const PRec* P = (tk.space ? prs1 : prs0) + tk.rec_base;
+    g_u32* G = (g_u32*)(P) + lane;
+    const uint32_t tmask = tk.space ? 0xffffu : 0xffu;   // wide AUX / packed SEQ records
+    uint32_t* ck = ck_r + tk.seg_base;
+    const uint32_t first = run.start_seg, last = tk.nseg - 1;
+    uint32_t r = run.r0;
+    uint32_t g = first;
+    uint32_t kv = 0;
+    set_chain_prio(prio);
+    if (g < last) {
+        uint32_t bad = 0;
+        // buf[j] holds the records of a segment = j (mod CODER_LA), loaded
+        // CODER_LA - 2 segments before the lanes put it into the ring
+        uint32_t buf[CODER_LA];
+#pragma unroll
+        for (uint32_t k = 0; k < CODER_LA; k++) buf[k] = G[(size_t)min(g + k, last) * SEG_SYMS];
+        rg_put(R, g, buf[0], tmask);
+        rg_put(R, g + 1, buf[1], tmask);
+        buf[0] = G[(size_t)min(g + CODER_LA, last) * SEG_SYMS];
+        buf[1] = G[(size_t)min(g + CODER_LA + 1, last) * SEG_SYMS];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rg_first(R + (g & 3) * RING_SLOT);
+        for (; g < last;) {
+#pragma unroll
+            for (uint32_t k = 0; k < CODER_LA; k++) {
+                if (g >= last) break;
+                const uint32_t kk = (k + 2) % CODER_LA;
+                rg_put(R, g + 2, buf[kk], tmask);
+                buf[kk] = G[(size_t)min(g + 2 + CODER_LA, last) * SEG_SYMS];
+                kv = lane == (g & 63) ? r : kv;
+                if ((g & 63) == 63) {
+                    const uint32_t s = g - 63 + lane;
+                    if (s >= first) ck[s] = kv;
+                }
+                r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+                const uint32_t r_seg = r;
+                // segment g+1's slot (stored one segment ago) is in L2 before its
+                // first group is loaded at the end of this segment: younger than
+                // that store are at least this segment's store and load
+                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                const uint32_t* cur = R + (g & 3) * RING_SLOT;
+                rg_group<0>(r, cur + 32, tmask);
+                rg_group<1>(r, cur + 64, tmask);
+                rg_group<0>(r, cur + 96, tmask);
+                rg_group<1>(r, R + ((g + 1) & 3) * RING_SLOT, tmask);
+                if (r == 0) {   // (records not in yet: seg_retry's own code may use the buffers' registers)
+                    rg_drain();
+                    r = seg_retry(P + (size_t)g * SEG_SYMS, r_seg, tmask, bad, tl.wait_ticks);
+                    rg_first(R + ((g + 1) & 3) * RING_SLOT);
+                }
+                g++;
+            }
+        }
+        rg_drain();
+        if (bad && lane == 0) atomicOr(err, (uint32_t)E_CODER);
+    }
+    kv = lane == (g & 63) ? r : kv;
+    const uint32_t s = (g & ~63u) + lane;
+    if (s >= first && s <= g) ck[s] = kv;
+}
+
 template <int V>
 __device__ __forceinline__ void coder_rv_chain(const uint32_t li, const CoderTask* __restrict__ tasks,
                                                const TaskList& tl, const PRec* __restrict__ prs0,
@@ -2959,7 +3116,7 @@ template <int V>
 __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const CoderTask* __restrict__ tasks, const TaskList tl, const PRec* __restrict__ prs0,
     const PRec* __restrict__ prs1, uint32_t* __restrict__ ck_r, uint32_t* __restrict__ err, const uint32_t prio,
-    uint64_t* __restrict__ probe)
+    uint64_t* __restrict__ probe, uint32_t* __restrict__ ring)
 {
     const uint32_t wpg = blockDim.x >> 6;
     const uint32_t wi = blockIdx.x * wpg + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -2974,7 +3131,8 @@ __global__ __launch_bounds__(64 * CODER_MAX_WAVES) void k_coder_rv(
     const uint32_t step = wi < nl ? 0u : gridDim.x * wpg - nl;
     uint32_t chains = 0;
     for (uint32_t li = wi; li < tl.count;) {
-        coder_rv_chain<V>(li, tasks, tl, prs0, prs1, ck_r, err, prio);
+        if constexpr (V == 6) coder_rg_chain(li, tasks, tl, prs0, prs1, ck_r, err, prio, ring + (size_t)wi * RING_DW);
+        else coder_rv_chain<V>(li, tasks, tl, prs0, prs1, ck_r, err, prio);
         chains++;
         if (!step) break;
         li += step;

@@ -23,7 +23,6 @@
 //   --host-parse     parse the blocks on host threads (default: on the device, sa_stage_text)
 //   --read-threads N plain-file reader threads (default 8; 0: the per-block window reader)
 //   --writers N      archive writer threads (default 8: page maps at the blocks' offsets; 1: write(2))
-//   --keep-clock 0|1 a companion process holding the GPU's clock while the encoders run (default 0)
 //   --ingest-only    the reader and block cut alone, batches dealt to devices x contexts
 //                    consumers (no device); --ingest-crc: the consumers CRC the texts
 //
@@ -47,7 +46,6 @@
 #include <string.h>
 #include <signal.h>
 #include <sys/mman.h>
-#include <sys/prctl.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
@@ -79,7 +77,7 @@ int usage()
             "usage: seqarc_amd -c [-t N] [-l R] [-n] [-f] [-p] -1 A.fq[.gz] [-2 B.fq[.gz]] (-o OUT | OUT)\n"
             "                  [--slevel K] [--qlevel Q] [--devices N] [--contexts K] [--batch BLOCKS]\n"
             "                  [--block-size MiB] [--device D] [--share-device] [--ramp] [--release]\n"
-            "                  [--stage-ahead] [--writers N] [--keep-clock 0|1] [--read-threads N]\n"
+            "                  [--stage-ahead] [--writers N] [--read-threads N]\n"
             "       seqarc_amd -d [-t N] [-f] [-p] [-P 1|2|3] [ref.fa] ARCHIVE.arc [PREFIX] [-o PREFIX]\n"
             "       seqarc_amd -i ref.fa            (HASH index: ref.fa.hash + ref.fa.md5)\n"
             "       (-s with -i / -c / -d and ref.fa: the index image in /dev/shm/<ref file name>)\n"
@@ -193,6 +191,9 @@ struct Buf {
     bool pinned = false;
     bool external = false;   // d belongs to an arena (TextPool): never freed here
     bool huge = false;       // (set while empty) 2 MiB-aligned with the huge-page hint (OutPool)
+    // how d was allocated (its allocator frees it, whatever the flags above ask
+    // of the next allocation)
+    enum Kind : uint8_t { K_NEW, K_ALIGNED, K_PINNED } kind = K_NEW;
     Buf() = default;
     Buf(const Buf&) = delete;
     Buf& operator=(const Buf&) = delete;
@@ -214,6 +215,7 @@ struct Buf {
         pinned = o.pinned;
         external = o.external;
         huge = o.huge;
+        kind = o.kind;
         o.d = nullptr;
         o.n = o.cap = 0;
         o.external = false;
@@ -222,23 +224,26 @@ struct Buf {
     {
         if (c <= cap) return;
         T* nd = pinned ? static_cast<T*>(sa_host_alloc(c * sizeof(T))) : nullptr;
-        const bool got_pinned = nd != nullptr;
+        Kind nk = K_PINNED;
         if (!nd && huge) {
             void* q = nullptr;
             if (posix_memalign(&q, 2u << 20, c * sizeof(T)) == 0) {
                 (void)madvise(q, c * sizeof(T), MADV_HUGEPAGE);
                 nd = static_cast<T*>(q);
-            } else {
-                huge = false;
+                nk = K_ALIGNED;
             }
         }
-        if (!nd) nd = new T[c];   // (pageable when page-locked memory runs out: staging is then a slower copy)
+        if (!nd) {   // (pageable when page-locked memory runs out: staging is then a slower copy)
+            nd = new T[c];
+            nk = K_NEW;
+        }
         if (n) memcpy(nd, d, n * sizeof(T));
-        free_(d);
+        free_(d);   // (with the old buffer's own allocator)
         d = nd;
+        kind = nk;
         cap = c;
         external = false;
-        pinned = got_pinned;
+        pinned = nk == K_PINNED;
     }
     void resize(size_t c)
     {
@@ -248,8 +253,8 @@ struct Buf {
     void free_(T* p)
     {
         if (!p || external) return;
-        if (pinned) sa_host_free(p);
-        else if (huge) free(p);
+        if (kind == K_PINNED) sa_host_free(p);
+        else if (kind == K_ALIGNED) free(p);
         else delete[] p;
     }
     void release()
@@ -1211,8 +1216,8 @@ public:
         std::lock_guard<std::mutex> g(mu_);
         if (mapped_ && end > size_) {   // (grown a GiB at a time; cut to the archive's size in finish)
             const uint64_t s = std::max<uint64_t>(end, size_ + (1ull << 30));
-            if (ftruncate(fd_, (off_t)s) != 0) bad_ = true;
-            size_ = s;
+            if (ftruncate(fd_, (off_t)s) == 0) size_ = s;   // (else the copies past size_ use pwrite: no map past EOF)
+            else bad_ = true;
         }
         end_ = end;
         q_.emplace_back(std::move(j), off);
@@ -1268,10 +1273,14 @@ private:
         }
         return true;
     }
+    // A block is copied into a map of its pages only where fallocate has
+    // allocated them (alloc_upto_ <= size_): a store to a page the file system
+    // cannot back (disk full, quota) raises SIGBUS and would kill the process
+    // with a partial archive; everywhere else pwrite, whose errors are reported.
     bool copy(const uint8_t* p, size_t n, uint64_t off)
     {
         if (!n) return true;
-        if (!mapped_) return put_at(p, n, off);
+        if (!mapped_ || off + n > alloc_upto_.load()) return put_at(p, n, off);
         static const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
         const uint64_t a = off & ~(pg - 1), len = off + n - a;
         void* m = mmap(nullptr, len, PROT_WRITE, MAP_SHARED, fd_, (off_t)a);
@@ -1309,8 +1318,11 @@ private:
                 if (stop_) return;
                 to = std::min(std::min(end_ + kAhead, size_), at + kStep);
             }
-            if (fallocate(fd_, FALLOC_FL_KEEP_SIZE, (off_t)at, (off_t)(to - at)) != 0) return;   // (unsupported: the copies fault)
+            // (a failure -- no space, a quota, unsupported -- ends the allocation:
+            // the copies past alloc_upto_ then write with pwrite and report errors)
+            if (fallocate(fd_, FALLOC_FL_KEEP_SIZE, (off_t)at, (off_t)(to - at)) != 0) return;
             at = to;
+            alloc_upto_ = at;
         }
     }
     int fd_ = -1;
@@ -1320,6 +1332,7 @@ private:
     std::condition_variable cv_;
     std::deque<std::pair<std::unique_ptr<Job>, uint64_t>> q_;
     uint64_t size_ = 0, end_ = 0;
+    std::atomic<uint64_t> alloc_upto_{0};   // bytes of the file fallocate has allocated (from 0)
     bool stop_ = false;
     std::atomic<bool> bad_{false};
     std::vector<std::thread> pool_;
@@ -1390,7 +1403,6 @@ struct Options {
          release = false, stage_ahead = false, shm = false, maxmis_set = false, ingest_crc = false;
     int read_threads = 8;   // --read-threads: the plain-file reader's fill threads (SegReader)
     int writers = 8;        // --writers: the archive writer's copy threads (ArcWriter; 1: write(2) in order)
-    int keep_clock = 0;     // --keep-clock 1: the companion process holding the GPU's clock (ClockKeeper)
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
     sa_cfg cfg{3, 2, 1, 0, 0.0};
@@ -1685,60 +1697,6 @@ double g_main_s = 0.0;
     std::_Exit(rc);
 }
 
-// The GPU's clock under the latency-bound phases (round-5 VERDICT item 2).
-// amd-smi's throttle record names the limiter: the firmware's activity-based
-// clock control (its low-utilization flag) lowered the shader clock to
-// 1.0-2.0 GHz while few waves were resident -- the phases where only the last
-// batches' pass-R chains, MD5 and long runs run (r5b, r5j) -- and pass R, a
-// dependent chain, slowed with it.  A companion process keeps one sleeping
-// wave per CU resident (sa_clock_keeper: the waves issue nothing) for as long
-// as the encoders run: the chains then ran at 2,356-2,386 MHz instead of
-// 1,685-2,152 (r5l, rv_probe).  It is forked before this process starts a
-// thread or touches a GPU, and ends when its pipe closes (the encoders are
-// done, or this process exits).  Off by default since the output pool: with
-// the device pipeline no longer stalled the chains keep the clock busy enough,
-// and the companion's own start-up delayed this process's (r5z3: 42.8 GB in
-// 4.03 / 4.19 s without it against 4.64 / 4.25 with it).  --keep-clock 1: on.
-struct ClockKeeper {
-    pid_t pid = -1;
-    int wfd = -1;
-    void start(const std::vector<int>& devs)
-    {
-        int p[2];
-        if (devs.empty() || pipe(p) != 0) return;
-        const pid_t c = fork();
-        if (c < 0) {
-            close(p[0]);
-            close(p[1]);
-            return;
-        }
-        if (c == 0) {   // the keeper: no output, gone with its parent
-            close(p[1]);
-            (void)prctl(PR_SET_PDEATHSIG, SIGKILL);
-            if (getppid() == 1) _exit(0);
-            const int nul = ::open("/dev/null", O_RDWR);
-            if (nul >= 0) {
-                dup2(nul, 0);
-                dup2(nul, 1);
-                dup2(nul, 2);
-                close(nul);
-            }
-            (void)fcntl(p[0], F_SETFL, O_NONBLOCK);
-            _exit(sa_clock_keeper(devs.data(), (int)devs.size(), p[0]) == 0 ? 0 : 1);
-        }
-        close(p[0]);
-        (void)fcntl(p[1], F_SETFD, FD_CLOEXEC);
-        pid = c;
-        wfd = p[1];
-    }
-    void stop()
-    {
-        if (wfd >= 0) close(wfd);   // (the keeper sees end of file and ends)
-        wfd = -1;
-    }
-    ~ClockKeeper() { stop(); }
-};
-
 int compress(const Options& o)
 {
     const auto t_start = std::chrono::steady_clock::now();
@@ -1752,13 +1710,6 @@ int compress(const Options& o)
             fprintf(stderr, "Error:The Src file %s may be not exist or empty!\n", f);
             return 1;
         }
-    }
-    ClockKeeper keeper;
-    if (o.keep_clock && !o.host_only && !o.ingest_only) {
-        std::vector<int> devs;
-        for (int d = 0; d < (o.share_device ? 1 : o.devices); d++) devs.push_back(o.device + d);
-        keeper.start(devs);
-        if (o.verbose && keeper.pid > 0) fprintf(stderr, "seqarc_amd: clock keeper pid %d\n", (int)keeper.pid);
     }
     if (!in1.open(o.f1) || (pe && !in2.open(o.f2))) {
         fprintf(stderr, "seqarc_amd: cannot open the input\n");
@@ -1897,6 +1848,9 @@ int compress(const Options& o)
         fprintf(stderr, "seqarc_amd: %s\n", ctx_err.c_str());
         return 1;
     }
+    if (!early_read && !o.host_only && !o.ingest_only && (int64_t)ctxs.size() != (int64_t)o.contexts * o.devices)
+        fprintf(stderr, "seqarc_amd: warning: %zu of %lld encoder contexts created\n", ctxs.size(),
+                (long long)o.contexts * o.devices);
     int64_t B = std::max(1, o.batch);
     // (the contexts the options ask for: with early_read they do not exist yet)
     const int64_t C = early_read ? (int64_t)o.contexts * (o.host_only ? 1 : o.devices) : (int64_t)ctxs.size();
@@ -2204,6 +2158,11 @@ int compress(const Options& o)
         if (create_contexts()) {
             reserve();
             t_ctx = now_s();
+            // (B, the ring and the in-flight bound were sized for C contexts
+            // before they existed: fewer only cost pace, but say so)
+            if ((int64_t)ctxs.size() != C)
+                fprintf(stderr, "seqarc_amd: warning: %zu of %lld encoder contexts created\n", ctxs.size(),
+                        (long long)C);
         } else {
             fail(ctx_err);
         }
@@ -2459,7 +2418,14 @@ int compress(const Options& o)
                         outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
                     }
                     if (!ctx) {   // --host-only
-                        for (sa_out& x : outs) x.size = 0;
+                        // (tests: SA_CLI_TEST_OUT=n gives each block n bytes of filler, so the
+                        // archive writer runs without a device)
+                        static const uint64_t test_out =
+                            std::getenv("SA_CLI_TEST_OUT") ? std::strtoull(std::getenv("SA_CLI_TEST_OUT"), nullptr, 10) : 0;
+                        for (sa_out& x : outs) {
+                            x.size = std::min<uint64_t>(test_out, x.cap);
+                            if (x.size) memset(x.data, 0x5a, x.size);
+                        }
                     } else if (chain) {   // (the batch's place in the chain: k)
                         if (sa_stage(ctx, in.data(), (int)in.size()) != 0 ||
                             sa_run_aligned(ctx, &c, &acfg[ctx], chain, (uint64_t)k) != 0 ||
@@ -2533,7 +2499,6 @@ int compress(const Options& o)
     reader.join();
     for (auto& t : parsers) t.join();
     for (auto& t : encoders) t.join();
-    keeper.stop();
     if (seg_free.joinable()) {
         {
             std::lock_guard<std::mutex> g(mu);
@@ -2926,7 +2891,6 @@ int main(int argc, char** argv)
         else if (!strcmp(a, "--ingest-crc")) o.ingest_crc = true;
         else if (!strcmp(a, "--read-threads")) { if (!ival(o.read_threads, 0)) return usage(); }
         else if (!strcmp(a, "--writers")) { if (!ival(o.writers, 1)) return usage(); }
-        else if (!strcmp(a, "--keep-clock")) { if (!ival(o.keep_clock, 0)) return usage(); }
         else if (!strcmp(a, "--no-ramp")) o.ramp = false;
         else if (!strcmp(a, "--ramp")) o.ramp = true;
         else if (!strcmp(a, "--release")) o.release = true;

@@ -114,15 +114,6 @@ int sa_stage_text(sa_ctx *ctx, const sa_text_block *in, int n, sa_text_info *inf
  * asked for, registered portable with the runtime); free with sa_host_free */
 void *sa_host_alloc(uint64_t bytes);
 void sa_host_free(void *p);
-/* The GPU's clock under latency-bound phases (no reference counterpart: the
- * command line's companion process, seqarc_cli.cpp).  Keeps one sleeping wave
- * per CU resident on each of the n devices -- waves that issue nothing, so the
- * firmware's activity-based clock control does not lower the shader clock
- * while only pass R's chains run -- relaunched every few ms until fd (a
- * non-blocking pipe read end) reports end of file.  Must run in a process of
- * its own: a kernel that stays resident holds up the caller's streams that
- * share its hardware queue.  0, or -1 when no device could be used. */
-int sa_clock_keeper(const int *devices, int n, int fd);
 int sa_run(sa_ctx *ctx, const sa_cfg *cfg);                /* encode the staged batch */
 int sa_fetch(sa_ctx *ctx, sa_out *out, int n);             /* D2H of the encaps     */
 /* per-phase device time (ms) of the last sa_run, measured with HIP events on

@@ -332,3 +332,63 @@ def test_gzip_ingest_plain_multimember_bgzf(tmp_path, capsys):
         assert r.returncode != 0, k
     with capsys.disabled():
         print("\n[ingest] " + ", ".join(f"{k} {v[3]:.0f} MB/s" for k, v in got.items()))
+
+
+def test_ingest_ring_at_its_floor(tmp_path):
+    """The segment ring at its floor: a batch's blocks keep
+    their segments until the batch is taken, so a ring smaller than one batch of
+    windows plus two segments deadlocks (r5i, fixed in be7581d by the floor in
+    SegReader::start).  4 MiB segments, 1 MiB blocks (576 KiB windows per file),
+    32-block batches spanning four segments of each file, six consumers,
+    SA_CLI_RING_SEGS=3 (clamped up to the floor, 7): the run ends in bounded
+    time and delivers the same text (CRC-32 over the blocks in order) as an
+    unconstrained ring.  (Checked when written: the same command with the
+    floor removed from the build hangs.)"""
+    a, b = synth.generate(60_000, paired=True, seed=66)
+    p1, p2 = tmp_path / "r_1.fq", tmp_path / "r_2.fq"
+    p1.write_bytes(a)
+    p2.write_bytes(b)
+    crcs = {}
+    for name, env in (("floor", {"SA_CLI_SEG_SLICES": "1", "SA_CLI_RING_SEGS": "3"}), ("default", {})):
+        r = subprocess.run([EXE, "-c", "-f", "--ingest-only", "--ingest-crc", "--devices", "2", "--contexts", "3",
+                            "--batch", "32", "--block-size", "1", "-1", str(p1), "-2", str(p2), "-o",
+                            str(tmp_path / name)], capture_output=True, cwd=tmp_path, timeout=120,
+                           env=dict(os.environ, **env))
+        assert r.returncode == 0, (name, r.stderr)
+        err = r.stderr.decode()
+        crcs[name] = ([ln for ln in err.splitlines() if "crc32" in ln][0].split()[-1],
+                      [ln for ln in err.splitlines() if "block(s)" in ln][0].split()[1])
+    assert crcs["floor"] == crcs["default"]
+    assert crcs["floor"][1] == str(len(fq.cut_pe(a, b, 1 << 20)))
+
+
+def test_archive_writer_reports_a_full_file_system(tmp_path):
+    """The archive writer (ArcWriter) copies blocks into maps of the file's
+    pages only where fallocate allocated them; elsewhere it uses pwrite.  A
+    store into a page the file system cannot back raises SIGBUS (the
+    process died silently with a partial archive); here the file cannot grow
+    past RLIMIT_FSIZE (ftruncate / pwrite fail with EFBIG, SIGXFSZ ignored):
+    the run must end with "write error" and a non-zero status, not a signal.
+    The blocks are SA_CLI_TEST_OUT bytes of filler (--host-only: no device)."""
+    import resource
+    import signal
+    a, b = synth.generate(20_000, paired=True, seed=67)
+    p1, p2 = tmp_path / "w_1.fq", tmp_path / "w_2.fq"
+    p1.write_bytes(a)
+    p2.write_bytes(b)
+    nblk = len(fq.cut_pe(a, b, 1 << 20))
+    args = [EXE, "-c", "-f", "--host-only", "--block-size", "1", "-1", str(p1), "-2", str(p2)]
+    env = dict(os.environ, SA_CLI_TEST_OUT="200000")
+    ok = subprocess.run(args + ["-o", str(tmp_path / "ok")], capture_output=True, cwd=tmp_path, timeout=120, env=env)
+    assert ok.returncode == 0, ok.stderr
+    arc = (tmp_path / "ok.arc").read_bytes()
+    assert arc[16:16 + nblk * 200000] == b"\x5a" * (nblk * 200000)
+
+    def limit():
+        signal.signal(signal.SIGXFSZ, signal.SIG_IGN)
+        resource.setrlimit(resource.RLIMIT_FSIZE, (600_000, 600_000))
+
+    r = subprocess.run(args + ["-o", str(tmp_path / "full")], capture_output=True, cwd=tmp_path, timeout=120,
+                       env=env, preexec_fn=limit)
+    assert r.returncode == 1, (r.returncode, r.stderr)
+    assert b"write error" in r.stderr, r.stderr
