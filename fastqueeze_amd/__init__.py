@@ -117,6 +117,7 @@ def load_library(path: str | None = None):
         "sa_decode_block": ([P, U64, P, P, I32, P], I64),
         "sa_host_register": ([P, U64], I32), "sa_host_unregister": ([P], I32),
         "sa_stage_text": ([P, P, I32, P], I32), "sa_host_alloc": ([U64], P), "sa_host_free": ([P], None),
+        "sa_text_upload": ([P, P, I32, I32, I32, P, U64], I32), "sa_text_parse": ([P, P, I32, P, I32, U64, P], I32),
         "sa_hash_build": ([P, P, U64, C.c_uint32, C.c_uint32, C.c_uint32], P),
         "sa_hash_file_bytes": ([P], U64), "sa_hash_serialize": ([P, P, P, U64], I32),
         "sa_hash_genome_length": ([P], C.c_uint32), "sa_hash_destroy": ([P], None),
@@ -314,6 +315,30 @@ class Encoder:
         if self._lib.sa_stage_text(self._ctx, arr, len(keep), info) != 0:
             self._staged = None
             self._err("sa_stage_text")
+        self._staged = [int(info[i].out_bound) for i in range(len(keep))]
+        return [{"nreads": int(info[i].nreads), "len_long": int(info[i].len_long),
+                 "name_bytes": int(info[i].name_bytes), "seq_bytes": int(info[i].seq_bytes)} for i in range(len(keep))]
+
+    def stage_text_streamed(self, texts, slot: int = 0, stride: int | None = None) -> list[dict]:
+        """sa_text_upload block by block into text arena `slot`, then
+        sa_text_parse: what the command line does as its reader cuts blocks.
+        Returns per-block counts as stage_text does."""
+        keep = [(_as_u8(a), None if b is None else _as_u8(b)) for a, b in texts]
+        if stride is None:
+            stride = max([a.size for a, _ in keep] + [0 if b is None else b.size for _, b in keep] + [1])
+        dummy = np.zeros(1, np.uint8)
+        blks = [_SaTextBlock(_ptr(a) or dummy.ctypes.data, a.size,
+                             None if b is None else (_ptr(b) or dummy.ctypes.data), 0 if b is None else b.size)
+                for a, b in keep]
+        for i, tb in enumerate(blks):
+            if self._lib.sa_text_upload(self._ctx, None, slot, i, len(blks), C.byref(tb), stride) != 0:
+                self._staged = None
+                self._err("sa_text_upload")
+        arr = (_SaTextBlock * max(1, len(blks)))(*blks)
+        info = (_SaTextInfo * max(1, len(keep)))()
+        if self._lib.sa_text_parse(self._ctx, None, slot, arr, len(keep), stride, info) != 0:
+            self._staged = None
+            self._err("sa_text_parse")
         self._staged = [int(info[i].out_bound) for i in range(len(keep))]
         return [{"nreads": int(info[i].nreads), "len_long": int(info[i].len_long),
                  "name_bytes": int(info[i].name_bytes), "seq_bytes": int(info[i].seq_bytes)} for i in range(len(keep))]

@@ -172,11 +172,12 @@ struct sa_input {
     // sa_stage_text: the texts and the device parse's scratch (sa_parse.hip)
     DBuf d_text, d_tile_text, d_tile_cnt, d_tile_base, d_ptexts, d_ntiles, d_text_nl, d_pblocks, d_btot, d_perr, d_nl,
         d_src;
+    DBuf d_text_b;   // (round 6) the second text arena of sa_text_upload / sa_text_parse (slot 1)
     ~sa_input()
     {
         for (DBuf* b : {&d_names, &d_seq, &d_qual, &d_read_block, &d_name_off, &d_name_len, &d_seq_off, &d_seq_len,
                         &d_text, &d_tile_text, &d_tile_cnt, &d_tile_base, &d_ptexts, &d_ntiles, &d_text_nl, &d_pblocks,
-                        &d_btot, &d_perr, &d_nl, &d_src})
+                        &d_btot, &d_perr, &d_nl, &d_src, &d_text_b})
             b->release();
     }
 };
@@ -193,6 +194,11 @@ struct sa_ctx {
     // on its stream (st3).
     hipStream_t st5 = nullptr;
     hipEvent_t ev_r_done = nullptr;
+    // (round 6) sa_text_upload's copies: a stream of their own, made on first
+    // use (from whichever thread uploads), so the next batch's texts go to the
+    // device while this context's kernels run
+    hipStream_t st_copy = nullptr;
+    std::mutex copy_mu;
     // the dense AUX sort (k_aux_presence / k_aux_dense: one 9-bit pass over the
     // blocks' dense model ids instead of two over the 17-bit ids).  The emit's
     // target buffer depends on the number of passes, so the batch follows this
@@ -415,6 +421,7 @@ struct sa_ctx {
         if (st3) (void)hipStreamDestroy(st3);
         if (st4) (void)hipStreamDestroy(st4);
         if (st5) (void)hipStreamDestroy(st5);
+        if (st_copy) (void)hipStreamDestroy(st_copy);
         if (ev_r_done) (void)hipEventDestroy(ev_r_done);
         if (ev_dense) (void)hipEventDestroy(ev_dense);
         if (h_aux_nmod) (void)hipHostFree(h_aux_nmod);

@@ -597,6 +597,22 @@ template <bool PACKED, uint32_t CH = RC_CHUNK, class Fn>
 SA_HD void seg_for_each(const PRec* P, const uint16_t* cum, uint32_t n, Fn&& fn)
 {
     const uint32_t tmask = PACKED ? 0xffu : 0xffffu;
+    if (n == SEG_SYMS) {   // (round 6) a full segment -- all but a stream's last: no per-symbol bound test
+#pragma unroll 1
+        for (uint32_t b = 0; b < SEG_SYMS; b += CH) {
+            PRec p[CH];
+            uint32_t c[PACKED ? 1 : CH];
+#pragma unroll
+            for (uint32_t k = 0; k < CH; k++) {
+                p[k] = P[b + k];
+                if constexpr (!PACKED) c[k] = cum[b + k];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < CH; k++)
+                fn(p[k], recip32z(p[k].tf & tmask), PACKED ? (p[k].tf >> 8) & 0xffu : c[PACKED ? 0 : k]);
+        }
+        return;
+    }
     for (uint32_t b = 0; b < n; b += CH) {
         PRec p[CH];
         uint32_t c[PACKED ? 1 : CH];
@@ -906,25 +922,78 @@ struct RbInfo {
     uint32_t last_start;   // start (chunk offset) of the run open at the chunk's end
 };
 
+// round(sqrt(n)) for n <= 255 * 255 without a loop: the float root (n and
+// its root are exact in a float's mantissa; v_sqrt_f32 may be off by an ulp)
+// corrected in integers -- equal to rb_round_sqrt (tests/cpu_emu checks every n)
+SA_HD uint32_t rb_round_sqrt_fast(uint32_t n)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t g = (uint32_t)__builtin_amdgcn_sqrtf((float)n);   // (v_sqrt_f32 alone: n is no denormal)
+#else
+    uint32_t g = (uint32_t)__builtin_sqrtf((float)n);
+#endif
+    g -= g * g > n ? 1u : 0u;
+    g += (g + 1) * (g + 1) <= n ? 1u : 0u;
+    return n > g * g + g ? g + 1 : g;
+}
+
+// rb_extend with selects instead of branches: true if c extends the open run
+// (its min / max updated), false if the run closes before c (then s holds the
+// run of c alone, start left to the caller)
+SA_HD bool rb_extend_sel(RbRun& s, uint32_t c, const RbTab& t)
+{
+    const uint32_t mn = s.mn, mx = s.mx;
+    const bool bl = rb_tab_bit(t.lo, c, mx), bh = rb_tab_bit(t.hi, c, mn);
+    const bool ext = c > mx ? bh : (c >= mn || bl);
+    s.mn = ext && c > mn ? mn : c;
+    s.mx = ext && c < mx ? mx : c;
+    return ext;
+}
+
 // Speculative pass (rb_spec) recording run values: vals = the chunk's
 // RB_CHUNK bytes, vals[s] = the value of the run starting at s if it closes in
 // the chunk.  The speculative pass opens a run at byte 0, so no run enters.
+// (Round 6: every lane of a wave walks RB_CHUNK bytes in step, 16 per load --
+// past its chunk's end a lane's state stays as it is -- and each byte is one
+// straight sequence of selects: the round-5 walk branched per byte on the run
+// decision and looped rb_round_sqrt's 16 steps at every close, in divergent
+// lanes, and k_rb_spec took most of the ONT front.)
 SA_HD RbRun rb_spec_vals(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_t* opens, uint8_t* vals,
                          RbInfo& info)
 {
     RbRun s{ck.base, q[ck.base], q[ck.base]};
     uint32_t w = 1u;   // a run opens at the chunk's first byte
-    rb_for_bytes(q, ck.base, 1, ck.len, [&](uint32_t i, uint32_t c) {
-        if (!rb_extend(s, c, R)) {
-            vals[s.start - ck.base] = (uint8_t)rb_round_sqrt(s.mn * s.mx);
-            s = RbRun{ck.base + i, c, c};
-            w |= 1u << (i & 31);
+    const uint32_t len = ck.len;
+    for (uint32_t i0 = 0; i0 < RB_CHUNK; i0 += 16) {
+        uint32_t x[4];
+        // (a lane past its chunk's end reads its chunk's first line again: in bounds)
+        const uint8_t* p = q + ck.base + (i0 < len ? i0 : 0u);
+        if (((ck.base + i0) & 15) == 0 && i0 + 16 <= len) {
+            __builtin_memcpy(x, __builtin_assume_aligned(p, 16), 16);
+        } else {
+            for (uint32_t j = 0; j < 4; j++) x[j] = 0;
+            for (uint32_t j = 0; j < 16; j++)
+                if (i0 + j < len) x[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
         }
-        if ((i & 31) == 31) { opens[i >> 5] = w; w = 0; }
-        return true;
-    });
-    if ((ck.len & 31) != 0) opens[(ck.len - 1) >> 5] = w;
-    for (uint32_t k = (ck.len + 31) >> 5; k < RB_WORDS; k++) opens[k] = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++) {
+            const uint32_t i = i0 + j;
+            const uint32_t c = (x[j >> 2] >> (8 * (j & 3))) & 0xffu;
+            const bool live = i >= 1 && i < len;
+            const uint32_t v = rb_round_sqrt_fast(s.mn * s.mx);   // (the open run's value, were it to close at i)
+            RbRun t = s;
+            const bool ext = rb_extend_sel(t, c, R) || !live;
+            if (!ext) vals[s.start - ck.base] = (uint8_t)v;
+            s.mn = live ? t.mn : s.mn;
+            s.mx = live ? t.mx : s.mx;
+            s.start = ext ? s.start : ck.base + i;
+            w |= (ext ? 0u : 1u) << (i & 31);
+            if ((i & 31) == 31) {
+                opens[i >> 5] = w;
+                w = 0;
+            }
+        }
+    }
     info.entry_val = 0;
     if (ck.flags & RB_LAST) {   // the final run closes at the block's end
         vals[s.start - ck.base] = (uint8_t)rb_round_sqrt(s.mn * s.mx);

@@ -311,8 +311,13 @@ void sa_host_free(void* p)
 namespace {
 
 // Stages the texts into input I with context c's stream and mailbox
-// (sa_stage_text: c's own input; sa_stage_text_input: any input of the device)
-int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_info* info)
+// (sa_stage_text: c's own input; sa_stage_text_input: any input of the device).
+// stride = 0: the texts are copied here, packed (a text starts on a tile);
+// stride > 0 (sa_text_parse): they are already in I's text arena `slot`, the
+// file-1 text of block b at 2b x stride and its file-2 text at (2b + 1) x
+// stride (sa_text_upload), and `in` gives only their lengths.
+int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_info* info, uint64_t stride = 0,
+               int slot = 0)
 {
     const ReserveScope reserve(c ? c->reserve_blocks : 0, n > 0 ? (uint32_t)n : 0);
     if (!c) return -1;
@@ -342,9 +347,9 @@ int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_i
     std::vector<uint32_t> ntiles;
     uint64_t off = 0;
     uint32_t tiles = 0;
-    auto add_text = [&](uint64_t len) -> int64_t {
-        if (len >= (1ull << 32)) return -1;
-        ParseText t{off, 0, (uint32_t)len, tiles};
+    auto add_text = [&](uint64_t len, uint64_t at) -> int64_t {
+        if (len >= (1ull << 32) || (stride && len > stride)) return -1;
+        ParseText t{stride ? at : off, 0, (uint32_t)len, tiles};
         const uint32_t nt = (uint32_t)((len + PARSE_TILE - 1) / PARSE_TILE);
         texts.push_back(t);
         ntiles.push_back(nt);
@@ -354,13 +359,14 @@ int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_i
     };
     for (int b = 0; b < n; b++) {
         const bool pe = in[b].text2 != nullptr;
-        if ((!in[b].text1 && in[b].len1) || (pe && !in[b].text2 && in[b].len2)) {
+        if (!stride && ((!in[b].text1 && in[b].len1) || (pe && !in[b].text2 && in[b].len2))) {
             c->err = "sa_stage_text: missing text";
             return -1;
         }
-        const int64_t t1 = add_text(in[b].len1), t2 = pe ? add_text(in[b].len2) : t1;
+        const int64_t t1 = add_text(in[b].len1, 2ull * b * stride),
+                      t2 = pe ? add_text(in[b].len2, (2ull * b + 1) * stride) : t1;
         if (t1 < 0 || t2 < 0) {
-            c->err = "sa_stage_text: text of 4 GiB or more";
+            c->err = stride ? "sa_text_parse: a text longer than the stride" : "sa_stage_text: text of 4 GiB or more";
             return -1;
         }
         pb[(size_t)b] = ParseBlock{(uint32_t)t1, (uint32_t)t2, 0, 0, 0, 0, pe ? 1u : 0u, 0};
@@ -370,7 +376,13 @@ int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_i
     for (uint32_t t = 0; t < ntext; t++)
         for (uint32_t k = 0; k < ntiles[t]; k++) tile_text[texts[t].tile0 + k] = t;
 
-    SA_CHECK(c, I->d_text.ensure(std::max<uint64_t>(off, 16)));
+    DBuf& arena = slot ? I->d_text_b : I->d_text;
+    if (!stride) SA_CHECK(c, arena.ensure(std::max<uint64_t>(off, 16)));
+    else if (arena.cap < 2ull * n * stride) {
+        c->err = "sa_text_parse: the text arena holds fewer blocks (sa_text_upload's nmax)";
+        return -1;
+    }
+    uint8_t* const dtext = arena.as<uint8_t>();
     SA_CHECK(c, I->d_tile_text.ensure((size_t)tiles * 4));
     SA_CHECK(c, I->d_tile_cnt.ensure((size_t)tiles * 4));
     SA_CHECK(c, I->d_tile_base.ensure((size_t)tiles * 4));
@@ -380,21 +392,19 @@ int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_i
     SA_CHECK(c, I->d_pblocks.ensure(sizeof(ParseBlock) * (size_t)n));
     SA_CHECK(c, I->d_btot.ensure(sizeof(BlockTotals) * (size_t)n));
     SA_CHECK(c, I->d_perr.ensure(4));
-    for (int b = 0; b < n; b++) {   // the texts (a DMA when the host buffer is pinned)
+    for (int b = 0; b < n && !stride; b++) {   // the texts (a DMA when the host buffer is pinned)
         const ParseBlock& p = pb[(size_t)b];
         if (in[b].len1)
-            SA_CHECK(c, hipMemcpyAsync(I->d_text.as<uint8_t>() + texts[p.text1].off, in[b].text1, in[b].len1,
-                                       hipMemcpyHostToDevice, st));
+            SA_CHECK(c, hipMemcpyAsync(dtext + texts[p.text1].off, in[b].text1, in[b].len1, hipMemcpyHostToDevice, st));
         if (p.pe && in[b].len2)
-            SA_CHECK(c, hipMemcpyAsync(I->d_text.as<uint8_t>() + texts[p.text2].off, in[b].text2, in[b].len2,
-                                       hipMemcpyHostToDevice, st));
+            SA_CHECK(c, hipMemcpyAsync(dtext + texts[p.text2].off, in[b].text2, in[b].len2, hipMemcpyHostToDevice, st));
     }
     SA_CHECK(c, h2d(c, I->d_tile_text.p, tile_text.data(), (size_t)tiles * 4, st));
     SA_CHECK(c, h2d(c, I->d_ptexts.p, texts.data(), sizeof(ParseText) * ntext, st));
     SA_CHECK(c, h2d(c, I->d_ntiles.p, ntiles.data(), (size_t)ntext * 4, st));
     SA_CHECK(c, hipMemsetAsync(I->d_perr.p, 0, 4, st));
     if (tiles) {
-        hipLaunchKernelGGL(k_nl_count, dim3(tiles), dim3(256), 0, st, I->d_text.as<uint8_t>(),
+        hipLaunchKernelGGL(k_nl_count, dim3(tiles), dim3(256), 0, st, dtext,
                            I->d_tile_text.as<uint32_t>(), I->d_ptexts.as<ParseText>(), I->d_tile_cnt.as<uint32_t>());
         SA_CHECK(c, hipGetLastError());
     }
@@ -450,7 +460,7 @@ int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_i
     SA_CHECK(c, h2d(c, I->d_ptexts.p, texts.data(), sizeof(ParseText) * ntext, st));
     SA_CHECK(c, h2d(c, I->d_pblocks.p, pb.data(), sizeof(ParseBlock) * (size_t)n, st));
     if (tiles) {
-        hipLaunchKernelGGL(k_nl_emit, dim3(tiles), dim3(256), 0, st, I->d_text.as<uint8_t>(),
+        hipLaunchKernelGGL(k_nl_emit, dim3(tiles), dim3(256), 0, st, dtext,
                            I->d_tile_text.as<uint32_t>(), I->d_ptexts.as<ParseText>(), I->d_tile_base.as<uint32_t>(),
                            I->d_nl.as<uint32_t>());
         SA_CHECK(c, hipGetLastError());
@@ -521,7 +531,7 @@ int stage_text(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_i
     SA_CHECK(c, h2d(c, I->d_pblocks.p, pb.data(), sizeof(ParseBlock) * (size_t)n, st));
     if (nreads) {
         hipLaunchKernelGGL(k_copy_reads, dim3(wave_grid(c, nreads)), dim3(256), 0, st, I->d_pblocks.as<ParseBlock>(),
-                           I->d_ptexts.as<ParseText>(), I->d_text.as<uint8_t>(), nreads, I->d_src.as<uint32_t>(),
+                           I->d_ptexts.as<ParseText>(), dtext, nreads, I->d_src.as<uint32_t>(),
                            I->d_name_len.as<uint16_t>(), I->d_seq_len.as<uint32_t>(), I->d_read_block.as<uint32_t>(),
                            I->d_name_off.as<uint32_t>(), I->d_seq_off.as<uint32_t>(), I->d_names.as<uint8_t>(),
                            I->d_seq.as<uint8_t>(), I->d_qual.as<uint8_t>());
@@ -558,6 +568,58 @@ sa_input* sa_input_empty(int device)
 int sa_stage_text_input(sa_ctx* c, sa_input* I, const sa_text_block* in, int n, sa_text_info* info)
 {
     return stage_text(c, I, in, n, info);
+}
+
+// (round 6) the streaming form of sa_stage_text: one block's texts to the
+// device as the reader cuts it (the host text may be reused on return), into
+// text arena `slot` of the input at the fixed stride, on the context's copy
+// stream -- a thread of its own may call this while the context encodes from
+// its other arena.  Then sa_text_parse.
+int sa_text_upload(sa_ctx* c, sa_input* I, int slot, int index, int nmax, const sa_text_block* blk, uint64_t stride)
+{
+    if (!c) return -1;
+    if (!I) I = &c->own;
+    stride = (stride + PARSE_TILE - 1) / PARSE_TILE * PARSE_TILE;
+    const bool pe = blk && blk->text2 != nullptr;
+    if (!blk || slot < 0 || slot > 1 || index < 0 || index >= nmax || !stride || blk->len1 > stride ||
+        (pe && blk->len2 > stride) || (!blk->text1 && blk->len1) || I->device != c->device) {
+        c->err = "sa_text_upload: invalid block, slot, index or stride";
+        return -1;
+    }
+    std::lock_guard<std::mutex> g(c->copy_mu);   // (one uploader per context at a time)
+    SA_CHECK(c, hipSetDevice(c->device));
+    if (!c->st_copy) SA_CHECK(c, hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking));
+    DBuf& arena = slot ? I->d_text_b : I->d_text;
+    // (the whole batch's arena at its first block: a later growth would move
+    // the blocks already there)
+    if (index == 0 && arena.cap < 2ull * (uint64_t)nmax * stride) SA_CHECK(c, arena.ensure(2ull * (uint64_t)nmax * stride));
+    if (arena.cap < 2ull * (uint64_t)(index + 1) * stride) {
+        c->err = "sa_text_upload: block 0 of the batch was not uploaded first";
+        return -1;
+    }
+    uint8_t* d = arena.as<uint8_t>() + 2ull * (uint64_t)index * stride;
+    if (blk->len1) SA_CHECK(c, hipMemcpyAsync(d, blk->text1, blk->len1, hipMemcpyHostToDevice, c->st_copy));
+    if (pe && blk->len2) SA_CHECK(c, hipMemcpyAsync(d + stride, blk->text2, blk->len2, hipMemcpyHostToDevice, c->st_copy));
+    SA_CHECK(c, hipStreamSynchronize(c->st_copy));
+    return 0;
+}
+
+// parses the n blocks sa_text_upload put into text arena `slot` (lens: their
+// text lengths; text1 / text2 only tell SE from PE) into the input, as
+// sa_stage_text would have
+int sa_text_parse(sa_ctx* c, sa_input* I, int slot, const sa_text_block* lens, int n, uint64_t stride,
+                  sa_text_info* info)
+{
+    if (!c) return -1;
+    if (!I) {
+        I = &c->own;
+        c->have_output = false;
+    }
+    if (slot < 0 || slot > 1 || !stride) {
+        c->err = "sa_text_parse: invalid slot or stride";
+        return -1;
+    }
+    return stage_text(c, I, lens, n, info, (stride + PARSE_TILE - 1) / PARSE_TILE * PARSE_TILE, slot);
 }
 
 }  // extern "C"

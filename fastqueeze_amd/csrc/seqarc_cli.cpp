@@ -1877,7 +1877,12 @@ int compress(const Options& o)
             B = (est + C - 1) / C;
         }
     }
-    const size_t max_inflight = (size_t)B * ((size_t)C + 2);   // blocks read but not yet written
+    // blocks read but not yet written: C batches encoding and two ahead; with the
+    // streamed staging (below) each context's helper holds one more batch on the
+    // device, its text already back with the reader
+    const bool stream_opt = dev_parse && !o.ingest_only && !o.stage_ahead && std::getenv("SA_CLI_STREAM") &&
+                            std::atoi(std::getenv("SA_CLI_STREAM")) != 0;
+    const size_t max_inflight = (size_t)B * ((size_t)C * (stream_opt ? 2 : 1) + 2);
     std::vector<int64_t> ramp_start{0};
     for (int64_t k = 0; ramp && k < C; k++) ramp_start.push_back(ramp_start.back() + std::max<int64_t>(1, B * (k + 1) / (C + 1)));
     auto bstart = [&](int64_t k) -> int64_t {
@@ -2322,7 +2327,156 @@ int compress(const Options& o)
             }
         });
     const double t_enc_start = now_s();
-    for (size_t ci = 0; !stage_ahead && ci < ctxs.size(); ci++)
+    // (round 6) the device parse, streamed: a context takes its batch as soon as
+    // the reader has cut the batch's first block and copies each block's text to
+    // the device as it is cut (sa_text_upload: the reader's segments are free
+    // again at once, so the reader is not held to the pace of whole-batch
+    // staging), then parses the batch (sa_text_parse) and encodes it; meanwhile
+    // a helper thread takes the next batch and uploads it into the input's other
+    // text arena, so the next cycle starts with its text already on the device.
+    // SA_CLI_STREAM=1 (A/B; off by default): the reader ran faster with it
+    // (17.8 GB read in 0.69 against 0.92 s, 42.8 GB in 1.84 against 2.39 s) but
+    // the device pipeline slower -- pass R 744-1,019 against 605-694 ms a batch,
+    // the run's end 2.28 / 4.46 against 2.08-2.14 / 3.48-3.59 s (r6e, one box):
+    // with every batch on the device at once the fronts queue up all the same
+    // and the concurrent uploads slow the chains.  By default the round-5 path:
+    // sa_stage_text of a whole batch once the reader has cut it.
+    const bool stream_stage = stream_opt && !stage_ahead && !ctxs.empty() && ctxs[0];
+    // bytes reserved per text on the device: the reader's window (a block's text
+    // never exceeds it) and some slack
+    const uint64_t tstride = (pe ? (uint64_t)((uint32_t)bs >> 1) : bs) + (128u << 10);
+    // batch k once its first block is cut (and the ID template known): false
+    // when the input ended before it or the run failed
+    auto claim_first = [&](int64_t& k) -> bool {
+        std::unique_lock<std::mutex> lk(mu);
+        if (failed) return false;
+        k = next_batch++;
+        cv.wait(lk, [&] { return failed || (nblocks >= 0 && bstart(k) >= nblocks) || (tmpl_ready && nread > bstart(k)); });
+        return !(failed || (nblocks >= 0 && bstart(k) >= nblocks));
+    };
+    // the blocks of batch k to the device (text arena `slot` of ctx's input),
+    // each as soon as the reader has cut it; its text goes back to the reader
+    auto upload = [&](sa_ctx* ctx, int slot, int64_t k, std::vector<Job*>& js) -> bool {
+        js.clear();
+        const int nmax = (int)(bstart(k + 1) - bstart(k));
+        for (int64_t i = bstart(k); i < bstart(k + 1); i++) {
+            Job* j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return failed || (nblocks >= 0 && i >= nblocks) || (jobs.count(i) && jobs[i]->state >= 1); });
+                if (failed) return false;
+                if (nblocks >= 0 && i >= nblocks) break;
+                j = jobs[i].get();
+            }
+            const sa_text_block tb{j->t1.data(), j->t1.size(), pe ? j->t2.data() : nullptr, pe ? j->t2.size() : 0};
+            const double t0 = now_s();
+            if (sa_text_upload(ctx, nullptr, slot, (int)(i - bstart(k)), nmax, &tb, tstride) != 0) {
+                fail(std::string("staging failed: ") + sa_last_error(ctx));
+                return false;
+            }
+            give_back(*j, texts);   // (the device holds the text now)
+            {
+                std::lock_guard<std::mutex> g(mu);
+                staged++;
+                double cur = stage_busy.load();
+                while (!stage_busy.compare_exchange_weak(cur, cur + now_s() - t0)) {}
+            }
+            cv.notify_all();
+            js.push_back(j);
+        }
+        return true;
+    };
+    static const char kPe = 0;   // (a non-NULL text2 marks a PE block for sa_text_parse)
+    const bool prefetch = !(std::getenv("SA_CLI_PREFETCH") && std::atoi(std::getenv("SA_CLI_PREFETCH")) == 0);
+    for (size_t ci = 0; stream_stage && ci < ctxs.size(); ci++)
+        encoders.emplace_back([&, ctx = ctxs[ci]]() {
+            int slot = 0;
+            int64_t k = -1;
+            std::vector<Job*> js;
+            double tw = now_s();
+            if (!claim_first(k) || !upload(ctx, slot, k, js)) return;
+            double te = now_s();
+            for (;;) {
+                const double tp = now_s();
+                std::vector<sa_text_block> lens(js.size());
+                std::vector<sa_text_info> ti(js.size());
+                for (size_t i = 0; i < js.size(); i++)
+                    lens[i] = sa_text_block{nullptr, js[i]->text1, pe ? reinterpret_cast<const uint8_t*>(&kPe) : nullptr,
+                                            pe ? js[i]->text2 : 0};
+                if (sa_text_parse(ctx, nullptr, slot, lens.data(), (int)js.size(), tstride, ti.data()) != 0)
+                    return fail(std::string("staging failed: ") + sa_last_error(ctx));
+                std::vector<sa_out> outs(js.size());
+                for (size_t i = 0; i < js.size(); i++) {
+                    js[i]->nreads = ti[i].nreads;
+                    js[i]->len_long = ti[i].len_long;
+                    outpool.take(js[i]->out, ti[i].out_bound);
+                    outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                }
+                // the next batch into the other arena while this one encodes
+                // (SA_CLI_PREFETCH=0: after it, A/B)
+                int64_t k2 = -1;
+                std::vector<Job*> js2;
+                double tw2 = 0, te2 = 0;
+                auto take_next = [&, slot2 = slot ^ 1]() -> int {
+                    tw2 = now_s();
+                    if (!claim_first(k2)) return 0;
+                    const bool ok = upload(ctx, slot2, k2, js2);
+                    te2 = now_s();
+                    return ok ? 1 : -1;
+                };
+                std::future<int> next;
+                if (prefetch) next = std::async(std::launch::async, take_next);
+                {
+                    double c0 = t_first_enc.load();
+                    while (te < c0 && !t_first_enc.compare_exchange_weak(c0, te)) {}
+                }
+                const sa_cfg c = cfg;
+                const double tr = now_s();
+                if ((chain ? sa_run_aligned(ctx, &c, &acfg[ctx], chain, (uint64_t)k) : sa_run(ctx, &c)) != 0)
+                    return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                const double tf = now_s();
+                if (sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
+                    return fail(std::string("fetch failed: ") + sa_last_error(ctx));
+                if (o.verbose) {
+                    const char* pn[16];
+                    float pm[16];
+                    const int np = sa_phase_times(ctx, pn, pm, 16);
+                    std::string ph;
+                    for (int x = 0; x < np; x++) {
+                        char pb[48];
+                        snprintf(pb, sizeof pb, " %s %.0f", pn[x], pm[x]);
+                        ph += pb;
+                    }
+                    fprintf(stderr,
+                            "seqarc_amd: batch %lld (%zu blocks) context %p: asked %.3f s, uploaded %.3f s, parse %.3f s, "
+                            "run %.3f s, fetch %.3f s; device ms:%s\n",
+                            (long long)k, js.size(), (void*)ctx, tw, te, tr - tp, tf - tr, now_s() - tf, ph.c_str());
+                }
+                {
+                    const double t1 = now_s();
+                    double c0 = enc_busy.load();
+                    while (!enc_busy.compare_exchange_weak(c0, c0 + t1 - tp)) {}
+                    c0 = t_last_enc.load();
+                    while (t1 > c0 && !t_last_enc.compare_exchange_weak(c0, t1)) {}
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    for (size_t i = 0; i < js.size(); i++) {
+                        js[i]->out.n = outs[i].size;
+                        js[i]->state = 2;
+                    }
+                }
+                cv.notify_all();
+                const int r = prefetch ? next.get() : take_next();
+                if (r <= 0) return;   // (no more batches, or the upload failed: fail() was called)
+                k = k2;
+                js = std::move(js2);
+                slot ^= 1;
+                tw = tw2;
+                te = te2;
+            }
+        });
+    for (size_t ci = 0; !stage_ahead && !stream_stage && ci < ctxs.size(); ci++)
         encoders.emplace_back([&, ctx = ctxs[ci]]() {
             for (;;) {
                 int64_t k, b0, b1;
@@ -2944,9 +3098,14 @@ int main(int argc, char** argv)
     // default of four queues (which the GPU boxes preset), the contexts' streams
     // share queues and one context's packets wait behind another's (DESIGN.md
     // 5); set before the device is used, overriding a preset value
+    // (round 6: five per context with the streamed staging's copy stream;
+    // SA_CLI_HWQ=n: n per context, A/B)
     {
+        const bool stream = std::getenv("SA_CLI_STREAM") && std::atoi(std::getenv("SA_CLI_STREAM")) != 0;
+        int per = stream ? 5 : 4;
+        if (const char* e = std::getenv("SA_CLI_HWQ")) per = std::max(1, std::atoi(e));
         char q[16];
-        snprintf(q, sizeof q, "%d", std::min(32, 4 * o.contexts + 4));   // (per device)
+        snprintf(q, sizeof q, "%d", std::min(32, per * o.contexts + 4));   // (per device)
         setenv("GPU_MAX_HW_QUEUES", q, 1);
     }
     const int rc = compress(o);

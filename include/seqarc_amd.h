@@ -141,6 +141,22 @@ int sa_run_input(sa_ctx *ctx, const sa_input *in, const sa_cfg *cfg);   /* then 
  * batch while the context encodes the current one) */
 sa_input *sa_input_empty(int device);
 int sa_stage_text_input(sa_ctx *ctx, sa_input *in, const sa_text_block *blocks, int n, sa_text_info *info);
+/* Streaming form of sa_stage_text (round 6): the reader hands each block's text
+ * over as it cuts it (doReadPEJob@0x432d10 / ReadBufPool::addFullbuf@0x434900),
+ * and its bytes go to the device at once, so the reader's buffer is free again
+ * before the rest of the batch is cut.  in = NULL: the context's own input.
+ * Each input has two text arenas (slot 0 / 1): a thread of its own may fill one
+ * while the context encodes the batch parsed from the other.  Block `index` of
+ * a batch of at most nmax blocks lands at 2 x index x stride (file 1) and
+ * (2 x index + 1) x stride (file 2); stride >= every text length (the reader's
+ * window).  Block 0 of a batch first.  Returns once the copy is done. */
+int sa_text_upload(sa_ctx *ctx, sa_input *in, int slot, int index, int nmax, const sa_text_block *blk,
+                   uint64_t stride);
+/* Parses the n blocks uploaded into arena `slot` (lens: their lengths; text2
+ * non-NULL for PE) into the input, byte for byte what sa_stage_text gives.
+ * The input must not be in use (its previous sa_run* returned). */
+int sa_text_parse(sa_ctx *ctx, sa_input *in, int slot, const sa_text_block *lens, int n, uint64_t stride,
+                  sa_text_info *info);
 
 /* ---- range coder over pre-modelled symbols ---------------------------- */
 /* The carry-less range coder inlined in every EncapFqzComp::encode_* (e.g.

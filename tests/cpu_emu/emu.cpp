@@ -333,6 +333,11 @@ int main(int argc, char** argv)
     // checked against the oracle's serial restatement block by block
     std::vector<uint8_t> qual_q;
     if (lossy > 0.0) {
+        for (uint32_t n = 0; n <= 255u * 255u; n++)   // (the walks' loop-free root, round 6)
+            if (rb_round_sqrt_fast(n) != rb_round_sqrt(n)) {
+                std::printf("FAIL rb_round_sqrt_fast(%u)\n", n);
+                return 1;
+            }
         qual_q.assign(qual.size(), 0);
         std::vector<uint32_t> tabw(2 * RB_TAB_WORDS);   // (the R decision tables the kernels stage in LDS)
         rb_tab_build(lossy, tabw.data(), tabw.data() + RB_TAB_WORDS);

@@ -396,11 +396,22 @@ def test_cli_multi_device_gather(tmp_path, test_pair):
     # the blocks parsed on host threads (--host-parse) instead of on the device
     r5 = subprocess.run(base[:-1] + ["2", "--contexts", "2", "--host-parse", "-t", "2", "-o", str(tmp_path / "five")],
                         capture_output=True, text=True, timeout=120)
+    # the streamed uploads (SA_CLI_STREAM=1: every block's text to the device as
+    # it is cut, the next batch into the other text arena) against the default
+    # staging of whole batches; and the streamed path over a ring of 4 MiB
+    # segments (every slot refilled while batches are in flight)
+    env0 = dict(os.environ, SA_CLI_STREAM="1")
+    r6 = subprocess.run(base[:-1] + ["2", "--contexts", "3", "-t", "2", "-o", str(tmp_path / "six")],
+                        capture_output=True, text=True, timeout=120, env=env0)
+    env7 = dict(os.environ, SA_CLI_SEG_SLICES="1", SA_CLI_STREAM="1")
+    r7 = subprocess.run(base[:-1] + ["3", "--contexts", "2", "-o", str(tmp_path / "seven")],
+                        capture_output=True, text=True, timeout=120, env=env7)
     assert r1.returncode == 0 and r3.returncode == 0 and r4.returncode == 0, (r1.stderr, r3.stderr, r4.stderr)
-    assert r5.returncode == 0, r5.stderr
+    assert r5.returncode == 0 and r6.returncode == 0 and r7.returncode == 0, (r5.stderr, r6.stderr, r7.stderr)
     one = open(tmp_path / "one.arc", "rb").read()
     assert one == open(tmp_path / "three.arc", "rb").read() == open(tmp_path / "four.arc", "rb").read()
     assert one == open(tmp_path / "five.arc", "rb").read()
+    assert one == open(tmp_path / "six.arc", "rb").read() == open(tmp_path / "seven.arc", "rb").read()
     blocks = fq.blocks_from_fastq(*test_pair, 1 << 20)
     assert len(blocks) > 3
     tmpl = fq.analyze_ids(blocks[0], False)
@@ -561,6 +572,33 @@ def test_stage_text_edge_cases(enc):
     _check_text(enc, a, short, fq.Config(), bs=400_000)
     # no newline at the end of the file: the partial last line is dropped by both parsers
     _check_text(enc, synth.edge_cases() + b"@tail", None, fq.Config())
+
+
+def test_text_upload_streamed_equals_stage_text(enc, test_pair):
+    """sa_text_upload block by block (each into its stride slot of either text
+    arena) + sa_text_parse give the batch sa_stage_text gives: the encoded
+    blocks equal, for PE with several blocks per batch, SE, mates of unequal
+    length, a wider stride than the texts, and arena 1 after arena 0 (the
+    command line alternates them)."""
+    tmpl = fq.analyze_ids(fq.blocks_from_fastq(*test_pair)[0], False)
+    a, _ = synth.generate(3000, paired=True, seed=95)
+    _, short = synth.generate(3000, paired=True, seed=96, read_len=90)
+    cases = [(test_pair[0], test_pair[1], fq.Config(bin_mode=int(tmpl[0])), 1 << 20),
+             (test_pair[0], None, fq.Config(bin_mode=1), 300_000),
+             (a, short, fq.Config(), 400_000),
+             (synth.edge_cases(), None, fq.Config(qlevel=3), fq.BLOCK_SIZE)]
+    for k, (t1, t2, cfg, bs) in enumerate(cases):
+        texts = _texts(t1, t2, bs)
+        enc.stage_text(texts)
+        enc.run(cfg)
+        want = enc.fetch()
+        for slot, extra in ((0, 0), (1, 12345), (0, 4096)):
+            stride = max(max(len(x), 0 if y is None else len(y)) for x, y in texts) + extra
+            enc.stage_text_streamed(texts, slot=slot, stride=stride)
+            enc.run(cfg)
+            assert enc.fetch() == want, (k, slot, extra)
+    with pytest.raises(fq.SeqArcError):   # a text longer than the stride is refused
+        enc.stage_text_streamed(_texts(a, short, 400_000), stride=1000)
 
 
 def test_stage_text_full_size_batch(enc):
