@@ -111,11 +111,13 @@ struct FrontShare {
     hipEvent_t ev_free = nullptr;
     bool have_ev = false;
     DBuf d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
+    DBuf d_bkt_spare;   // (k_replay_seq_bkt: the inactive lanes' record stores)
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux, d_seq_longs, d_nseq_long, d_short_at;
     std::vector<DBuf*> buffers()
     {
         return {&d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_auxs_k, &d_auxs_v, &d_hist_seq, &d_hist_aux,
-                &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_seq_longs, &d_nseq_long, &d_short_at};
+                &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_seq_longs, &d_nseq_long, &d_short_at,
+                &d_bkt_spare};
     }
     uint64_t held_bytes()
     {
@@ -251,6 +253,16 @@ struct sa_ctx {
     // SEQ sort + replay 84 against 88-98 ms); by the top bits it had lost
     // (r5e-r5h: 14.9-15.4 against 15.9-16.8 GB/s)
     bool seq_bucket = !(std::getenv("SA_SEQ_BUCKET") && std::atoi(std::getenv("SA_SEQ_BUCKET")) == 0);
+    // the bucket replay's records in sorted order (coalesced stores), then put
+    // in stream order by a gather through the sort's inverse permutation, which
+    // the bucket pass writes in stream order instead of the positions
+    // (k_seq_unpermute); SA_SEQ_INV=0: one scattered 4-byte store per symbol
+    bool seq_inv = !(std::getenv("SA_SEQ_INV") && std::atoi(std::getenv("SA_SEQ_INV")) == 0);
+    bool bkt_db10 = std::getenv("SA_BKT_DB") && std::atoi(std::getenv("SA_BKT_DB")) == 10;
+    // SA_BKT_PROBE=file: per bucket-replay wave its clocks and steps, appended
+    // to file (the front waits for the replay to read them back: diagnostics)
+    const char* bkt_probe = std::getenv("SA_BKT_PROBE");
+    DBuf d_bkt_probe;
     // workgroups per CU of the grid-stride wave-per-read kernels (SA_WAVE_GRID)
     uint32_t wg_per_cu = std::getenv("SA_WAVE_GRID") ? (uint32_t)std::max(1, std::atoi(std::getenv("SA_WAVE_GRID"))) : 8u;
     // k_md5<true> reads the next block's words while the chain runs: 148 VGPRs instead
@@ -347,12 +359,13 @@ struct sa_ctx {
     DBuf d_rb_vals, d_rb_info;   // (round 5: run values per chunk byte, RbInfo per chunk)
     // SA_RB_APPLY=1: the round-4 second full walk (k_rb_apply) instead of k_rb_true + k_rb_fill (A/B)
     bool rb_apply_walk = std::getenv("SA_RB_APPLY") && std::atoi(std::getenv("SA_RB_APPLY")) != 0;
-    // R-Block chunk length (A/B, round 5): SA_RB_CHUNK=n, a multiple of 32 up
-    // to RB_CHUNK (the arrays keep RB_CHUNK's stride; a shorter chunk is what
-    // a block's last chunk always was): shorter serial walks, more lanes
+    // R-Block chunk length, also the stride of the per-chunk arrays (opens,
+    // vals): SA_RB_CHUNK=n, a multiple of 32 up to RB_CHUNK.  Not a power of
+    // two: the lanes of k_rb_spec walk their chunks in step, so at 8192 every
+    // lane's load and store of a step fell on addresses 8 KiB apart (round 6)
     uint32_t rb_chunk = [] {
         const char* e = std::getenv("SA_RB_CHUNK");
-        const uint32_t n = e ? (uint32_t)std::atoi(e) : RB_CHUNK;
+        const uint32_t n = e ? (uint32_t)std::atoi(e) : RB_CHUNK_DEFAULT;
         return n >= 32 && n <= RB_CHUNK && n % 32 == 0 ? n : RB_CHUNK;
     }();
     std::vector<uint32_t> rb_tab_host;   // the R decision tables (RbTab) of rb_tab_r
@@ -385,7 +398,7 @@ struct sa_ctx {
                 &d_list_ids[0], &d_list_gbase[0], &d_list_run[0], &d_list_ids[1], &d_list_gbase[1], &d_list_run[1],
                 &d_al_ret[0], &d_al_rev[0], &d_al_pos[0], &d_al_mp[0], &d_al_mt[0], &d_al_ret[1], &d_al_rev[1],
                 &d_al_pos[1], &d_al_mp[1], &d_al_mt[1], &d_al_st, &d_al_sel, &d_al_scr, &d_acounts, &d_atot,
-                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe, &d_ring, &d_aux_bm,
+                &d_seq_skip, &d_counts, &d_name_p, &d_name_s, &d_maxlen, &d_dege_maxq, &d_probe, &d_bkt_probe, &d_ring, &d_aux_bm,
                 &d_aux_tab, &d_aux_nmod};
     }
     uint64_t held_bytes()
@@ -510,13 +523,13 @@ uint32_t wave_grid(const sa_ctx* c, uint32_t nreads)
 // SORT_MAX_DB bits, widths as even as possible and at least SORT_MIN_DB (a
 // digit may reach above hi: those key bits are 0, or 1 in the pad keys, which
 // sort last anyway).
-std::vector<int> sort_digits(int lo, int hi)
+std::vector<int> sort_digits(int lo, int hi, int max_db = SORT_MAX_DB)
 {
     std::vector<int> w;
     if (hi <= lo) return w;
     static const int min_db = std::getenv("SA_SORT_MIN_DB") ? std::max(7, std::min(9, std::atoi(std::getenv("SA_SORT_MIN_DB"))))
                                                            : SORT_MIN_DB;
-    const int bits = hi - lo, passes = (bits + SORT_MAX_DB - 1) / SORT_MAX_DB;
+    const int bits = hi - lo, passes = (bits + max_db - 1) / max_db;
     for (int p = 0, done = 0; p < passes; p++) {
         const int d = (bits - done + (passes - p) - 1) / (passes - p);
         w.push_back(std::max(d, min_db));
@@ -526,16 +539,16 @@ std::vector<int> sort_digits(int lo, int hi)
 }
 
 // histogram words per tile of a sort over bits [lo, hi)
-uint64_t sort_hist_per_tile(int lo, int hi)
+uint64_t sort_hist_per_tile(int lo, int hi, int max_db = SORT_MAX_DB)
 {
     int m = 0;
-    for (int d : sort_digits(lo, hi)) m = std::max(m, d);
+    for (int d : sort_digits(lo, hi, max_db)) m = std::max(m, d);
     return 1ull << m;
 }
 
 template <int DB>
 void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-               uint32_t* vout, uint32_t shift, bool wide)
+               uint32_t* vout, uint32_t shift, bool wide, bool inv = false)
 {
     const dim3 hgrid((sv.ntiles + HIST_TILES - 1) / HIST_TILES);
     if (sv.dense)
@@ -551,6 +564,8 @@ void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const ui
     } else if (sv.dense) {
         if (vin) scatter(k_sort_scatter<DB, false, true, false>);
         else scatter(k_sort_scatter<DB, false, true, true>);
+    } else if (inv) {   // (one pass over implicit values: run_sort checks)
+        scatter(k_sort_scatter<DB, false, false, true, true>);
     } else {
         if (vin) scatter(k_sort_scatter<DB, false, false, false>);
         else scatter(k_sort_scatter<DB, false, false, true>);
@@ -565,7 +580,7 @@ void sort_pass(hipStream_t st, const SortView& sv, const uint32_t* kin, const ui
 // [lo, hi) of the dense id)
 int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& tiles, DBuf& hist,
              DBuf* const* keys, DBuf* const* vals, int lo, int hi, int& result_buf, bool index_vals = false,
-             const uint64_t* dense = nullptr)
+             const uint64_t* dense = nullptr, bool inv_vals = false, int max_db = SORT_MAX_DB)
 {
     result_buf = 0;
     if (plan.total && hi <= lo && index_vals) {
@@ -591,19 +606,28 @@ int run_sort(sa_ctx* c, hipStream_t st, const SortPlan& plan, DBuf& segs, DBuf& 
             return -1;
         }
     }
+    if (inv_vals && (!index_vals || wide || dense || sort_digits(lo, hi, max_db).size() != 1)) {
+        c->err = "internal: an inverse-permutation sort that is not one plain pass over implicit values";
+        return -1;
+    }
     if (wide && dense) {
         c->err = "internal: a dense sort of a segment of 2^30 keys or more";
         return -1;
     }
     int cur = 0, shift = lo;
-    for (const int db : sort_digits(lo, hi)) {
+    for (const int db : sort_digits(lo, hi, max_db)) {
         const uint32_t* kin = keys[cur]->as<uint32_t>();
         const uint32_t* vin = index_vals && shift == lo ? nullptr : vals[cur]->as<uint32_t>();
         uint32_t* kout = keys[cur ^ 1]->as<uint32_t>();
         uint32_t* vout = vals[cur ^ 1]->as<uint32_t>();
-        if (db == 7) sort_pass<7>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide);
-        else if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide);
-        else sort_pass<9>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide);
+        if (db == 7) sort_pass<7>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide, inv_vals);
+        else if (db == 8) sort_pass<8>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide, inv_vals);
+        else if (db == 9) sort_pass<9>(st, sv, kin, vin, kout, vout, (uint32_t)shift, wide, inv_vals);
+        else if (db == 10 && inv_vals) sort_pass<10>(st, sv, kin, vin, kout, vout, (uint32_t)shift, false, true);
+        else {
+            c->err = "internal: no sort pass of this digit width";
+            return -1;
+        }
         shift += db;
         cur ^= 1;
     }
@@ -668,21 +692,22 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     }
     uint8_t* vals = walk ? nullptr : c->d_rb_vals.as<uint8_t>();
     RbInfo* info = walk ? nullptr : c->d_rb_info.as<RbInfo>();
+    const uint32_t cs = c->rb_chunk;   // (the arrays' stride per chunk: bytes, opens words * 32)
     hipLaunchKernelGGL(k_rb_spec, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
-                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), vals, info);
+                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), vals, info, cs);
     hipLaunchKernelGGL(k_rb_guess, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
-                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>());
+                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(), cs);
     hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk,
                        tab, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
-                       c->d_rb_entry.as<RbRun>());
+                       c->d_rb_entry.as<RbRun>(), cs);
     if (walk) {
         hipLaunchKernelGGL(k_rb_apply, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck,
                            nck, tab, c->d_rb_entry.as<RbRun>());
     } else {
         hipLaunchKernelGGL(k_rb_true, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
-                           c->d_rb_opens.as<uint32_t>(), vals, info, c->d_rb_entry.as<RbRun>());
+                           c->d_rb_opens.as<uint32_t>(), vals, info, c->d_rb_entry.as<RbRun>(), cs);
         hipLaunchKernelGGL(k_rb_fill, dim3(nck), dim3(RB_WORDS), 0, st, c->d_qual_q.as<uint8_t>(), dck,
-                           c->d_rb_opens.as<uint32_t>(), vals, info);
+                           c->d_rb_opens.as<uint32_t>(), vals, info, cs);
     }
     SA_CHECK(c, hipGetLastError());
     return 0;
@@ -1373,7 +1398,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // 8 (9) bits, the high bkt_sb bits replayed per bucket with the models in LDS
     // (k_replay_seq_bkt); longer contexts: the full sort and k_replay_seq
     const bool seq_bkt = c->seq_bucket && seq_sh == 2 && seq_bits >= 12 && seq_bits <= 22;
-    const int bkt_sb = seq_bits <= 20 ? seq_bits - 8 : seq_bits - 9;
+    // (SA_BKT_DB=10: a 10-bit bucket pass for 22-bit contexts, models of 2^12
+    // contexts in 20 KB of LDS instead of 2^13 in 40 KB -- twice the replay
+    // waves per CU -- with the inverse-permutation pass only)
+    const int bkt_db = seq_bits <= 20 ? 8 : (c->bkt_db10 && c->seq_inv ? 10 : 9);
+    const int bkt_sb = seq_bits - bkt_db;
+    const int seq_max_db = seq_bkt ? std::max(bkt_db, (int)SORT_MAX_DB) : (int)SORT_MAX_DB;
     // (the bucket pass sorts by the context's LOW bits: k_replay_seq_bkt)
     const int seq_lo = (int)seq_sh,
               seq_hi = ns > 1 ? (int)seq_sh + (seq_bkt ? seq_bits - bkt_sb : seq_bits) : 0;
@@ -1587,7 +1617,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     SA_CHECK(c, F->d_nseq_long.ensure(4));
     SA_CHECK(c, F->d_short_at.ensure(max_short * 8));
     SA_CHECK(c, F->d_hist_seq.ensure(std::max<uint64_t>(ps.tile_seg.size(), 1) * 4 *
-                                     sort_hist_per_tile(seq_lo, seq_hi)));
+                                     sort_hist_per_tile(seq_lo, seq_hi, seq_max_db)));
     SA_CHECK(c, F->d_hist_aux.ensure(std::max<uint64_t>(pa.tile_seg.size(), 1) * 4 *
                                      sort_hist_per_tile(AUX_SYM_BITS, AUX_SYM_BITS + aux_bits)));
     SA_CHECK(c, F->d_segs_seq.ensure(sizeof(SortSeg) * nbk));
@@ -1704,20 +1734,59 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     c->prs_zero_cap = 0;   // (until this batch's tail zeroes what it wrote)
     c->prs_zero_pending = false;
     ev_begin(c, PH_SORT_SEQ, st);
+    const bool seq_inv = seq_bkt && c->seq_inv;   // (see sa_ctx::seq_inv)
     if (run_sort(c, st, ps, F->d_segs_seq, F->d_tile_seq, F->d_hist_seq, skb, svb, seq_lo, seq_hi, seq_sorted_buf,
-                 seq_sh != 0))
+                 seq_sh != 0, nullptr, seq_inv, seq_max_db))
         return -1;
     ev_finish(c, PH_SORT_SEQ, st);
     ev_begin(c, PH_REPLAY_SEQ, st);
     if (ps.total && seq_bkt) {
-        const std::vector<int> dg = sort_digits(seq_lo, seq_hi);   // (one pass: its digit width)
+        const std::vector<int> dg = sort_digits(seq_lo, seq_hi, seq_max_db);   // (one pass: its digit width)
         if (dg.size() != 1) {
             c->err = "internal: the SEQ bucket sort is not one pass";
             return -1;
         }
-        hipLaunchKernelGGL(k_replay_seq_bkt, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
-                           F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
-                           sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]));
+        const uint32_t bgrid = nbk << dg[0];
+        SA_CHECK(c, F->d_bkt_spare.ensure(256ull * bgrid));
+        PRec* spare = F->d_bkt_spare.as<PRec>();
+        uint64_t* bprobe = nullptr;
+        if (c->bkt_probe) {
+            SA_CHECK(c, c->d_bkt_probe.ensure(32ull * bgrid));
+            SA_CHECK(c, hipMemsetAsync(c->d_bkt_probe.p, 0, 32ull * bgrid, st));
+            bprobe = c->d_bkt_probe.as<uint64_t>();
+        }
+        if (seq_inv) {
+            // records in sorted order into the other value buffer (the bucket
+            // pass over implicit values never read it), then gathered through
+            // the inverse permutation the pass left in d_seq_v[sorted]
+            PRec* rs = F->d_seq_v[seq_sorted_buf ^ 1].as<PRec>();
+            hipLaunchKernelGGL(k_replay_seq_bkt<true>, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
+                               F->d_seq_k[seq_sorted_buf].as<uint32_t>(), nullptr, SymSink{rs, nullptr},
+                               (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe);
+            hipLaunchKernelGGL(k_seq_unpermute, dim3(8 * (uint32_t)((ps.tile_seg.size() + 7) / 8)),
+                               dim3(SORT_THREADS), 0, st, svs, F->d_seq_v[seq_sorted_buf].as<uint32_t>(), rs,
+                               c->d_prs_seq.as<PRec>());
+        } else {
+            hipLaunchKernelGGL(k_replay_seq_bkt<false>, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
+                               F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
+                               sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe);
+        }
+        if (bprobe) {   // one line per wave: block, digit, start / end (us, 100 MHz), cycles, steps, shared steps, xcc
+            std::vector<uint64_t> pr(4ull * bgrid);
+            SA_CHECK(c, hipMemcpyAsync(pr.data(), bprobe, 32ull * bgrid, hipMemcpyDeviceToHost, st));
+            SA_CHECK(c, hipStreamSynchronize(st));
+            if (FILE* f = std::fopen(c->bkt_probe, "a")) {
+                for (uint32_t w = 0; w < bgrid; w++) {
+                    const uint64_t* q = &pr[4ull * w];
+                    if (!q[1]) continue;
+                    std::fprintf(f, "%u %u %.2f %.2f %llu %llu %llu %llu\n", w >> dg[0], w & ((1u << dg[0]) - 1),
+                                 (double)q[0] / 100.0, (double)q[1] / 100.0, (unsigned long long)q[2],
+                                 (unsigned long long)(q[3] & 0xffffff), (unsigned long long)((q[3] >> 24) & 0xffffff),
+                                 (unsigned long long)(q[3] >> 48));
+                }
+                std::fclose(f);
+            }
+        }
     } else if (ps.total) {
         SA_CHECK(c, hipMemsetAsync(F->d_nseq_long.p, 0, 4, st));
         hipLaunchKernelGGL(k_replay_seq, dim3((uint32_t)ps.tile_seg.size()), dim3(SORT_THREADS), 0, st, svs,

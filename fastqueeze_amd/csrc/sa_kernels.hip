@@ -607,14 +607,15 @@ __device__ __forceinline__ RbTab rb_stage_tab(const uint32_t* __restrict__ tab, 
 __global__ __launch_bounds__(RB_THREADS) void k_rb_spec(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
                                                         uint32_t nck, const uint32_t* __restrict__ tab,
                                                         uint32_t* __restrict__ opens, RbRun* __restrict__ spec_exit,
-                                                        uint8_t* __restrict__ vals, RbInfo* __restrict__ info)
+                                                        uint8_t* __restrict__ vals, RbInfo* __restrict__ info,
+                                                        uint32_t cs)
 {
     __shared__ uint32_t sh[2 * RB_TAB_WORDS];
     const RbTab t = rb_stage_tab(tab, sh);
     const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck) return;
-    if (vals) spec_exit[c] = rb_spec_vals(q, ck[c], t, opens + (size_t)c * RB_WORDS, vals + (size_t)c * RB_CHUNK, info[c]);
-    else spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * RB_WORDS);
+    if (vals) spec_exit[c] = rb_spec_vals(q, ck[c], t, opens + (size_t)c * (cs / 32), vals + (size_t)c * cs, info[c], cs);
+    else spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * (cs / 32), cs / 32);
 }
 
 // k_rb_guess: one lane per chunk, the chunk's exit if the run open before it
@@ -625,20 +626,21 @@ __global__ __launch_bounds__(RB_THREADS) void k_rb_spec(const uint8_t* __restric
 __global__ __launch_bounds__(RB_THREADS) void k_rb_guess(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
                                                          uint32_t nck, const uint32_t* __restrict__ tab,
                                                          const uint32_t* __restrict__ opens,
-                                                         const RbRun* __restrict__ spec_exit, RbRun* __restrict__ guess)
+                                                         const RbRun* __restrict__ spec_exit, RbRun* __restrict__ guess,
+                                                         uint32_t cs)
 {
     __shared__ uint32_t sh[2 * RB_TAB_WORDS];
     const RbTab t = rb_stage_tab(tab, sh);
     const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck || c == 0 || (ck[c].flags & RB_FIRST)) return;
-    guess[c] = rb_carry(q, ck[c], spec_exit[c - 1], t, opens + (size_t)c * RB_WORDS, spec_exit[c]);
+    guess[c] = rb_carry(q, ck[c], spec_exit[c - 1], t, opens + (size_t)c * (cs / 32), spec_exit[c]);
 }
 
 __global__ __launch_bounds__(64) void k_rb_fix(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
                                                const uint32_t* __restrict__ ck0, uint32_t nblk,
                                                const uint32_t* __restrict__ tab, const uint32_t* __restrict__ opens,
                                                const RbRun* __restrict__ spec_exit, const RbRun* __restrict__ guess,
-                                               RbRun* __restrict__ entry)
+                                               RbRun* __restrict__ entry, uint32_t cs)
 {
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
     if (b >= nblk) return;
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(64) void k_rb_fix(const uint8_t* __restrict__ q, co
         entry[c] = cur;
         const RbRun sp = spec_exit[c - 1];
         if (cur.start == sp.start && cur.mn == sp.mn && cur.mx == sp.mx) cur = guess[c];
-        else cur = rb_carry(q, ck[c], cur, t, opens + (size_t)c * RB_WORDS, spec_exit[c]);
+        else cur = rb_carry(q, ck[c], cur, t, opens + (size_t)c * (cs / 32), spec_exit[c]);
     }
 }
 
@@ -675,18 +677,20 @@ __global__ __launch_bounds__(RB_THREADS) void k_rb_apply(const uint8_t* __restri
 __global__ __launch_bounds__(RB_THREADS) void k_rb_true(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
                                                         uint32_t nck, const uint32_t* __restrict__ tab,
                                                         uint32_t* __restrict__ opens, uint8_t* __restrict__ vals,
-                                                        RbInfo* __restrict__ info, const RbRun* __restrict__ entry)
+                                                        RbInfo* __restrict__ info, const RbRun* __restrict__ entry,
+                                                        uint32_t cs)
 {
     __shared__ uint32_t sh[2 * RB_TAB_WORDS];
     const RbTab t = rb_stage_tab(tab, sh);
     const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
     if (c >= nck || (ck[c].flags & RB_FIRST)) return;
-    rb_true(q, ck[c], entry[c], t, opens + (size_t)c * RB_WORDS, vals + (size_t)c * RB_CHUNK, info[c]);
+    rb_true(q, ck[c], entry[c], t, opens + (size_t)c * (cs / 32), vals + (size_t)c * cs, info[c]);
 }
 
 __global__ __launch_bounds__(RB_WORDS) void k_rb_fill(uint8_t* __restrict__ out, const RbChunk* __restrict__ ck,
                                                       const uint32_t* __restrict__ opens,
-                                                      const uint8_t* __restrict__ vals, const RbInfo* __restrict__ info)
+                                                      const uint8_t* __restrict__ vals, const RbInfo* __restrict__ info,
+                                                      uint32_t cs)
 {
     __shared__ int32_t wl[RB_WORDS / 64];
     __shared__ uint32_t ev[2];
@@ -696,7 +700,7 @@ __global__ __launch_bounds__(RB_WORDS) void k_rb_fill(uint8_t* __restrict__ out,
         ev[0] = info[c].entry_val & 0xffu;
         ev[1] = rb_chase(info, ck, c);
     }
-    const uint32_t word = opens[(size_t)c * RB_WORDS + t];
+    const uint32_t word = t < cs / 32 ? opens[(size_t)c * (cs / 32) + t] : 0u;
     // the last open at or before the end of each word, then exclusive over the words
     int32_t m = word ? (int32_t)(32 * t + 31 - __clz(word)) : -1;
 #pragma unroll
@@ -709,7 +713,7 @@ __global__ __launch_bounds__(RB_WORDS) void k_rb_fill(uint8_t* __restrict__ out,
     int32_t prev = __shfl_up(m, 1, 64);
     if (lane == 0) prev = -1;
     for (uint32_t k2 = 0; k2 < w; k2++) prev = prev > wl[k2] ? prev : wl[k2];
-    if (32 * t < k.len) rb_fill_word(out, k, t, word, prev, vals + (size_t)c * RB_CHUNK, info[c], ev[0], ev[1]);
+    if (32 * t < k.len) rb_fill_word(out, k, t, word, prev, vals + (size_t)c * cs, info[c], ev[0], ev[1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1557,7 +1561,10 @@ __global__ __launch_bounds__(1024) void k_sort_scan(const SortView sv)
 // bases sorts all its seeds as one segment): 64-bit element offsets
 // IDX: the input values are the elements' index in the segment (vin unused;
 // each value is computed where it is written, so no register holds it)
-template <int DB, bool WIDE, bool DENSE, bool IDX>
+// INV (with IDX, one pass): vout gets the inverse permutation instead, in
+// input order -- vout[index] = the element's sorted slot in its segment --
+// coalesced, where the positions would go out scattered (k_seq_unpermute)
+template <int DB, bool WIDE, bool DENSE, bool IDX, bool INV = false>
 __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv,
                                                                const uint32_t* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin,
@@ -1688,6 +1695,13 @@ __global__ __launch_bounds__(SORT_THREADS) void k_sort_scatter(const SortView sv
             const uint32_t kk = sb[i];
             ro[r] = (gstart[DENSE ? (uint32_t)sd[i] : (kk >> shift) & (ND - 1)] + i) << 2;
             *reinterpret_cast<uint32_t*>(ko + ro[r]) = kk;
+        }
+        if constexpr (INV) {
+            static_assert(IDX && !DENSE, "INV: one pass over implicit values");
+            uint32_t* const vi = vout + sg.base;
+#pragma unroll
+            for (int r = 0; r < SORT_ITEMS; r++) vi[val(r)] = gstart[dg[r]] + rk[r];
+            return;
         }
         __syncthreads();
 #pragma unroll
@@ -1871,14 +1885,21 @@ __device__ __forceinline__ uint32_t bm_counts(uint64_t m, uint64_t b0, uint64_t 
            (uint32_t)__popcll(m & b3) << 24;
 }
 
-// grid: nsegs << tb workgroups of one wave; dynamic LDS (4 + 1) << sb bytes.
+// grid: nsegs << tb workgroups of one wave; dynamic LDS (4 + 1) << sb bytes;
+// spare: 64 records per workgroup (the inactive lanes' stores).
 // hist: the bucket pass's scanned histogram (row tile0 of a segment = its
 // digit starts); keys = context << 2 | base, values = stream positions.
+// SORTED: vals unused, each record goes to its symbol's sorted slot (the
+// wave's 64 stores of a step are one run of 256 bytes); k_seq_unpermute puts
+// them in stream order
+template <bool SORTED>
 __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals, const SymSink rec,
-                                                       uint32_t tb, uint32_t sb, uint32_t subsh)
+                                                       uint32_t tb, uint32_t sb, uint32_t subsh,
+                                                       PRec* __restrict__ spare, uint64_t* __restrict__ probe)
 {
     extern __shared__ uint32_t bkt_lds[];
+    const uint64_t t0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull, c0 = probe ? __builtin_amdgcn_s_memtime() : 0ull;
     __shared__ uint32_t fl[64];
     const uint32_t nsub = 1u << sb, nd = 1u << tb;
     // (plain LDS pointers and compiler barriers, not volatile ones: a volatile
@@ -1903,8 +1924,10 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
     PRec* out = rec.prs + sg.base;
     const uint32_t smask = nsub - 1;
     const uint64_t below = (1ull << lane) - 1ull;
-    // one step: 64 symbols of the bucket in stream order (k: key, p: position)
-    auto step = [&](const uint32_t k, const uint32_t p, const bool act) __attribute__((always_inline)) {
+    uint32_t nshared = 0;   // (probe: steps with a context shared by lanes)
+    // one step: 64 symbols of the bucket in stream order (k: key); the lane's
+    // record (for an inactive lane: anything)
+    auto step = [&](const uint32_t k, const bool act) __attribute__((always_inline)) -> uint32_t {
         const uint32_t sub = (k >> subsh) & smask, b = k & 3u;
         if (act) tag[sub] = (uint8_t)lane;
         asm volatile("" ::: "memory");   // (LDS operations of a wave complete in order)
@@ -1914,16 +1937,17 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
         const uint64_t lm = __ballot(loser);
         bool member = false;            // shares its context with another lane
         if (lm) {
+            nshared++;
             vfl[lane] = 0u;
             asm volatile("" ::: "memory");
             if (loser) vfl[t] = 1u;
             asm volatile("" ::: "memory");
             member = loser || vfl[lane] != 0u;
         }
+        uint32_t r = 0;
         if (act && !member) {
-            const uint32_t r = bm_rec(s, b);
+            r = bm_rec(s, b);
             mst[sub] = s + (1u << (8 * b));
-            out[p] = PRec{r};
         }
         if (lm) {
             const uint64_t b0 = __ballot(member && b == 0), b1 = __ballot(member && b == 1),
@@ -1946,7 +1970,7 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
                 if (in_g) {
                     uint32_t si = gi < h ? s0 + bm_counts(G & below, b0, b1, b2, b3)
                                          : sh + bm_counts(G & below & ~lo, b0, b1, b2, b3);
-                    out[p] = PRec{bm_rec(si, b)};   // (no halving left for bm_rec: total <= 253)
+                    r = bm_rec(si, b);   // (no halving left for bm_rec: total <= 253)
                 }
                 if (lane == L)
                     mst[gs] = G == lo ? s0 + bm_counts(G, b0, b1, b2, b3) : sh + bm_counts(G & ~lo, b0, b1, b2, b3);
@@ -1954,36 +1978,87 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
             }
         }
         asm volatile("" ::: "memory");
+        return r;
     };
-    // BKT_AHEAD steps of symbols are loaded a chunk ahead: the wait for them
-    // (vmcnt, which counts the record stores too) comes once per chunk, when
-    // the previous chunk's scattered stores are mostly done, not once per step
+    // (round 6) Every step issues exactly one store -- an inactive lane's goes
+    // to `spare` -- and every step runs (past the bucket's end with no lane
+    // active), so the number of stores between two points of the loop is
+    // fixed and the waits for the keys (vmcnt, which counts the stores too) are
+    // exact: the keys of two chunks ahead are in flight, and a wait never
+    // covers the stores of the last eight steps.  Before, a step's store sat
+    // in the branches and steps past the end were skipped, so the loop waited
+    // for every outstanding store once per chunk -- a full store round trip
+    // per eight steps.  The prologue's eight stores to `spare` give the first
+    // pass through the loop the same count as every later one.
     constexpr uint32_t BKT_AHEAD = 8;
-    uint32_t ck[BKT_AHEAD], cp[BKT_AHEAD];
+    uint32_t ka[BKT_AHEAD], pa[SORTED ? 1 : BKT_AHEAD], kb[BKT_AHEAD], pb[SORTED ? 1 : BKT_AHEAD];
+    auto load = [&](uint32_t* kk, uint32_t* pp, uint32_t b0) __attribute__((always_inline)) {
 #pragma unroll
-    for (uint32_t j = 0; j < BKT_AHEAD; j++) {
-        const uint32_t i = min(start + 64 * j + lane, end - 1);   // (branch-free loads)
-        ck[j] = K[i];
-        cp[j] = V[i];
+        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
+            const uint32_t i = min(b0 + 64 * j + lane, end - 1);   // (branch-free loads)
+            kk[j] = K[i];
+            if constexpr (!SORTED) pp[j] = V[i];
+        }
+    };
+    auto run = [&](const uint32_t* kk, const uint32_t* pp, uint32_t b0) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
+            const uint32_t i = b0 + 64 * j + lane;
+            const bool act = i < end;
+            const uint32_t r = step(kk[j], act);
+            PRec* dst = act ? out + (SORTED ? i : pp[SORTED ? 0 : j]) : spare + 64 * blockIdx.x + lane;
+            *dst = PRec{r};
+        }
+    };
+    load(ka, pa, start);
+#pragma unroll
+    for (uint32_t j = 0; j < BKT_AHEAD; j++) spare[64 * blockIdx.x + lane] = PRec{0u};
+    load(kb, pb, start + 64 * BKT_AHEAD);
+    for (uint32_t base = start; base < end; base += 128 * BKT_AHEAD) {
+        run(ka, pa, base);
+        load(ka, pa, base + 128 * BKT_AHEAD);
+        run(kb, pb, base + 64 * BKT_AHEAD);
+        load(kb, pb, base + 192 * BKT_AHEAD);
     }
-    for (uint32_t base = start; base < end; base += 64 * BKT_AHEAD) {
-        uint32_t nk[BKT_AHEAD], np[BKT_AHEAD];
-#pragma unroll
-        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
-            const uint32_t i = min(base + 64 * (BKT_AHEAD + j) + lane, end - 1);
-            nk[j] = K[i];
-            np[j] = V[i];
+    if (probe) {   // (SA_BKT_PROBE) this wave's clocks, steps and placement
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (lane == 0) {
+            uint64_t* pr = probe + 4ull * blockIdx.x;
+            pr[0] = t0;
+            pr[1] = t1;
+            pr[2] = c1 - c0;
+            pr[3] = (uint64_t)((end - start + 63) / 64) | (uint64_t)nshared << 24 | (uint64_t)(xcc & 0xffu) << 48;
         }
+    }
+}
+
+// The SEQ records from sorted order (rs, k_replay_seq_bkt<true>) to stream
+// order: prs[p] = rs[inv[p]] in every segment, inv from the bucket pass
+// (k_sort_scatter<INV>).  One workgroup per sort tile; inv read and prs written
+// coalesced.  The records of one bucket are consecutive in rs, so the tiles
+// near each other in the stream gather from the same lines: tile ranges go
+// to the XCDs contiguously (workgroup g runs on XCD g % 8) to meet in one L2.
+__global__ __launch_bounds__(SORT_THREADS) void k_seq_unpermute(const SortView sv, const uint32_t* __restrict__ inv,
+                                                                const PRec* __restrict__ rs, PRec* __restrict__ prs)
+{
+    const uint32_t g = blockIdx.x, per = (sv.ntiles + 7) / 8;
+    const uint32_t t = (g & 7) * per + (g >> 3);
+    if (t >= sv.ntiles) return;
+    const SortSeg& sg = sv.segs[sv.tile_seg[t]];
+    const uint32_t i0 = (t - sg.tile0) * SORT_TILE;
+    const uint32_t* I = inv + sg.base;
+    const PRec* R = rs + sg.base;
+    PRec* O = prs + sg.base;
+    uint32_t q[SORT_ITEMS];
 #pragma unroll
-        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
-            const uint32_t i = base + 64 * j;
-            if (i < end) step(ck[j], cp[j], i + lane < end);
-        }
+    for (int r = 0; r < SORT_ITEMS; r++) q[r] = I[i0 + threadIdx.x + r * SORT_THREADS];   // (pads included)
 #pragma unroll
-        for (uint32_t j = 0; j < BKT_AHEAD; j++) {
-            ck[j] = nk[j];
-            cp[j] = np[j];
-        }
+    for (int r = 0; r < SORT_ITEMS; r++) {
+        const uint32_t i = i0 + threadIdx.x + r * SORT_THREADS;
+        if (i < sg.count) O[i] = R[q[r]];
     }
 }
 

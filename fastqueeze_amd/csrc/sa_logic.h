@@ -811,8 +811,9 @@ SA_HD bool rb_extend(RbRun& s, uint32_t c, const RbTab& t)
     return false;
 }
 
-constexpr uint32_t RB_CHUNK = 8192;
+constexpr uint32_t RB_CHUNK = 8192;   // the longest chunk (SA_RB_CHUNK)
 constexpr uint32_t RB_WORDS = RB_CHUNK / 32;
+constexpr uint32_t RB_CHUNK_DEFAULT = 7904;   // (247 words: see sa_ctx::rb_chunk)
 
 // The bytes [from, len) of the chunk starting at q + base, in order, to
 // f(i, c) until it returns false.  16 bytes per load (a lane walks its own
@@ -843,8 +844,9 @@ SA_HD void rb_for_bytes(const uint8_t* q, uint64_t base, uint32_t from, uint32_t
     }
 }
 
-// Speculative pass over one chunk: bit i of opens = a run opens at byte i.
-SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_t* opens)
+// Speculative pass over one chunk: bit i of opens = a run opens at byte i
+// (nwords: the chunk stride's words of opens, all written).
+SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_t* opens, uint32_t nwords = RB_WORDS)
 {
     RbRun s{ck.base, q[ck.base], q[ck.base]};
     uint32_t w = 1u;   // a run opens at the chunk's first byte
@@ -857,7 +859,7 @@ SA_HD RbRun rb_spec(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_
         return true;
     });
     if ((ck.len & 31) != 0) opens[(ck.len - 1) >> 5] = w;
-    for (uint32_t k = (ck.len + 31) >> 5; k < RB_WORDS; k++) opens[k] = 0;
+    for (uint32_t k = (ck.len + 31) >> 5; k < nwords; k++) opens[k] = 0;
     return s;
 }
 
@@ -959,12 +961,12 @@ SA_HD bool rb_extend_sel(RbRun& s, uint32_t c, const RbTab& t)
 // decision and looped rb_round_sqrt's 16 steps at every close, in divergent
 // lanes, and k_rb_spec took most of the ONT front.)
 SA_HD RbRun rb_spec_vals(const uint8_t* q, const RbChunk& ck, const RbTab& R, uint32_t* opens, uint8_t* vals,
-                         RbInfo& info)
+                         RbInfo& info, uint32_t span = RB_CHUNK)
 {
     RbRun s{ck.base, q[ck.base], q[ck.base]};
     uint32_t w = 1u;   // a run opens at the chunk's first byte
     const uint32_t len = ck.len;
-    for (uint32_t i0 = 0; i0 < RB_CHUNK; i0 += 16) {
+    for (uint32_t i0 = 0; i0 < span; i0 += 16) {   // (span: the chunk length, >= len)
         uint32_t x[4];
         // (a lane past its chunk's end reads its chunk's first line again: in bounds)
         const uint8_t* p = q + ck.base + (i0 < len ? i0 : 0u);

@@ -345,40 +345,45 @@ int main(int argc, char** argv)
         for (int64_t b = 0; b < nb; b++) {
             const DevBlock& d = blocks[(size_t)b];
             std::vector<RbChunk> ck;
-            // (SA_RB_CHUNK: the engine's shorter chunk length, the same arrays' stride)
+            // (SA_RB_CHUNK: the engine's chunk length, also the arrays' stride)
             const char* rce = std::getenv("SA_RB_CHUNK");
-            const uint64_t rc = rce && std::atoi(rce) >= 32 && (uint32_t)std::atoi(rce) <= RB_CHUNK ? (uint64_t)std::atoi(rce) : RB_CHUNK;
+            const uint64_t rc = rce && std::atoi(rce) >= 32 && (uint32_t)std::atoi(rce) <= RB_CHUNK &&
+                                        std::atoi(rce) % 32 == 0
+                                    ? (uint64_t)std::atoi(rce)
+                                    : RB_CHUNK_DEFAULT;
+            const uint64_t rw = rc / 32;
             for (uint64_t o = 0; o < d.seq_bytes; o += rc) {
                 const uint32_t len = (uint32_t)std::min<uint64_t>(rc, d.seq_bytes - o);
                 ck.push_back(RbChunk{d.seq_base + o, len, (o == 0 ? RB_FIRST : 0u) | (o + len == d.seq_bytes ? RB_LAST : 0u)});
             }
             if (ck.empty()) continue;
-            std::vector<uint32_t> opens(ck.size() * RB_WORDS);
+            std::vector<uint32_t> opens(ck.size() * rw);
             std::vector<RbRun> spec(ck.size()), entry(ck.size());
-            std::vector<uint8_t> vals(ck.size() * RB_CHUNK);
+            std::vector<uint8_t> vals(ck.size() * rc);
             std::vector<RbInfo> info(ck.size());
             // k_rb_spec (with the run values, round 5), k_rb_fix's carry,
             // then k_rb_true + k_rb_fill -- or (SA_RB_APPLY=1) the round-4 k_rb_apply
             const bool walk = std::getenv("SA_RB_APPLY") != nullptr;
             for (size_t c = 0; c < ck.size(); c++)
-                spec[c] = walk ? rb_spec(qual.data(), ck[c], tab, &opens[c * RB_WORDS])
-                               : rb_spec_vals(qual.data(), ck[c], tab, &opens[c * RB_WORDS], &vals[c * RB_CHUNK], info[c]);
+                spec[c] = walk ? rb_spec(qual.data(), ck[c], tab, &opens[c * rw], (uint32_t)rw)
+                               : rb_spec_vals(qual.data(), ck[c], tab, &opens[c * rw], &vals[c * rc], info[c],
+                                              (uint32_t)rc);
             RbRun cur = spec[0];
             for (size_t c = 1; c < ck.size(); c++) {
                 entry[c] = cur;
-                cur = rb_carry(qual.data(), ck[c], cur, tab, &opens[c * RB_WORDS], spec[c]);
+                cur = rb_carry(qual.data(), ck[c], cur, tab, &opens[c * rw], spec[c]);
             }
             if (walk) {
                 for (size_t c = ck.size(); c-- > 0;) rb_apply(qual.data(), qual_q.data(), ck[c], entry[c], tab);
             } else {
                 for (size_t c = 1; c < ck.size(); c++)
-                    rb_true(qual.data(), ck[c], entry[c], tab, &opens[c * RB_WORDS], &vals[c * RB_CHUNK], info[c]);
+                    rb_true(qual.data(), ck[c], entry[c], tab, &opens[c * rw], &vals[c * rc], info[c]);
                 for (size_t c = 0; c < ck.size(); c++) {
                     const uint32_t ev = info[c].entry_val & 0xffu, tv = rb_chase(info.data(), ck.data(), (uint32_t)c);
                     int32_t prev = -1;
-                    for (uint32_t t = 0; t < RB_WORDS && 32 * t < ck[c].len; t++) {
-                        const uint32_t w = opens[c * RB_WORDS + t];
-                        rb_fill_word(qual_q.data(), ck[c], t, w, prev, &vals[c * RB_CHUNK], info[c], ev, tv);
+                    for (uint32_t t = 0; t < rw && 32 * t < ck[c].len; t++) {
+                        const uint32_t w = opens[c * rw + t];
+                        rb_fill_word(qual_q.data(), ck[c], t, w, prev, &vals[c * rc], info[c], ev, tv);
                         if (w) prev = (int32_t)(32 * t + 31 - (uint32_t)__builtin_clz(w));
                     }
                 }

@@ -254,14 +254,19 @@ def _low_complexity_fastq(seed, n):
     return b"".join(recs)
 
 
-@pytest.mark.parametrize("lanes,bucket,variant", [(0, 0, 6), (1, 1, 6), (1, 0, 6), (0, 1, 6), (0, 1, 5), (0, 1, 0)])
-def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant):
+@pytest.mark.parametrize("lanes,bucket,variant,inv,db", [(0, 0, 6, 1, 9), (1, 1, 6, 1, 9), (1, 0, 6, 1, 9),
+                                                         (0, 1, 6, 1, 9), (0, 1, 5, 1, 9), (0, 1, 0, 1, 9),
+                                                         (0, 1, 5, 0, 9), (0, 1, 5, 1, 10)])
+def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, db):
     """Both pass-R kernels (k_coder_rv: a chain per wave on the scalar unit --
     its operands through SMEM from the lanes' ring (6) or through
     v_readlane (5: batched, the default; 0: per step), SA_RV_VARIANT; k_coder_rl: a chain
     per lane in the VALU fed through an LDS ring, SA_RV_LANES) and both SEQ
     replays (the full sort + k_replay_seq; one bucket sort pass +
-    k_replay_seq_bkt, SA_SEQ_BUCKET) give the oracle's bytes: multi-block PE
+    k_replay_seq_bkt, SA_SEQ_BUCKET; its records stored in sorted order and
+    gathered back through the bucket pass's inverse permutation, or stored
+    scattered, SA_SEQ_INV; a 9- or 10-bit bucket pass at Slevel 4, SA_BKT_DB)
+    give the oracle's bytes: multi-block PE
     batches (chains of ~2.9 M symbols and of a few), low-complexity reads
     (context runs far past the first halving, contexts shared inside a
     64-symbol step), Slevel 1 / 3 / 4 (8 / 12 / 13 low context bits per
@@ -269,6 +274,8 @@ def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant):
     monkeypatch.setenv("SA_RV_LANES", str(lanes))
     monkeypatch.setenv("SA_SEQ_BUCKET", str(bucket))
     monkeypatch.setenv("SA_RV_VARIANT", str(variant))
+    monkeypatch.setenv("SA_SEQ_INV", str(inv))
+    monkeypatch.setenv("SA_BKT_DB", str(db))
     e = fq.Encoder(0)
     try:
         a, b = synth.generate(40_000, paired=True, seed=91)

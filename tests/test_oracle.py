@@ -118,8 +118,9 @@ def test_cpu_decomposition(tmp_path):
     for args in runs:
         r = subprocess.run([str(exe)] + args, capture_output=True, text=True)
         assert r.returncode == 0 and r.stdout.startswith("OK"), (args, r.stdout, r.stderr)
-    # the engine's shorter R-Block chunks (SA_RB_CHUNK, the arrays keep RB_CHUNK's stride)
-    for chunk in ("4096", "1024"):
+    # the engine's other R-Block chunk lengths (SA_RB_CHUNK, also the arrays' stride;
+    # the default is 7904)
+    for chunk in ("8192", "4096", "1024"):
         for args in (["-l", "1.15", TEST1, TEST2], ["-l", "1.6", str(tmp_path / "long.fq")],
                      ["-l", "1.15", str(tmp_path / "const.fq")]):
             r = subprocess.run([str(exe)] + args, capture_output=True, text=True,
