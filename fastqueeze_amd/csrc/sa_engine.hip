@@ -112,12 +112,13 @@ struct FrontShare {
     bool have_ev = false;
     DBuf d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
     DBuf d_bkt_spare;   // (k_replay_seq_bkt: the inactive lanes' record stores)
+    DBuf d_bkt_order;   // (k_bkt_order: the digits, largest first)
     DBuf d_hist_seq, d_hist_aux, d_segs_seq, d_segs_aux, d_tile_seq, d_tile_aux, d_seq_longs, d_nseq_long, d_short_at;
     std::vector<DBuf*> buffers()
     {
         return {&d_seq_k[0], &d_seq_k[1], &d_seq_v[0], &d_seq_v[1], &d_auxs_k, &d_auxs_v, &d_hist_seq, &d_hist_aux,
                 &d_segs_seq, &d_segs_aux, &d_tile_seq, &d_tile_aux, &d_seq_longs, &d_nseq_long, &d_short_at,
-                &d_bkt_spare};
+                &d_bkt_spare, &d_bkt_order};
     }
     uint64_t held_bytes()
     {
@@ -259,6 +260,9 @@ struct sa_ctx {
     // (k_seq_unpermute); SA_SEQ_INV=0: one scattered 4-byte store per symbol
     bool seq_inv = !(std::getenv("SA_SEQ_INV") && std::atoi(std::getenv("SA_SEQ_INV")) == 0);
     bool bkt_db10 = std::getenv("SA_BKT_DB") && std::atoi(std::getenv("SA_BKT_DB")) == 10;
+    int prep_row = std::getenv("SA_PREP_ROW") ? std::atoi(std::getenv("SA_PREP_ROW")) : 0;
+    // the bucket replay's largest digits first (k_bkt_order); SA_BKT_LPT=0: digit order
+    bool bkt_lpt = !(std::getenv("SA_BKT_LPT") && std::atoi(std::getenv("SA_BKT_LPT")) == 0);
     // SA_BKT_PROBE=file: per bucket-replay wave its clocks and steps, appended
     // to file (the front waits for the replay to read them back: diagnostics)
     const char* bkt_probe = std::getenv("SA_BKT_PROBE");
@@ -1506,6 +1510,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // thread-per-read kernels: one thread per read (a grid-stride variant with
     // 8 workgroups per CU measured slower: k_prep 1.2 -> 1.7 ms, k_emit 6.8 -> 9.4)
     const uint32_t rgrid = (nr + 255) / 256;
+    // SA_PREP_ROW=64: a whole wave per read (round 6; for long reads the ONT
+    // batch's prep+scan measured the same as with 16-lane rows under load, r6l:
+    // 44.2 / 46.4 against 44.9 / 41.4 ms, so 16 stays the default)
+    const bool prep_wide = c->prep_row == 64;
     if (nr) {
         // k_prep (names, lengths: lane per read) and k_prep_sq16 (SEQ / QUAL /
         // N-IUPAC columns: a row per read).  SA_PREP_FUSED=1: k_prep_sq16 takes
@@ -1522,6 +1530,10 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             if (c->prep_wave)
                 hipLaunchKernelGGL(k_prep_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                    c->d_counts.as<uint32_t>(), d_err);
+            else if (prep_wide)
+                hipLaunchKernelGGL((wq_prep ? k_prep_sq16<true, 64> : k_prep_sq16<false, 64>), dim3(wave_grid(c, nr)),
+                                   dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(), d_err,
+                                   c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr, wq_prep);
             else
                 hipLaunchKernelGGL(wq_prep ? k_prep_sq16<true> : k_prep_sq16<false>,
                                    dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
@@ -1749,6 +1761,13 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         const uint32_t bgrid = nbk << dg[0];
         SA_CHECK(c, F->d_bkt_spare.ensure(256ull * bgrid));
         PRec* spare = F->d_bkt_spare.as<PRec>();
+        const uint32_t* border = nullptr;
+        if (c->bkt_lpt) {
+            SA_CHECK(c, F->d_bkt_order.ensure(4ull << dg[0]));
+            hipLaunchKernelGGL(k_bkt_order, dim3(1), dim3(1u << dg[0]), 0, st, svs, 1u << dg[0],
+                               F->d_bkt_order.as<uint32_t>());
+            border = F->d_bkt_order.as<uint32_t>();
+        }
         uint64_t* bprobe = nullptr;
         if (c->bkt_probe) {
             SA_CHECK(c, c->d_bkt_probe.ensure(32ull * bgrid));
@@ -1762,16 +1781,16 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             PRec* rs = F->d_seq_v[seq_sorted_buf ^ 1].as<PRec>();
             hipLaunchKernelGGL(k_replay_seq_bkt<true>, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
                                F->d_seq_k[seq_sorted_buf].as<uint32_t>(), nullptr, SymSink{rs, nullptr},
-                               (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe);
+                               (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe, border);
             hipLaunchKernelGGL(k_seq_unpermute, dim3(8 * (uint32_t)((ps.tile_seg.size() + 7) / 8)),
                                dim3(SORT_THREADS), 0, st, svs, F->d_seq_v[seq_sorted_buf].as<uint32_t>(), rs,
                                c->d_prs_seq.as<PRec>());
         } else {
             hipLaunchKernelGGL(k_replay_seq_bkt<false>, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
                                F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
-                               sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe);
+                               sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe, border);
         }
-        if (bprobe) {   // one line per wave: block, digit, start / end (us, 100 MHz), cycles, steps, shared steps, xcc
+        if (bprobe) {   // one line per wave: block, digit (its rank with k_bkt_order), start / end (us, 100 MHz), cycles, steps, shared steps, xcc
             std::vector<uint64_t> pr(4ull * bgrid);
             SA_CHECK(c, hipMemcpyAsync(pr.data(), bprobe, 32ull * bgrid, hipMemcpyDeviceToHost, st));
             SA_CHECK(c, hipStreamSynchronize(st));
@@ -1779,7 +1798,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                 for (uint32_t w = 0; w < bgrid; w++) {
                     const uint64_t* q = &pr[4ull * w];
                     if (!q[1]) continue;
-                    std::fprintf(f, "%u %u %.2f %.2f %llu %llu %llu %llu\n", w >> dg[0], w & ((1u << dg[0]) - 1),
+                    std::fprintf(f, "%u %u %.2f %.2f %llu %llu %llu %llu\n", border ? w % nbk : w >> dg[0],
+                                 border ? w / nbk : w & ((1u << dg[0]) - 1),   // (k_bkt_order: the digit's rank)
                                  (double)q[0] / 100.0, (double)q[1] / 100.0, (unsigned long long)q[2],
                                  (unsigned long long)(q[3] & 0xffffff), (unsigned long long)((q[3] >> 24) & 0xffffff),
                                  (unsigned long long)(q[3] >> 48));

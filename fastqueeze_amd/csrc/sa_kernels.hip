@@ -307,6 +307,7 @@ __device__ __forceinline__ uint32_t first_diff16(const uint32_t a[4], const uint
     return 0xffffffffu;
 }
 
+template <int W>
 __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint32_t r, uint32_t rl, int& p, int& sfx)
 {
     const uint8_t *nm = nullptr, *pv = nullptr;
@@ -324,7 +325,7 @@ __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint
     const uint32_t wlim = (uint32_t)wave_max_i32((int)lim);
     uint32_t lcp = lim, lcs = lim;
     bool pdone = false, sdone = false;
-    for (uint32_t i0 = 0; i0 < wlim; i0 += 16 * PREP_ROW) {
+    for (uint32_t i0 = 0; i0 < wlim; i0 += 16 * W) {
         const uint32_t t0 = i0 + 16 * rl;
         uint32_t dp = 0xffffffffu, ds = 0xffffffffu;
         if (t0 < lim) {
@@ -364,8 +365,8 @@ __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint
                 }
             }
         }
-        dp = row_min<PREP_ROW>(dp);
-        ds = row_min<PREP_ROW>(ds);
+        dp = row_min<W>(dp);
+        ds = row_min<W>(ds);
         if (!pdone && dp != 0xffffffffu) {
             lcp = dp;
             pdone = true;
@@ -388,7 +389,7 @@ __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint
 // arithmetic wait for it) take fewer reads instead of finishing last: a
 // grid-stride kernel's time is its slowest CU's.
 constexpr uint32_t WQ_CHUNK = 64;
-template <bool DYN>
+template <bool DYN, uint32_t RPW = 4>   // (RPW: reads per wave)
 struct WaveReads {
     uint32_t* wq;
     uint32_t base, stride, cur = 0, lim = 0;
@@ -408,26 +409,29 @@ struct WaveReads {
                 lim = cur + WQ_CHUNK;
             }
             b = cur;
-            cur += 4;
+            cur += RPW;
             return b < nr;
         }
     }
 };
 
-template <bool DYN>
+// W = 64 (round 6): one read per wave, for batches of long reads -- four reads
+// of 10-50 kbp in a wave all walked the longest one's length
+template <bool DYN, int W = PREP_ROW>
 __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ err, uint8_t* __restrict__ dege_maxq,
                                                    int16_t* __restrict__ name_p, int16_t* __restrict__ name_s,
                                                    uint32_t* __restrict__ wq)
 {
-    const uint32_t rl = threadIdx.x & (PREP_ROW - 1);
-    const uint32_t rows = gridDim.x * (blockDim.x / PREP_ROW);
-    const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / PREP_ROW;
+    constexpr uint32_t RPW = 64 / W;   // rows (reads) per wave
+    const uint32_t rl = threadIdx.x & (W - 1);
+    const uint32_t rows = gridDim.x * (blockDim.x / W);
+    const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / W;
     const uint32_t nr = bv.nreads_total;
     // wave-uniform trip count: every row of the wave loops while any row has a read
-    WaveReads<DYN> wr(wq, row0 & ~3u, rows);
+    WaveReads<DYN, RPW> wr(wq, row0 & ~(RPW - 1), rows);
     for (uint32_t base; wr.next(nr, base);) {
-        const uint32_t r = base + (row0 & 3u);
+        const uint32_t r = base + (row0 & (RPW - 1));
         const bool live = r < nr;
         uint32_t len = 0;
         const uint8_t *s = nullptr, *q = nullptr, *qv = nullptr;
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
         }
         uint32_t valid = 0, nonascii = 0, lastnz = 0, firstbad = 0xffffffffu, maxq = 0, hasn = 0;
         const uint32_t wlen = (uint32_t)wave_max_i32((int)len);   // (the wave's longest read)
-        for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * PREP_ROW) {
+        for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * W) {
             const uint32_t pos = i0 + 16 * rl;
             if (pos < len) {
                 const uint32_t cnt = len - pos < 16 ? len - pos : 16;
@@ -478,12 +482,12 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
                 }
             }
         }
-        valid = row_sum<PREP_ROW>(valid);
-        nonascii = row_max<PREP_ROW>(nonascii ? 1u : 0u);
-        lastnz = row_max<PREP_ROW>(lastnz);
-        firstbad = row_min<PREP_ROW>(firstbad);
-        maxq = row_max<PREP_ROW>(maxq);
-        hasn = row_max<PREP_ROW>(hasn);
+        valid = row_sum<W>(valid);
+        nonascii = row_max<W>(nonascii ? 1u : 0u);
+        lastnz = row_max<W>(lastnz);
+        firstbad = row_min<W>(firstbad);
+        maxq = row_max<W>(maxq);
+        hasn = row_max<W>(hasn);
         // seq_stat's second loop, row-parallel (long reads carry N / IUPAC bases
         // in nearly every read): over the positions with quality <= maxq, an
         // ACGT base adds 1 + bits(gap) symbols, gap = the eligible non-ACGT
@@ -495,7 +499,7 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
             uint32_t cg = 0;         // the row's carry from the previous step: gap after its last eligible ACGT
             const int mq = (int)(maxq & 0xffu);   // (0..127: the max of signed qualities, from 0)
             const uint32_t mq4 = 0x80808080u | ((uint32_t)mq * 0x01010101u);
-            for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * PREP_ROW) {
+            for (uint32_t i0 = 0; i0 < wlen; i0 += 16 * W) {
                 const uint32_t pos = i0 + 16 * rl;
                 uint32_t sw[4] = {0, 0, 0, 0}, qw[4] = {0, 0, 0, 0}, cnt = 0;
                 if (hasn && pos < len) {
@@ -527,14 +531,14 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
                 // inclusive row scan of (g, h): (A then B) = (hB ? gB : gA + gB, hA | hB)
                 uint32_t ig = g, ih = h;
 #pragma unroll
-                for (int d = 1; d < (int)PREP_ROW; d <<= 1) {
-                    const uint32_t pg = __shfl_up(ig, d, PREP_ROW), ph = __shfl_up(ih, d, PREP_ROW);
+                for (int d = 1; d < W; d <<= 1) {
+                    const uint32_t pg = __shfl_up(ig, d, W), ph = __shfl_up(ih, d, W);
                     if ((int)rl >= d) {
                         ig = ih ? ig : pg + ig;
                         ih |= ph;
                     }
                 }
-                uint32_t eg = __shfl_up(ig, 1, PREP_ROW), eh = __shfl_up(ih, 1, PREP_ROW);
+                uint32_t eg = __shfl_up(ig, 1, W), eh = __shfl_up(ih, 1, W);
                 if (rl == 0) eg = eh = 0;
                 // the gap entering this lane: the carry, then the lanes before it
                 const uint32_t gap = eh ? eg : cg + eg;
@@ -554,15 +558,15 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
                     }
                 }
                 // the row's total (lane 15's inclusive value) continues the carry
-                const uint32_t tg = __shfl(ig, PREP_ROW - 1, PREP_ROW), th = __shfl(ih, PREP_ROW - 1, PREP_ROW);
+                const uint32_t tg = __shfl(ig, W - 1, W), th = __shfl(ih, W - 1, W);
                 cg = th ? tg : cg + tg;
             }
-            exc = row_sum<PREP_ROW>(exc);
-            nsym = row_sum<PREP_ROW>(nsym);
+            exc = row_sum<W>(exc);
+            nsym = row_sum<W>(nsym);
         }
         // k_prep's columns (name_p == nullptr: k_prep runs, SA_PREP_WAVE)
         int np = 0, ns = 0;
-        if (name_p && !bv.bin_mode) name_cols16(bv, live, r, rl, np, ns);
+        if (name_p && !bv.bin_mode) name_cols16<W>(bv, live, r, rl, np, ns);
         if (live && rl == 0) {
             SeqStat st{valid, len - valid, maxq & 0xffu, hasn ? exc : 0u, hasn ? nsym : 0u,
                        nonascii ? (uint32_t)E_NONASCII : 0u};
@@ -1896,7 +1900,8 @@ template <bool SORTED>
 __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals, const SymSink rec,
                                                        uint32_t tb, uint32_t sb, uint32_t subsh,
-                                                       PRec* __restrict__ spare, uint64_t* __restrict__ probe)
+                                                       PRec* __restrict__ spare, uint64_t* __restrict__ probe,
+                                                       const uint32_t* __restrict__ order)
 {
     extern __shared__ uint32_t bkt_lds[];
     const uint64_t t0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull, c0 = probe ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -1908,7 +1913,10 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
     uint32_t* mst = bkt_lds;
     uint8_t* tag = reinterpret_cast<uint8_t*>(bkt_lds + nsub);
     uint32_t* vfl = fl;
-    const uint32_t seg = blockIdx.x >> tb, d = blockIdx.x & (nd - 1);
+    // (order: workgroup r * nsegs + seg takes the r-th largest digit, see
+    // k_bkt_order; without it, workgroup seg << tb | d)
+    const uint32_t seg = order ? blockIdx.x % sv.nsegs : blockIdx.x >> tb;
+    const uint32_t d = order ? order[blockIdx.x / sv.nsegs] : blockIdx.x & (nd - 1);
     const SortSeg& sg = sv.segs[seg];
     if (sg.count == 0) return;
     const uint32_t* H = sv.hist + (size_t)sg.tile0 * nd;
@@ -2032,6 +2040,33 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
             pr[2] = c1 - c0;
             pr[3] = (uint64_t)((end - start + 63) / 64) | (uint64_t)nshared << 24 | (uint64_t)(xcc & 0xffu) << 48;
         }
+    }
+}
+
+// (round 6) The bucket replay's digits, largest first over all segments: a
+// bucket's wave walks all its symbols in steps of 64, the heavy digits' waves
+// run 3-5x the median (SA_BKT_PROBE, r6l: 8-12 ms against 0.7 ms), and
+// started last they set the kernel's span.  One workgroup of nd threads.
+__global__ __launch_bounds__(1024) void k_bkt_order(const SortView sv, uint32_t nd, uint32_t* __restrict__ order)
+{
+    __shared__ uint32_t sz[1024];
+    const uint32_t d = threadIdx.x;
+    if (d < nd) {
+        uint32_t n = 0;
+        for (uint32_t g = 0; g < sv.nsegs; g++) {
+            const SortSeg& sg = sv.segs[g];
+            if (sg.count == 0) continue;
+            const uint32_t* H = sv.hist + (size_t)sg.tile0 * nd;
+            n += (d + 1 < nd ? H[d + 1] : sg.count) - H[d];
+        }
+        sz[d] = n;
+    }
+    __syncthreads();
+    if (d < nd) {
+        const uint32_t n = sz[d];
+        uint32_t r = 0;
+        for (uint32_t e = 0; e < nd; e++) r += sz[e] > n || (sz[e] == n && e < d) ? 1u : 0u;
+        order[r] = d;
     }
 }
 

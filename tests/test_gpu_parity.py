@@ -254,10 +254,12 @@ def _low_complexity_fastq(seed, n):
     return b"".join(recs)
 
 
-@pytest.mark.parametrize("lanes,bucket,variant,inv,db", [(0, 0, 6, 1, 9), (1, 1, 6, 1, 9), (1, 0, 6, 1, 9),
-                                                         (0, 1, 6, 1, 9), (0, 1, 5, 1, 9), (0, 1, 0, 1, 9),
-                                                         (0, 1, 5, 0, 9), (0, 1, 5, 1, 10)])
-def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, db):
+@pytest.mark.parametrize("lanes,bucket,variant,inv,db,lpt", [(0, 0, 6, 1, 9, 1), (1, 1, 6, 1, 9, 1),
+                                                             (1, 0, 6, 1, 9, 1), (0, 1, 6, 1, 9, 1),
+                                                             (0, 1, 5, 1, 9, 1), (0, 1, 0, 1, 9, 1),
+                                                             (0, 1, 5, 0, 9, 1), (0, 1, 5, 1, 10, 1),
+                                                             (0, 1, 5, 1, 9, 0)])
+def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, db, lpt):
     """Both pass-R kernels (k_coder_rv: a chain per wave on the scalar unit --
     its operands through SMEM from the lanes' ring (6) or through
     v_readlane (5: batched, the default; 0: per step), SA_RV_VARIANT; k_coder_rl: a chain
@@ -265,7 +267,8 @@ def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, d
     replays (the full sort + k_replay_seq; one bucket sort pass +
     k_replay_seq_bkt, SA_SEQ_BUCKET; its records stored in sorted order and
     gathered back through the bucket pass's inverse permutation, or stored
-    scattered, SA_SEQ_INV; a 9- or 10-bit bucket pass at Slevel 4, SA_BKT_DB)
+    scattered, SA_SEQ_INV; a 9- or 10-bit bucket pass at Slevel 4, SA_BKT_DB;
+    the buckets largest first or in digit order, SA_BKT_LPT)
     give the oracle's bytes: multi-block PE
     batches (chains of ~2.9 M symbols and of a few), low-complexity reads
     (context runs far past the first halving, contexts shared inside a
@@ -276,6 +279,7 @@ def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, d
     monkeypatch.setenv("SA_RV_VARIANT", str(variant))
     monkeypatch.setenv("SA_SEQ_INV", str(inv))
     monkeypatch.setenv("SA_BKT_DB", str(db))
+    monkeypatch.setenv("SA_BKT_LPT", str(lpt))
     e = fq.Encoder(0)
     try:
         a, b = synth.generate(40_000, paired=True, seed=91)
@@ -319,6 +323,22 @@ def test_long_reads_emit_steps(enc, slevel, qlevel):
     """SEQ contexts and QUAL contexts carried across k_emit_sq's 64-position steps."""
     blocks = fq.blocks_from_fastq(_long_read_fastq(5 + slevel, 700))
     _check(enc, blocks, fq.Config(slevel=slevel, qlevel=qlevel))
+
+
+def test_prep_wave_per_read(monkeypatch):
+    """k_prep_sq16 with a whole wave per read (SA_PREP_ROW=64, opt-in) gives the
+    oracle's bytes: long reads with N / IUPAC bases and '#' runs, lossy
+    qualities, and short PE reads."""
+    monkeypatch.setenv("SA_PREP_ROW", "64")
+    e = fq.Encoder(0)
+    try:
+        _check(e, fq.blocks_from_fastq(_long_read_fastq(77, 500)), fq.Config(slevel=3, qlevel=3))
+        t1, _ = synth.generate(40, paired=False, seed=12, read_len=20000)
+        _check(e, fq.blocks_from_fastq(t1), fq.Config(lossy=1.15))
+        a, b = synth.generate(20_000, paired=True, seed=13)
+        _check(e, fq.blocks_from_fastq(a, b, 4 << 20)[:2], fq.Config())
+    finally:
+        e.close()
 
 
 @pytest.mark.parametrize("ratio", [1.05, 1.15, 1.6])
