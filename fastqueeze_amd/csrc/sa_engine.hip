@@ -110,6 +110,7 @@ struct FrontShare {
     uint64_t next_ticket = 0, serving = 0;
     hipEvent_t ev_free = nullptr;
     bool have_ev = false;
+    std::atomic<int> tails{0};   // contexts of the device inside coder_run (pass R in flight)
     DBuf d_seq_k[2], d_seq_v[2], d_auxs_k, d_auxs_v;
     DBuf d_bkt_spare;   // (k_replay_seq_bkt: the inactive lanes' record stores)
     DBuf d_bkt_order;   // (k_bkt_order: the digits, largest first)
@@ -259,7 +260,9 @@ struct sa_ctx {
     // the bucket pass writes in stream order instead of the positions
     // (k_seq_unpermute); SA_SEQ_INV=0: one scattered 4-byte store per symbol
     bool seq_inv = !(std::getenv("SA_SEQ_INV") && std::atoi(std::getenv("SA_SEQ_INV")) == 0);
-    bool bkt_db10 = std::getenv("SA_BKT_DB") && std::atoi(std::getenv("SA_BKT_DB")) == 10;
+    // SA_BKT_DB=8 / 9 / 10: the bucket pass's digit bits (default 8 for contexts
+    // of <= 20 bits, 9 above; 10 with the inverse-permutation pass only)
+    int bkt_db_env = std::getenv("SA_BKT_DB") ? std::atoi(std::getenv("SA_BKT_DB")) : 0;
     int prep_row = std::getenv("SA_PREP_ROW") ? std::atoi(std::getenv("SA_PREP_ROW")) : 0;
     // the bucket replay's largest digits first (k_bkt_order); SA_BKT_LPT=0: digit order
     bool bkt_lpt = !(std::getenv("SA_BKT_LPT") && std::atoi(std::getenv("SA_BKT_LPT")) == 0);
@@ -297,9 +300,19 @@ struct sa_ctx {
     // 665-691) but it issues 10 SALU per symbol instead of 8 and holds its SIMD's
     // scalar issue ~90 % of the time, so the kernels that share those SIMDs
     // slow (L passes 89 against 52 ms, prep 16 against 10) and the bench lost
-    // 3 % (r6b / r6c: 16,623-16,904 against 17,281-17,493 MB/s).  Off by
-    // default; SA_RV_VARIANT=6 (A/B).
+    // 3 % (r6b / r6c: 16,623-16,904 against 17,281-17,493 MB/s).  On the tree
+    // with the full-segment L passes the bench is level (r6m: 19,301 / 19,237
+    // against 19,437 / 19,279) and the command line, whose batches' latency
+    // sets its pace, faster: 42.8 GB in 3.47 / 3.53 s against 4.22 / 3.89 s
+    // (r6o); and in r6q the bench too (19,339 / 19,422 against 18,386 /
+    // 18,851 MB/s), so 6 is the default for short-read batches since round 6.
     int rv_variant = std::getenv("SA_RV_VARIANT") ? std::atoi(std::getenv("SA_RV_VARIANT")) : -1;
+    // (default variant, A/B) 6 only while at most SA_RV_V6_MAX other contexts of
+    // the device are in pass R, else 5; -1: 5 always.  Unset: 6 always -- the
+    // limit measured no better (r6q: bench 19,106 / 19,264 with 2, 18,386 /
+    // 18,851 with -1, 19,339 / 19,422 without; 42.8 GB in 5.02 / 4.28 s with 2,
+    // 4.44 / 4.11 with -1, 4.35 / 4.17 without)
+    int rv_v6_max = std::getenv("SA_RV_V6_MAX") ? std::atoi(std::getenv("SA_RV_V6_MAX")) : 1 << 30;
     int rv_batch = 5;   // the current batch's (run_input)
     // pass R's wait for records the long runs have not written (SA_RV_WAIT_MS, default 20 s: the
     // long runs take ~0.4 s; a wave that waits longer gives up and the batch fails with E_CODER)
@@ -1402,10 +1415,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // 8 (9) bits, the high bkt_sb bits replayed per bucket with the models in LDS
     // (k_replay_seq_bkt); longer contexts: the full sort and k_replay_seq
     const bool seq_bkt = c->seq_bucket && seq_sh == 2 && seq_bits >= 12 && seq_bits <= 22;
-    // (SA_BKT_DB=10: a 10-bit bucket pass for 22-bit contexts, models of 2^12
-    // contexts in 20 KB of LDS instead of 2^13 in 40 KB -- twice the replay
-    // waves per CU -- with the inverse-permutation pass only)
-    const int bkt_db = seq_bits <= 20 ? 8 : (c->bkt_db10 && c->seq_inv ? 10 : 9);
+    // (SA_BKT_DB: one more digit bit halves the models a replay wave holds in
+    // LDS -- 2^12 contexts in 20 KB instead of 2^13 in 40 KB at 22 bits --
+    // for twice the waves per CU; 10 bits with the inverse-permutation pass only)
+    const int bkt_db = c->bkt_db_env >= 8 && c->bkt_db_env <= (c->seq_inv ? 10 : 9) && seq_bits - c->bkt_db_env >= 4
+                           ? c->bkt_db_env
+                           : (seq_bits <= 20 ? 8 : 9);
     const int bkt_sb = seq_bits - bkt_db;
     const int seq_max_db = seq_bkt ? std::max(bkt_db, (int)SORT_MAX_DB) : (int)SORT_MAX_DB;
     // (the bucket pass sorts by the context's LOW bits: k_replay_seq_bkt)
@@ -1417,7 +1432,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     FrontShare* F = c->fs;
     c->rv_batch = c->rv_variant == 0 || c->rv_variant == 5 || c->rv_variant == 6
                       ? c->rv_variant
-                      : (nr && I->seq_bytes / nr > 1000 ? 0 : 5);   // (see rv_variant)
+                      : (nr && I->seq_bytes / nr > 1000 ? 0 : 6);   // (see rv_variant)
 
     SA_CHECK(c, c->d_blocks.ensure(sizeof(DevBlock) * nbk));
     SA_CHECK(c, h2d(c, c->d_blocks.p, c->blocks.data(), sizeof(DevBlock) * nbk, st));
@@ -1887,7 +1902,12 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     if (!c->host_waits) SA_CHECK(c, hipStreamWaitEvent(st3, c->ev_fork_seq, 0));
     std::vector<uint32_t> out_len;
     {
+        // (SA_RV_V6_MAX, see rv_v6_max) the SMEM-fed chain only when few other
+        // contexts' chains are in flight
+        if (c->rv_variant < 0 && c->rv_batch == 6 && F->tails.load() > c->rv_v6_max) c->rv_batch = 5;
+        F->tails++;
         const int rc = coder_run(c, tasks, cv, st3, PH_CODER_R, PH_CODER_L, c->ev_long_done, exact, out_len, payload);
+        F->tails--;
         if (rc) return rc;
     }
     // the records this batch wrote back to zero, in its tail (after the L passes on st3)

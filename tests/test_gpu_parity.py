@@ -254,11 +254,11 @@ def _low_complexity_fastq(seed, n):
     return b"".join(recs)
 
 
-@pytest.mark.parametrize("lanes,bucket,variant,inv,db,lpt", [(0, 0, 6, 1, 9, 1), (1, 1, 6, 1, 9, 1),
-                                                             (1, 0, 6, 1, 9, 1), (0, 1, 6, 1, 9, 1),
-                                                             (0, 1, 5, 1, 9, 1), (0, 1, 0, 1, 9, 1),
-                                                             (0, 1, 5, 0, 9, 1), (0, 1, 5, 1, 10, 1),
-                                                             (0, 1, 5, 1, 9, 0)])
+@pytest.mark.parametrize("lanes,bucket,variant,inv,db,lpt", [(0, 0, 6, 1, 0, 1), (1, 1, 6, 1, 0, 1),
+                                                             (1, 0, 6, 1, 0, 1), (0, 1, 6, 1, 0, 1),
+                                                             (0, 1, 5, 1, 0, 1), (0, 1, 0, 1, 0, 1),
+                                                             (0, 1, 5, 0, 0, 1), (0, 1, 5, 1, 9, 1),
+                                                             (0, 1, 5, 1, 10, 1), (0, 1, 5, 1, 0, 0)])
 def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, db, lpt):
     """Both pass-R kernels (k_coder_rv: a chain per wave on the scalar unit --
     its operands through SMEM from the lanes' ring (6) or through
@@ -267,7 +267,8 @@ def test_pass_r_and_seq_replay_paths(monkeypatch, lanes, bucket, variant, inv, d
     replays (the full sort + k_replay_seq; one bucket sort pass +
     k_replay_seq_bkt, SA_SEQ_BUCKET; its records stored in sorted order and
     gathered back through the bucket pass's inverse permutation, or stored
-    scattered, SA_SEQ_INV; a 9- or 10-bit bucket pass at Slevel 4, SA_BKT_DB;
+    scattered, SA_SEQ_INV; the bucket pass's digit bits, SA_BKT_DB = 0 (the
+    default: 8 up to 20-bit contexts, 9 above), 9 or 10;
     the buckets largest first or in digit order, SA_BKT_LPT)
     give the oracle's bytes: multi-block PE
     batches (chains of ~2.9 M symbols and of a few), low-complexity reads
