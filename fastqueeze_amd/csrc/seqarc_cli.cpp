@@ -21,7 +21,7 @@
 //   --share-device   all contexts on one GPU (tests of the multi-GPU gather)
 //   --host-only      read, cut and parse only (no device; measures the host pipeline)
 //   --host-parse     parse the blocks on host threads (default: on the device, sa_stage_text)
-//   --read-threads N plain-file reader threads (default 8; 0: the per-block window reader)
+//   --read-threads N plain-file reader threads (default 16; 0: the per-block window reader)
 //   --writers N      archive writer threads (default 8: page maps at the blocks' offsets; 1: write(2))
 //   --ingest-only    the reader and block cut alone, batches dealt to devices x contexts
 //                    consumers (no device); --ingest-crc: the consumers CRC the texts
@@ -1401,7 +1401,11 @@ struct Options {
     bool compress = false, decompress = false, index = false, force = false, in_dir = false, share_device = false,
          verbose = false, host_only = false, host_parse = false, ingest_only = false, ramp = false,
          release = false, stage_ahead = false, shm = false, maxmis_set = false, ingest_crc = false;
-    int read_threads = 8;   // --read-threads: the plain-file reader's fill threads (SegReader)
+    // --read-threads: the plain-file reader's fill threads (SegReader).  16 since
+    // round 6: the whole-node ingest (--ingest-only --devices 8) 34.3 / 35.8
+    // against 18.2 / 28.7 GB/s with 8 (r6s; the reader two or three batches
+    // ahead instead: 21.5-25.4)
+    int read_threads = 16;
     int writers = 8;        // --writers: the archive writer's copy threads (ArcWriter; 1: write(2) in order)
     int threads = 0, pipe = 0, device = 0, devices = 1, contexts = 2, batch = 32, block_mib = 50, maxmis = 7;
     int insert = 0;
