@@ -1794,14 +1794,14 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             // pass over implicit values never read it), then gathered through
             // the inverse permutation the pass left in d_seq_v[sorted]
             PRec* rs = F->d_seq_v[seq_sorted_buf ^ 1].as<PRec>();
-            hipLaunchKernelGGL(k_replay_seq_bkt<true>, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
+            hipLaunchKernelGGL(k_replay_seq_bkt<true>, dim3(nbk << dg[0]), dim3(64), (size_t)5 * ((1u << bkt_sb) + 64), st, svs,
                                F->d_seq_k[seq_sorted_buf].as<uint32_t>(), nullptr, SymSink{rs, nullptr},
                                (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe, border);
             hipLaunchKernelGGL(k_seq_unpermute, dim3(8 * (uint32_t)((ps.tile_seg.size() + 7) / 8)),
                                dim3(SORT_THREADS), 0, st, svs, F->d_seq_v[seq_sorted_buf].as<uint32_t>(), rs,
                                c->d_prs_seq.as<PRec>());
         } else {
-            hipLaunchKernelGGL(k_replay_seq_bkt<false>, dim3(nbk << dg[0]), dim3(64), (size_t)5 << bkt_sb, st, svs,
+            hipLaunchKernelGGL(k_replay_seq_bkt<false>, dim3(nbk << dg[0]), dim3(64), (size_t)5 * ((1u << bkt_sb) + 64), st, svs,
                                F->d_seq_k[seq_sorted_buf].as<uint32_t>(), F->d_seq_v[seq_sorted_buf].as<uint32_t>(),
                                sink_seq, (uint32_t)dg[0], (uint32_t)bkt_sb, (uint32_t)(seq_sh + dg[0]), spare, bprobe, border);
         }

@@ -1889,7 +1889,7 @@ __device__ __forceinline__ uint32_t bm_counts(uint64_t m, uint64_t b0, uint64_t 
            (uint32_t)__popcll(m & b3) << 24;
 }
 
-// grid: nsegs << tb workgroups of one wave; dynamic LDS (4 + 1) << sb bytes;
+// grid: nsegs << tb workgroups of one wave; dynamic LDS 5 * ((1 << sb) + 64) bytes;
 // spare: 64 records per workgroup (the inactive lanes' stores).
 // hist: the bucket pass's scanned histogram (row tile0 of a segment = its
 // digit starts); keys = context << 2 | base, values = stream positions.
@@ -1905,13 +1905,13 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
 {
     extern __shared__ uint32_t bkt_lds[];
     const uint64_t t0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull, c0 = probe ? __builtin_amdgcn_s_memtime() : 0ull;
-    __shared__ uint32_t fl[64];
+    __shared__ uint32_t fl[128];
     const uint32_t nsub = 1u << sb, nd = 1u << tb;
     // (plain LDS pointers and compiler barriers, not volatile ones: a volatile
     // access becomes a flat access, and every flat access waits for all the
     // wave's outstanding global stores -- the scattered records -- r5e / r5g)
-    uint32_t* mst = bkt_lds;
-    uint8_t* tag = reinterpret_cast<uint8_t*>(bkt_lds + nsub);
+    uint32_t* mst = bkt_lds;   // (nsub models, then 64 lanes' spare slots)
+    uint8_t* tag = reinterpret_cast<uint8_t*>(bkt_lds + nsub + 64);
     uint32_t* vfl = fl;
     // (order: workgroup r * nsegs + seg takes the r-th largest digit, see
     // k_bkt_order; without it, workgroup seg << tb | d)
@@ -1935,12 +1935,19 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
     uint32_t nshared = 0;   // (probe: steps with a context shared by lanes)
     // one step: 64 symbols of the bucket in stream order (k: key); the lane's
     // record (for an inactive lane: anything)
+    // (round 6) The common path has no lane branches: an inactive lane works on
+    // a slot of its own past the bucket's models (sub = nsub + lane: its tag
+    // names itself, it shares nothing, its model write lands there), and a
+    // shared context's lanes write their (unused) uncontested update there too.
+    // Every exec-mask branch is scalar-unit work, which the other batches'
+    // pass-R chains hold: under the bench's load this kernel ran 2.4x its time
+    // alone, the VALU-only gather beside it 1.1x (r6p).
     auto step = [&](const uint32_t k, const bool act) __attribute__((always_inline)) -> uint32_t {
-        const uint32_t sub = (k >> subsh) & smask, b = k & 3u;
-        if (act) tag[sub] = (uint8_t)lane;
+        const uint32_t sub = act ? (k >> subsh) & smask : nsub + lane, b = k & 3u;
+        tag[sub] = (uint8_t)lane;
         asm volatile("" ::: "memory");   // (LDS operations of a wave complete in order)
-        const uint32_t t = act ? tag[sub] : lane;
-        uint32_t s = act ? mst[sub] : 0u;
+        const uint32_t t = tag[sub];
+        const uint32_t s = mst[sub];
         const bool loser = t != lane;   // another lane of the step has this context
         const uint64_t lm = __ballot(loser);
         bool member = false;            // shares its context with another lane
@@ -1948,15 +1955,13 @@ __global__ __launch_bounds__(64) void k_replay_seq_bkt(const SortView sv, const 
             nshared++;
             vfl[lane] = 0u;
             asm volatile("" ::: "memory");
-            if (loser) vfl[t] = 1u;
+            vfl[loser ? t : 64 + lane] = 1u;
             asm volatile("" ::: "memory");
             member = loser || vfl[lane] != 0u;
         }
-        uint32_t r = 0;
-        if (act && !member) {
-            r = bm_rec(s, b);
-            mst[sub] = s + (1u << (8 * b));
-        }
+        uint32_t s1 = s;
+        uint32_t r = bm_rec(s1, b);
+        mst[member ? nsub + lane : sub] = s1 + (1u << (8 * b));
         if (lm) {
             const uint64_t b0 = __ballot(member && b == 0), b1 = __ballot(member && b == 1),
                            b2 = __ballot(member && b == 2), b3 = __ballot(member && b == 3);
