@@ -122,6 +122,11 @@ def parse_args(argv=None):
                     help="PE pairs of the HASH leg's batch (5 M: 69 blocks, the headline's batch)")
     ap.add_argument("--hash-align-reads", type=int, default=4_000_000, help="single reads of the aligner leg")
     ap.add_argument("--leg-steps", type=int, default=10, help="timed steps of the ONT and HASH legs")
+    ap.add_argument("--legs-fresh", type=int, default=1,
+                    help="run the SE / ONT / HASH legs each in a process of its own (1) or in this one after "
+                         "the headline (0: a second set of contexts in the process ran the ONT leg's front "
+                         "~40 %% slower, r6s / r6v / r6w)")
+    ap.add_argument("--leg-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--text-leg", type=int, default=1,
                     help="staged-text leg: each step hands its batch over as FASTQ text in page-locked host "
                          "memory (sa_stage_text: H2D + device parse), encodes and fetches (0: skip)")
@@ -839,7 +844,7 @@ def main():
     # default), under which the contexts' streams share queues:
     # 13.45-13.48 GB/s with 8 / 24 queues against 13.0-13.3 with 4 (round 3 g4b)
     hwq0 = os.environ.get("GPU_MAX_HW_QUEUES")
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, 4 * args.contexts + 4))
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SA_BENCH_HWQ") or str(min(32, 4 * args.contexts + 4))   # (A/B)
 
     import numpy as np
     import torch
@@ -858,6 +863,12 @@ def main():
     share = cpu_share()
     workers = args.gen_workers or max(1, min(16, share["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
                                                                                                world)))))
+    if args.leg_child:   # (--legs-fresh: one leg in this fresh process, its result as one JSON line)
+        legs = {"se_leg": se_leg, "ont_lossy": ont_leg, "hash_path": hash_leg}
+        leg = legs[args.leg_child]
+        r = hash_leg(args, local) if leg is hash_leg else leg(args, workers, local)
+        print(json.dumps(r), flush=True)
+        return
     # ---- this rank's batches (global ids dealt round robin) ----
     gids = shard_indices(world * args.batches, rank, world)
     t0 = time.time()
@@ -1168,6 +1179,22 @@ def main():
                 res["ingest_8way_mb_s"] = ing.get("value")
         finally:
             shutil.rmtree(os.path.dirname(e2e_files[0]), True)
+    def leg_in_child(name: str) -> dict:
+        """One leg in a process of its own (this script, --leg-child NAME, the
+        same arguments): a fresh process's contexts, like the headline's."""
+        import subprocess
+        cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:] + ["--leg-child", name]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
+        sys.stderr.write(r.stderr)
+        if r.returncode != 0:
+            if r.returncode == 1 and "differs from the CPU restatement" in r.stderr:
+                raise SystemExit(r.stderr.strip().splitlines()[-1])
+            raise RuntimeError(f"leg process exit {r.returncode}: {r.stderr[-400:]}")
+        out = r.stdout.strip().splitlines()
+        leg_res = json.loads(out[-1])
+        leg_res["process"] = "its own (--legs-fresh 1)"
+        return leg_res
+
     if rank == 0 and world == 1:
         for name, leg, on in (("se_leg", se_leg, args.se_leg), ("ont_lossy", ont_leg, args.ont_leg),
                               ("hash_path", hash_leg, args.hash_leg)):
@@ -1175,7 +1202,10 @@ def main():
                 continue
             t0 = time.perf_counter()
             try:
-                res[name] = hash_leg(args, local) if leg is hash_leg else leg(args, workers, local)
+                if args.legs_fresh:
+                    res[name] = leg_in_child(name)
+                else:
+                    res[name] = hash_leg(args, local) if leg is hash_leg else leg(args, workers, local)
             except SystemExit:
                 raise
             except Exception as e:   # (recorded: the headline line stands on its own)
