@@ -376,6 +376,9 @@ struct sa_ctx {
     DBuf d_rb_vals, d_rb_info;   // (round 5: run values per chunk byte, RbInfo per chunk)
     // SA_RB_APPLY=1: the round-4 second full walk (k_rb_apply) instead of k_rb_true + k_rb_fill (A/B)
     bool rb_apply_walk = std::getenv("SA_RB_APPLY") && std::atoi(std::getenv("SA_RB_APPLY")) != 0;
+    // SA_RB_FIX_SERIAL=1: the entries by k_rb_fix (a lane per block, chunk by
+    // chunk) instead of k_rb_fix_w (a wave per block, 64 chunks a step; A/B)
+    bool rb_fix_serial = std::getenv("SA_RB_FIX_SERIAL") && std::atoi(std::getenv("SA_RB_FIX_SERIAL")) != 0;
     // R-Block chunk length, also the stride of the per-chunk arrays (opens,
     // vals): SA_RB_CHUNK=n, a multiple of 32 up to RB_CHUNK.  Not a power of
     // two: the lanes of k_rb_spec walk their chunks in step, so at 8192 every
@@ -714,9 +717,14 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), vals, info, cs);
     hipLaunchKernelGGL(k_rb_guess, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(), cs);
-    hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk,
-                       tab, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
-                       c->d_rb_entry.as<RbRun>(), cs);
+    if (c->rb_fix_serial)
+        hipLaunchKernelGGL(k_rb_fix, dim3((nbk + 63) / 64), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(),
+                           nbk, tab, c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(),
+                           c->d_rb_guess.as<RbRun>(), c->d_rb_entry.as<RbRun>(), cs);
+    else
+        hipLaunchKernelGGL(k_rb_fix_w, dim3(nbk), dim3(64), 0, st, bv.qual, dck, c->d_rb_ck0.as<uint32_t>(), nbk, tab,
+                           c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(),
+                           c->d_rb_entry.as<RbRun>(), cs);
     if (walk) {
         hipLaunchKernelGGL(k_rb_apply, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, c->d_qual_q.as<uint8_t>(), dck,
                            nck, tab, c->d_rb_entry.as<RbRun>());

@@ -660,6 +660,60 @@ __global__ __launch_bounds__(64) void k_rb_fix(const uint8_t* __restrict__ q, co
     }
 }
 
+// (round 6) k_rb_fix_w: the same entries, a wave per block and 64 chunks a
+// step.  While every check passes, the entry of chunk c is the speculative
+// exit of chunk c - 1 (the guess of chunk c - 1 equals it whenever the check
+// at chunk c passes), so the checks of a window are independent: lane i tests
+// chunk c + i's entry -- `cur` for lane 0, guess[c + i - 1] for the others --
+// against spec_exit[c + i - 1]; the window's entries up to the first failing
+// lane are written at once, and only that lane runs rb_carry.  k_rb_fix walked
+// a block's ~3,300 chunks of an ONT batch one dependent load pair at a time
+// (1.6 ms alone, 2.5 ms under the batch's load, r6f / r6j).
+__device__ __forceinline__ RbRun rb_shfl(const RbRun& r, uint32_t src)
+{
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)r.start, (int)src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(r.start >> 32), (int)src, 64);
+    return RbRun{(uint64_t)hi << 32 | lo, (uint32_t)__shfl((int)r.mn, (int)src, 64),
+                 (uint32_t)__shfl((int)r.mx, (int)src, 64)};
+}
+
+__global__ __launch_bounds__(64) void k_rb_fix_w(const uint8_t* __restrict__ q, const RbChunk* __restrict__ ck,
+                                                 const uint32_t* __restrict__ ck0, uint32_t nblk,
+                                                 const uint32_t* __restrict__ tab, const uint32_t* __restrict__ opens,
+                                                 const RbRun* __restrict__ spec_exit, const RbRun* __restrict__ guess,
+                                                 RbRun* __restrict__ entry, uint32_t cs)
+{
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= nblk) return;
+    const RbTab t{tab, tab + RB_TAB_WORDS};
+    const uint32_t c0 = ck0[b], c1 = ck0[b + 1];
+    if (c0 == c1) return;
+    RbRun cur = spec_exit[c0];   // (wave-uniform: the true run open after chunk c)
+    for (uint32_t c = c0 + 1; c < c1;) {
+        const uint32_t n = c1 - c < 64 ? c1 - c : 64;
+        const uint32_t ci = c + lane;
+        RbRun e = cur;
+        bool ok = true;
+        if (lane < n) {
+            if (lane > 0) e = guess[ci - 1];
+            const RbRun sp = spec_exit[ci - 1];
+            ok = e.start == sp.start && e.mn == sp.mn && e.mx == sp.mx;
+        }
+        const uint64_t bad = __ballot(!ok);
+        const uint32_t f = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1u : n;   // first failing chunk
+        if (lane < n && lane <= f) entry[ci] = e;
+        if (f < n) {
+            RbRun nx = e;
+            if (lane == f) nx = rb_carry(q, ck[ci], e, t, opens + (size_t)ci * (cs / 32), spec_exit[ci]);
+            cur = rb_shfl(nx, f);
+            c += f + 1;
+        } else {
+            cur = guess[c + n - 1];
+            c += n;
+        }
+    }
+}
+
 __global__ __launch_bounds__(RB_THREADS) void k_rb_apply(const uint8_t* __restrict__ q, uint8_t* __restrict__ out,
                                                          const RbChunk* __restrict__ ck, uint32_t nck,
                                                          const uint32_t* __restrict__ tab,

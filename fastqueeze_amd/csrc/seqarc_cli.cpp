@@ -2708,6 +2708,23 @@ int compress(const Options& o)
         rc = 1;
     }
     const double t_closed = now_s();
+    // (diagnostics, SA_CLI_EXIT_PROBE=1: what the exit would tear down, timed
+    // here instead -- the output pool's buffers, then the contexts)
+    if (std::getenv("SA_CLI_EXIT_PROBE") && std::atoi(std::getenv("SA_CLI_EXIT_PROBE")) != 0) {
+        size_t nb = 0, cap = 0;
+        const double p0 = now_s();
+        {
+            std::lock_guard<std::mutex> g(outpool.mu);
+            nb = outpool.free.size();
+            for (auto& b : outpool.free) cap += b.cap;
+            outpool.free.clear();
+        }
+        const double p1 = now_s();
+        release();
+        const double p2 = now_s();
+        fprintf(stderr, "seqarc_amd: exit probe: output pool %zu buffers, %.3f GB reserved, freed in %.3f s; contexts "
+                        "released in %.3f s\n", nb, (double)cap / 1e9, p1 - p0, p2 - p1);
+    }
     // the contexts' device buffers (~200 GB for five contexts) are left to the
     // process exit unless --release: the command line exits right after this
     // (main, g_fast_exit), and the driver reclaims them without the ~1.4 s of

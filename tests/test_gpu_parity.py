@@ -354,6 +354,49 @@ def test_lossy_rblock(enc, test_pair, ratio):
     _check(enc, fq.blocks_from_fastq(synth.edge_cases()), fq.Config(lossy=ratio, md5=False))
 
 
+def _rblock_runs_fastq(seed, n, read_len):
+    """Long reads whose qualities alternate long near-constant stretches (runs
+    of rblock that cross many R-Block chunks: their speculative exits differ
+    from the true ones, so the entry pass takes rb_carry) with noisy ones
+    (chunks that converge), at random lengths, so the failing chunks fall at
+    every position of the 64-chunk windows of k_rb_fix_w."""
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        q = bytearray()
+        while len(q) < read_len:
+            if rng.random() < 0.5:
+                v = int(rng.integers(40, 70))
+                m = int(rng.integers(500, 40000))
+                q += bytes(np.where(rng.random(m) < 0.5, v, v + 1).astype(np.uint8))
+            else:
+                q += bytes(rng.integers(35, 75, size=int(rng.integers(50, 6000)), dtype=np.uint8))
+        q = bytes(q[:read_len])
+        s = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=read_len))
+        recs.append(b"@rb%d\n%s\n+\n%s\n" % (i, s, q))
+    return b"".join(recs)
+
+
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_rblock_entry_pass(monkeypatch, serial):
+    """The R-Block entry pass -- k_rb_fix_w (a wave per block, 64 chunks a step,
+    the default) and k_rb_fix (SA_RB_FIX_SERIAL=1) -- where many chunks do not
+    converge (rb_carry at arbitrary window positions), blocks of several
+    windows, and a constant-quality block where no chunk converges: == the
+    oracle's serial rblock@0x426c10."""
+    monkeypatch.setenv("SA_RB_FIX_SERIAL", serial)
+    e = fq.Encoder(0)
+    try:
+        blocks = fq.blocks_from_fastq(_rblock_runs_fastq(31, 120, 30000), None, 2 << 20)
+        assert len(blocks) >= 3
+        for r in (1.05, 1.15, 1.6):
+            _check(e, blocks, fq.Config(lossy=r))
+        const = b"".join(b"@c%d\n%s\n+\n%s\n" % (i, b"ACGT" * 5000, b"I" * 20000) for i in range(60))
+        _check(e, fq.blocks_from_fastq(const), fq.Config(lossy=1.15))
+    finally:
+        e.close()
+
+
 def test_long_length_path(enc):
     """Reads > 65535 bp switch the block to compressLen_long@0x423710 (four length
     bytes); a block of short reads next to it keeps compressLen_short."""
