@@ -242,6 +242,10 @@ struct sa_ctx {
     // k_prep_sq16 / k_emit_sq16 with the round-4 static grid stride instead of
     // reads taken from a counter (WaveReads; SA_FRONT_STATIC=1, A/B)
     bool front_static = std::getenv("SA_FRONT_STATIC") && std::atoi(std::getenv("SA_FRONT_STATIC")) != 0;
+    // reads a front wave takes from the counter at a time (WaveReads): 0 = by the
+    // batch's mean read length (front_wq_chunk), SA_WQ_CHUNK=n to fix it (A/B;
+    // 64 was the only value until round 6)
+    uint32_t wq_chunk_env = std::getenv("SA_WQ_CHUNK") ? (uint32_t)std::atoi(std::getenv("SA_WQ_CHUNK")) : 0u;
     // pass R with one chain per lane in the VALU (k_coder_rl: the scalar units
     // stay free for the front kernels of the other batches) instead of one
     // chain per wave on the scalar unit (k_coder_rv); SA_RV_LANES=1 / 0.  Off:
@@ -534,6 +538,18 @@ hipError_t sync_d2h(sa_ctx* c, hipStream_t st)
 
 // grid of a wave-per-read, grid-stride kernel (EMIT_WAVES waves per workgroup):
 // 8 workgroups per CU, fewer for a small batch
+// Reads per take of the front kernels' read counter: ~64 reads' worth of
+// 150 bp (about 10 KB of bases) a take, so short-read batches keep WQ_CHUNK
+// and long-read batches take one wave's four reads at a time; a multiple of
+// four (the rows of a wave).
+uint32_t front_wq_chunk(const sa_ctx* c, uint64_t seq_bytes, uint32_t nreads)
+{
+    if (c->wq_chunk_env) return std::max<uint32_t>(4, std::min<uint32_t>(1024, c->wq_chunk_env & ~3u));
+    const uint64_t mean = nreads ? std::max<uint64_t>(1, seq_bytes / nreads) : 1;
+    const uint64_t k = (uint64_t)WQ_CHUNK * 150 / mean;
+    return (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(WQ_CHUNK, k) & ~3ull);
+}
+
 uint32_t wave_grid(const sa_ctx* c, uint32_t nreads)
 {
     return std::max<uint32_t>(1, std::min<uint32_t>((nreads + EMIT_WAVES - 1) / EMIT_WAVES, c->wg_per_cu * c->n_cu));
@@ -1500,6 +1516,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     // the front kernels' dynamic read counters (nullptr: the static grid stride)
     uint32_t* wq_prep = c->front_static ? nullptr : d_err + 8;
     uint32_t* wq_emit = c->front_static ? nullptr : d_err + 9;
+    const uint32_t wqc = front_wq_chunk(c, I->seq_bytes, nr);
 
     ev_begin(c, PH_TOTAL, st);
     // ---- MD5 of every block's IDs/bases/quals (calcBlockMd5@0x414d90) on st2,
@@ -1546,7 +1563,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
         if (c->prep_fused) {
             hipLaunchKernelGGL(wq_prep ? k_prep_sq16<true> : k_prep_sq16<false>, dim3(wave_grid(c, (nr + 3) / 4)),
                                dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(), d_err, c->d_dege_maxq.as<uint8_t>(),
-                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), wq_prep);
+                               c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), wq_prep, wqc);
         } else {
             hipLaunchKernelGGL(k_prep, dim3(rgrid), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
                                c->d_name_p.as<int16_t>(), c->d_name_s.as<int16_t>(), d_err);
@@ -1556,11 +1573,11 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             else if (prep_wide)
                 hipLaunchKernelGGL((wq_prep ? k_prep_sq16<true, 64> : k_prep_sq16<false, 64>), dim3(wave_grid(c, nr)),
                                    dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(), d_err,
-                                   c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr, wq_prep);
+                                   c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr, wq_prep, wqc);
             else
                 hipLaunchKernelGGL(wq_prep ? k_prep_sq16<true> : k_prep_sq16<false>,
                                    dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0, st, bv, c->d_counts.as<uint32_t>(),
-                                   d_err, c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr, wq_prep);
+                                   d_err, c->d_dege_maxq.as<uint8_t>(), nullptr, nullptr, wq_prep, wqc);
         }
     }
     hipLaunchKernelGGL(k_scan_reads, dim3(nbk), dim3(1024), 0, st, bv, c->d_counts.as<uint32_t>(),
@@ -1706,7 +1723,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                                       : (wq_emit ? k_emit_sq16<0, true> : k_emit_sq16<0, false>),
                                dim3(wave_grid(c, (nr + 3) / 4)), dim3(256), 0,
                                st, bv, c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
-                               F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr, wq_emit);
+                               F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr, wq_emit, wqc);
             if (dege_maxq && n_ch) {   // the N / IUPAC side streams of the reads that have such bases
                 SA_CHECK(c, c->d_dege_list.ensure(4ull * ((uint64_t)nr + 1)));
                 SA_CHECK(c, hipMemsetAsync(c->d_dege_list.p, 0, 4, st));

@@ -388,12 +388,17 @@ __device__ __forceinline__ void name_cols16(const BatchView& bv, bool live, uint
 // scalar unit other batches' pass-R chains keep busy (their loops and address
 // arithmetic wait for it) take fewer reads instead of finishing last: a
 // grid-stride kernel's time is its slowest CU's.
+// (round 6) `chunk`, the reads a wave takes at a time, is the host's choice
+// per batch (front_wq_chunk): WQ_CHUNK for short reads, down to one wave's
+// reads for long ones -- 64 reads of 10-50 kbp a take left an ONT batch's
+// 60,000 reads to ~940 waves, each walking 64 reads in series.
 constexpr uint32_t WQ_CHUNK = 64;
 template <bool DYN, uint32_t RPW = 4>   // (RPW: reads per wave)
 struct WaveReads {
     uint32_t* wq;
-    uint32_t base, stride, cur = 0, lim = 0;
-    __device__ WaveReads(uint32_t* q, uint32_t wrow0, uint32_t rows) : wq(q), base(wrow0), stride(rows) {}
+    uint32_t base, stride, chunk, cur = 0, lim = 0;
+    __device__ WaveReads(uint32_t* q, uint32_t wrow0, uint32_t rows, uint32_t ch)
+        : wq(q), base(wrow0), stride(rows), chunk(ch) {}
     // the wave's next first row (wave-uniform); false when the reads are done
     __device__ __forceinline__ bool next(uint32_t nr, uint32_t& b)
     {
@@ -404,9 +409,9 @@ struct WaveReads {
         } else {
             if (cur >= lim) {
                 uint32_t g = 0;
-                if ((threadIdx.x & 63) == 0) g = atomicAdd(wq, WQ_CHUNK);
+                if ((threadIdx.x & 63) == 0) g = atomicAdd(wq, chunk);
                 cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0, 64));
-                lim = cur + WQ_CHUNK;
+                lim = cur + chunk;
             }
             b = cur;
             cur += RPW;
@@ -421,7 +426,7 @@ template <bool DYN, int W = PREP_ROW>
 __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ err, uint8_t* __restrict__ dege_maxq,
                                                    int16_t* __restrict__ name_p, int16_t* __restrict__ name_s,
-                                                   uint32_t* __restrict__ wq)
+                                                   uint32_t* __restrict__ wq, uint32_t wq_chunk)
 {
     constexpr uint32_t RPW = 64 / W;   // rows (reads) per wave
     const uint32_t rl = threadIdx.x & (W - 1);
@@ -429,7 +434,7 @@ __global__ __launch_bounds__(256) void k_prep_sq16(const BatchView bv, uint32_t*
     const uint32_t row0 = (blockIdx.x * blockDim.x + threadIdx.x) / W;
     const uint32_t nr = bv.nreads_total;
     // wave-uniform trip count: every row of the wave loops while any row has a read
-    WaveReads<DYN, RPW> wr(wq, row0 & ~(RPW - 1), rows);
+    WaveReads<DYN, RPW> wr(wq, row0 & ~(RPW - 1), rows, wq_chunk);
     for (uint32_t base; wr.next(nr, base);) {
         const uint32_t r = base + (row0 & (RPW - 1));
         const bool live = r < nr;
@@ -1102,7 +1107,7 @@ template <uint32_t SH, bool DYN>
 __global__ __launch_bounds__(256, 4) void k_emit_sq16(const BatchView bv, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ seq_key, uint32_t* __restrict__ seq_val,
                                                    uint32_t* __restrict__ aux_key, uint32_t* __restrict__ aux_val,
-                                                   uint32_t* __restrict__ wq)
+                                                   uint32_t* __restrict__ wq, uint32_t wq_chunk)
 {
     // (one slot past each row's ER_STEP: the stores of the branch-free loops
     // below that carry no symbol land there)
@@ -1120,7 +1125,7 @@ __global__ __launch_bounds__(256, 4) void k_emit_sq16(const BatchView bv, const 
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
     };
-    WaveReads<DYN> wr(wq, row0 & ~3u, rows);   // (wave-uniform: the rows of a wave shuffle together)
+    WaveReads<DYN> wr(wq, row0 & ~3u, rows, wq_chunk);   // (wave-uniform: the rows of a wave shuffle together)
     for (uint32_t base; wr.next(nr, base);) {
         const uint32_t r = base + (row0 & 3u);
         const bool live = r < nr;

@@ -365,15 +365,16 @@ def _rblock_runs_fastq(seed, n, read_len):
     for i in range(n):
         q = bytearray()
         while len(q) < read_len:
+            # (qualities below '@': a quality line never looks like a header to the cut)
             if rng.random() < 0.5:
-                v = int(rng.integers(40, 70))
+                v = int(rng.integers(40, 62))
                 m = int(rng.integers(500, 40000))
                 q += bytes(np.where(rng.random(m) < 0.5, v, v + 1).astype(np.uint8))
             else:
-                q += bytes(rng.integers(35, 75, size=int(rng.integers(50, 6000)), dtype=np.uint8))
+                q += bytes(rng.integers(35, 64, size=int(rng.integers(50, 6000)), dtype=np.uint8))
         q = bytes(q[:read_len])
         s = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=read_len))
-        recs.append(b"@rb%d\n%s\n+\n%s\n" % (i, s, q))
+        recs.append(b"@SIMRDrb%d\n%s\n+\n%s\n" % (i, s, q))   # (the cut matches > 5 bytes of the first header)
     return b"".join(recs)
 
 
@@ -391,8 +392,26 @@ def test_rblock_entry_pass(monkeypatch, serial):
         assert len(blocks) >= 3
         for r in (1.05, 1.15, 1.6):
             _check(e, blocks, fq.Config(lossy=r))
-        const = b"".join(b"@c%d\n%s\n+\n%s\n" % (i, b"ACGT" * 5000, b"I" * 20000) for i in range(60))
+        const = b"".join(b"@SIMRDc%d\n%s\n+\n%s\n" % (i, b"ACGT" * 5000, b"5" * 20000) for i in range(60))
         _check(e, fq.blocks_from_fastq(const), fq.Config(lossy=1.15))
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("chunk", ["4", "12", "1024"])
+def test_front_read_counter_chunks(monkeypatch, chunk):
+    """The front kernels' reads taken from the counter `chunk` at a time
+    (SA_WQ_CHUNK; by default from the batch's mean read length: 64 for short
+    reads, 4 for ONT-length ones) give the oracle's bytes: short PE reads,
+    long reads with N / IUPAC bases and '#' runs, lossy long reads."""
+    monkeypatch.setenv("SA_WQ_CHUNK", chunk)
+    e = fq.Encoder(0)
+    try:
+        a, b = synth.generate(20_000, paired=True, seed=17)
+        _check(e, fq.blocks_from_fastq(a, b, 2 << 20), fq.Config())
+        _check(e, fq.blocks_from_fastq(_long_read_fastq(78, 500)), fq.Config(slevel=3, qlevel=3))
+        t1, _ = synth.generate(40, paired=False, seed=14, read_len=20000)
+        _check(e, fq.blocks_from_fastq(t1), fq.Config(lossy=1.15))
     finally:
         e.close()
 
