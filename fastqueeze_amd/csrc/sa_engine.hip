@@ -2053,6 +2053,13 @@ int sa_fetch(sa_ctx* c, sa_out* out, int n)
     return 0;
 }
 
+int sa_fetch_sizes(const sa_ctx* c, uint64_t* sizes, int n)
+{
+    if (!c || !c->have_output || (n && !sizes) || (uint32_t)n != c->final_len.size()) return -1;
+    for (int b = 0; b < n; b++) sizes[b] = c->final_len[(size_t)b];
+    return 0;
+}
+
 int sa_code_records(sa_ctx* c, int nstreams, const uint32_t* lens, const uint16_t* cum, const uint16_t* freq,
                     const uint16_t* tot, uint8_t* out, uint64_t out_cap, uint64_t* out_lens)
 {

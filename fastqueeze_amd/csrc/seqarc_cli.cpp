@@ -1735,6 +1735,11 @@ int compress(const Options& o)
     const bool dev_parse = !o.host_parse && !o.host_only;
     ParsedPool pool;   // (declared before the jobs: outlive them)
     OutPool outpool;
+    // (round 6) the device-parse path sizes each block's output buffer by its
+    // encoded size (sa_fetch_sizes after sa_run) instead of its output bound:
+    // the pool held ~270 buffers of ~180 MB of address space for ~7 MB blocks,
+    // whose teardown was most of the exit (r6z).  SA_CLI_OUT_EXACT=0: the bound (A/B)
+    const bool out_exact = !(std::getenv("SA_CLI_OUT_EXACT") && std::atoi(std::getenv("SA_CLI_OUT_EXACT")) == 0);
     TextPool texts;
     texts.pinned = dev_parse && !o.ingest_only;
     texts.win = (pe ? (size_t)((uint32_t)bs >> 1) : (size_t)bs) + (64u << 10);   // a window + slack for the carry
@@ -2539,13 +2544,24 @@ int compress(const Options& o)
                         give_back(*js[i], texts);   // (the device holds the text now)
                         js[i]->nreads = ti[i].nreads;
                         js[i]->len_long = ti[i].len_long;
-                        outpool.take(js[i]->out, ti[i].out_bound);
-                        outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                        if (!out_exact) {
+                            outpool.take(js[i]->out, ti[i].out_bound);
+                            outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                        }
                     }
                     cv.notify_all();   // (text windows are free for the reader)
                     const double tr = now_s();
                     if ((chain ? sa_run_aligned(ctx, &c, &acfg[ctx], chain, (uint64_t)k) : sa_run(ctx, &c)) != 0)
                         return fail(std::string("encode failed: ") + sa_last_error(ctx));
+                    if (out_exact) {   // the output buffers sized by the encoded blocks
+                        std::vector<uint64_t> fs(js.size());
+                        if (sa_fetch_sizes(ctx, fs.data(), (int)fs.size()) != 0)
+                            return fail(std::string("fetch failed: ") + sa_last_error(ctx));
+                        for (size_t i = 0; i < js.size(); i++) {
+                            outpool.take(js[i]->out, fs[i]);
+                            outs[i] = sa_out{js[i]->out.data(), js[i]->out.size(), 0};
+                        }
+                    }
                     const double tf = now_s();
                     if (sa_fetch(ctx, outs.data(), (int)outs.size()) != 0)
                         return fail(std::string("fetch failed: ") + sa_last_error(ctx));

@@ -116,6 +116,10 @@ void *sa_host_alloc(uint64_t bytes);
 void sa_host_free(void *p);
 int sa_run(sa_ctx *ctx, const sa_cfg *cfg);                /* encode the staged batch */
 int sa_fetch(sa_ctx *ctx, sa_out *out, int n);             /* D2H of the encaps     */
+/* the encoded size of each of the last run's n blocks (what sa_fetch will
+ * copy), so a caller can size its output buffers before the fetch instead of
+ * reserving sa_output_bound for every block; -1 on a count mismatch */
+int sa_fetch_sizes(const sa_ctx *ctx, uint64_t *sizes, int n);
 /* per-phase device time (ms) of the last sa_run, measured with HIP events on
  * the stream each phase runs on; returns the number of phases written */
 int sa_phase_times(const sa_ctx *ctx, const char **names, float *ms, int max);

@@ -32,6 +32,13 @@ def run(d, env_extra):
             res["exit_to_reaped_s"] = round(m1 - me, 3)
         if "exit probe" in ln or "contexts ready" in ln or "blocks written" in ln:
             res.setdefault("lines", []).append(ln.split(": ", 1)[1])
+    if r.returncode == 0 and os.environ.get("AB_MD5"):
+        import hashlib
+        h = hashlib.md5()
+        with open(os.path.join(d, "e2e.arc"), "rb") as f:
+            for chunk in iter(lambda: f.read(64 << 20), b""):
+                h.update(chunk)
+        res["arc_md5"] = h.hexdigest()
     try:
         os.remove(os.path.join(d, "e2e.arc"))
     except OSError:
