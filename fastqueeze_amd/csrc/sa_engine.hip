@@ -536,8 +536,6 @@ hipError_t sync_d2h(sa_ctx* c, hipStream_t st)
     return e;
 }
 
-// grid of a wave-per-read, grid-stride kernel (EMIT_WAVES waves per workgroup):
-// 8 workgroups per CU, fewer for a small batch
 // Reads per take of the front kernels' read counter: ~64 reads' worth of
 // 150 bp (about 10 KB of bases) a take, so short-read batches keep WQ_CHUNK
 // and long-read batches take one wave's four reads at a time; a multiple of
@@ -550,6 +548,8 @@ uint32_t front_wq_chunk(const sa_ctx* c, uint64_t seq_bytes, uint32_t nreads)
     return (uint32_t)std::max<uint64_t>(4, std::min<uint64_t>(WQ_CHUNK, k) & ~3ull);
 }
 
+// grid of a wave-per-read, grid-stride kernel (EMIT_WAVES waves per workgroup):
+// 8 workgroups per CU, fewer for a small batch
 uint32_t wave_grid(const sa_ctx* c, uint32_t nreads)
 {
     return std::max<uint32_t>(1, std::min<uint32_t>((nreads + EMIT_WAVES - 1) / EMIT_WAVES, c->wg_per_cu * c->n_cu));
