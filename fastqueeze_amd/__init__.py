@@ -103,7 +103,7 @@ def load_library(path: str | None = None):
         "sa_create": ([I32], P), "sa_destroy": ([P], None), "sa_last_error": ([P], C.c_char_p),
         "sa_version": ([], C.c_char_p), "sa_output_bound": ([P], U64),
         "sa_encode_blocks": ([P, P, I32, P, P], I32), "sa_stage": ([P, P, I32], I32),
-        "sa_run": ([P, P], I32), "sa_fetch": ([P, P, I32], I32),
+        "sa_run": ([P, P], I32), "sa_fetch": ([P, P, I32], I32), "sa_fetch_sizes": ([P, P, I32], I32),
         "sa_phase_times": ([P, P, P, I32], I32), "sa_set_timing": ([P, I32], None),
         "sa_cut_se": ([P, U64, U64, P, U64], I64), "sa_cut_pe": ([P, U64, P, U64, U64, P, P, U64], I64),
         "sa_parse_se": ([P, U64, P, P, P, P, P], I64), "sa_parse_pe": ([P, U64, P, U64, P, P, P, P, P], I64),
@@ -347,6 +347,17 @@ class Encoder:
         c = cfg._c()
         if self._lib.sa_run(self._ctx, C.byref(c)) != 0:
             self._err("sa_run")
+
+    def fetch_sizes(self) -> list[int]:
+        """The encoded size of each block of the last run (sa_fetch_sizes: what
+        fetch() will return, known before the copies)."""
+        if self._staged is None:
+            raise SeqArcError("fetch_sizes(): nothing staged")
+        n = len(self._staged)
+        sizes = np.zeros(max(1, n), dtype=np.uint64)
+        if self._lib.sa_fetch_sizes(self._ctx, _ptr(sizes), n) != 0:
+            self._err("sa_fetch_sizes")
+        return [int(x) for x in sizes[:n]]
 
     def fetch(self) -> list[bytes]:
         if self._staged is None:

@@ -162,6 +162,22 @@ def test_exact_payload_fallback(enc, monkeypatch):
     _check(enc, blocks, fq.Config())
 
 
+def test_fetch_sizes(enc):
+    """sa_fetch_sizes after sa_run gives each block's encoded size (the command
+    line sizes its output buffers by it), equal to what sa_fetch copies; a
+    count that is not the batch's is refused."""
+    a, b = synth.generate(6000, paired=True, seed=44)
+    blocks = fq.blocks_from_fastq(a, b, 300_000)
+    assert len(blocks) >= 4
+    first = enc.encode(blocks, fq.Config())
+    enc.run(fq.Config())
+    sizes = enc.fetch_sizes()
+    assert sizes == [len(o) for o in first]
+    assert enc.fetch() == first
+    bad = np.zeros(len(blocks) + 1, dtype=np.uint64)
+    assert enc._lib.sa_fetch_sizes(enc._ctx, fq._ptr(bad), len(blocks) + 1) == -1
+
+
 def test_deterministic_rerun(enc):
     a, b = synth.generate(2000, paired=True, seed=4)
     blocks = fq.blocks_from_fastq(a, b)
