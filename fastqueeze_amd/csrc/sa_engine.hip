@@ -1517,6 +1517,8 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
     uint32_t* wq_prep = c->front_static ? nullptr : d_err + 8;
     uint32_t* wq_emit = c->front_static ? nullptr : d_err + 9;
     const uint32_t wqc = front_wq_chunk(c, I->seq_bytes, nr);
+    // k_emit_sq's listed reads from a counter (one a take) for long-read batches
+    uint32_t* wq_dege = c->front_static || wqc >= WQ_CHUNK ? nullptr : d_err + 10;
 
     ev_begin(c, PH_TOTAL, st);
     // ---- MD5 of every block's IDs/bases/quals (calcBlockMd5@0x414d90) on st2,
@@ -1717,7 +1719,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
             hipLaunchKernelGGL(k_emit_sq, dim3(wave_grid(c, nr)), dim3(64 * EMIT_WAVES), 0, st, bv,
                                c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(), F->d_seq_v[0].as<uint32_t>(),
                                akb[0]->as<uint32_t>(), nullptr, c->d_totals.as<uint32_t>(), dege_maxq, seq_sh,
-                               (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE), nullptr);
+                               (uint32_t)(EMIT_SEQ | EMIT_QUAL | EMIT_DEGE), nullptr, nullptr);
         } else {
             hipLaunchKernelGGL(seq_sh ? (wq_emit ? k_emit_sq16<2, true> : k_emit_sq16<2, false>)
                                       : (wq_emit ? k_emit_sq16<0, true> : k_emit_sq16<0, false>),
@@ -1734,7 +1736,7 @@ int run_input(sa_ctx* c, const sa_input* I, const sa_cfg* cfg, bool exact, const
                                    c->d_counts.as<uint32_t>(), F->d_seq_k[0].as<uint32_t>(),
                                    F->d_seq_v[0].as<uint32_t>(), akb[0]->as<uint32_t>(), nullptr,
                                    c->d_totals.as<uint32_t>(), dege_maxq, seq_sh, (uint32_t)EMIT_DEGE,
-                                   c->d_dege_list.as<uint32_t>());
+                                   c->d_dege_list.as<uint32_t>(), wq_dege);
             }
         }
         if (al)   // the alignment streams (AlignInfoProcess[PE], decomposeAlignInfo)

@@ -1051,7 +1051,8 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
                                                               const uint32_t* __restrict__ totals,
                                                               const uint8_t* __restrict__ dege_maxq, const uint32_t seq_sh,
                                                               const uint32_t parts,
-                                                              const uint32_t* __restrict__ dege_list)
+                                                              const uint32_t* __restrict__ dege_list,
+                                                              uint32_t* __restrict__ wq)
 {
     __shared__ uint32_t comp[EMIT_WAVES][64];
     __shared__ uint8_t stage[EMIT_WAVES][2][EMIT_STAGE];
@@ -1062,7 +1063,21 @@ __global__ __launch_bounds__(64 * EMIT_WAVES) void k_emit_sq(const BatchView bv,
         // flagged reads of their own 64-read group -- for long reads, where
         // nearly every read has some, 60,000 reads on ~940 waves, 76 ms per
         // ONT batch, profiles/round5_r5b_ont_kernel_stats.txt)
+        // (round 6) wq: long-read batches take the listed reads one at a time
+        // from a counter, so the waves on CUs that other batches' chains keep
+        // busy take fewer of the 10-50 kbp reads instead of finishing last
         const uint32_t n = dege_list[0];
+        if (wq) {
+            for (;;) {
+                uint32_t i = 0;
+                if (lane == 0) i = atomicAdd(wq, 1u);
+                i = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)i, 0, 64));
+                if (i >= n) break;
+                emit_sq_read(bv, dege_list[1 + i], lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key,
+                             aux_val, totals, dege_maxq, seq_sh, parts);
+            }
+            return;
+        }
         for (uint32_t i = blockIdx.x * EMIT_WAVES + w; i < n; i += gridDim.x * EMIT_WAVES)
             emit_sq_read(bv, dege_list[1 + i], lane, comp[w], stage[w], counts, seq_key, seq_val, aux_key, aux_val,
                          totals, dege_maxq, seq_sh, parts);
