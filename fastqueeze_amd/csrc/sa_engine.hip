@@ -383,6 +383,11 @@ struct sa_ctx {
     // SA_RB_FIX_SERIAL=1: the entries by k_rb_fix (a lane per block, chunk by
     // chunk) instead of k_rb_fix_w (a wave per block, 64 chunks a step; A/B)
     bool rb_fix_serial = std::getenv("SA_RB_FIX_SERIAL") && std::atoi(std::getenv("SA_RB_FIX_SERIAL")) != 0;
+    // k_rb_spec on n workgroups per CU taking 64 chunks at a time from a
+    // counter (round 6: n = 2, the ONT batch's prep+scan 25.0 / 26.4 against
+    // 28.6 / 29.7 ms with one grid of a lane per chunk, r6z8; 4: no gain);
+    // SA_RB_SPEC_WG=n to change, 0 = the one grid
+    uint32_t rb_spec_wg = std::getenv("SA_RB_SPEC_WG") ? (uint32_t)std::max(0, std::atoi(std::getenv("SA_RB_SPEC_WG"))) : 2u;
     // R-Block chunk length, also the stride of the per-chunk arrays (opens,
     // vals): SA_RB_CHUNK=n, a multiple of 32 up to RB_CHUNK.  Not a power of
     // two: the lanes of k_rb_spec walk their chunks in step, so at 8192 every
@@ -729,8 +734,11 @@ int run_rblock(sa_ctx* c, double ratio, uint64_t seq_bytes, BatchView& bv)
     uint8_t* vals = walk ? nullptr : c->d_rb_vals.as<uint8_t>();
     RbInfo* info = walk ? nullptr : c->d_rb_info.as<RbInfo>();
     const uint32_t cs = c->rb_chunk;   // (the arrays' stride per chunk: bytes, opens words * 32)
-    hipLaunchKernelGGL(k_rb_spec, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
-                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), vals, info, cs);
+    // (rb_spec_wg workgroups per CU taking chunks from a counter; 0: one grid)
+    uint32_t* wq_spec = c->rb_spec_wg > 0 ? c->d_err.as<uint32_t>() + 11 : nullptr;
+    const uint32_t sgrid = wq_spec ? std::max<uint32_t>(1, std::min<uint32_t>(rgrid, c->rb_spec_wg * c->n_cu)) : rgrid;
+    hipLaunchKernelGGL(k_rb_spec, dim3(sgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
+                       c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), vals, info, cs, wq_spec);
     hipLaunchKernelGGL(k_rb_guess, dim3(rgrid), dim3(RB_THREADS), 0, st, bv.qual, dck, nck, tab,
                        c->d_rb_opens.as<uint32_t>(), c->d_rb_spec.as<RbRun>(), c->d_rb_guess.as<RbRun>(), cs);
     if (c->rb_fix_serial)

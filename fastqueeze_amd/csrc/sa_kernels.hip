@@ -617,14 +617,30 @@ __global__ __launch_bounds__(RB_THREADS) void k_rb_spec(const uint8_t* __restric
                                                         uint32_t nck, const uint32_t* __restrict__ tab,
                                                         uint32_t* __restrict__ opens, RbRun* __restrict__ spec_exit,
                                                         uint8_t* __restrict__ vals, RbInfo* __restrict__ info,
-                                                        uint32_t cs)
+                                                        uint32_t cs, uint32_t* __restrict__ wq)
 {
     __shared__ uint32_t sh[2 * RB_TAB_WORDS];
     const RbTab t = rb_stage_tab(tab, sh);
-    const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
-    if (c >= nck) return;
-    if (vals) spec_exit[c] = rb_spec_vals(q, ck[c], t, opens + (size_t)c * (cs / 32), vals + (size_t)c * cs, info[c], cs);
-    else spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * (cs / 32), cs / 32);
+    auto one = [&](uint32_t c) __attribute__((always_inline)) {
+        if (vals) spec_exit[c] = rb_spec_vals(q, ck[c], t, opens + (size_t)c * (cs / 32), vals + (size_t)c * cs, info[c], cs);
+        else spec_exit[c] = rb_spec(q, ck[c], t, opens + (size_t)c * (cs / 32), cs / 32);
+    };
+    if (!wq) {   // a lane per chunk, one grid
+        const uint32_t c = blockIdx.x * RB_THREADS + threadIdx.x;
+        if (c < nck) one(c);
+        return;
+    }
+    // (round 6, the default: SA_RB_SPEC_WG workgroups per CU) a smaller grid
+    // whose waves take 64 chunks at a time from a counter, so the waves on CUs
+    // that other batches' chains keep busy take fewer
+    const uint32_t lane = threadIdx.x & 63;
+    for (;;) {
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(wq, 64u);
+        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)b, 0, 64));
+        if (b >= nck) break;
+        if (b + lane < nck) one(b + lane);
+    }
 }
 
 // k_rb_guess: one lane per chunk, the chunk's exit if the run open before it

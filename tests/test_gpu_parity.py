@@ -394,14 +394,15 @@ def _rblock_runs_fastq(seed, n, read_len):
     return b"".join(recs)
 
 
-@pytest.mark.parametrize("serial", ["0", "1"])
-def test_rblock_entry_pass(monkeypatch, serial):
+@pytest.mark.parametrize("serial,spec_wg", [("0", "2"), ("1", "2"), ("0", "0")])
+def test_rblock_entry_pass(monkeypatch, serial, spec_wg):
     """The R-Block entry pass -- k_rb_fix_w (a wave per block, 64 chunks a step,
     the default) and k_rb_fix (SA_RB_FIX_SERIAL=1) -- where many chunks do not
     converge (rb_carry at arbitrary window positions), blocks of several
     windows, and a constant-quality block where no chunk converges: == the
     oracle's serial rblock@0x426c10."""
     monkeypatch.setenv("SA_RB_FIX_SERIAL", serial)
+    monkeypatch.setenv("SA_RB_SPEC_WG", spec_wg)   # (0: k_rb_spec's one grid; 2, the default: a counter)
     e = fq.Encoder(0)
     try:
         blocks = fq.blocks_from_fastq(_rblock_runs_fastq(31, 120, 30000), None, 2 << 20)
